@@ -1,0 +1,471 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY (see orc_core.h header).
+// Restates the graphd GoExecutor (src/graph/GoExecutor.cpp:33-1419) for `GO [M TO] N STEPS FROM
+// <literal vids> OVER ... [REVERSELY|BIDIRECT] [WHERE ...] YIELD [DISTINCT] ...`, the WhereWrapper
+// pushdown rewrite (src/graph/TraverseExecutor.cpp:426-538), calculateExprType (:88-165) and the
+// StorageClient routing (vid -> part by ID_HASH, src/storage/client/StorageClient.cpp:439-449) for
+// a single storaged host (completeness is 0 as soon as any part fails, StorageClient.inl:134-151).
+#include <unordered_set>
+
+#include "orc_query.h"
+
+namespace orc {
+
+namespace {
+
+bool canPushdown(Expression* expr) {                                  // TraverseExecutor.cpp:525-538
+    ExpressionContext ctx;
+    if (!expr->prepare(&ctx).ok()) return false;
+    if (ctx.hasInputProp() || ctx.hasVariableProp() || ctx.hasDstTagProp()) return false;
+    return true;
+}
+
+SupportedType columnTypeToSupportedType(ColumnType t) {
+    switch (t) {
+        case ColumnType::INT: return INT;
+        case ColumnType::STRING: return STRING;
+        case ColumnType::DOUBLE: return DOUBLE;
+        case ColumnType::BOOL: return BOOL;
+        case ColumnType::TIMESTAMP: return TIMESTAMP;
+    }
+    return UNKNOWN;
+}
+
+}  // namespace
+
+bool rewriteForPushdown(Expression* expr) {                           // TraverseExecutor.cpp:461-523
+    switch (expr->kind()) {
+        case Expression::kLogical: {
+            auto* l = static_cast<LogicalExpression*>(expr);
+            if (l->op_ == LogicalExpression::XOR) return canPushdown(l);
+            bool lp = rewriteForPushdown(l->left_.get());
+            bool rp = rewriteForPushdown(l->right_.get());
+            switch (l->op_) {
+                case LogicalExpression::OR: return lp && rp;
+                case LogicalExpression::AND:
+                    if (!lp && !rp) return false;
+                    if (!lp) l->left_ = std::make_unique<PrimaryExpression>(Variant(true));
+                    else if (!rp) l->right_ = std::make_unique<PrimaryExpression>(Variant(true));
+                    return true;
+                default: return false;
+            }
+        }
+        case Expression::kUnary: case Expression::kTypeCasting: case Expression::kArithmetic:
+        case Expression::kRelational: case Expression::kFunctionCall:
+            return canPushdown(expr);
+        case Expression::kPrimary: case Expression::kSourceProp: case Expression::kEdgeRank:
+        case Expression::kEdgeDstId: case Expression::kEdgeSrcId: case Expression::kEdgeType:
+        case Expression::kAliasProp:
+            return true;
+        default:
+            return false;
+    }
+}
+
+namespace {
+
+struct GoExec {
+    const StorageEngine& eng;
+    const SchemaManager& sm;
+    GraphSpaceID space;
+    const GoSentence& s;
+    GoFlags flags;
+    GoResult res;
+    ExpressionContext ctx;
+    uint32_t recordFrom = 1, steps = 1, curStep = 1;
+    std::vector<EdgeType> edgeTypes;
+    std::shared_ptr<Expression> filter;
+    std::string filterPushdown;
+    std::vector<std::shared_ptr<Expression>> yields;
+    std::vector<std::string> yieldAliases;
+    std::vector<VertexID> starts;
+    std::vector<QueryResponse> records;
+    // VertexHolder (GoExecutor.cpp:1337-1412): (vid, tag) -> (row, schema)
+    std::map<std::pair<VertexID, TagID>, std::pair<std::string, std::shared_ptr<Schema>>> vertexHolder;
+    std::map<TagID, std::shared_ptr<Schema>> vertexHolderSchemas;
+
+    GoExec(const StorageEngine& e, GraphSpaceID sp, const GoSentence& sent, GoFlags f)
+        : eng(e), sm(e.schemas), space(sp), s(sent), flags(f) {}
+
+    bool fail(const std::string& msg) { res.ok = false; res.error = msg; res.rows.clear(); return false; }
+    bool isFinalStep() const { return curStep == steps; }
+    bool isRecord() const { return curStep >= recordFrom && curStep <= steps; }
+
+    bool addToEdgeTypes(EdgeType t) {                                  // GoExecutor.cpp:297-319
+        if (s.direction == 0) edgeTypes.push_back(t);
+        else if (s.direction == 1) edgeTypes.push_back(-t);
+        else { edgeTypes.push_back(t); edgeTypes.push_back(-t); }
+        return true;
+    }
+
+    bool prepareClauses() {                                            // :38-89
+        recordFrom = s.recordFrom;
+        steps = s.recordTo;
+        // prepareOver (:254-295) / prepareOverAll (:225-252)
+        if (s.overAll) {
+            ctx.overAll = true;
+            for (auto& name : sm.getAllEdge(space)) {
+                auto t = sm.toEdgeType(space, name);
+                if (!t.ok()) return fail(t.status().msg_);
+                addToEdgeTypes(t.value());
+                if (!ctx.addEdge(name, std::abs(t.value()))) return fail("edge alias(" + name + ") was dup");
+            }
+        } else {
+            for (auto& e : s.over) {
+                auto t = sm.toEdgeType(space, e.first);
+                if (!t.ok()) return fail(t.status().msg_);
+                addToEdgeTypes(t.value());
+                const std::string& alias = e.second.empty() ? e.first : e.second;
+                if (!ctx.addEdge(alias, std::abs(t.value()))) return fail("edge alias(" + alias + ") was dup");
+            }
+        }
+        // prepareWhere (:321-326) -> WhereWrapper::prepare (TraverseExecutor.cpp:426-459)
+        if (s.hasWhere) {
+            auto d = Expression::decode(s.where);
+            if (!d.ok()) return fail(d.status().msg_);
+            filter = d.value();
+            auto st = filter->prepare(&ctx);
+            if (!st.ok()) return fail(st.msg_);
+            if (flags.filter_pushdown) {
+                auto copy = Expression::decode(Expression::encode(filter.get()));
+                if (!copy.ok()) return fail(copy.status().msg_);
+                if (rewriteForPushdown(copy.value().get())) filterPushdown = Expression::encode(copy.value().get());
+            }
+        }
+        // prepareYield / prepareNeededProps (:329-407)
+        for (auto& y : s.yields) {
+            auto d = Expression::decode(y.expr);
+            if (!d.ok()) return fail(d.status().msg_);
+            yields.push_back(d.value());
+            yieldAliases.push_back(y.alias);
+        }
+        for (auto& y : yields) {
+            auto st = y->prepare(&ctx);
+            if (!st.ok()) return fail(st.msg_);
+        }
+        if (ctx.hasVariableProp()) return fail("A variable must be referred in FROM before used in WHERE or YIELD");
+        if (ctx.hasInputProp()) return fail("`$-' must be referred in FROM before used in WHERE or YIELD");
+        for (auto& e : ctx.tagMap) {
+            auto id = sm.toTagID(space, e.first);
+            if (!id.ok()) return fail("Tag `" + e.first + "' not found.");
+            e.second = id.value();
+        }
+        // checkNeededProps (:422-468)
+        auto tagProps = ctx.srcTagProps;
+        tagProps.insert(ctx.dstTagProps.begin(), ctx.dstTagProps.end());
+        for (auto& p : tagProps) {
+            TagID tagId;
+            if (!ctx.getTagId(p.first, tagId)) return fail("Tag `" + p.first + "' not found.");
+            auto ts = sm.getTagSchema(space, tagId);
+            if (!ts) return fail("No tag schema for " + p.first);
+            if (ts->getFieldIndex(p.second) == -1) return fail("`" + p.second + "' is not a prop of `" + p.first + "'");
+        }
+        for (auto& p : ctx.aliasProps) {
+            EdgeType et;
+            if (!ctx.getEdgeType(p.first, et)) return fail("Edge `" + p.first + "' not found.");
+            if (p.second == "_src" || p.second == "_dst" || p.second == "_rank" || p.second == "_type") continue;
+            auto es = sm.getEdgeSchema(space, std::abs(et));
+            if (!es) return fail("No edge schema for " + p.first);
+            if (es->getFieldIndex(p.second) == -1) return fail("`" + p.second + "' is not a prop of `" + p.first + "'");
+        }
+        return true;
+    }
+
+    // getStepOutProps (:840-914)
+    std::vector<PropDef> getStepOutProps() {
+        std::vector<PropDef> props;
+        for (auto e : edgeTypes) props.push_back(PropDef{EDGE, e, "_dst"});
+        if (!isRecord()) return props;
+        for (auto& tp : ctx.srcTagProps) {
+            auto id = sm.toTagID(space, tp.first);
+            props.push_back(PropDef{SOURCE, id.ok() ? id.value() : 0, tp.second});
+        }
+        for (auto& ap : ctx.aliasProps) {
+            if (ap.second == "_dst") continue;
+            EdgeType et = 0;
+            ctx.getEdgeType(ap.first, et);
+            if (s.direction == 0) props.push_back(PropDef{EDGE, et, ap.second});
+            else if (s.direction == 1) props.push_back(PropDef{EDGE, -et, ap.second});
+            else { props.push_back(PropDef{EDGE, et, ap.second}); props.push_back(PropDef{EDGE, -et, ap.second}); }
+        }
+        return props;
+    }
+
+    // StorageClient::clusterIdsToHosts + getNeighbors for one host.
+    GetNeighborsRequest makeRequest(const std::vector<VertexID>& vids) {
+        GetNeighborsRequest req;
+        req.space = space;
+        int32_t numParts = sm.partsNum(space);
+        std::map<PartitionID, size_t> slot;
+        for (auto v : vids) {
+            PartitionID p = idHash(v, numParts);
+            auto it = slot.find(p);
+            if (it == slot.end()) {
+                slot[p] = req.parts.size();
+                req.parts.push_back({p, {v}});
+            } else {
+                req.parts[it->second].second.push_back(v);
+            }
+        }
+        return req;
+    }
+
+    int64_t countScanned(const std::vector<VertexID>& vids) {
+        auto it = eng.stores.find(space);
+        if (it == eng.stores.end()) return 0;
+        int32_t numParts = sm.partsNum(space);
+        int64_t n = 0;
+        for (auto v : vids) {
+            for (auto t : edgeTypes) {
+                auto r = it->second.prefix(keys::edgePrefix(idHash(v, numParts), v, t));
+                n += static_cast<int64_t>(r.second - r.first);
+            }
+        }
+        return n;
+    }
+
+    bool stepOutLoop() {                                               // :520-606
+        while (true) {
+            auto returns = getStepOutProps();
+            std::string pushed;
+            if (flags.filter_pushdown && isFinalStep() && s.direction == 0) pushed = filterPushdown;
+            auto req = makeRequest(starts);
+            req.edge_types = edgeTypes;
+            req.filter = pushed;
+            req.return_columns = returns;
+            res.hopFrontier.push_back(static_cast<int64_t>(starts.size()));
+            res.hopScanned.push_back(countScanned(starts));
+            auto resp = eng.getBound(req);
+            if (!resp.failed_codes.empty()) return fail("Get neighbors failed");
+            records.push_back(std::move(resp));
+            // getDstIdsFromRespWithBackTrack (:675-718) — the frontier is the set of distinct dsts
+            std::unordered_set<VertexID> set;
+            for (auto& vd : records.back().vertices)
+                for (auto& ed : vd.edge_data)
+                    for (auto& e : ed.edges) set.insert(e.dst);
+            if (isFinalStep()) return true;
+            starts.assign(set.begin(), set.end());
+            if (starts.empty()) {
+                if (!isRecord()) { records.clear(); return true; }   // onEmptyInputs
+                return true;
+            }
+            curStep++;
+        }
+    }
+
+    bool fetchVertexProps() {                                          // :610-635, :937-973
+        if (!ctx.hasDstTagProp()) return true;
+        std::unordered_set<VertexID> set;
+        for (size_t i = recordFrom - 1; i < records.size(); i++)
+            for (auto& vd : records[i].vertices)
+                for (auto& ed : vd.edge_data)
+                    for (auto& e : ed.edges) set.insert(e.dst);
+        if (set.empty()) { records.clear(); return true; }
+        std::vector<VertexID> ids(set.begin(), set.end());
+        auto req = makeRequest(ids);
+        req.has_edge_types = false;
+        for (auto& tp : ctx.dstTagProps) {
+            auto id = sm.toTagID(space, tp.first);
+            if (!id.ok()) return fail("No schema found for '" + tp.first + "'");
+            req.return_columns.push_back(PropDef{DEST, id.value(), tp.second});
+        }
+        auto resp = eng.getBound(req, /*onlyVertexProps=*/true);
+        if (!resp.failed_codes.empty()) return fail("Get dest props failed");
+        for (auto& kv : resp.vertex_schema) vertexHolderSchemas.emplace(kv.first, kv.second);
+        for (auto& vd : resp.vertices) {
+            for (auto& td : vd.tag_data) {
+                vertexHolder.emplace(std::make_pair(vd.vertex_id, td.tag_id),
+                                     std::make_pair(td.data, vertexHolderSchemas[td.tag_id]));
+            }
+        }
+        return true;
+    }
+
+    SupportedType calculateExprType(const Expression* e) {             // TraverseExecutor.cpp:88-165
+        switch (e->kind()) {
+            case Expression::kPrimary: case Expression::kFunctionCall:
+            case Expression::kUnary: case Expression::kArithmetic: return UNKNOWN;
+            case Expression::kTypeCasting:
+                return columnTypeToSupportedType(static_cast<const TypeCastingExpression*>(e)->type_);
+            case Expression::kRelational: case Expression::kLogical: return BOOL;
+            case Expression::kDestProp: case Expression::kSourceProp: {
+                auto* a = static_cast<const AliasPropertyExpression*>(e);
+                auto id = sm.toTagID(space, a->alias());
+                if (id.ok()) {
+                    auto ts = sm.getTagSchema(space, id.value());
+                    if (ts) return ts->getFieldType(a->prop());
+                }
+                return UNKNOWN;
+            }
+            case Expression::kEdgeDstId: case Expression::kEdgeSrcId: return VID;
+            case Expression::kEdgeRank: case Expression::kEdgeType: return INT;
+            case Expression::kAliasProp: {
+                auto* a = static_cast<const AliasPropertyExpression*>(e);
+                auto et = sm.toEdgeType(space, a->alias());
+                if (et.ok()) {
+                    auto es = sm.getEdgeSchema(space, et.value());
+                    if (es) return es->getFieldType(a->prop());
+                }
+                return UNKNOWN;
+            }
+            default: return UNKNOWN;
+        }
+    }
+
+    bool processFinalResult() {                                        // :1082-1335
+        std::vector<SupportedType> colTypes;
+        for (auto& y : yields) colTypes.push_back(calculateExprType(y.get()));
+        res.colTypes = colTypes;
+        std::map<TagID, std::shared_ptr<Schema>> tagSchema;
+        std::map<EdgeType, std::shared_ptr<Schema>> edgeSchema;
+        VertexID srcId = 0, dstId = 0;
+        EdgeType edgeType = 0;
+        const std::vector<TagData>* tagData = nullptr;
+        std::unique_ptr<RowReader> reader;
+        const std::string* rowBytes = nullptr;
+
+        Getters g;
+        g.getEdgeDstId = [&](const std::string& edgeName) -> OptVariant {
+            if (edgeTypes.size() > 1) {
+                EdgeType t;
+                if (!ctx.getEdgeType(edgeName, t)) return Status::Error("Get edge type failed in getters.");
+                if (t != std::abs(edgeType)) return OptVariant(int64_t(0));
+            }
+            return OptVariant(dstId);
+        };
+        g.getSrcTagProp = [&](const std::string& tag, const std::string& prop) -> OptVariant {
+            TagID tagId;
+            if (!ctx.getTagId(tag, tagId)) return Status::Error("Get tag id failed in getters.");
+            const TagData* found = nullptr;
+            for (auto& td : *tagData) if (td.tag_id == tagId) { found = &td; break; }
+            if (!found) {
+                auto ts = sm.getTagSchema(space, tagId);
+                if (!ts) return Status::Error("No tag schema");
+                auto d = RowReader::getDefaultProp(ts.get(), prop);
+                if (!d.ok()) return d.status();
+                return OptVariant(d.value());
+            }
+            auto vr = RowReader::make(found->data, tagSchema[tagId]);
+            if (!vr) return Status::Error("bad tag row");
+            auto r = RowReader::getPropByName(vr.get(), prop);
+            if (!r.ok()) return Status::Error("get prop failed");
+            return OptVariant(r.v);
+        };
+        g.getDstTagProp = [&](const std::string& tag, const std::string& prop) -> OptVariant {
+            TagID tagId;
+            if (!ctx.getTagId(tag, tagId)) return Status::Error("Get tag id failed in getters.");
+            auto it = vertexHolder.find({dstId, tagId});
+            bool ok = false;
+            Variant v;
+            if (it != vertexHolder.end()) {
+                auto vr = RowReader::make(it->second.first, it->second.second);
+                if (vr) {
+                    auto r = RowReader::getPropByName(vr.get(), prop);
+                    if (r.ok()) { ok = true; v = r.v; }
+                }
+            } else {
+                // VertexHolder::getDefaultProp: the holder's response schema, else the latest one
+                auto hs = vertexHolderSchemas.find(tagId);
+                StatusOr<Variant> d = hs != vertexHolderSchemas.end()
+                    ? RowReader::getDefaultProp(hs->second.get(), prop)
+                    : (sm.getTagSchema(space, tagId) ? RowReader::getDefaultProp(sm.getTagSchema(space, tagId).get(), prop)
+                                                     : StatusOr<Variant>(Status::Error("No tag schema")));
+                if (d.ok()) { ok = true; v = d.value(); }
+            }
+            if (!ok) {
+                auto ts = sm.getTagSchema(space, tagId);
+                if (!ts) return Status::Error("No tag schema");
+                auto d = RowReader::getDefaultProp(ts.get(), prop);
+                if (!d.ok()) return d.status();
+                return OptVariant(d.value());
+            }
+            return OptVariant(v);
+        };
+        g.getAliasProp = [&](const std::string& edgeName, const std::string& prop) -> OptVariant {
+            EdgeType type;
+            if (!ctx.getEdgeType(edgeName, type)) return Status::Error("Get edge type failed in getters.");
+            if (std::abs(edgeType) != type) {
+                auto sit = edgeSchema.find(s.direction == 1 ? -type : type);
+                if (sit == edgeSchema.end()) return Status::Error("Can't find schema when get default.");
+                auto d = RowReader::getDefaultProp(sit->second.get(), prop);
+                if (!d.ok()) return d.status();
+                return OptVariant(d.value());
+            }
+            if (prop == "_src") return OptVariant(srcId);
+            if (!reader) return Status::Error("null reader");
+            auto r = RowReader::getPropByName(reader.get(), prop);
+            if (!r.ok()) return Status::Error("get prop failed");
+            return OptVariant(r.v);
+        };
+
+        std::set<std::vector<Variant>> uniq;
+        for (size_t ri = recordFrom - 1; ri < records.size(); ri++) {
+            auto& resp = records[ri];
+            for (auto& kv : resp.vertex_schema) tagSchema.emplace(kv.first, kv.second);
+            for (auto& kv : resp.edge_schema) edgeSchema.emplace(kv.first, kv.second);
+            for (auto& vd : resp.vertices) {
+                tagData = &vd.tag_data;
+                srcId = vd.vertex_id;
+                for (auto& ed : vd.edge_data) {
+                    edgeType = ed.type;
+                    auto sit = edgeSchema.find(edgeType);
+                    for (auto& e : ed.edges) {
+                        dstId = e.dst;
+                        rowBytes = &e.props;
+                        reader = sit != edgeSchema.end() ? RowReader::make(*rowBytes, sit->second) : nullptr;
+                        if (filter) {
+                            auto v = filter->eval(g);
+                            if (!v.ok()) return fail(v.status().msg_);
+                            if (!Expression::asBool(v.value())) continue;
+                        }
+                        std::vector<Variant> record;
+                        for (auto& y : yields) {
+                            auto v = y->eval(g);
+                            if (!v.ok()) return fail(v.status().msg_);
+                            record.push_back(v.value());
+                        }
+                        if (s.distinct && !uniq.insert(record).second) continue;
+                        res.rows.push_back(std::move(record));
+                    }
+                }
+            }
+        }
+        return true;
+    }
+
+    GoResult run() {
+        if (!prepareClauses()) return res;
+        for (size_t i = 0; i < yields.size(); i++) {
+            res.columnNames.push_back(yieldAliases[i].empty() ? yields[i]->toString() : yieldAliases[i]);
+        }
+        if (steps == 0) return res;                                    // :99-104
+        if (recordFrom == 0) recordFrom = 1;
+        starts = s.vids;
+        if (starts.empty()) return res;
+        if (s.distinct) {
+            std::unordered_set<VertexID> u(starts.begin(), starts.end());
+            starts.assign(u.begin(), u.end());
+        }
+        if (!stepOutLoop()) return res;
+        if (records.empty()) return res;
+        if (!fetchVertexProps()) return res;
+        if (records.empty()) return res;
+        if (ctx.overAll && yields.empty()) {                           // :723-732
+            for (auto& a : ctx.edgeAlias) {
+                auto e = std::make_shared<AliasPropertyExpression>("", a, "_dst");
+                e->setKind(Expression::kEdgeDstId);
+                yields.push_back(e);
+            }
+        }
+        processFinalResult();
+        return res;
+    }
+};
+
+}  // namespace
+
+GoResult runGo(const StorageEngine& eng, GraphSpaceID space, const GoSentence& s, const GoFlags& f) {
+    GoExec e(eng, space, s, f);
+    return e.run();
+}
+
+}  // namespace orc
