@@ -53,7 +53,7 @@ def lib():
             getattr(L, fn).restype = vp
         L.orc_go.argtypes = [vp, ctypes.c_int32, ctypes.c_char_p, ctypes.c_uint64, u64p]
         L.orc_go.restype = vp
-        for fn in ("orc_expr_eval", "orc_expr_roundtrip", "orc_expr_pushdown"):
+        for fn in ("orc_expr_eval", "orc_expr_roundtrip", "orc_expr_pushdown", "orc_expr_to_string"):
             getattr(L, fn).argtypes = [ctypes.c_char_p, ctypes.c_uint64, u64p]
             getattr(L, fn).restype = vp
         L.orc_std_hash_string.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
@@ -145,6 +145,10 @@ def expr_roundtrip(enc: bytes) -> bytes:
 
 def expr_pushdown(enc: bytes) -> bytes:
     return _call(lib().orc_expr_pushdown, enc, len(enc))
+
+
+def expr_to_string(enc: bytes) -> str:
+    return _call(lib().orc_expr_to_string, enc, len(enc)).decode()
 
 
 def std_hash(s: str) -> int:

@@ -262,6 +262,12 @@ char* orc_expr_pushdown(const uint8_t* buf, uint64_t len, uint64_t* outLen) {
     return toHeap(Expression::encode(d.value().get()), outLen);
 }
 
+char* orc_expr_to_string(const uint8_t* buf, uint64_t len, uint64_t* outLen) {
+    auto d = Expression::decode(std::string(reinterpret_cast<const char*>(buf), len));
+    if (!d.ok()) { *outLen = 0; return toHeap("", outLen); }
+    return toHeap(d.value()->toString(), outLen);
+}
+
 int64_t orc_std_hash_string(const char* s, uint64_t n) {
     return static_cast<int64_t>(std::hash<std::string>()(std::string(s, n)));
 }
