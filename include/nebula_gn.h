@@ -1,0 +1,229 @@
+/*
+ * nebula_gn.h — C ABI of the MI355X GetNeighbors / GO engine (libnebula_gn.so).
+ *
+ * Drop-in boundary for the storage-side neighbor expansion + property filter of NebulaGraph v1
+ * (the reference at /root/reference) and the graphd GoExecutor multi-hop driver. Plain C types
+ * only; no exceptions cross it; every call returns an int32 status whose negative values are the
+ * reference's storage.thrift ErrorCode numbers (src/interface/storage.thrift:13-59) or the
+ * NGX_E_* codes below. One in-flight call per ngx_ctx (calls on one context are serialized by an
+ * internal mutex). The context owns one HIP device and one stream; with world > 1 it also owns an
+ * RCCL communicator whose ranks are the GPUs of one node (one process per GPU).
+ *
+ * Reference interfaces replaced (file:line in /root/reference):
+ *   ngx_open / ngx_close        StorageServer::start + NebulaStore instance (src/storage/StorageServer.cpp:99-168)
+ *   ngx_add_space / _schema     meta::SchemaManager::getTagSchema/getEdgeSchema/toEdgeType/toTagID
+ *                               (src/meta/SchemaManager.h:18-56) and partsNum (StorageClient.h:292-295)
+ *   ngx_load_kv / ngx_commit    the part -> CSR snapshot export: KVStore::prefix over a part
+ *                               (src/kvstore/KVStore.h:108-111, NebulaStore.cpp:451-464) as dumped by
+ *                               DumpEdgesTool (src/tools/dump-edges/DumpEdgesTool.cpp:17-50)
+ *   ngx_get_neighbors           QueryBoundProcessor::process (src/storage/query/QueryBaseProcessor.inl:800-855,
+ *                               src/storage/query/QueryBoundProcessor.cpp:18-261), invoked from
+ *                               StorageServiceHandler::future_getBound (src/storage/StorageServiceHandler.cpp:45-53)
+ *   ngx_go                      GoExecutor::execute .. toThriftResponse (src/graph/GoExecutor.cpp:92-838, 1082-1335)
+ *   ngx_*_free                  results are library-allocated, host-visible, freed only by the library
+ */
+#ifndef NEBULA_GN_H_
+#define NEBULA_GN_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes: 0 ok, reference ErrorCode values, and these */
+#define NGX_OK 0
+#define NGX_E_INVALID_FILTER (-31)      /* storage.thrift E_INVALID_FILTER */
+#define NGX_E_EDGE_PROP_NOT_FOUND (-21)
+#define NGX_E_TAG_PROP_NOT_FOUND (-22)
+#define NGX_E_IMPROPER_DATA_TYPE (-23)
+#define NGX_E_EDGE_NOT_FOUND (-24)
+#define NGX_E_TAG_NOT_FOUND (-25)
+#define NGX_E_SPACE_NOT_FOUND (-13)
+#define NGX_E_BAD_ARGUMENT (-1001)
+#define NGX_E_UNSUPPORTED (-1002)       /* a construct the device path does not implement */
+#define NGX_E_QUERY (-1003)             /* graphd-side evaluation error (GoExecutor doError) */
+#define NGX_E_DEVICE (-1004)            /* HIP / RCCL failure */
+#define NGX_E_NOT_LOADED (-1005)
+
+/* SupportedType (src/interface/common.thrift:30-56) */
+#define NGX_T_BOOL 1
+#define NGX_T_INT 2
+#define NGX_T_VID 3
+#define NGX_T_FLOAT 4
+#define NGX_T_DOUBLE 5
+#define NGX_T_STRING 6
+#define NGX_T_TIMESTAMP 21
+
+typedef struct ngx_ctx ngx_ctx;
+
+typedef struct {
+    int32_t device;               /* HIP device ordinal */
+    int32_t rank;                 /* this shard (GPU) 0..world-1 */
+    int32_t world;                /* shards on the node; part p lives on shard p % world */
+    const void* nccl_unique_id;   /* 128-byte ncclUniqueId when world > 1 */
+} ngx_config;
+
+int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out);
+void ngx_close(ngx_ctx* ctx);
+const char* ngx_last_error(ngx_ctx* ctx);
+/* rank 0 calls this and broadcasts the 128 bytes to the other ranks before ngx_open */
+int32_t ngx_get_unique_id(void* out128);
+
+/* ---------------------------------------------------------------- schema registry */
+int32_t ngx_add_space(ngx_ctx* ctx, int32_t space, int32_t num_parts);
+int32_t ngx_add_schema(ngx_ctx* ctx, int32_t space, int32_t is_edge, int32_t id, const char* name,
+                       int64_t version, int32_t nfields, const char* const* field_names,
+                       const int32_t* field_types, const char* ttl_col, int64_t ttl_duration);
+
+/* ---------------------------------------------------------------- snapshot export */
+typedef struct {
+    uint64_t n;                   /* rows */
+    const uint8_t* keys;          /* reference NebulaKeyUtils keys, concatenated */
+    const uint64_t* key_off;      /* n + 1 offsets into keys */
+    const uint8_t* vals;          /* RowWriter values, concatenated */
+    const uint64_t* val_off;      /* n + 1 offsets into vals */
+} ngx_kv_batch;
+
+/* Stage rows; rows of parts this shard does not own are dropped. May be called repeatedly. */
+int32_t ngx_load_kv(ngx_ctx* ctx, int32_t space, const ngx_kv_batch* batch);
+/* Build the per-part CSR + columnar props from the staged rows and upload them to HBM.
+ * Collective when world > 1 (vertex tables are exchanged to resolve destination rows). */
+int32_t ngx_commit(ngx_ctx* ctx, int32_t space);
+
+typedef struct {
+    uint64_t vertices;            /* rows in this shard's vertex table */
+    uint64_t edges;               /* CSR edges over all edge-type slots (after version dedup) */
+    uint64_t device_bytes;        /* HBM held by the snapshot */
+    int32_t slots;                /* signed edge types present */
+    int32_t tags;
+} ngx_graph_info;
+int32_t ngx_graph_info_get(ngx_ctx* ctx, int32_t space, ngx_graph_info* out);
+
+/* ---------------------------------------------------------------- result cells */
+/* One typed value, mirroring graph.thrift ColumnValue (src/interface/graph.thrift:80-127) as set
+ * by GoExecutor::toThriftResponse (GoExecutor.cpp:775-829). */
+#define NGX_CELL_EMPTY 0
+#define NGX_CELL_BOOL 1
+#define NGX_CELL_INT 2
+#define NGX_CELL_ID 3
+#define NGX_CELL_FLOAT 4
+#define NGX_CELL_DOUBLE 5
+#define NGX_CELL_STR 6
+#define NGX_CELL_TIMESTAMP 21
+typedef struct {
+    int32_t kind;                 /* NGX_CELL_* */
+    int32_t str_len;              /* for NGX_CELL_STR */
+    union { int64_t i; double d; uint64_t str_off; } v;   /* str_off indexes the result's strings */
+} ngx_cell;
+
+/* ---------------------------------------------------------------- GetNeighbors */
+typedef struct {
+    int32_t owner;                /* PropOwner: 1 SOURCE, 2 DEST, 3 EDGE (storage.thrift:62-83) */
+    int32_t id;                   /* tag id, or signed edge type */
+    const char* name;
+} ngx_prop_def;
+
+typedef struct {
+    int32_t space;
+    int32_t nparts;
+    const int32_t* parts;         /* part id of each group */
+    const uint32_t* part_nvids;   /* vids per group */
+    const int64_t* vids;          /* all vids, group after group */
+    int32_t nedge_types;
+    const int32_t* edge_types;    /* signed: > 0 out-edges, < 0 in-edges */
+    const uint8_t* filter;        /* Expression::encode bytes, may be empty */
+    uint32_t filter_len;
+    int32_t ncols;
+    const ngx_prop_def* cols;     /* return_columns */
+    int32_t max_edges_per_vertex; /* FLAGS_max_edge_returned_per_vertex, <= 0: unlimited */
+    int64_t now_sec;              /* clock for TTL (WallClock::fastNowInSec) */
+} ngx_gn_request;
+
+typedef struct {
+    int32_t code;                 /* NGX_OK, or the code pushed for every part (checkAndBuildContexts) */
+    int32_t nfailed;
+    const int32_t* failed_codes;  /* (code, part) pairs */
+    uint64_t nedges;              /* total_edges */
+    const uint32_t* edge_vertex;  /* request vid index of each returned edge */
+    const int32_t* edge_type;
+    const int64_t* edge_dst;
+    int32_t ncols;                /* = request ncols; cells[e * ncols + c]; SOURCE/DEST cols are per vertex */
+    const ngx_cell* edge_cells;
+    uint32_t nvertices;           /* request vids (duplicates included) */
+    const ngx_cell* vertex_cells; /* vertex_cells[v * ncols + c] for SOURCE columns; EMPTY if no tag row */
+    const uint8_t* vertex_has_tag;/* [v * ncols + c] 1 if the vertex has that tag row */
+    const char* strings;
+    uint64_t strings_len;
+} ngx_gn_result;
+
+int32_t ngx_get_neighbors(ngx_ctx* ctx, const ngx_gn_request* req, ngx_gn_result** out);
+void ngx_gn_result_free(ngx_gn_result* r);
+
+/* ---------------------------------------------------------------- GO */
+#define NGX_DIR_FORWARD 0
+#define NGX_DIR_REVERSELY 1
+#define NGX_DIR_BIDIRECT 2
+
+typedef struct {
+    int32_t space;
+    uint32_t record_from, record_to;   /* StepClause: GO [M TO] N STEPS */
+    uint64_t nstarts;
+    const int64_t* starts;             /* FROM vids (evaluated) */
+    int32_t nover;
+    const char* const* over_names;     /* edge names */
+    const char* const* over_aliases;   /* alias or NULL/"" */
+    int32_t over_all;                  /* OVER * */
+    int32_t direction;                 /* NGX_DIR_* */
+    const uint8_t* where;              /* encoded WHERE, may be NULL */
+    uint32_t where_len;
+    int32_t nyields;
+    const uint8_t* const* yields;      /* encoded YIELD expressions */
+    const uint32_t* yield_lens;
+    int32_t distinct;                  /* YIELD DISTINCT */
+    int32_t filter_pushdown;           /* FLAGS_filter_pushdown */
+    int64_t now_sec;
+} ngx_go_plan;
+
+typedef struct {
+    int32_t code;                      /* NGX_OK or an error (message in ngx_last_error) */
+    int32_t ncols;
+    const int32_t* col_types;          /* calculateExprType per YIELD column */
+    uint64_t nrows;
+    const ngx_cell* cells;             /* cells[row * ncols + col] */
+    const int64_t* row_src;            /* src vid, dst vid, rank, signed type of the edge behind each row */
+    const int64_t* row_dst;
+    const int64_t* row_rank;
+    const int32_t* row_type;
+    const char* strings;
+    uint64_t strings_len;
+    /* statistics of the run on this shard */
+    int32_t nhops;
+    const uint64_t* hop_frontier;      /* frontier entries expanded per hop */
+    const uint64_t* hop_edges;         /* edges scanned per hop (TEPS numerator) */
+    const uint64_t* hop_next;          /* unique next-frontier vertices per hop (this shard) */
+    double device_ms;                  /* HIP-event time from the first kernel to the last result write */
+} ngx_go_result;
+
+int32_t ngx_go(ngx_ctx* ctx, const ngx_go_plan* plan, ngx_go_result** out);
+void ngx_go_result_free(ngx_go_result* r);
+
+/* ---------------------------------------------------------------- measurement hooks */
+/* Per-kernel device times of the last ngx_go (HIP events on the engine stream), for bench.py. */
+typedef struct {
+    const char* name;
+    uint32_t launches;
+    double total_ms;
+    uint64_t algo_bytes;               /* algorithmic bytes attributed to this kernel class */
+} ngx_kernel_stat;
+int32_t ngx_set_profiling(ngx_ctx* ctx, int32_t on);
+int32_t ngx_kernel_stats(ngx_ctx* ctx, const ngx_kernel_stat** out, int32_t* n);
+
+/* libstdc++ std::hash<std::string>, the NBA fixture's vid function (TraverseTestBase.h:122-126) */
+int64_t ngx_hash_string(const char* s, uint64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif  /* NEBULA_GN_H_ */

@@ -1,0 +1,337 @@
+// Synthetic graph generators emitting reference-format KV rows (NebulaKeyUtils keys + RowWriter
+// values), the form in which a storaged part would be exported (src/common/utils/NebulaKeyUtils.cpp:
+// 12-45, src/dataman/RowWriter.cpp:39-263). Used by bench.py and the parity tests for the BASELINE
+// configs: RMAT (C2/C3), power-law with supernodes (C4) and an LDBC-SNB-like multi-type schema (C5).
+//
+// Every random draw is a counter-based hash of (seed, stream, index), so the generated graph is a
+// pure function of the parameters, independent of thread count and of (rank, world) filtering:
+// with world > 1 only the rows of parts p with p % world == rank are materialised.
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+inline uint64_t mix64(uint64_t x) {             // splitmix64 finaliser
+    x += 0x9e3779b97f4a7c15ULL;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
+    return x ^ (x >> 31);
+}
+inline uint64_t draw(uint64_t seed, uint64_t stream, uint64_t i) {
+    return mix64(seed * 0x100000001b3ULL ^ mix64(stream * 0x9e3779b97f4a7c15ULL + i));
+}
+
+// RowWriter with a schema of ints / doubles / strings, schema version 0 and < 16 fields:
+// header byte (offset width - 1) then the fields (RowWriter.cpp:49-75, RowWriter.inl).
+struct Row {
+    std::string cord;
+    void i64(int64_t v) {
+        uint64_t u = static_cast<uint64_t>(v);
+        while (u >= 0x80) { cord.push_back(static_cast<char>((u & 0x7F) | 0x80)); u >>= 7; }
+        cord.push_back(static_cast<char>(u));
+    }
+    void f64(double d) { cord.append(reinterpret_cast<const char*>(&d), 8); }
+    void str(const std::string& s) { i64(static_cast<int64_t>(s.size())); cord += s; }
+    void encodeTo(std::vector<uint8_t>& out) const {
+        uint64_t n = cord.size();
+        int ob = 0;
+        do { ob++; n >>= 8; } while (n);
+        out.push_back(static_cast<uint8_t>(ob - 1));
+        out.insert(out.end(), cord.begin(), cord.end());
+    }
+};
+
+struct Sink {                                    // one thread's output
+    std::vector<uint8_t> keys, vals;
+    std::vector<uint64_t> klen, vlen;            // per-row lengths; offsets are built in finish()
+    uint64_t n = 0;
+    void edge(int32_t part, int64_t src, int32_t etype, int64_t rank, int64_t dst, const Row& r) {
+        uint8_t k[40];
+        int32_t item = (part << 8) | 1;
+        uint32_t et = static_cast<uint32_t>(etype) | 0x40000000u;
+        int64_t ver = 0;
+        std::memcpy(k, &item, 4); std::memcpy(k + 4, &src, 8); std::memcpy(k + 12, &et, 4);
+        std::memcpy(k + 16, &rank, 8); std::memcpy(k + 24, &dst, 8); std::memcpy(k + 32, &ver, 8);
+        keys.insert(keys.end(), k, k + 40);
+        klen.push_back(40);
+        size_t before = vals.size();
+        r.encodeTo(vals);
+        vlen.push_back(vals.size() - before);
+        n++;
+    }
+    void vertex(int32_t part, int64_t vid, int32_t tag, const Row& r) {
+        uint8_t k[24];
+        int32_t item = (part << 8) | 1;
+        int64_t ver = 0;
+        std::memcpy(k, &item, 4); std::memcpy(k + 4, &vid, 8); std::memcpy(k + 12, &tag, 4);
+        std::memcpy(k + 16, &ver, 8);
+        keys.insert(keys.end(), k, k + 24);
+        klen.push_back(24);
+        size_t before = vals.size();
+        r.encodeTo(vals);
+        vlen.push_back(vals.size() - before);
+        n++;
+    }
+};
+
+struct Gen {
+    int32_t numParts, rank, world;
+    int threads;
+    std::vector<Sink> sinks;
+    int32_t partOf(int64_t vid) const { return static_cast<int32_t>(static_cast<uint64_t>(vid) % numParts + 1); }
+    bool owned(int64_t vid) const { return world <= 1 || partOf(vid) % world == rank; }
+    template <typename F>
+    void run(uint64_t n, F&& f) {                // f(sink, i) for i in [0, n), contiguous chunks per thread
+        sinks.assign(threads, Sink());
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; t++) {
+            th.emplace_back([&, t] {
+                uint64_t lo = n * t / threads, hi = n * (t + 1) / threads;
+                for (uint64_t i = lo; i < hi; i++) f(sinks[t], i);
+            });
+        }
+        for (auto& x : th) x.join();
+        flush();
+    }
+    std::vector<Sink> done;
+    void flush() { for (auto& s : sinks) done.push_back(std::move(s)); sinks.clear(); }
+};
+
+}  // namespace
+
+extern "C" {
+
+typedef struct {
+    uint64_t n;
+    uint8_t* keys;
+    uint64_t* key_off;
+    uint8_t* vals;
+    uint64_t* val_off;
+} ngd_rows;
+
+void ngd_free(ngd_rows* r) {
+    if (!r) return;
+    std::free(r->keys); std::free(r->key_off); std::free(r->vals); std::free(r->val_off);
+    std::memset(r, 0, sizeof(*r));
+}
+
+}  // extern "C"
+
+namespace {
+
+// concatenate the thread sinks into one ngd_rows (key offsets from the per-row key lengths)
+void finish(Gen& g, ngd_rows* out) {
+    uint64_t n = 0, kb = 0, vb = 0;
+    for (auto& s : g.done) { n += s.n; kb += s.keys.size(); vb += s.vals.size(); }
+    out->n = n;
+    out->keys = static_cast<uint8_t*>(std::malloc(std::max<uint64_t>(kb, 1)));
+    out->vals = static_cast<uint8_t*>(std::malloc(std::max<uint64_t>(vb, 1)));
+    out->key_off = static_cast<uint64_t*>(std::malloc((n + 1) * 8));
+    out->val_off = static_cast<uint64_t*>(std::malloc((n + 1) * 8));
+    out->key_off[0] = out->val_off[0] = 0;
+    uint64_t ki = 0, vi = 0, r = 0;
+    for (auto& s : g.done) {
+        std::memcpy(out->keys + ki, s.keys.data(), s.keys.size());
+        std::memcpy(out->vals + vi, s.vals.data(), s.vals.size());
+        for (uint64_t j = 0; j < s.n; j++) {
+            r++;
+            out->key_off[r] = out->key_off[r - 1] + s.klen[j];
+            out->val_off[r] = out->val_off[r - 1] + s.vlen[j];
+        }
+        ki += s.keys.size();
+        vi += s.vals.size();
+        std::vector<uint8_t>().swap(s.keys);
+        std::vector<uint8_t>().swap(s.vals);
+    }
+    g.done.clear();
+}
+
+// RMAT quadrant walk with 16-bit probabilities, four levels per 64-bit draw
+inline void rmatEdge(uint64_t seed, uint64_t i, int scale, uint32_t a, uint32_t ab, uint32_t abc, uint64_t& s,
+                     uint64_t& d) {
+    s = 0; d = 0;
+    uint64_t bits = 0;
+    for (int l = 0; l < scale; l++) {
+        if ((l & 3) == 0) bits = draw(seed, 1 + l / 4, i);
+        uint32_t r = static_cast<uint32_t>(bits & 0xFFFF);
+        bits >>= 16;
+        uint64_t sb = 0, db = 0;
+        if (r < a) { } else if (r < ab) { db = 1; } else if (r < abc) { sb = 1; } else { sb = 1; db = 1; }
+        s = (s << 1) | sb;
+        d = (d << 1) | db;
+    }
+}
+
+// bijective scramble of [0, 2^scale): hubs are spread over the id space (Graph500 permutes ids)
+inline uint64_t scramble(uint64_t v, int scale, uint64_t seed) {
+    uint64_t mask = (scale >= 64) ? ~0ULL : ((1ULL << scale) - 1);
+    uint64_t k1 = (mix64(seed ^ 0xa5a5) | 1) & mask, k2 = mix64(seed ^ 0x5a5a) & mask;
+    for (int r = 0; r < 2; r++) {
+        v = (v * k1) & mask;
+        v ^= (v >> (scale / 2 + 1));
+        v = (v + k2) & mask;
+    }
+    return v;
+}
+
+}  // namespace
+
+extern "C" {
+
+// RMAT (Graph500 A/B/C/D) with `ef * 2^scale` edges of one type `etype` carrying two INT props
+// p0 = h(src,dst) % 100 and p1 = h'(src,dst) % 1000000 (deterministic per (src,dst), so duplicate
+// generated edges write byte-identical rows). rank 0. with_in also writes the in-edge rows
+// (dst, -etype, rank, src), as InsertEdgeExecutor does. with_tag writes tag `tag` (v0 INT = vid % 1000,
+// name STRING = "v<vid>") for every vertex id.
+int32_t ngd_rmat(int32_t scale, int32_t ef, double A, double B, double C, uint64_t seed, int32_t num_parts,
+                 int32_t etype, int32_t with_in, int32_t with_tag, int32_t tag, int32_t rank, int32_t world,
+                 int32_t threads, ngd_rows* out) {
+    if (scale < 1 || scale > 40 || ef < 1 || num_parts < 1 || !out) return -1;
+    Gen g{num_parts, rank, world, threads < 1 ? 1 : threads};
+    uint32_t a = static_cast<uint32_t>(A * 65536), ab = static_cast<uint32_t>((A + B) * 65536),
+             abc = static_cast<uint32_t>((A + B + C) * 65536);
+    uint64_t E = static_cast<uint64_t>(ef) << scale;
+    g.run(E, [&](Sink& s, uint64_t i) {
+        uint64_t su, du;
+        rmatEdge(seed, i, scale, a, ab, abc, su, du);
+        int64_t src = static_cast<int64_t>(scramble(su, scale, seed));
+        int64_t dst = static_cast<int64_t>(scramble(du, scale, seed));
+        uint64_t h = mix64((static_cast<uint64_t>(src) << 20) ^ static_cast<uint64_t>(dst) ^ seed);
+        Row r;
+        r.i64(static_cast<int64_t>(h % 100));
+        r.i64(static_cast<int64_t>((h >> 32) % 1000000));
+        if (g.owned(src)) { s.edge(g.partOf(src), src, etype, 0, dst, r); }
+        if (with_in && g.owned(dst)) { s.edge(g.partOf(dst), dst, -etype, 0, src, r); }
+    });
+    if (with_tag) {
+        uint64_t V = 1ULL << scale;
+        g.run(V, [&](Sink& s, uint64_t v) {
+            int64_t vid = static_cast<int64_t>(v);
+            if (!g.owned(vid)) return;
+            Row r;
+            r.i64(vid % 1000);
+            r.str("v" + std::to_string(vid));
+            s.vertex(g.partOf(vid), vid, tag, r);
+        });
+    }
+    finish(g, out);
+    return 0;
+}
+
+// Power-law graph with supernodes (C4): n vertices, ef * n background edges whose dst follows a
+// Zipf-like law (dst = floor(n * u^alpha)), plus `nsuper` supernodes each receiving `superdeg`
+// in-edges from uniform sources. Two edge props (INT w = h % 100, DOUBLE score in [0, 1)).
+// Always writes out- and in-edge rows (the config runs REVERSELY).
+int32_t ngd_powerlaw(int64_t n, int32_t ef, double alpha, int32_t nsuper, int64_t superdeg, uint64_t seed,
+                     int32_t num_parts, int32_t etype, int32_t rank, int32_t world, int32_t threads, ngd_rows* out) {
+    if (n < 2 || num_parts < 1 || !out) return -1;
+    Gen g{num_parts, rank, world, threads < 1 ? 1 : threads};
+    uint64_t E = static_cast<uint64_t>(ef) * static_cast<uint64_t>(n);
+    uint64_t S = static_cast<uint64_t>(nsuper) * static_cast<uint64_t>(superdeg);
+    g.run(E + S, [&](Sink& s, uint64_t i) {
+        int64_t src, dst;
+        if (i < E) {
+            src = static_cast<int64_t>(draw(seed, 11, i) % static_cast<uint64_t>(n));
+            double u = (draw(seed, 12, i) >> 11) * (1.0 / 9007199254740992.0);
+            dst = static_cast<int64_t>(std::floor(static_cast<double>(n) * std::pow(u, alpha)));
+            if (dst >= n) dst = n - 1;
+        } else {
+            uint64_t j = i - E;
+            dst = static_cast<int64_t>((j / superdeg) * 7919 % static_cast<uint64_t>(n));
+            src = static_cast<int64_t>(draw(seed, 13, j) % static_cast<uint64_t>(n));
+        }
+        uint64_t h = mix64((static_cast<uint64_t>(src) << 24) ^ static_cast<uint64_t>(dst) ^ seed);
+        Row r;
+        r.i64(static_cast<int64_t>(h % 100));
+        r.f64((h >> 11) * (1.0 / 9007199254740992.0));
+        if (g.owned(src)) { s.edge(g.partOf(src), src, etype, 0, dst, r); }
+        if (g.owned(dst)) { s.edge(g.partOf(dst), dst, -etype, 0, src, r); }
+    });
+    finish(g, out);
+    return 0;
+}
+
+// LDBC-SNB-like social graph (C5). Persons 0..np-1 (tag person: firstName STRING, age INT,
+// gender STRING), posts np..np+nposts-1 (tag post: content STRING, length INT, lang STRING).
+// Edge types (ids from the caller): knows person->person (creationDate INT, weight DOUBLE),
+// likes person->post (creationDate INT), hasCreator post->person (creationDate INT).
+// Out- and in-edge rows for every edge.
+int32_t ngd_snb(int64_t np, int32_t knowsDeg, int64_t nposts, int32_t likesDeg, uint64_t seed, int32_t num_parts,
+                int32_t tPerson, int32_t tPost, int32_t eKnows, int32_t eLikes, int32_t eHasCreator, int32_t rank,
+                int32_t world, int32_t threads, ngd_rows* out) {
+    if (np < 2 || nposts < 1 || num_parts < 1 || !out) return -1;
+    Gen g{num_parts, rank, world, threads < 1 ? 1 : threads};
+    static const char* kNames[] = {"Ada", "Bo", "Chen", "Dara", "Eli", "Fay", "Gus", "Hana", "Ivo", "Jun",
+                                   "Kai", "Lea", "Mo", "Nia", "Oto", "Pia"};
+    static const char* kLang[] = {"en", "de", "zh", "es", "fr"};
+    auto both = [&](Sink& s, int64_t src, int32_t et, int64_t rank_, int64_t dst, const Row& r) {
+        if (g.owned(src)) { s.edge(g.partOf(src), src, et, rank_, dst, r); }
+        if (g.owned(dst)) { s.edge(g.partOf(dst), dst, -et, rank_, src, r); }
+    };
+    // vertices
+    g.run(static_cast<uint64_t>(np + nposts), [&](Sink& s, uint64_t i) {
+        int64_t vid = static_cast<int64_t>(i);
+        if (!g.owned(vid)) return;
+        uint64_t h = draw(seed, 21, i);
+        Row r;
+        if (vid < np) {
+            r.str(kNames[h % 16]);
+            r.i64(static_cast<int64_t>(18 + (h >> 8) % 60));
+            r.str(((h >> 20) & 1) ? "female" : "male");
+            s.vertex(g.partOf(vid), vid, tPerson, r);
+        } else {
+            uint64_t len = 8 + (h >> 8) % 120;
+            std::string content;
+            for (uint64_t k = 0; k < len; k++) content.push_back(static_cast<char>('a' + (mix64(h + k) % 26)));
+            r.str(content);
+            r.i64(static_cast<int64_t>(len));
+            r.str(kLang[(h >> 30) % 5]);
+            s.vertex(g.partOf(vid), vid, tPost, r);
+        }
+    });
+    // knows: Zipf-ish popularity of the target, rank 0
+    uint64_t EK = static_cast<uint64_t>(np) * knowsDeg;
+    g.run(EK, [&](Sink& s, uint64_t i) {
+        int64_t a = static_cast<int64_t>(i / knowsDeg);
+        double u = (draw(seed, 22, i) >> 11) * (1.0 / 9007199254740992.0);
+        int64_t b = static_cast<int64_t>(std::floor(static_cast<double>(np) * u * u));
+        if (b >= np) b = np - 1;
+        if (b == a) return;
+        Row r;
+        uint64_t h = mix64((static_cast<uint64_t>(a) << 24) ^ static_cast<uint64_t>(b) ^ seed);
+        r.i64(static_cast<int64_t>(1262304000 + h % 315360000));
+        r.f64((h >> 11) * (1.0 / 9007199254740992.0) * 10.0);
+        both(s, a, eKnows, 0, b, r);
+    });
+    uint64_t EL = static_cast<uint64_t>(np) * likesDeg;
+    g.run(EL, [&](Sink& s, uint64_t i) {
+        int64_t a = static_cast<int64_t>(i / likesDeg);
+        int64_t p = np + static_cast<int64_t>(draw(seed, 23, i) % static_cast<uint64_t>(nposts));
+        Row r;
+        r.i64(static_cast<int64_t>(1262304000 + mix64(i ^ seed) % 315360000));
+        both(s, a, eLikes, 0, p, r);
+    });
+    g.run(static_cast<uint64_t>(nposts), [&](Sink& s, uint64_t i) {
+        int64_t p = np + static_cast<int64_t>(i);
+        int64_t a = static_cast<int64_t>(draw(seed, 24, i) % static_cast<uint64_t>(np));
+        Row r;
+        r.i64(static_cast<int64_t>(1262304000 + mix64(i ^ seed ^ 77) % 315360000));
+        both(s, p, eHasCreator, 0, a, r);
+    });
+    finish(g, out);
+    return 0;
+}
+
+// deterministic sample of `k` vids in [0, range) (the GO FROM list), with repetitions possible
+void ngd_sample_vids(uint64_t seed, uint64_t range, uint64_t k, int64_t* out) {
+    for (uint64_t i = 0; i < k; i++) out[i] = static_cast<int64_t>(draw(seed, 99, i) % range);
+}
+
+}  // extern "C"

@@ -1,0 +1,1242 @@
+// libnebula_gn engine: context, schema registry, snapshot upload, the GO multi-hop driver and the
+// GetNeighbors processor, behind the C ABI of include/nebula_gn.h.
+//
+// The hop loop restates GoExecutor (src/graph/GoExecutor.cpp:92-131 execute, :520-606 stepOut /
+// onStepOutResponse, :840-914 getStepOutProps, :1082-1335 processFinalResult) on device:
+// non-record hops only expand and dedup (storage returns `_dst` only and graphd keeps the set of
+// dsts), record hops run the storage filter (pushed only on the last forward hop, :528-533), the
+// graphd WHERE and the YIELD columns. With world > 1 every shard expands its own parts and the
+// per-hop frontier is exchanged as bitmaps over RCCL (ncclSend/ncclRecv all-to-all).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <unordered_set>
+
+#include "exprc.h"
+#include "kernels.h"
+
+using namespace ngx;
+
+#define HIP_OK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { throw Error{NGX_E_DEVICE, std::string("HIP: ") + hipGetErrorString(e_) + " at " #x}; } } while (0)
+#define NCCL_OK(x) do { ncclResult_t r_ = (x); if (r_ != ncclSuccess) { throw Error{NGX_E_DEVICE, std::string("RCCL: ") + ncclGetErrorString(r_)}; } } while (0)
+
+namespace ngx {
+
+struct DeviceGraph {
+    uint64_t V = 0, vglobal = 0, gbase = 0;
+    std::vector<uint64_t> shardBase;
+    int32_t* vpart = nullptr;
+    int64_t* vid = nullptr;
+    std::vector<DSlot> slots;
+    std::vector<DTag> tags;
+    std::vector<DCol> cols;
+    DSlot* dslots = nullptr;
+    DTag* dtags = nullptr;
+    DCol* dcols = nullptr;
+    std::vector<void*> allocs;
+    uint64_t bytes = 0;
+    struct Range { uint64_t dev; const char* host; uint64_t len; };
+    std::vector<Range> strRanges;                       // device string bytes -> host copy
+    ~DeviceGraph() { for (void* p : allocs) (void)hipFree(p); }
+
+    template <typename T>
+    T* upload(const T* src, uint64_t n) {
+        if (n == 0) return nullptr;
+        void* p = nullptr;
+        HIP_OK(hipMalloc(&p, n * sizeof(T)));
+        HIP_OK(hipMemcpy(p, src, n * sizeof(T), hipMemcpyHostToDevice));
+        allocs.push_back(p);
+        bytes += n * sizeof(T);
+        return static_cast<T*>(p);
+    }
+};
+
+}  // namespace ngx
+
+namespace {
+
+// growable device buffer
+struct DBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    template <typename T>
+    T* get(size_t n) {
+        size_t bytes = std::max<size_t>(n * sizeof(T), 64);
+        if (bytes > cap) {
+            if (p) (void)hipFree(p);
+            p = nullptr;
+            size_t c = std::max(bytes, cap * 3 / 2);
+            HIP_OK(hipMalloc(&p, c));
+            cap = c;
+        }
+        return static_cast<T*>(p);
+    }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+};
+
+struct Timer {
+    hipEvent_t a = nullptr, b = nullptr;
+};
+
+}  // namespace
+
+struct ngx_ctx {
+    int32_t device = 0, rank = 0, world = 1;
+    hipStream_t stream = nullptr;
+    ncclComm_t comm = nullptr;
+    std::map<int32_t, std::unique_ptr<Space>> spaces;
+    std::string lastError;
+    std::mutex mu;
+    // scratch
+    DBuf visited, F0, F1, estart, tileSums, counters, mask, chunkCount, chunkOff, seedPart, seedVid;
+    DBuf oSrc, oDst, oRank, oType, oEntry, oCells, progBuf, sendBits, recvBits, vcells, misc;
+    uint64_t visitedSize = 0;
+    uint8_t epoch = 0;
+    // profiling
+    bool prof = false;
+    struct Stat { std::string name; uint32_t launches = 0; double ms = 0; uint64_t bytes = 0; };
+    std::vector<Stat> stats;
+    std::vector<ngx_kernel_stat> statView;
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
+    std::vector<hipEvent_t> eventPool;
+    size_t eventNext = 0;
+
+    hipEvent_t ev() {
+        if (eventNext == eventPool.size()) {
+            hipEvent_t e;
+            HIP_OK(hipEventCreate(&e));
+            eventPool.push_back(e);
+        }
+        return eventPool[eventNext++];
+    }
+    int statIndex(const char* name) {
+        for (size_t i = 0; i < stats.size(); i++) if (stats[i].name == name) return static_cast<int>(i);
+        stats.push_back(Stat{name});
+        return static_cast<int>(stats.size()) - 1;
+    }
+    // bracket a launch group with events when profiling
+    template <typename F>
+    void timed(const char* name, uint64_t algoBytes, F&& f) {
+        if (!prof) { f(); return; }
+        int k = statIndex(name);
+        hipEvent_t a = ev(), b = ev();
+        HIP_OK(hipEventRecord(a, stream));
+        f();
+        HIP_OK(hipEventRecord(b, stream));
+        pending.push_back({k, {a, b}});
+        stats[k].launches++;
+        stats[k].bytes += algoBytes;
+    }
+    void collectTimings() {
+        if (!prof) return;
+        for (auto& p : pending) {
+            HIP_OK(hipEventSynchronize(p.second.second));
+            float ms = 0;
+            HIP_OK(hipEventElapsedTime(&ms, p.second.first, p.second.second));
+            stats[p.first].ms += ms;
+        }
+        pending.clear();
+        eventNext = 0;
+    }
+};
+
+namespace {
+
+int32_t fail(ngx_ctx* c, int32_t code, const std::string& msg) {
+    c->lastError = msg;
+    return code;
+}
+
+Space* findSpace(ngx_ctx* c, int32_t id) {
+    auto it = c->spaces.find(id);
+    return it == c->spaces.end() ? nullptr : it->second.get();
+}
+
+// ------------------------------------------------------------------------ upload
+void uploadColumns(DeviceGraph& d, std::vector<HostColumn>& hc, uint64_t n) {
+    for (auto& c : hc) {
+        DCol dc{};
+        dc.type = c.type;
+        switch (c.type) {
+            case T_INT: case T_TIMESTAMP: case T_VID: dc.data = d.upload(c.i64.data(), n); break;
+            case T_FLOAT: case T_DOUBLE: dc.data = d.upload(c.f64.data(), n); break;
+            case T_BOOL: dc.data = d.upload(c.b.data(), n); break;
+            case T_STRING: {
+                dc.soff = d.upload(c.soff.data(), n + 1);
+                dc.sbytes = c.sbytes.empty() ? nullptr : d.upload(c.sbytes.data(), c.sbytes.size());
+                if (dc.sbytes) d.strRanges.push_back({reinterpret_cast<uint64_t>(dc.sbytes), c.sbytes.data(), c.sbytes.size()});
+                break;
+            }
+            default: break;
+        }
+        if (!c.allValid) dc.valid = d.upload(c.valid.data(), n);
+        d.cols.push_back(dc);
+    }
+}
+
+std::unique_ptr<DeviceGraph> upload(HostGraph& g) {
+    auto d = std::make_unique<DeviceGraph>();
+    d->V = g.vid.size();
+    d->gbase = g.gbase;
+    d->vglobal = g.vglobal ? g.vglobal : d->V;
+    d->shardBase = g.shardBase;
+    d->vpart = d->upload(g.vpart.data(), d->V);
+    d->vid = d->upload(g.vid.data(), d->V);
+    for (auto& s : g.slots) {
+        DSlot ds{};
+        ds.etype = s.etype;
+        ds.colBase = static_cast<int32_t>(d->cols.size());
+        ds.ncols = static_cast<int32_t>(s.cols.size());
+        ds.off = d->upload(s.off.data(), s.off.size());
+        ds.dst = d->upload(s.dst.data(), s.dst.size());
+        ds.dgid = d->upload(s.dgid.data(), s.dgid.size());
+        ds.rank = d->upload(s.rank.data(), s.rank.size());
+        ds.hasFlags = s.anyFlags ? 1 : 0;
+        ds.eflags = s.anyFlags ? d->upload(s.eflags.data(), s.eflags.size()) : nullptr;
+        uploadColumns(*d, s.cols, s.dst.size());
+        d->slots.push_back(ds);
+    }
+    for (auto& t : g.tags) {
+        DTag dt{};
+        dt.tag = t.tag;
+        dt.colBase = static_cast<int32_t>(d->cols.size());
+        dt.ncols = static_cast<int32_t>(t.cols.size());
+        dt.present = d->upload(t.present.data(), t.present.size());
+        uploadColumns(*d, t.cols, d->V);
+        d->tags.push_back(dt);
+    }
+    d->dslots = d->upload(d->slots.data(), d->slots.size());
+    d->dtags = d->upload(d->tags.data(), d->tags.size());
+    d->dcols = d->upload(d->cols.data(), d->cols.size());
+    std::sort(d->strRanges.begin(), d->strRanges.end(), [](const DeviceGraph::Range& a, const DeviceGraph::Range& b) { return a.dev < b.dev; });
+    return d;
+}
+
+// ------------------------------------------------------------------------ compiled programs on device
+struct Programs {
+    std::vector<Insn> code;
+    std::string pool;
+    int32_t P = -1, W = -1;
+    std::vector<int32_t> yOff;
+    bool usesDst = false;
+    int32_t add(const Program& p) {
+        int32_t off = static_cast<int32_t>(code.size());
+        int64_t poolBase = static_cast<int64_t>(pool.size());
+        pool += p.pool;
+        for (auto in : p.code) {
+            if (in.op == OP_PUSH && in.t1 == V_STR) in.imm += poolBase;
+            code.push_back(in);
+        }
+        usesDst = usesDst || p.usesDstTag;
+        return off;
+    }
+};
+
+struct DevPrograms {
+    const Insn* code = nullptr;
+    const char* pool = nullptr;
+    const int32_t* yOff = nullptr;
+    const int32_t* ySlotType = nullptr;
+};
+
+DevPrograms uploadPrograms(ngx_ctx* c, const Programs& pr, const std::vector<int32_t>& ySlotType) {
+    size_t codeBytes = pr.code.size() * sizeof(Insn);
+    size_t yBytes = pr.yOff.size() * 4;
+    size_t tBytes = ySlotType.size() * 4;
+    size_t poolOff = (codeBytes + yBytes + tBytes + 63) & ~size_t(63);
+    size_t total = poolOff + pr.pool.size() + 64;
+    char* base = c->progBuf.get<char>(total);
+    std::vector<char> host(total, 0);
+    std::memcpy(host.data(), pr.code.data(), codeBytes);
+    std::memcpy(host.data() + codeBytes, pr.yOff.data(), yBytes);
+    std::memcpy(host.data() + codeBytes + yBytes, ySlotType.data(), tBytes);
+    std::memcpy(host.data() + poolOff, pr.pool.data(), pr.pool.size());
+    HIP_OK(hipMemcpyAsync(base, host.data(), total, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    DevPrograms d;
+    d.code = reinterpret_cast<const Insn*>(base);
+    d.yOff = reinterpret_cast<const int32_t*>(base + codeBytes);
+    d.ySlotType = reinterpret_cast<const int32_t*>(base + codeBytes + yBytes);
+    d.pool = base + poolOff;
+    return d;
+}
+
+// VM string pointer -> host bytes
+std::string hostString(const DeviceGraph& d, const DevPrograms& dp, const std::string& pool, uint64_t ptr, uint32_t len) {
+    if (len == 0) return std::string();
+    uint64_t pb = reinterpret_cast<uint64_t>(dp.pool);
+    if (ptr >= pb && ptr + len <= pb + pool.size()) return pool.substr(ptr - pb, len);
+    auto it = std::upper_bound(d.strRanges.begin(), d.strRanges.end(), ptr,
+                               [](uint64_t v, const DeviceGraph::Range& r) { return v < r.dev; });
+    if (it == d.strRanges.begin()) return std::string();
+    --it;
+    if (ptr + len > it->dev + it->len) return std::string();
+    return std::string(it->host + (ptr - it->dev), len);
+}
+
+// ColumnValue per calculateExprType (GoExecutor::toThriftResponse, GoExecutor.cpp:775-829)
+bool toCell(const OutCell& v, int32_t colType, ngx_cell& out, std::string& strings,
+            const DeviceGraph& d, const DevPrograms& dp, const std::string& pool) {
+    out.str_len = 0;
+    out.v.i = 0;
+    auto str = [&]() {
+        std::string s = hostString(d, dp, pool, static_cast<uint64_t>(v.x), v.len);
+        out.kind = NGX_CELL_STR;
+        out.str_len = static_cast<int32_t>(s.size());
+        out.v.str_off = strings.size();
+        strings += s;
+    };
+    switch (colType) {
+        case T_BOOL: if (v.t != V_BOOL) return false; out.kind = NGX_CELL_BOOL; out.v.i = v.x; return true;
+        case T_INT: if (v.t != V_INT) return false; out.kind = NGX_CELL_INT; out.v.i = v.x; return true;
+        case T_VID: if (v.t != V_INT) return false; out.kind = NGX_CELL_ID; out.v.i = v.x; return true;
+        case T_TIMESTAMP: if (v.t != V_INT) return false; out.kind = NGX_CELL_TIMESTAMP; out.v.i = v.x; return true;
+        case T_FLOAT: if (v.t != V_DBL) return false; out.kind = NGX_CELL_FLOAT; out.v.i = v.x; return true;
+        case T_DOUBLE: if (v.t != V_DBL) return false; out.kind = NGX_CELL_DOUBLE; out.v.i = v.x; return true;
+        case T_STRING: if (v.t != V_STR) return false; str(); return true;
+        default:
+            switch (v.t) {
+                case V_INT: out.kind = NGX_CELL_INT; out.v.i = v.x; return true;
+                case V_DBL: out.kind = NGX_CELL_DOUBLE; out.v.i = v.x; return true;
+                case V_BOOL: out.kind = NGX_CELL_EMPTY; return true;          // left unset by the reference
+                case V_STR: str(); return true;
+                default: out.kind = NGX_CELL_EMPTY; return true;
+            }
+    }
+}
+
+// raw value cell (GetNeighbors columns): kind from the VM type
+void rawCell(const OutCell& v, ngx_cell& out, std::string& strings, const DeviceGraph& d, const DevPrograms& dp,
+             const std::string& pool) {
+    out.str_len = 0;
+    out.v.i = v.x;
+    switch (v.t) {
+        case V_INT: out.kind = NGX_CELL_INT; break;
+        case V_DBL: out.kind = NGX_CELL_DOUBLE; break;
+        case V_BOOL: out.kind = NGX_CELL_BOOL; break;
+        case V_STR: {
+            std::string s = hostString(d, dp, pool, static_cast<uint64_t>(v.x), v.len);
+            out.kind = NGX_CELL_STR;
+            out.str_len = static_cast<int32_t>(s.size());
+            out.v.str_off = strings.size();
+            strings += s;
+            break;
+        }
+        default: out.kind = NGX_CELL_EMPTY; out.v.i = 0; break;
+    }
+}
+
+uint8_t nextEpoch(ngx_ctx* c) {
+    if (c->epoch == 255) {
+        HIP_OK(hipMemsetAsync(c->visited.p, 0, c->visitedSize, c->stream));
+        c->epoch = 0;
+    }
+    return ++c->epoch;
+}
+
+void ensureVisited(ngx_ctx* c, uint64_t n) {
+    if (c->visitedSize < n || c->visited.p == nullptr) {
+        c->visited.get<uint8_t>(n);
+        HIP_OK(hipMemsetAsync(c->visited.p, 0, n, c->stream));
+        c->visitedSize = n;
+        c->epoch = 0;
+    }
+}
+
+template <typename T>
+T readScalar(ngx_ctx* c, const T* dev) {
+    T v;
+    HIP_OK(hipMemcpyAsync(&v, dev, sizeof(T), hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return v;
+}
+
+// Result holders: the C structs point into these vectors
+struct GoResultHolder {
+    ngx_go_result r{};
+    std::vector<int32_t> colTypes;
+    std::vector<ngx_cell> cells;
+    std::vector<int64_t> src, dst, rank;
+    std::vector<int32_t> type;
+    std::string strings;
+    std::vector<uint64_t> hopFrontier, hopEdges, hopNext;
+};
+struct GnResultHolder {
+    ngx_gn_result r{};
+    std::vector<int32_t> failed;
+    std::vector<uint32_t> edgeVertex;
+    std::vector<int32_t> edgeType;
+    std::vector<int64_t> edgeDst;
+    std::vector<ngx_cell> edgeCells, vertexCells;
+    std::vector<uint8_t> vertexHasTag;
+    std::string strings;
+};
+
+HopSlots makeHopSlots(const Space& sp, const DeviceGraph& d, const std::vector<int32_t>& types,
+                      std::vector<int32_t>& hopTypes) {
+    HopSlots hs{};
+    hs.n = 0;
+    hopTypes.clear();
+    for (int32_t t : types) {
+        int32_t si = sp.slotOf(t);
+        if (si < 0) continue;                                  // no edges of this type here
+        if (hs.n >= kMaxSlots) throw Error{NGX_E_UNSUPPORTED, "too many edge types in one hop"};
+        const DSlot& ds = d.slots[si];
+        hs.slotIdx[hs.n] = si;
+        hs.etype[hs.n] = t;
+        hs.off[hs.n] = ds.off;
+        hs.dgid[hs.n] = ds.dgid;
+        hs.dst[hs.n] = ds.dst;
+        hs.rank[hs.n] = ds.rank;
+        hs.n++;
+        hopTypes.push_back(t);
+    }
+    return hs;
+}
+
+}  // namespace
+
+// ============================================================================ C ABI
+extern "C" {
+
+int32_t ngx_get_unique_id(void* out128) {
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return NGX_E_DEVICE;
+    std::memcpy(out128, &id, sizeof(id));
+    return NGX_OK;
+}
+
+int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
+    if (!cfg || !out) return NGX_E_BAD_ARGUMENT;
+    auto c = std::make_unique<ngx_ctx>();
+    c->device = cfg->device;
+    c->rank = cfg->rank;
+    c->world = cfg->world < 1 ? 1 : cfg->world;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return NGX_E_DEVICE;
+    if (hipSetDevice(c->device) != hipSuccess) return NGX_E_DEVICE;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return NGX_E_DEVICE;
+    if (c->world > 1) {
+        if (!cfg->nccl_unique_id) return NGX_E_BAD_ARGUMENT;
+        ncclUniqueId id;
+        std::memcpy(&id, cfg->nccl_unique_id, sizeof(id));
+        if (ncclCommInitRank(&c->comm, c->world, id, c->rank) != ncclSuccess) return NGX_E_DEVICE;
+    }
+    *out = c.release();
+    return NGX_OK;
+}
+
+void ngx_close(ngx_ctx* c) {
+    if (!c) return;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->stream);
+        c->spaces.clear();
+        for (DBuf* b : {&c->visited, &c->F0, &c->F1, &c->estart, &c->tileSums, &c->counters, &c->mask, &c->chunkCount,
+                        &c->chunkOff, &c->seedPart, &c->seedVid, &c->oSrc, &c->oDst, &c->oRank, &c->oType, &c->oEntry,
+                        &c->oCells, &c->progBuf, &c->sendBits, &c->recvBits, &c->vcells, &c->misc}) b->release();
+        for (auto e : c->eventPool) (void)hipEventDestroy(e);
+        if (c->comm) ncclCommDestroy(c->comm);
+        (void)hipStreamDestroy(c->stream);
+    }
+    delete c;
+}
+
+const char* ngx_last_error(ngx_ctx* c) { return c ? c->lastError.c_str() : "no context"; }
+
+int32_t ngx_add_space(ngx_ctx* c, int32_t space, int32_t numParts) {
+    std::lock_guard<std::mutex> g(c->mu);
+    auto& sp = c->spaces[space];
+    if (!sp) sp = std::make_unique<Space>();
+    sp->id = space;
+    sp->numParts = numParts;
+    return NGX_OK;
+}
+
+int32_t ngx_add_schema(ngx_ctx* c, int32_t space, int32_t isEdge, int32_t id, const char* name, int64_t ver,
+                       int32_t nfields, const char* const* names, const int32_t* types, const char* ttlCol,
+                       int64_t ttlDur) {
+    std::lock_guard<std::mutex> g(c->mu);
+    Space* sp = findSpace(c, space);
+    if (!sp) return fail(c, NGX_E_SPACE_NOT_FOUND, "space not found");
+    SchemaDef s;
+    s.ver = ver;
+    for (int32_t i = 0; i < nfields; i++) s.fields.push_back(FieldDef{names[i], types[i]});
+    s.ttlCol = ttlCol ? ttlCol : "";
+    s.ttlDur = ttlDur;
+    auto& set = isEdge ? sp->edges[id] : sp->tags[id];
+    set.id = id;
+    set.name = name;
+    set.versions[ver] = s;
+    if (isEdge) {
+        sp->edgeByName[name] = id;
+        if (std::find(sp->edgeOrder.begin(), sp->edgeOrder.end(), name) == sp->edgeOrder.end()) sp->edgeOrder.push_back(name);
+    } else {
+        sp->tagByName[name] = id;
+    }
+    return NGX_OK;
+}
+
+int32_t ngx_load_kv(ngx_ctx* c, int32_t space, const ngx_kv_batch* b) {
+    std::lock_guard<std::mutex> g(c->mu);
+    Space* sp = findSpace(c, space);
+    if (!sp) return fail(c, NGX_E_SPACE_NOT_FOUND, "space not found");
+    auto& st = sp->staged;
+    if (st.voff.empty()) st.voff.push_back(0);
+    for (uint64_t i = 0; i < b->n; i++) {
+        uint64_t kl = b->key_off[i + 1] - b->key_off[i];
+        const uint8_t* k = b->keys + b->key_off[i];
+        if (kl < 4) continue;
+        int32_t item;
+        std::memcpy(&item, k, 4);
+        int32_t part = item >> 8;
+        if (c->world > 1 && ((part % c->world) + c->world) % c->world != c->rank) continue;   // not ours
+        st.koff.push_back(st.keys.size());
+        st.klen.push_back(static_cast<uint32_t>(kl));
+        st.keys.insert(st.keys.end(), k, k + kl);
+        uint64_t vl = b->val_off[i + 1] - b->val_off[i];
+        st.vals.insert(st.vals.end(), b->vals + b->val_off[i], b->vals + b->val_off[i] + vl);
+        st.voff.push_back(st.vals.size());
+    }
+    return NGX_OK;
+}
+
+int32_t ngx_commit(ngx_ctx* c, int32_t space) {
+    std::lock_guard<std::mutex> g(c->mu);
+    Space* sp = findSpace(c, space);
+    if (!sp) return fail(c, NGX_E_SPACE_NOT_FOUND, "space not found");
+    try {
+        HIP_OK(hipSetDevice(c->device));
+        auto hg = std::make_unique<HostGraph>();
+        if (sp->staged.voff.empty()) sp->staged.voff.push_back(0);
+        Error e = exportSnapshot(*sp, c->rank, c->world, *hg);
+        if (e.code != NGX_OK) return fail(c, e.code, e.msg);
+        // vertex tables of every shard -> destination rows
+        std::vector<std::vector<std::pair<int32_t, int64_t>>> tables(c->world);
+        std::vector<std::pair<int32_t, int64_t>> mine(hg->vid.size());
+        for (size_t i = 0; i < mine.size(); i++) mine[i] = {hg->vpart[i], hg->vid[i]};
+        if (c->world == 1) {
+            tables[0] = mine;
+        } else {
+            // allgather counts, then the (part, vid) tables, through RCCL
+            uint64_t* dcnt = c->misc.get<uint64_t>(c->world * 2);
+            uint64_t myCount = mine.size();
+            HIP_OK(hipMemcpyAsync(dcnt + c->world, &myCount, 8, hipMemcpyHostToDevice, c->stream));
+            NCCL_OK(ncclAllGather(dcnt + c->world, dcnt, 1, ncclUint64, c->comm, c->stream));
+            std::vector<uint64_t> counts(c->world);
+            HIP_OK(hipMemcpyAsync(counts.data(), dcnt, 8 * c->world, hipMemcpyDeviceToHost, c->stream));
+            HIP_OK(hipStreamSynchronize(c->stream));
+            uint64_t maxc = *std::max_element(counts.begin(), counts.end());
+            std::vector<int64_t> packed(maxc * 2, 0);
+            for (size_t i = 0; i < mine.size(); i++) { packed[2 * i] = mine[i].first; packed[2 * i + 1] = mine[i].second; }
+            int64_t* sendb = c->sendBits.get<int64_t>(std::max<uint64_t>(maxc * 2, 2));
+            int64_t* recvb = c->recvBits.get<int64_t>(std::max<uint64_t>(maxc * 2 * c->world, 2));
+            HIP_OK(hipMemcpyAsync(sendb, packed.data(), maxc * 16, hipMemcpyHostToDevice, c->stream));
+            NCCL_OK(ncclAllGather(sendb, recvb, maxc * 2, ncclInt64, c->comm, c->stream));
+            std::vector<int64_t> all(maxc * 2 * c->world);
+            HIP_OK(hipMemcpyAsync(all.data(), recvb, all.size() * 8, hipMemcpyDeviceToHost, c->stream));
+            HIP_OK(hipStreamSynchronize(c->stream));
+            for (int w = 0; w < c->world; w++) {
+                tables[w].resize(counts[w]);
+                for (uint64_t i = 0; i < counts[w]; i++) {
+                    tables[w][i] = {static_cast<int32_t>(all[(w * maxc + i) * 2]), all[(w * maxc + i) * 2 + 1]};
+                }
+            }
+        }
+        resolveDstRows(*sp, *hg, tables, c->world);
+        if (hg->shardBase.empty()) { hg->shardBase = {0, hg->vid.size()}; hg->vglobal = hg->vid.size(); }
+        hg->gbase = hg->shardBase[c->rank];
+        sp->dev = upload(*hg);
+        sp->host = std::move(hg);
+        sp->staged = StagedRows();
+        return NGX_OK;
+    } catch (const Error& e) {
+        return fail(c, e.code, e.msg);
+    }
+}
+
+int32_t ngx_graph_info_get(ngx_ctx* c, int32_t space, ngx_graph_info* out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    Space* sp = findSpace(c, space);
+    if (!sp || !sp->dev) return fail(c, NGX_E_NOT_LOADED, "space not committed");
+    out->vertices = sp->dev->V;
+    out->edges = sp->host->edges;
+    out->device_bytes = sp->dev->bytes;
+    out->slots = static_cast<int32_t>(sp->dev->slots.size());
+    out->tags = static_cast<int32_t>(sp->dev->tags.size());
+    return NGX_OK;
+}
+
+int32_t ngx_set_profiling(ngx_ctx* c, int32_t on) {
+    std::lock_guard<std::mutex> g(c->mu);
+    c->prof = on != 0;
+    c->stats.clear();
+    return NGX_OK;
+}
+
+int32_t ngx_kernel_stats(ngx_ctx* c, const ngx_kernel_stat** out, int32_t* n) {
+    std::lock_guard<std::mutex> g(c->mu);
+    c->statView.clear();
+    for (auto& s : c->stats) c->statView.push_back(ngx_kernel_stat{s.name.c_str(), s.launches, s.ms, s.bytes});
+    *out = c->statView.data();
+    *n = static_cast<int32_t>(c->statView.size());
+    return NGX_OK;
+}
+
+int64_t ngx_hash_string(const char* s, uint64_t n) {
+    return static_cast<int64_t>(std::hash<std::string>()(std::string(s, n)));
+}
+
+void ngx_go_result_free(ngx_go_result* r) {
+    if (r) delete reinterpret_cast<GoResultHolder*>(r);
+}
+void ngx_gn_result_free(ngx_gn_result* r) {
+    if (r) delete reinterpret_cast<GnResultHolder*>(r);
+}
+
+}  // extern "C"
+
+// ============================================================================ GO
+namespace {
+
+struct GoPlan {
+    std::vector<int32_t> edgeTypes;                          // signed, GoExecutor::addToEdgeTypes order
+    std::map<std::string, int32_t> aliasType;
+    std::vector<std::string> aliasOrder;
+    std::unique_ptr<ExprNode> where, pushed;
+    std::vector<std::unique_ptr<ExprNode>> yields;
+    PropRefs refs;
+    std::vector<int32_t> colTypes;
+};
+
+int32_t prepareGo(ngx_ctx* c, const Space& sp, const ngx_go_plan& p, GoPlan& gp) {
+    auto addTypes = [&](int32_t t) {                         // GoExecutor.cpp:297-319
+        if (p.direction == NGX_DIR_FORWARD) gp.edgeTypes.push_back(t);
+        else if (p.direction == NGX_DIR_REVERSELY) gp.edgeTypes.push_back(-t);
+        else { gp.edgeTypes.push_back(t); gp.edgeTypes.push_back(-t); }
+    };
+    if (p.over_all) {
+        for (auto& name : sp.edgeOrder) {
+            int32_t t = sp.edgeByName.at(name);
+            addTypes(t);
+            if (gp.aliasType.count(name)) return fail(c, NGX_E_QUERY, "edge alias(" + name + ") was dup");
+            gp.aliasType[name] = std::abs(t);
+            gp.aliasOrder.push_back(name);
+        }
+    } else {
+        for (int32_t i = 0; i < p.nover; i++) {
+            std::string name = p.over_names[i];
+            auto it = sp.edgeByName.find(name);
+            if (it == sp.edgeByName.end()) return fail(c, NGX_E_QUERY, "Edge `" + name + "' not found");
+            addTypes(it->second);
+            std::string alias = (p.over_aliases && p.over_aliases[i] && p.over_aliases[i][0]) ? p.over_aliases[i] : name;
+            if (gp.aliasType.count(alias)) return fail(c, NGX_E_QUERY, "edge alias(" + alias + ") was dup");
+            gp.aliasType[alias] = std::abs(it->second);
+            gp.aliasOrder.push_back(alias);
+        }
+    }
+    std::string err;
+    if (p.where && p.where_len) {
+        gp.where = decodeExpr(p.where, p.where_len, err);
+        if (!gp.where) return fail(c, NGX_E_QUERY, err);
+        collectRefs(*gp.where, gp.refs);
+        if (p.filter_pushdown) {
+            auto copy = cloneExpr(*gp.where);
+            if (rewritePushdown(*copy)) gp.pushed = std::move(copy);
+        }
+    }
+    for (int32_t i = 0; i < p.nyields; i++) {
+        auto y = decodeExpr(p.yields[i], p.yield_lens[i], err);
+        if (!y) return fail(c, NGX_E_QUERY, err);
+        collectRefs(*y, gp.refs);
+        gp.yields.push_back(std::move(y));
+    }
+    if (p.over_all && gp.yields.empty()) {                    // GoExecutor.cpp:723-732
+        for (auto& a : gp.aliasOrder) {
+            auto n = std::make_unique<ExprNode>();
+            n->kind = K_EDGE_DST; n->alias = a; n->prop = "_dst";
+            gp.yields.push_back(std::move(n));
+        }
+    }
+    if (gp.refs.variable) return fail(c, NGX_E_QUERY, "A variable must be referred in FROM before used in WHERE or YIELD");
+    if (gp.refs.input) return fail(c, NGX_E_QUERY, "`$-' must be referred in FROM before used in WHERE or YIELD");
+    for (auto& tp : gp.refs.srcTag) if (!sp.tagByName.count(tp.first)) return fail(c, NGX_E_QUERY, "Tag `" + tp.first + "' not found.");
+    for (auto& tp : gp.refs.dstTag) if (!sp.tagByName.count(tp.first)) return fail(c, NGX_E_QUERY, "Tag `" + tp.first + "' not found.");
+    // checkNeededProps (GoExecutor.cpp:422-468)
+    for (auto* set : {&gp.refs.srcTag, &gp.refs.dstTag}) {
+        for (auto& tp : *set) {
+            const SchemaSet* ss = sp.tag(sp.tagByName.at(tp.first));
+            if (!ss) return fail(c, NGX_E_QUERY, "No tag schema for " + tp.first);
+            if (ss->latest().index(tp.second) < 0) return fail(c, NGX_E_QUERY, "`" + tp.second + "' is not a prop of `" + tp.first + "'");
+        }
+    }
+    for (auto& ap : gp.refs.alias) {
+        auto at = gp.aliasType.find(ap.first);
+        if (at == gp.aliasType.end()) return fail(c, NGX_E_QUERY, "Edge `" + ap.first + "' not found.");
+        if (ap.second == "_src" || ap.second == "_dst" || ap.second == "_rank" || ap.second == "_type") continue;
+        const SchemaSet* es = sp.edge(at->second);
+        if (!es) return fail(c, NGX_E_QUERY, "No edge schema for " + ap.first);
+        if (es->latest().index(ap.second) < 0) return fail(c, NGX_E_QUERY, "`" + ap.second + "' is not a prop of `" + ap.first + "'");
+    }
+    for (auto& f : gp.refs.funcs) (void)f;
+    for (auto& y : gp.yields) gp.colTypes.push_back(exprType(*y, sp));
+    return NGX_OK;
+}
+
+// exchange the hop's marks: every shard sends peer q the bitmap of q's rows it marked
+void exchangeFrontier(ngx_ctx* c, const DeviceGraph& d, uint8_t epoch) {
+    int W = c->world;
+    const auto& sb = d.shardBase;
+    uint64_t maxWords = 0;
+    for (int q = 0; q < W; q++) maxWords = std::max(maxWords, (sb[q + 1] - sb[q] + 63) / 64);
+    uint64_t* send = c->sendBits.get<uint64_t>(std::max<uint64_t>(maxWords * W, 1));
+    uint64_t* recv = c->recvBits.get<uint64_t>(std::max<uint64_t>(maxWords * W, 1));
+    uint64_t myRows = sb[c->rank + 1] - sb[c->rank];
+    uint64_t myWords = (myRows + 63) / 64;
+    for (int q = 0; q < W; q++) {
+        if (q == c->rank) continue;
+        uint64_t n = sb[q + 1] - sb[q];
+        if (launchPack(c->visited.get<uint8_t>(d.vglobal), epoch, sb[q], n, send + q * maxWords, c->stream)) throw Error{NGX_E_DEVICE, "pack"};
+    }
+    NCCL_OK(ncclGroupStart());
+    for (int q = 0; q < W; q++) {
+        if (q == c->rank) continue;
+        uint64_t nq = (sb[q + 1] - sb[q] + 63) / 64;
+        if (nq) NCCL_OK(ncclSend(send + q * maxWords, nq * 8, ncclUint8, q, c->comm, c->stream));
+        if (myWords) NCCL_OK(ncclRecv(recv + q * maxWords, myWords * 8, ncclUint8, q, c->comm, c->stream));
+    }
+    NCCL_OK(ncclGroupEnd());
+    for (int q = 0; q < W; q++) {
+        if (q == c->rank) continue;
+        if (launchMerge(recv + q * maxWords, myRows, c->visited.get<uint8_t>(d.vglobal), sb[c->rank], epoch, c->stream))
+            throw Error{NGX_E_DEVICE, "merge"};
+    }
+}
+
+int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
+    DeviceGraph& d = *sp.dev;
+    GoPlan gp;
+    int32_t rc = prepareGo(c, sp, p, gp);
+    if (rc) return rc;
+    R.colTypes = gp.colTypes;
+    uint32_t recordFrom = p.record_from, steps = p.record_to;
+    if (steps == 0) return NGX_OK;                               // GoExecutor.cpp:99-104
+    if (recordFrom == 0) recordFrom = 1;
+
+    // ---- final-hop request (getStepOutProps for record hops)
+    GraphdCtx gctx;
+    gctx.sp = &sp;
+    gctx.aliasType = gp.aliasType;
+    gctx.direction = p.direction;
+    gctx.nEdgeTypes = gp.edgeTypes.size();
+    for (auto& ap : gp.refs.alias) {
+        if (ap.second == "_dst") continue;
+        int32_t t = gp.aliasType.at(ap.first);
+        int32_t ptype = (ap.second == "_src") ? T_VID : (ap.second == "_rank" || ap.second == "_type") ? T_INT
+                      : sp.edge(t)->latest().typeOf(ap.second);
+        std::vector<int32_t> signedTypes;
+        if (p.direction == NGX_DIR_FORWARD) signedTypes = {t};
+        else if (p.direction == NGX_DIR_REVERSELY) signedTypes = {-t};
+        else signedTypes = {t, -t};
+        for (int32_t st : signedTypes) gctx.respSchema[st][ap.second] = ptype;
+    }
+    StorageCtx sctx;
+    sctx.sp = &sp;
+    sctx.haveEdgeContexts = true;
+    for (int32_t t : gp.edgeTypes) {
+        const SchemaSet* es = sp.edge(std::abs(t));
+        if (es) sctx.edgeMap[es->name] = std::abs(t);
+    }
+    Programs progs;
+    std::string err;
+    bool pushHere = p.filter_pushdown && p.direction == NGX_DIR_FORWARD && gp.pushed;
+    if (pushHere) {
+        Program pp;
+        int32_t crc = compileStorage(*gp.pushed, sctx, pp, err);
+        if (crc == NGX_E_INVALID_FILTER) return fail(c, NGX_E_QUERY, "Get neighbors failed");   // every part fails
+        if (crc) return fail(c, crc, err);
+        // a $^ tag referenced only by the filter: every src tag prop of WHERE/YIELD is requested too
+        progs.P = progs.add(pp);
+    }
+    if (gp.where) {
+        Program wp;
+        int32_t crc = compileGraphd(*gp.where, gctx, wp, err);
+        if (crc) return fail(c, crc, err);
+        progs.W = progs.add(wp);
+    }
+    for (auto& y : gp.yields) {
+        Program yp;
+        int32_t crc = compileGraphd(*y, gctx, yp, err);
+        if (crc) return fail(c, crc, err);
+        progs.yOff.push_back(progs.add(yp));
+    }
+    if (progs.usesDst && c->world > 1) return fail(c, NGX_E_UNSUPPORTED, "$$ props across shards are not fetched yet");
+    for (auto& t : sp.tags) {
+        if (!t.second.latest().ttlCol.empty() && t.second.latest().ttlDur > 0)
+            return fail(c, NGX_E_UNSUPPORTED, "tag TTL is not evaluated on the device");
+    }
+    std::vector<int32_t> ySlotType(progs.yOff.size(), 0);
+    DevPrograms dp = uploadPrograms(c, progs, ySlotType);
+
+    // ---- seeds (starts_), routed by ID_HASH; duplicates kept unless DISTINCT (:123-129)
+    std::vector<int64_t> starts(p.starts, p.starts + p.nstarts);
+    if (p.distinct) {
+        std::unordered_set<int64_t> u(starts.begin(), starts.end());
+        starts.assign(u.begin(), u.end());
+    }
+    std::vector<int32_t> sparts;
+    std::vector<int64_t> svids;
+    for (int64_t v : starts) {
+        int32_t part = idHash(v, sp.numParts);
+        if (c->world > 1 && part % c->world != c->rank) continue;
+        sparts.push_back(part);
+        svids.push_back(v);
+    }
+    ensureVisited(c, d.vglobal);
+    hipEvent_t t0 = c->ev(), t1 = c->ev();
+    HIP_OK(hipEventRecord(t0, c->stream));
+    uint64_t nF = svids.size();
+    uint32_t* F = c->F0.get<uint32_t>(std::max<uint64_t>(nF, 1));
+    if (nF) {
+        int32_t* dp_ = c->seedPart.get<int32_t>(nF);
+        int64_t* dv = c->seedVid.get<int64_t>(nF);
+        HIP_OK(hipMemcpyAsync(dp_, sparts.data(), nF * 4, hipMemcpyHostToDevice, c->stream));
+        HIP_OK(hipMemcpyAsync(dv, svids.data(), nF * 8, hipMemcpyHostToDevice, c->stream));
+        c->timed("lookup", nF * 12, [&] {
+            if (launchLookup(dp_, dv, nF, d.vpart, d.vid, d.V, F, c->stream)) throw Error{NGX_E_DEVICE, "lookup"};
+        });
+    }
+    uint64_t* counters = c->counters.get<uint64_t>(8);
+    uint32_t* errFlag = reinterpret_cast<uint32_t*>(counters + 4);
+    HIP_OK(hipMemsetAsync(counters, 0, 64, c->stream));
+    uint64_t totalRows = 0;
+    std::vector<int32_t> hopTypes;
+    HopSlots hs = makeHopSlots(sp, d, gp.edgeTypes, hopTypes);
+
+    for (uint32_t h = 1; h <= steps; h++) {
+        bool isRecord = h >= recordFrom;
+        bool isFinal = h == steps;
+        uint64_t nEnt = nF * static_cast<uint64_t>(hs.n);
+        uint64_t* estart = c->estart.get<uint64_t>(nEnt + 1);
+        uint64_t* tiles = c->tileSums.get<uint64_t>((std::max<uint64_t>(nEnt, 1) + kTile - 1) / kTile + 1);
+        uint64_t E = 0;
+        if (nEnt) {
+            c->timed("degree_scan", nEnt * 24, [&] {
+                if (launchDegreeScan(F, nEnt, hs, estart, tiles, c->stream)) throw Error{NGX_E_DEVICE, "degree scan"};
+            });
+            E = readScalar(c, estart + nEnt);
+        }
+        R.hopFrontier.push_back(nF);
+        R.hopEdges.push_back(E);
+        if (isRecord && E) {
+            FinalArgs a{};
+            a.F = F; a.estart = estart; a.nEnt = nEnt; a.E = E; a.hs = hs;
+            a.vid = d.vid; a.V = d.V; a.gbase = d.gbase;
+            a.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1};
+            a.P = (isFinal && progs.P >= 0) ? dp.code + progs.P : nullptr;
+            a.W = progs.W >= 0 ? dp.code + progs.W : nullptr;
+            a.propsMask = 0;
+            for (int s = 0; s < hs.n; s++) {
+                if (gctx.respSchema.count(hs.etype[s]) && !gctx.respSchema[hs.etype[s]].empty()) a.propsMask |= 1u << s;
+                a.ttlCol[s] = -1;
+                const SchemaSet* es = sp.edge(std::abs(hs.etype[s]));
+                if (es && !es->latest().ttlCol.empty() && es->latest().ttlDur > 0) {
+                    a.ttlCol[s] = es->latest().index(es->latest().ttlCol);
+                    a.ttlDur[s] = es->latest().ttlDur;
+                }
+            }
+            a.now = p.now_sec;
+            uint64_t chunks = (E + kTile - 1) / kTile;
+            a.mask = c->mask.get<uint64_t>(chunks * (kTile / 64));
+            a.chunkCount = c->chunkCount.get<uint32_t>(chunks);
+            a.err = errFlag;
+            a.nY = static_cast<int32_t>(progs.yOff.size());
+            a.yCode = dp.code;
+            a.yOff = dp.yOff;
+            a.ySlotType = nullptr;
+            uint64_t* chunkOff = c->chunkOff.get<uint64_t>(chunks + 1);
+            uint64_t* ctiles = c->tileSums.get<uint64_t>((std::max<uint64_t>(nEnt, chunks) + kTile - 1) / kTile + 1);
+            (void)ctiles;
+            uint64_t* rowsThisHop = counters + 1;
+            c->timed("final_eval", E * 8 * (1 + 1), [&] {
+                if (launchFinal(a, chunkOff, c->tileSums.get<uint64_t>((chunks + kTile - 1) / kTile + 1), rowsThisHop, c->stream))
+                    throw Error{NGX_E_DEVICE, "final eval"};
+            });
+            uint64_t nrows = readScalar(c, rowsThisHop);
+            uint64_t cap = totalRows + nrows;
+            // grow outputs preserving earlier record hops
+            auto grow = [&](DBuf& b, size_t elem) {
+                if (b.cap < std::max<size_t>(cap * elem, 64) && totalRows) {
+                    DBuf nb;
+                    nb.get<char>(cap * elem);
+                    HIP_OK(hipMemcpyAsync(nb.p, b.p, totalRows * elem, hipMemcpyDeviceToDevice, c->stream));
+                    HIP_OK(hipStreamSynchronize(c->stream));
+                    b.release();
+                    b = nb;
+                } else {
+                    b.get<char>(std::max<size_t>(cap * elem, 64));
+                }
+            };
+            grow(c->oSrc, 8); grow(c->oDst, 8); grow(c->oRank, 8); grow(c->oType, 4);
+            grow(c->oCells, sizeof(OutCell) * std::max<size_t>(a.nY, 1));
+            a.oSrc = static_cast<int64_t*>(c->oSrc.p) + totalRows;
+            a.oDst = static_cast<int64_t*>(c->oDst.p) + totalRows;
+            a.oRank = static_cast<int64_t*>(c->oRank.p) + totalRows;
+            a.oType = static_cast<int32_t*>(c->oType.p) + totalRows;
+            a.oEntry = nullptr;
+            a.oCells = static_cast<OutCell*>(c->oCells.p) + totalRows * a.nY;
+            c->timed("final_emit", nrows * (32 + 8ull * a.nY), [&] {
+                if (launchEmit(a, chunkOff, c->stream)) throw Error{NGX_E_DEVICE, "final emit"};
+            });
+            totalRows += nrows;
+        }
+        if (isFinal) break;
+        // ---- expand to the next frontier (set of distinct dsts)
+        uint8_t ep = nextEpoch(c);
+        if (E) {
+            c->timed("expand", E * 8 + nEnt * 24, [&] {
+                if (launchExpandMark(F, estart, nEnt, E, hs, c->visited.get<uint8_t>(d.vglobal), ep, c->stream))
+                    throw Error{NGX_E_DEVICE, "expand"};
+            });
+        }
+        if (c->world > 1) c->timed("exchange", 0, [&] { exchangeFrontier(c, d, ep); });
+        uint32_t* Fn = (F == c->F0.p) ? c->F1.get<uint32_t>(std::max<uint64_t>(d.V, 1)) : c->F0.get<uint32_t>(std::max<uint64_t>(d.V, 1));
+        uint64_t* tiles2 = c->tileSums.get<uint64_t>((std::max<uint64_t>(d.V, 1) + kTile - 1) / kTile + 1);
+        c->timed("compact", d.V, [&] {
+            if (launchCompact(c->visited.get<uint8_t>(d.vglobal), d.gbase, d.V, ep, Fn, tiles2, counters + 2, c->stream))
+                throw Error{NGX_E_DEVICE, "compact"};
+        });
+        nF = readScalar(c, counters + 2);
+        R.hopNext.push_back(nF);
+        F = Fn;
+        if (nF == 0 && c->world == 1) break;                    // GO_EXIT: empty frontier
+    }
+    HIP_OK(hipEventRecord(t1, c->stream));
+    HIP_OK(hipEventSynchronize(t1));
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, t0, t1));
+    c->collectTimings();
+    R.r.device_ms = ms;
+    uint32_t flags[2];
+    HIP_OK(hipMemcpy(flags, errFlag, 8, hipMemcpyDeviceToHost));
+    if (flags[1]) return fail(c, NGX_E_UNSUPPORTED, "an expression needs a host-only construct (string building or parsing)");
+    if (flags[0]) return fail(c, NGX_E_QUERY, "an expression of WHERE / YIELD failed to evaluate");
+
+    // ---- results to the host
+    int32_t nY = static_cast<int32_t>(progs.yOff.size());
+    R.src.resize(totalRows); R.dst.resize(totalRows); R.rank.resize(totalRows); R.type.resize(totalRows);
+    std::vector<OutCell> raw(totalRows * nY);
+    if (totalRows) {
+        HIP_OK(hipMemcpyAsync(R.src.data(), c->oSrc.p, totalRows * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipMemcpyAsync(R.dst.data(), c->oDst.p, totalRows * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipMemcpyAsync(R.rank.data(), c->oRank.p, totalRows * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipMemcpyAsync(R.type.data(), c->oType.p, totalRows * 4, hipMemcpyDeviceToHost, c->stream));
+        if (nY) HIP_OK(hipMemcpyAsync(raw.data(), c->oCells.p, raw.size() * sizeof(OutCell), hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipStreamSynchronize(c->stream));
+    }
+    R.cells.resize(totalRows * nY);
+    for (uint64_t r = 0; r < totalRows; r++) {
+        for (int32_t y = 0; y < nY; y++) {
+            if (!toCell(raw[r * nY + y], gp.colTypes[y], R.cells[r * nY + y], R.strings, d, dp, progs.pool)) {
+                return fail(c, NGX_E_QUERY, "YIELD value does not match its column type (boost::get)");
+            }
+        }
+    }
+    if (p.distinct && totalRows) {                            // processFinalResult DISTINCT (:1298-1305)
+        std::vector<uint64_t> keep;
+        std::unordered_set<std::string> seen;
+        for (uint64_t r = 0; r < totalRows; r++) {
+            std::string key;
+            for (int32_t y = 0; y < nY; y++) {
+                const ngx_cell& cl = R.cells[r * nY + y];
+                key.append(reinterpret_cast<const char*>(&cl.kind), 4);
+                if (cl.kind == NGX_CELL_STR) { key += R.strings.substr(cl.v.str_off, cl.str_len); key.push_back('\0'); }
+                else key.append(reinterpret_cast<const char*>(&cl.v.i), 8);
+            }
+            if (seen.insert(key).second) keep.push_back(r);
+        }
+        auto compact = [&](auto& v, size_t w) {
+            std::remove_reference_t<decltype(v)> out;
+            for (auto r : keep) for (size_t k = 0; k < w; k++) out.push_back(v[r * w + k]);
+            v.swap(out);
+        };
+        compact(R.src, 1); compact(R.dst, 1); compact(R.rank, 1); compact(R.type, 1); compact(R.cells, nY);
+        totalRows = keep.size();
+    }
+    R.r.nrows = totalRows;
+    return NGX_OK;
+}
+
+}  // namespace
+
+extern "C" int32_t ngx_go(ngx_ctx* c, const ngx_go_plan* p, ngx_go_result** out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    auto R = std::make_unique<GoResultHolder>();
+    int32_t rc;
+    try {
+        HIP_OK(hipSetDevice(c->device));
+        Space* sp = findSpace(c, p->space);
+        if (!sp || !sp->dev) rc = fail(c, NGX_E_NOT_LOADED, "space not committed");
+        else rc = runGo(c, *sp, *p, *R);
+    } catch (const Error& e) {
+        rc = fail(c, e.code, e.msg);
+    }
+    R->r.code = rc;
+    R->r.ncols = static_cast<int32_t>(R->colTypes.size());
+    R->r.col_types = R->colTypes.data();
+    R->r.cells = R->cells.data();
+    R->r.row_src = R->src.data();
+    R->r.row_dst = R->dst.data();
+    R->r.row_rank = R->rank.data();
+    R->r.row_type = R->type.data();
+    R->r.strings = R->strings.data();
+    R->r.strings_len = R->strings.size();
+    R->r.nhops = static_cast<int32_t>(R->hopEdges.size());
+    R->hopNext.resize(R->hopEdges.size(), 0);
+    R->r.hop_frontier = R->hopFrontier.data();
+    R->r.hop_edges = R->hopEdges.data();
+    R->r.hop_next = R->hopNext.data();
+    if (rc != NGX_OK) { R->r.nrows = 0; }
+    *out = &R.release()->r;
+    return rc;
+}
+
+// ============================================================================ GetNeighbors
+namespace {
+
+const std::map<std::string, int> kKeyProps = {{"_src", 0}, {"_dst", 1}, {"_rank", 2}, {"_type", 3}};
+
+int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResultHolder& R) {
+    DeviceGraph& d = *sp.dev;
+    auto failAll = [&](int32_t code) {
+        R.r.code = code;
+        for (int32_t i = 0; i < q.nparts; i++) { R.failed.push_back(code); R.failed.push_back(q.parts[i]); }
+        return NGX_OK;
+    };
+    // checkAndBuildContexts (QueryBaseProcessor.inl:66-170)
+    std::map<int32_t, std::vector<int32_t>> edgeCols;            // signed type -> return column indices
+    std::set<int32_t> tagCols;
+    StorageCtx sctx;
+    sctx.sp = &sp;
+    for (int32_t i = 0; i < q.nedge_types; i++) edgeCols[q.edge_types[i]];
+    for (int32_t i = 0; i < q.ncols; i++) {
+        const ngx_prop_def& col = q.cols[i];
+        std::string name = col.name ? col.name : "";
+        if (col.owner == 1 || col.owner == 2) {
+            const SchemaSet* ts = sp.tag(col.id);
+            if (!ts) return failAll(NGX_E_TAG_PROP_NOT_FOUND);
+            if (ts->latest().typeOf(name) == T_UNKNOWN) return failAll(NGX_E_IMPROPER_DATA_TYPE);
+            tagCols.insert(col.id);
+        } else {
+            const SchemaSet* es = sp.edge(std::abs(col.id));
+            if (!es) return failAll(NGX_E_EDGE_NOT_FOUND);
+            sctx.edgeMap[es->name] = std::abs(col.id);
+            if (!kKeyProps.count(name) && es->latest().typeOf(name) == T_UNKNOWN) return failAll(NGX_E_IMPROPER_DATA_TYPE);
+            edgeCols[col.id].push_back(i);
+        }
+    }
+    sctx.haveEdgeContexts = !edgeCols.empty();
+    Programs progs;
+    std::string err;
+    if (q.filter && q.filter_len) {
+        auto f = decodeExpr(q.filter, q.filter_len, err);
+        if (!f) return failAll(NGX_E_INVALID_FILTER);
+        Program pp;
+        int32_t crc = compileStorage(*f, sctx, pp, err);
+        if (crc == NGX_E_INVALID_FILTER) return failAll(NGX_E_INVALID_FILTER);
+        if (crc) return fail(c, crc, err);
+        progs.P = progs.add(pp);
+        for (int32_t t : sctx.filterTags) {
+            if (!tagCols.count(t)) {                              // processVertex: no response schema
+                for (int32_t i = 0; i < q.nparts; i++) {
+                    if (q.part_nvids[i]) { R.failed.push_back(-25); R.failed.push_back(q.parts[i]); }
+                }
+                return NGX_OK;
+            }
+        }
+    }
+    if (q.max_edges_per_vertex > 0 && q.max_edges_per_vertex < INT32_MAX)
+        return fail(c, NGX_E_UNSUPPORTED, "max_edge_returned_per_vertex is not applied on the device yet");
+    for (auto& t : sp.tags) {
+        if (tagCols.count(t.first) && !t.second.latest().ttlCol.empty() && t.second.latest().ttlDur > 0)
+            return fail(c, NGX_E_UNSUPPORTED, "tag TTL is not evaluated on the device");
+    }
+    // processed types: edge contexts with props (QueryBoundProcessor.cpp:65-81)
+    std::vector<int32_t> types;
+    for (auto& kv : edgeCols) if (!kv.second.empty()) types.push_back(kv.first);
+    // column programs: collectProps semantics (key props from the key, others value-or-default)
+    std::vector<int32_t> ySlotType;
+    for (int32_t i = 0; i < q.ncols; i++) {
+        const ngx_prop_def& col = q.cols[i];
+        Program yp;
+        Insn in{};
+        std::string name = col.name ? col.name : "";
+        if (col.owner == 3) {
+            auto kp = kKeyProps.find(name);
+            if (kp != kKeyProps.end()) { in.op = OP_EKEY; in.a = kp->second; in.b = 0; }
+            else {
+                in.op = OP_ECOL;
+                in.a = sp.edge(std::abs(col.id))->latest().index(name);
+                in.b = std::abs(col.id);
+                in.mode = 2;
+            }
+            ySlotType.push_back(col.id);
+        } else {
+            in.op = OP_ERR;                                       // per-vertex columns: k_vertex_cells
+            ySlotType.push_back(INT32_MIN);
+        }
+        yp.code.push_back(in);
+        Insn end{};
+        yp.code.push_back(end);
+        progs.yOff.push_back(progs.add(yp));
+    }
+    DevPrograms dp = uploadPrograms(c, progs, ySlotType);
+    // seeds in request order
+    std::vector<int32_t> sparts;
+    std::vector<int64_t> svids;
+    uint64_t k = 0;
+    for (int32_t i = 0; i < q.nparts; i++) {
+        for (uint32_t j = 0; j < q.part_nvids[i]; j++) { sparts.push_back(q.parts[i]); svids.push_back(q.vids[k++]); }
+    }
+    uint64_t nF = svids.size();
+    uint32_t* F = c->F0.get<uint32_t>(std::max<uint64_t>(nF, 1));
+    if (nF) {
+        int32_t* dpart = c->seedPart.get<int32_t>(nF);
+        int64_t* dv = c->seedVid.get<int64_t>(nF);
+        HIP_OK(hipMemcpyAsync(dpart, sparts.data(), nF * 4, hipMemcpyHostToDevice, c->stream));
+        HIP_OK(hipMemcpyAsync(dv, svids.data(), nF * 8, hipMemcpyHostToDevice, c->stream));
+        if (launchLookup(dpart, dv, nF, d.vpart, d.vid, d.V, F, c->stream)) throw Error{NGX_E_DEVICE, "lookup"};
+    }
+    std::vector<int32_t> hopTypes;
+    HopSlots hs = makeHopSlots(sp, d, types, hopTypes);
+    uint64_t* counters = c->counters.get<uint64_t>(8);
+    uint32_t* errFlag = reinterpret_cast<uint32_t*>(counters + 4);
+    HIP_OK(hipMemsetAsync(counters, 0, 64, c->stream));
+    uint64_t nEnt = nF * static_cast<uint64_t>(hs.n);
+    uint64_t E = 0;
+    uint64_t* estart = c->estart.get<uint64_t>(nEnt + 1);
+    if (nEnt) {
+        uint64_t* tiles = c->tileSums.get<uint64_t>((nEnt + kTile - 1) / kTile + 1);
+        if (launchDegreeScan(F, nEnt, hs, estart, tiles, c->stream)) throw Error{NGX_E_DEVICE, "degree"};
+        E = readScalar(c, estart + nEnt);
+    }
+    uint64_t nrows = 0;
+    int32_t nY = q.ncols;
+    std::vector<OutCell> raw;
+    if (E) {
+        FinalArgs a{};
+        a.F = F; a.estart = estart; a.nEnt = nEnt; a.E = E; a.hs = hs;
+        a.vid = d.vid; a.V = d.V; a.gbase = d.gbase;
+        a.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1};
+        a.P = progs.P >= 0 ? dp.code + progs.P : nullptr;
+        a.W = nullptr;
+        for (int s = 0; s < hs.n; s++) {
+            bool onlyStructure = true;
+            for (int32_t ci : edgeCols[hs.etype[s]]) if (std::string(q.cols[ci].name) != "_dst") onlyStructure = false;
+            if (!onlyStructure) a.propsMask |= 1u << s;
+            a.ttlCol[s] = -1;
+            const SchemaSet* es = sp.edge(std::abs(hs.etype[s]));
+            if (es && !es->latest().ttlCol.empty() && es->latest().ttlDur > 0) {
+                a.ttlCol[s] = es->latest().index(es->latest().ttlCol);
+                a.ttlDur[s] = es->latest().ttlDur;
+            }
+        }
+        a.now = q.now_sec;
+        uint64_t chunks = (E + kTile - 1) / kTile;
+        a.mask = c->mask.get<uint64_t>(chunks * (kTile / 64));
+        a.chunkCount = c->chunkCount.get<uint32_t>(chunks);
+        a.err = errFlag;
+        a.nY = nY;
+        a.yCode = dp.code;
+        a.yOff = dp.yOff;
+        a.ySlotType = dp.ySlotType;
+        uint64_t* chunkOff = c->chunkOff.get<uint64_t>(chunks + 1);
+        if (launchFinal(a, chunkOff, c->tileSums.get<uint64_t>((chunks + kTile - 1) / kTile + 1), counters + 1, c->stream))
+            throw Error{NGX_E_DEVICE, "final"};
+        nrows = readScalar(c, counters + 1);
+        a.oSrc = c->oSrc.get<int64_t>(nrows);
+        a.oDst = c->oDst.get<int64_t>(nrows);
+        a.oRank = c->oRank.get<int64_t>(nrows);
+        a.oType = c->oType.get<int32_t>(nrows);
+        a.oEntry = c->oEntry.get<uint32_t>(nrows);
+        a.oCells = c->oCells.get<OutCell>(std::max<uint64_t>(nrows * std::max(nY, 1), 1));
+        if (launchEmit(a, chunkOff, c->stream)) throw Error{NGX_E_DEVICE, "emit"};
+        R.edgeVertex.resize(nrows);
+        R.edgeType.resize(nrows);
+        R.edgeDst.resize(nrows);
+        raw.resize(nrows * nY);
+        if (nrows) {
+            HIP_OK(hipMemcpyAsync(R.edgeVertex.data(), a.oEntry, nrows * 4, hipMemcpyDeviceToHost, c->stream));
+            HIP_OK(hipMemcpyAsync(R.edgeType.data(), a.oType, nrows * 4, hipMemcpyDeviceToHost, c->stream));
+            HIP_OK(hipMemcpyAsync(R.edgeDst.data(), a.oDst, nrows * 8, hipMemcpyDeviceToHost, c->stream));
+            if (nY) HIP_OK(hipMemcpyAsync(raw.data(), a.oCells, raw.size() * sizeof(OutCell), hipMemcpyDeviceToHost, c->stream));
+        }
+    }
+    // per-vertex tag columns
+    std::vector<OutCell> vraw(nF * std::max(nY, 1));
+    if (nF && nY) {
+        std::vector<int32_t> tslot(nY, -1), tcol(nY, 0);
+        for (int32_t i = 0; i < nY; i++) {
+            if (q.cols[i].owner == 1 || q.cols[i].owner == 2) {
+                tslot[i] = sp.tagSlotOf(q.cols[i].id);
+                tcol[i] = sp.tag(q.cols[i].id)->latest().index(q.cols[i].name);
+            }
+        }
+        int32_t* dts = c->misc.get<int32_t>(2 * nY);
+        std::vector<int32_t> both(tslot);
+        both.insert(both.end(), tcol.begin(), tcol.end());
+        HIP_OK(hipMemcpyAsync(dts, both.data(), both.size() * 4, hipMemcpyHostToDevice, c->stream));
+        VertexCellArgs va{};
+        va.rows = F; va.n = nF; va.ncols = nY; va.tagSlot = dts; va.col = dts + nY;
+        va.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1};
+        va.out = c->vcells.get<OutCell>(nF * nY);
+        if (launchVertexCells(va, c->stream)) throw Error{NGX_E_DEVICE, "vertex cells"};
+        HIP_OK(hipMemcpyAsync(vraw.data(), va.out, nF * nY * sizeof(OutCell), hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_OK(hipStreamSynchronize(c->stream));
+    R.edgeCells.resize(nrows * nY);
+    for (uint64_t i = 0; i < nrows * nY; i++) rawCell(raw[i], R.edgeCells[i], R.strings, d, dp, progs.pool);
+    R.vertexCells.resize(nF * nY);
+    R.vertexHasTag.assign(nF * nY, 0);
+    for (uint64_t i = 0; i < nF * static_cast<uint64_t>(nY); i++) {
+        rawCell(vraw[i], R.vertexCells[i], R.strings, d, dp, progs.pool);
+        R.vertexHasTag[i] = vraw[i].t != 0xFF ? 1 : 0;
+    }
+    R.r.nvertices = static_cast<uint32_t>(nF);
+    R.r.nedges = nrows;
+    return NGX_OK;
+}
+
+}  // namespace
+
+extern "C" int32_t ngx_get_neighbors(ngx_ctx* c, const ngx_gn_request* q, ngx_gn_result** out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    auto R = std::make_unique<GnResultHolder>();
+    int32_t rc;
+    try {
+        HIP_OK(hipSetDevice(c->device));
+        Space* sp = findSpace(c, q->space);
+        if (!sp || !sp->dev) rc = fail(c, NGX_E_NOT_LOADED, "space not committed");
+        else rc = runGetNeighbors(c, *sp, *q, *R);
+    } catch (const Error& e) {
+        rc = fail(c, e.code, e.msg);
+    }
+    if (rc != NGX_OK) R->r.code = rc;
+    R->r.nfailed = static_cast<int32_t>(R->failed.size() / 2);
+    R->r.failed_codes = R->failed.data();
+    R->r.edge_vertex = R->edgeVertex.data();
+    R->r.edge_type = R->edgeType.data();
+    R->r.edge_dst = R->edgeDst.data();
+    R->r.ncols = q->ncols;
+    R->r.edge_cells = R->edgeCells.data();
+    R->r.vertex_cells = R->vertexCells.data();
+    R->r.vertex_has_tag = R->vertexHasTag.data();
+    R->r.strings = R->strings.data();
+    R->r.strings_len = R->strings.size();
+    *out = &R.release()->r;
+    return rc;
+}

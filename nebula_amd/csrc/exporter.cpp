@@ -1,0 +1,536 @@
+// Part -> CSR snapshot exporter (the north star's src/kvstore + src/dataman changes).
+//
+// Input: reference-format KV rows of the parts this shard owns (NebulaKeyUtils keys,
+// src/common/utils/NebulaKeyUtils.cpp:12-45; RowWriter values, src/dataman/RowWriter.cpp:39-263).
+// Output (HostGraph): a vertex table sorted by (part, vid), one CSR per signed edge type with
+// adjacency in RocksDB bytewise key order (what KVStore::prefix(edgePrefix(part, vid, type)) walks,
+// src/storage/query/QueryBaseProcessor.inl:485-518), latest-version dedup applied, and every prop
+// of the latest schema decoded into a typed column the way RowReader::getPropByName reads it
+// (src/dataman/RowReader.h:136-193, RowReader.cpp:171-365) — including block offsets every 16
+// fields. Tag rows become per-vertex tag columns (first key of vertexPrefix = latest version,
+// QueryBaseProcessor.inl:440-476).
+#include <algorithm>
+#include <atomic>
+#include <numeric>
+#include <thread>
+
+#include "ngx_internal.h"
+
+namespace ngx {
+
+namespace {
+
+inline uint64_t be64(const uint8_t* p) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    return __builtin_bswap64(v);
+}
+template <typename T>
+inline T rd(const uint8_t* p) { T v; std::memcpy(&v, p, sizeof(T)); return v; }
+
+int hwThreads() {
+    unsigned n = std::thread::hardware_concurrency();
+    return static_cast<int>(std::max(1u, std::min(n, 16u)));
+}
+
+template <typename F>
+void parallelFor(uint64_t n, F&& f) {
+    int T = hwThreads();
+    if (n < 4096 || T == 1) { f(0, n); return; }
+    std::vector<std::thread> ts;
+    for (int t = 0; t < T; t++) {
+        uint64_t lo = n * t / T, hi = n * (t + 1) / T;
+        ts.emplace_back([&f, lo, hi] { f(lo, hi); });
+    }
+    for (auto& th : ts) th.join();
+}
+
+template <typename It, typename Cmp>
+void parallelSort(It begin, It end, Cmp cmp) {
+    uint64_t n = static_cast<uint64_t>(end - begin);
+    int T = hwThreads();
+    if (n < (1u << 16) || T == 1) { std::sort(begin, end, cmp); return; }
+    std::vector<uint64_t> cuts;
+    for (int t = 0; t <= T; t++) cuts.push_back(n * t / T);
+    std::vector<std::thread> ts;
+    for (int t = 0; t < T; t++) ts.emplace_back([&, t] { std::sort(begin + cuts[t], begin + cuts[t + 1], cmp); });
+    for (auto& th : ts) th.join();
+    for (int w = 1; w < T; w <<= 1) {
+        std::vector<std::thread> ms;
+        for (int t = 0; t + w < T; t += 2 * w) {
+            uint64_t lo = cuts[t], mid = cuts[t + w], hi = cuts[std::min(t + 2 * w, T)];
+            ms.emplace_back([&, lo, mid, hi] { std::inplace_merge(begin + lo, begin + mid, begin + hi, cmp); });
+        }
+        for (auto& th : ms) th.join();
+    }
+}
+
+// ---------------------------------------------------------------- row decoding
+// Decodes one field of a row with its own (version) schema, following RowReader: the header
+// (low 3 bits + 1 = offset width, top 3 bits = version bytes), block offsets for fields 16, 32, ...,
+// and a sequential walk inside the field's block.
+struct RowView {
+    const uint8_t* data = nullptr;     // after the header
+    uint64_t size = 0;
+    std::vector<uint64_t> blockStart;  // block k starts at blockStart[k]
+    bool ok = false;
+};
+
+bool parseHeader(const uint8_t* row, uint64_t len, uint32_t numFields, RowView& rv) {
+    if (len == 0) return false;
+    uint32_t offBytes = (row[0] & 0x07) + 1;
+    uint32_t verBytes = row[0] >> 5;
+    uint32_t numOffsets = numFields >> 4;
+    if (static_cast<uint64_t>(offBytes) * numOffsets + verBytes + 1 > len) return false;
+    const uint8_t* it = row + 1 + verBytes;
+    rv.blockStart.assign(numOffsets + 1, 0);
+    for (uint32_t i = 0; i < numOffsets; i++) {
+        uint64_t o = 0;
+        for (uint32_t j = 0; j < offBytes; j++) o |= static_cast<uint64_t>(*it++) << (8 * j);
+        rv.blockStart[i + 1] = o;
+    }
+    uint64_t hdr = static_cast<uint64_t>(it - row);
+    rv.data = it;
+    rv.size = len - hdr;
+    rv.ok = true;
+    return true;
+}
+
+int32_t varint(const uint8_t* p, uint64_t avail, uint64_t& out) {
+    uint64_t v = 0;
+    for (int i = 0; i < 10; i++) {
+        if (static_cast<uint64_t>(i) >= avail) return -1;
+        uint8_t b = p[i];
+        v |= static_cast<uint64_t>(b & 0x7f) << (7 * i);
+        if (!(b & 0x80)) { out = v; return i + 1; }
+    }
+    return -1;
+}
+
+// byte length of field `t` at offset `off`, or -1
+int64_t fieldLen(const RowView& rv, int32_t t, uint64_t off) {
+    switch (t) {
+        case T_BOOL: return 1;
+        case T_INT: case T_TIMESTAMP: {
+            uint64_t v;
+            if (off > rv.size) return -1;
+            int32_t n = varint(rv.data + off, rv.size - off, v);
+            return n <= 0 ? -1 : n;
+        }
+        case T_FLOAT: return 4;
+        case T_DOUBLE: return 8;
+        case T_VID: return 8;
+        case T_STRING: {
+            uint64_t l;
+            if (off > rv.size) return -1;
+            int32_t n = varint(rv.data + off, rv.size - off, l);
+            if (n <= 0) return -1;
+            return static_cast<int64_t>(n + l);
+        }
+        default: return -1;
+    }
+}
+
+// offset of field i (RowReader::skipToField)
+int64_t fieldOffset(const RowView& rv, const SchemaDef& s, uint32_t i) {
+    uint32_t k = i >> 4;
+    uint64_t off = rv.blockStart[k];
+    for (uint32_t j = k << 4; j < i; j++) {
+        int64_t l = fieldLen(rv, s.fields[j].type, off);
+        if (l < 0) return -1;
+        off += static_cast<uint64_t>(l);
+        if (off > rv.size) return -1;
+    }
+    return static_cast<int64_t>(off);
+}
+
+struct Cell {
+    bool ok = false;
+    int64_t i = 0;
+    double d = 0;
+    const uint8_t* s = nullptr;
+    uint64_t slen = 0;
+};
+
+// RowReader::getPropByName for field i of the version schema (RowReader.h:136-193)
+Cell readField(const RowView& rv, const SchemaDef& s, uint32_t i) {
+    Cell c;
+    int64_t off = fieldOffset(rv, s, i);
+    if (off < 0) return c;
+    uint64_t o = static_cast<uint64_t>(off);
+    switch (s.fields[i].type) {
+        case T_BOOL:
+            if (o >= rv.size) return c;
+            c.i = rv.data[o] != 0; c.ok = true; return c;
+        case T_INT: case T_TIMESTAMP: {
+            uint64_t v;
+            if (o > rv.size || varint(rv.data + o, rv.size - o, v) < 0) return c;
+            c.i = static_cast<int64_t>(v); c.ok = true; return c;
+        }
+        case T_VID:
+            if (o + 8 > rv.size) return c;
+            c.i = rd<int64_t>(rv.data + o); c.ok = true; return c;
+        case T_FLOAT:
+            if (o + 4 > rv.size) return c;
+            c.d = static_cast<double>(rd<float>(rv.data + o)); c.ok = true; return c;
+        case T_DOUBLE:
+            if (o + 8 > rv.size) return c;
+            c.d = rd<double>(rv.data + o); c.ok = true; return c;
+        case T_STRING: {
+            uint64_t l;
+            if (o > rv.size) return c;
+            int32_t n = varint(rv.data + o, rv.size - o, l);
+            if (n <= 0 || o + n + l > rv.size) return c;
+            c.s = rv.data + o + n; c.slen = l; c.ok = true; return c;
+        }
+        default: return c;
+    }
+}
+
+int32_t rowSchemaVer(const uint8_t* row, uint64_t len) {     // RowReader::getSchemaVer
+    if (len == 0) return -1;
+    uint32_t verBytes = row[0] >> 5;
+    if (verBytes == 0) return 0;
+    if (verBytes + 1 > len) return -1;
+    int32_t v = 0;
+    for (uint32_t i = 0; i < verBytes; i++) v |= static_cast<int32_t>(static_cast<uint32_t>(row[1 + i]) << (8 * i));
+    return v;
+}
+
+// A version schema mapped onto the latest schema's columns.
+struct VersionMap {
+    const SchemaDef* schema = nullptr;
+    std::vector<int32_t> colToField;   // latest column -> field index in this version, -1 if absent
+};
+
+Error buildVersionMaps(const SchemaSet& ss, std::map<int64_t, VersionMap>& out) {
+    const SchemaDef& latest = ss.latest();
+    for (auto& kv : ss.versions) {
+        VersionMap vm;
+        vm.schema = &kv.second;
+        for (auto& f : latest.fields) {
+            int32_t i = kv.second.index(f.name);
+            if (i >= 0 && kv.second.fields[i].type != f.type) {
+                return Error{NGX_E_UNSUPPORTED, "schema `" + ss.name + "' changes the type of `" + f.name +
+                             "' across versions; not supported by the columnar export"};
+            }
+            vm.colToField.push_back(i);
+        }
+        out[kv.first] = std::move(vm);
+    }
+    return Error{NGX_OK, ""};
+}
+
+void initColumns(std::vector<HostColumn>& cols, const SchemaDef& latest, uint64_t n) {
+    cols.resize(latest.fields.size());
+    for (size_t c = 0; c < cols.size(); c++) {
+        auto& col = cols[c];
+        col.type = latest.fields[c].type;
+        switch (col.type) {
+            case T_INT: case T_TIMESTAMP: case T_VID: col.i64.assign(n, 0); break;
+            case T_FLOAT: case T_DOUBLE: col.f64.assign(n, 0.0); break;
+            case T_BOOL: col.b.assign(n, 0); break;
+            case T_STRING: col.soff.assign(n + 1, 0); break;
+            default: break;
+        }
+        col.valid.assign(n, 1);
+    }
+}
+
+// Decodes `row` into element `e` of `cols`. String bytes are collected per element in `strs`
+// and packed afterwards (strings are the only variable-size column).
+// Returns EF_* flags for the row.
+uint8_t decodeInto(const uint8_t* row, uint64_t len, const std::map<int64_t, VersionMap>& vmaps,
+                   std::vector<HostColumn>& cols, uint64_t e, std::vector<std::vector<std::string>>& strs) {
+    auto invalidAll = [&]() {
+        for (auto& col : cols) { col.valid[e] = 0; }
+    };
+    if (len == 0) { invalidAll(); return EF_EMPTY_VALUE; }
+    int32_t ver = rowSchemaVer(row, len);
+    auto it = ver < 0 ? vmaps.end() : vmaps.find(ver);
+    if (it == vmaps.end()) { invalidAll(); return EF_BAD_ROW; }
+    const VersionMap& vm = it->second;
+    RowView rv;
+    if (!parseHeader(row, len, static_cast<uint32_t>(vm.schema->fields.size()), rv)) { invalidAll(); return EF_BAD_ROW; }
+    for (size_t c = 0; c < cols.size(); c++) {
+        auto& col = cols[c];
+        int32_t fi = vm.colToField[c];
+        Cell v;
+        if (fi >= 0) v = readField(rv, *vm.schema, static_cast<uint32_t>(fi));
+        if (!v.ok) { col.valid[e] = 0; continue; }
+        switch (col.type) {
+            case T_INT: case T_TIMESTAMP: case T_VID: col.i64[e] = v.i; break;
+            case T_FLOAT: case T_DOUBLE: col.f64[e] = v.d; break;
+            case T_BOOL: col.b[e] = static_cast<uint8_t>(v.i); break;
+            case T_STRING: strs[c][e].assign(reinterpret_cast<const char*>(v.s), v.slen); break;
+            default: break;
+        }
+    }
+    return 0;
+}
+
+void packStrings(std::vector<HostColumn>& cols, std::vector<std::vector<std::string>>& strs) {
+    for (size_t c = 0; c < cols.size(); c++) {
+        auto& col = cols[c];
+        col.allValid = std::all_of(col.valid.begin(), col.valid.end(), [](uint8_t v) { return v != 0; });
+        if (col.allValid) { col.valid.clear(); col.valid.shrink_to_fit(); }
+        if (col.type != T_STRING) continue;
+        uint64_t total = 0;
+        for (size_t e = 0; e < strs[c].size(); e++) { col.soff[e] = total; total += strs[c][e].size(); }
+        col.soff[strs[c].size()] = total;
+        col.sbytes.reserve(total);
+        for (auto& s : strs[c]) col.sbytes += s;
+        strs[c].clear();
+        strs[c].shrink_to_fit();
+    }
+}
+
+struct EdgeRec {
+    uint64_t w[5];     // key bytes as big-endian words: memcmp order
+    uint64_t row;
+};
+
+}  // namespace
+
+int32_t Space::slotOf(int32_t signedType) const {
+    if (!host) return -1;
+    for (size_t i = 0; i < host->slots.size(); i++) if (host->slots[i].etype == signedType) return static_cast<int32_t>(i);
+    return -1;
+}
+int32_t Space::tagSlotOf(int32_t tagId) const {
+    if (!host) return -1;
+    for (size_t i = 0; i < host->tags.size(); i++) if (host->tags[i].tag == tagId) return static_cast<int32_t>(i);
+    return -1;
+}
+
+Error exportSnapshot(Space& sp, int32_t rank, int32_t world, HostGraph& g) {
+    (void)rank; (void)world;
+    auto& st = sp.staged;
+    uint64_t n = st.klen.size();
+    // ---- classify rows
+    std::vector<EdgeRec> edges;
+    std::vector<EdgeRec> verts;
+    edges.reserve(n);
+    for (uint64_t i = 0; i < n; i++) {
+        const uint8_t* k = st.keys.data() + st.koff[i];
+        uint32_t kl = st.klen[i];
+        if (kl != 40 && kl != 24) continue;
+        if ((rd<uint32_t>(k) & 0xFF) != 1) continue;          // NebulaKeyType::kData
+        int32_t t = rd<int32_t>(k + 12);
+        bool isEdge = (t & 0x40000000) != 0;
+        if (kl == 40 && isEdge) {
+            EdgeRec r;
+            for (int j = 0; j < 5; j++) r.w[j] = be64(k + 8 * j);
+            r.row = i;
+            edges.push_back(r);
+        } else if (kl == 24 && !isEdge) {
+            EdgeRec r{};
+            r.w[0] = be64(k); r.w[1] = be64(k + 8); r.w[2] = be64(k + 16); r.row = i;
+            verts.push_back(r);
+        }
+    }
+    auto lessRec = [](const EdgeRec& a, const EdgeRec& b) {
+        for (int j = 0; j < 5; j++) if (a.w[j] != b.w[j]) return a.w[j] < b.w[j];
+        return a.row > b.row;      // duplicates: the later put first (RocksDB overwrite keeps it)
+    };
+    bool sorted = true;
+    for (uint64_t i = 1; i < edges.size() && sorted; i++) if (lessRec(edges[i], edges[i - 1])) sorted = false;
+    if (!sorted) parallelSort(edges.begin(), edges.end(), lessRec);
+    parallelSort(verts.begin(), verts.end(), lessRec);
+    auto keyOf = [&](const EdgeRec& r) { return st.keys.data() + st.koff[r.row]; };
+
+    // ---- dedup: identical keys (keep the latest write) and latest version per (rank, dst)
+    std::vector<EdgeRec> kept;
+    kept.reserve(edges.size());
+    for (uint64_t i = 0; i < edges.size(); i++) {
+        const EdgeRec& r = edges[i];
+        if (!kept.empty()) {
+            const EdgeRec& p = kept.back();
+            // same 16-byte prefix (part, src, type) and same (rank, dst) => older version of one edge
+            const uint8_t* a = keyOf(r);
+            const uint8_t* b = keyOf(p);
+            if (std::memcmp(a, b, 16) == 0 && std::memcmp(a + 16, b + 16, 16) == 0) continue;
+        }
+        kept.push_back(r);
+    }
+    edges.swap(kept);
+    std::vector<EdgeRec>().swap(kept);
+
+    // ---- vertex table: (part, vid) of every edge source and tag row
+    std::vector<std::pair<int32_t, int64_t>> vt;
+    vt.reserve(edges.size() / 4 + verts.size());
+    for (auto& r : edges) {
+        const uint8_t* k = keyOf(r);
+        std::pair<int32_t, int64_t> pv{rd<int32_t>(k) >> 8, rd<int64_t>(k + 4)};
+        if (vt.empty() || vt.back() != pv) vt.push_back(pv);
+    }
+    for (auto& r : verts) {
+        const uint8_t* k = keyOf(r);
+        vt.emplace_back(rd<int32_t>(k) >> 8, rd<int64_t>(k + 4));
+    }
+    parallelSort(vt.begin(), vt.end(), std::less<std::pair<int32_t, int64_t>>());
+    vt.erase(std::unique(vt.begin(), vt.end()), vt.end());
+    uint64_t V = vt.size();
+    g.vpart.resize(V);
+    g.vid.resize(V);
+    for (uint64_t i = 0; i < V; i++) { g.vpart[i] = vt[i].first; g.vid[i] = vt[i].second; }
+    auto rowOf = [&](int32_t part, int64_t vid) -> uint64_t {
+        auto it = std::lower_bound(vt.begin(), vt.end(), std::make_pair(part, vid));
+        return static_cast<uint64_t>(it - vt.begin());
+    };
+
+    // ---- slots (signed edge types present)
+    std::map<int32_t, int32_t> slotIdx;
+    for (auto& r : edges) {
+        int32_t t = rd<int32_t>(keyOf(r) + 12);
+        int32_t et = t > 0 ? (t & ~0x40000000) : t;             // NebulaKeyUtils::getEdgeType
+        if (!slotIdx.count(et)) slotIdx[et] = 0;
+    }
+    int32_t si = 0;
+    for (auto& kv : slotIdx) kv.second = si++;
+    g.slots.assign(slotIdx.size(), HostSlot());
+    for (auto& kv : slotIdx) {
+        auto& s = g.slots[kv.second];
+        s.etype = kv.first;
+        s.off.assign(V + 1, 0);
+    }
+    std::vector<uint64_t> eRow(edges.size());
+    std::vector<int32_t> eSlot(edges.size());
+    parallelFor(edges.size(), [&](uint64_t lo, uint64_t hi) {
+        uint64_t cachedRow = 0;
+        int32_t cp = INT32_MIN;
+        int64_t cv = 0;
+        for (uint64_t i = lo; i < hi; i++) {
+            const uint8_t* k = keyOf(edges[i]);
+            int32_t part = rd<int32_t>(k) >> 8;
+            int64_t src = rd<int64_t>(k + 4);
+            if (part != cp || src != cv) { cachedRow = rowOf(part, src); cp = part; cv = src; }
+            eRow[i] = cachedRow;
+            int32_t t = rd<int32_t>(k + 12);
+            eSlot[i] = slotIdx.at(t > 0 ? (t & ~0x40000000) : t);
+        }
+    });
+    for (uint64_t i = 0; i < edges.size(); i++) g.slots[eSlot[i]].off[eRow[i] + 1]++;
+    for (auto& s : g.slots) {
+        for (uint64_t v = 0; v < V; v++) s.off[v + 1] += s.off[v];
+        uint64_t ne = s.off[V];
+        s.dst.resize(ne);
+        s.rank.resize(ne);
+        s.dgid.assign(ne, kNoRow);
+        s.eflags.assign(ne, 0);
+    }
+    // position of each edge in its slot: edges are sorted by (part, src, type, rank, dst) so
+    // within one (row, slot) they are consecutive and already in key order
+    std::vector<uint64_t> ePos(edges.size());
+    {
+        std::vector<uint64_t> cursor;
+        for (uint64_t i = 0; i < edges.size(); i++) {
+            auto& s = g.slots[eSlot[i]];
+            if (i == 0 || eRow[i] != eRow[i - 1] || eSlot[i] != eSlot[i - 1]) ePos[i] = s.off[eRow[i]];
+            else ePos[i] = ePos[i - 1] + 1;
+        }
+    }
+    // ---- key fields + props
+    std::map<int32_t, std::map<int64_t, VersionMap>> vmapsByType;
+    for (auto& s : g.slots) {
+        const SchemaSet* ss = sp.edge(std::abs(s.etype));
+        if (!ss) continue;                                   // no schema: structure only
+        if (!vmapsByType.count(std::abs(s.etype))) {
+            auto err = buildVersionMaps(*ss, vmapsByType[std::abs(s.etype)]);
+            if (err.code != NGX_OK) return err;
+        }
+        initColumns(s.cols, ss->latest(), s.dst.size());
+    }
+    std::vector<std::vector<std::vector<std::string>>> strs(g.slots.size());
+    for (size_t k = 0; k < g.slots.size(); k++) {
+        strs[k].resize(g.slots[k].cols.size());
+        for (size_t c = 0; c < g.slots[k].cols.size(); c++) {
+            if (g.slots[k].cols[c].type == T_STRING) strs[k][c].resize(g.slots[k].dst.size());
+        }
+    }
+    parallelFor(edges.size(), [&](uint64_t lo, uint64_t hi) {
+        for (uint64_t i = lo; i < hi; i++) {
+            const uint8_t* k = keyOf(edges[i]);
+            auto& s = g.slots[eSlot[i]];
+            uint64_t p = ePos[i];
+            s.rank[p] = rd<int64_t>(k + 16);
+            s.dst[p] = rd<int64_t>(k + 24);
+            auto vm = vmapsByType.find(std::abs(s.etype));
+            uint64_t row = edges[i].row;
+            const uint8_t* val = st.vals.data() + st.voff[row];
+            uint64_t vlen = st.voff[row + 1] - st.voff[row];
+            if (vm == vmapsByType.end()) {
+                s.eflags[p] = vlen == 0 ? EF_EMPTY_VALUE : EF_BAD_ROW;
+                continue;
+            }
+            s.eflags[p] = decodeInto(val, vlen, vm->second, s.cols, p, strs[eSlot[i]]);
+        }
+    });
+    for (size_t k = 0; k < g.slots.size(); k++) {
+        auto& s = g.slots[k];
+        s.anyFlags = std::any_of(s.eflags.begin(), s.eflags.end(), [](uint8_t f) { return f != 0; });
+        if (!s.anyFlags) { s.eflags.clear(); s.eflags.shrink_to_fit(); }
+        packStrings(s.cols, strs[k]);
+        g.edges += s.dst.size();
+    }
+
+    // ---- tags: first row under vertexPrefix(part, vid, tag) is the latest version
+    std::map<int32_t, int32_t> tagIdx;
+    for (auto& kv : sp.tags) { tagIdx[kv.first] = static_cast<int32_t>(g.tags.size()); g.tags.emplace_back(); g.tags.back().tag = kv.first; }
+    std::map<int32_t, std::map<int64_t, VersionMap>> tvmaps;
+    for (auto& t : g.tags) {
+        const SchemaSet& ss = sp.tags.at(t.tag);
+        auto err = buildVersionMaps(ss, tvmaps[t.tag]);
+        if (err.code != NGX_OK) return err;
+        initColumns(t.cols, ss.latest(), V);
+        t.present.assign(V, 0);
+    }
+    std::vector<std::vector<std::vector<std::string>>> tstrs(g.tags.size());
+    for (size_t k = 0; k < g.tags.size(); k++) {
+        tstrs[k].resize(g.tags[k].cols.size());
+        for (size_t c = 0; c < g.tags[k].cols.size(); c++) if (g.tags[k].cols[c].type == T_STRING) tstrs[k][c].resize(V);
+    }
+    for (uint64_t i = 0; i < verts.size(); i++) {
+        const uint8_t* k = keyOf(verts[i]);
+        if (i > 0 && std::memcmp(k, keyOf(verts[i - 1]), 16) == 0) continue;   // older version
+        int32_t tag = rd<int32_t>(k + 12);
+        auto ti = tagIdx.find(tag);
+        if (ti == tagIdx.end()) continue;
+        auto& t = g.tags[ti->second];
+        uint64_t v = rowOf(rd<int32_t>(k) >> 8, rd<int64_t>(k + 4));
+        uint64_t row = verts[i].row;
+        const uint8_t* val = st.vals.data() + st.voff[row];
+        uint64_t vlen = st.voff[row + 1] - st.voff[row];
+        uint8_t f = decodeInto(val, vlen, tvmaps[tag], t.cols, v, tstrs[ti->second]);
+        // collectVertexProps: an unreadable tag row is ERR_CORRUPT_DATA; treated as absent here
+        t.present[v] = (f == 0) ? 1 : 0;
+    }
+    for (size_t k = 0; k < g.tags.size(); k++) packStrings(g.tags[k].cols, tstrs[k]);
+    return Error{NGX_OK, ""};
+}
+
+void resolveDstRows(const Space& sp, HostGraph& g,
+                    const std::vector<std::vector<std::pair<int32_t, int64_t>>>& shardTables, int32_t world) {
+    if (sp.numParts <= 0) return;                    // test-only layouts: no ID_HASH routing
+    g.shardBase.assign(world + 1, 0);
+    for (int32_t w = 0; w < world; w++) g.shardBase[w + 1] = g.shardBase[w] + shardTables[w].size();
+    g.vglobal = g.shardBase[world];
+    for (auto& s : g.slots) {
+        parallelFor(s.dst.size(), [&](uint64_t lo, uint64_t hi) {
+            for (uint64_t e = lo; e < hi; e++) {
+                int64_t d = s.dst[e];
+                int32_t part = idHash(d, sp.numParts);
+                int32_t owner = part % world;
+                auto& tab = shardTables[owner];
+                auto it = std::lower_bound(tab.begin(), tab.end(), std::make_pair(part, d));
+                if (it != tab.end() && it->first == part && it->second == d) {
+                    s.dgid[e] = static_cast<uint32_t>(g.shardBase[owner] + (it - tab.begin()));
+                } else {
+                    s.dgid[e] = kNoRow;                 // the destination has no edges or tags here
+                }
+            }
+        });
+    }
+}
+
+}  // namespace ngx

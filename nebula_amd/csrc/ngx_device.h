@@ -1,0 +1,93 @@
+// POD types shared by the host engine and the HIP kernels: device column / slot / tag
+// descriptors and the flat filter bytecode the host compiles WHERE / YIELD expressions into
+// (exprc.cpp) and the device VM executes per edge (kernels.hip).
+#pragma once
+
+#include <cstdint>
+
+namespace ngx {
+
+constexpr uint32_t kNoRow = 0xFFFFFFFFu;
+constexpr int kMaxSlots = 16;
+constexpr int kMaxStack = 12;
+
+// per-edge flags (HostSlot::eflags)
+enum : uint8_t {
+    EF_EMPTY_VALUE = 1,    // the KV value was empty: no RowReader, filter not evaluated (.inl:520)
+    EF_BAD_ROW = 2,        // getEdgePropReader returned null: skipped when props are read (.inl:525-528)
+};
+
+// device column descriptor
+struct DCol {
+    int32_t type;          // SType of the latest schema
+    int32_t pad;
+    const void* data;      // int64_t (INT/TIMESTAMP/VID), double (FLOAT/DOUBLE), uint8_t (BOOL)
+    const uint64_t* soff;  // STRING: n + 1 offsets
+    const char* sbytes;    // STRING bytes
+    const uint8_t* valid;  // nullptr when every row had the field
+};
+
+struct DSlot {
+    int32_t etype;         // signed edge type
+    int32_t ncols;
+    int32_t colBase;       // first DCol of this slot in the column table
+    int32_t hasFlags;
+    const uint64_t* off;   // V + 1
+    const int64_t* dst;
+    const uint32_t* dgid;
+    const int64_t* rank;
+    const uint8_t* eflags;
+};
+
+struct DTag {
+    int32_t tag;
+    int32_t ncols;
+    int32_t colBase;
+    int32_t pad;
+    const uint8_t* present;
+};
+
+// ------------------------------------------------------------------ bytecode
+// VM values
+enum : uint8_t { V_ERR = 0, V_INT = 1, V_DBL = 2, V_BOOL = 3, V_STR = 4 };
+
+enum Op : uint8_t {
+    OP_END = 0,
+    OP_PUSH,           // push constant: t1 = value type, imm = bits (string: imm = pool offset, a = len)
+    OP_ERR,            // push an error (a getter that always fails)
+    OP_ECOL,           // edge column: a = column index in |type| schema, b = |type| required
+                       //   mode bit0: mismatch -> default (graphd) instead of error (storage)
+                       //   mode bit1: invalid field -> default (graphd) instead of error
+                       //   t2/imm: default value type/bits
+    OP_EKEY,           // key prop: a = 0 src,1 dst,2 rank,3 type; b = |type| required (0: any)
+                       //   mode bit0 as OP_ECOL; t2/imm default
+    OP_EDST,           // EdgeDstIdExpression in graphd: b = alias type (0: no check), mismatch -> 0
+    OP_SRCTAG,         // src tag column: a = column, b = tag slot; mode bit0: missing -> default
+    OP_DSTTAG,         // dst tag column (graphd $$): a = column, b = tag slot; missing -> default
+    OP_NEG, OP_PLUS, OP_NOT,
+    OP_CAST,           // t1 = ColumnType target (INT=0, STRING=1, DOUBLE=2, BOOL=3, TIMESTAMP=4)
+    OP_ADD, OP_SUB, OP_MUL, OP_DIV, OP_MOD, OP_AXOR,
+    OP_LT, OP_LE, OP_GT, OP_GE, OP_EQ, OP_NE, OP_CONTAINS,
+    OP_AND, OP_OR, OP_LXOR,
+    OP_FUNC,           // a = function id, b = argc
+};
+
+enum Func : int32_t {
+    F_ABS = 0, F_FLOOR, F_CEIL, F_ROUND, F_SQRT, F_CBRT, F_EXP, F_EXP2, F_LOG, F_LOG2, F_LOG10,
+    F_SIN, F_ASIN, F_COS, F_ACOS, F_TAN, F_ATAN, F_HYPOT, F_POW, F_STRCASECMP, F_LENGTH, F_HASH,
+    F_UDF_IS_IN,
+};
+
+struct Insn {
+    uint8_t op;
+    uint8_t t1;
+    uint8_t t2;
+    uint8_t mode;
+    int32_t a;
+    int32_t b;
+    int32_t pad;
+    int64_t imm;
+};
+static_assert(sizeof(Insn) == 24, "Insn layout");
+
+}  // namespace ngx

@@ -1,0 +1,348 @@
+"""Host-side mirror of the reference's GetNeighbors / GO interface over libnebula_gn.so.
+
+`Engine` is one shard (one GPU). Its methods follow the reference call surface for the path:
+  add_space / add_schema   meta::SchemaManager (src/meta/SchemaManager.h:18-56)
+  load_kv / commit         the KV rows of the space's parts (NebulaKeyUtils keys + RowWriter values)
+                           -> per-part CSR + columnar props in HBM
+  get_neighbors            StorageClient::getNeighbors -> QueryBoundProcessor
+                           (src/storage/client/StorageClient.cpp:121-157, QueryBoundProcessor.cpp)
+  go                       GoExecutor (src/graph/GoExecutor.cpp) for `GO [M TO] N STEPS FROM ...
+                           OVER ... [REVERSELY|BIDIRECT] [WHERE ...] YIELD [DISTINCT] ...`
+There is no CPU fallback: a missing library raises at import of the first Engine.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+from . import ngql
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libnebula_gn.so")
+
+NGX_OK = 0
+E_UNSUPPORTED = -1002
+E_QUERY = -1003
+E_DEVICE = -1004
+
+SOURCE, DEST, EDGE = 1, 2, 3
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+# ----------------------------------------------------------------------------- C structs
+c_i32, c_i64, c_u32, c_u64, c_dbl = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_double
+P = ctypes.POINTER
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("device", c_i32), ("rank", c_i32), ("world", c_i32), ("nccl_unique_id", ctypes.c_void_p)]
+
+
+class KVBatchC(ctypes.Structure):
+    _fields_ = [("n", c_u64), ("keys", ctypes.c_void_p), ("key_off", ctypes.c_void_p), ("vals", ctypes.c_void_p),
+                ("val_off", ctypes.c_void_p)]
+
+
+class GraphInfo(ctypes.Structure):
+    _fields_ = [("vertices", c_u64), ("edges", c_u64), ("device_bytes", c_u64), ("slots", c_i32), ("tags", c_i32)]
+
+
+class CellV(ctypes.Union):
+    _fields_ = [("i", c_i64), ("d", c_dbl), ("str_off", c_u64)]
+
+
+class Cell(ctypes.Structure):
+    _fields_ = [("kind", c_i32), ("str_len", c_i32), ("v", CellV)]
+
+
+class PropDef(ctypes.Structure):
+    _fields_ = [("owner", c_i32), ("id", c_i32), ("name", ctypes.c_char_p)]
+
+
+class GnRequest(ctypes.Structure):
+    _fields_ = [("space", c_i32), ("nparts", c_i32), ("parts", P(c_i32)), ("part_nvids", P(c_u32)),
+                ("vids", P(c_i64)), ("nedge_types", c_i32), ("edge_types", P(c_i32)), ("filter", ctypes.c_char_p),
+                ("filter_len", c_u32), ("ncols", c_i32), ("cols", P(PropDef)), ("max_edges_per_vertex", c_i32),
+                ("now_sec", c_i64)]
+
+
+class GnResult(ctypes.Structure):
+    _fields_ = [("code", c_i32), ("nfailed", c_i32), ("failed_codes", P(c_i32)), ("nedges", c_u64),
+                ("edge_vertex", P(c_u32)), ("edge_type", P(c_i32)), ("edge_dst", P(c_i64)), ("ncols", c_i32),
+                ("edge_cells", P(Cell)), ("nvertices", c_u32), ("vertex_cells", P(Cell)),
+                ("vertex_has_tag", P(ctypes.c_uint8)), ("strings", ctypes.c_void_p), ("strings_len", c_u64)]
+
+
+class GoPlan(ctypes.Structure):
+    _fields_ = [("space", c_i32), ("record_from", c_u32), ("record_to", c_u32), ("nstarts", c_u64),
+                ("starts", P(c_i64)), ("nover", c_i32), ("over_names", P(ctypes.c_char_p)),
+                ("over_aliases", P(ctypes.c_char_p)), ("over_all", c_i32), ("direction", c_i32),
+                ("where", ctypes.c_char_p), ("where_len", c_u32), ("nyields", c_i32),
+                ("yields", P(ctypes.c_char_p)), ("yield_lens", P(c_u32)), ("distinct", c_i32),
+                ("filter_pushdown", c_i32), ("now_sec", c_i64)]
+
+
+class GoResultC(ctypes.Structure):
+    _fields_ = [("code", c_i32), ("ncols", c_i32), ("col_types", P(c_i32)), ("nrows", c_u64), ("cells", P(Cell)),
+                ("row_src", P(c_i64)), ("row_dst", P(c_i64)), ("row_rank", P(c_i64)), ("row_type", P(c_i32)),
+                ("strings", ctypes.c_void_p), ("strings_len", c_u64), ("nhops", c_i32),
+                ("hop_frontier", P(c_u64)), ("hop_edges", P(c_u64)), ("hop_next", P(c_u64)),
+                ("device_ms", c_dbl)]
+
+
+class KernelStat(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("launches", c_u32), ("total_ms", c_dbl), ("algo_bytes", c_u64)]
+
+
+# every symbol include/nebula_gn.h declares: (name, restype, argtypes)
+SIGNATURES = {
+    "ngx_open": (c_i32, [P(Config), P(ctypes.c_void_p)]),
+    "ngx_close": (None, [ctypes.c_void_p]),
+    "ngx_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
+    "ngx_get_unique_id": (c_i32, [ctypes.c_void_p]),
+    "ngx_add_space": (c_i32, [ctypes.c_void_p, c_i32, c_i32]),
+    "ngx_add_schema": (c_i32, [ctypes.c_void_p, c_i32, c_i32, c_i32, ctypes.c_char_p, c_i64, c_i32,
+                               P(ctypes.c_char_p), P(c_i32), ctypes.c_char_p, c_i64]),
+    "ngx_load_kv": (c_i32, [ctypes.c_void_p, c_i32, P(KVBatchC)]),
+    "ngx_commit": (c_i32, [ctypes.c_void_p, c_i32]),
+    "ngx_graph_info_get": (c_i32, [ctypes.c_void_p, c_i32, P(GraphInfo)]),
+    "ngx_get_neighbors": (c_i32, [ctypes.c_void_p, P(GnRequest), P(P(GnResult))]),
+    "ngx_gn_result_free": (None, [P(GnResult)]),
+    "ngx_go": (c_i32, [ctypes.c_void_p, P(GoPlan), P(P(GoResultC))]),
+    "ngx_go_result_free": (None, [P(GoResultC)]),
+    "ngx_set_profiling": (c_i32, [ctypes.c_void_p, c_i32]),
+    "ngx_kernel_stats": (c_i32, [ctypes.c_void_p, P(P(KernelStat)), P(c_i32)]),
+    "ngx_hash_string": (c_i64, [ctypes.c_char_p, c_u64]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libnebula_gn.so. Raises if it is not built: there is no other implementation."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise EngineError(E_DEVICE, f"{LIB_PATH} is missing; build it with `make -C nebula_amd/csrc`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    rc = lib().ngx_get_unique_id(buf)
+    if rc:
+        raise EngineError(rc, "ncclGetUniqueId failed")
+    return buf.raw
+
+
+# ----------------------------------------------------------------------------- results
+def _cells(cells, n, ncols, strings: bytes):
+    out = []
+    kinds = {0: "empty", 1: "bool", 2: "int", 3: "id", 4: "float", 5: "double", 6: "str", 21: "timestamp"}
+    for r in range(n):
+        row = []
+        for c in range(ncols):
+            cl = cells[r * ncols + c]
+            k = kinds.get(cl.kind, str(cl.kind))
+            if cl.kind == 0:
+                row.append(("empty", None))
+            elif cl.kind == 1:
+                row.append(("bool", bool(cl.v.i)))
+            elif cl.kind in (4, 5):
+                row.append((k, cl.v.d))
+            elif cl.kind == 6:
+                o = cl.v.str_off
+                row.append(("str", strings[o:o + cl.str_len].decode("utf-8", "surrogateescape")))
+            else:
+                row.append((k, cl.v.i))
+        out.append(tuple(row))
+    return out
+
+
+@dataclass
+class GoResult:
+    ok: bool
+    error: str
+    code: int
+    col_types: List[int]
+    rows: List[tuple]
+    src: np.ndarray = None
+    dst: np.ndarray = None
+    rank: np.ndarray = None
+    etype: np.ndarray = None
+    hop_frontier: List[int] = field(default_factory=list)
+    hop_edges: List[int] = field(default_factory=list)
+    hop_next: List[int] = field(default_factory=list)
+    device_ms: float = 0.0
+
+
+@dataclass
+class NeighborsResult:
+    code: int
+    failed_codes: List[Tuple[int, int]]
+    total_edges: int
+    edge_vertex: np.ndarray
+    edge_type: np.ndarray
+    edge_dst: np.ndarray
+    edge_cells: List[tuple]
+    vertex_cells: List[tuple]
+    vertex_has_tag: np.ndarray
+
+
+def _arr(ptr, n, dtype):
+    if n == 0 or not ptr:
+        return np.zeros(0, dtype=dtype)
+    return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dtype, copy=True)
+
+
+# ----------------------------------------------------------------------------- engine
+class Engine:
+    def __init__(self, device: int = 0, rank: int = 0, world: int = 1, nccl_id: Optional[bytes] = None):
+        self.L = lib()
+        self._uid = ctypes.create_string_buffer(nccl_id, 128) if nccl_id else None
+        cfg = Config(device, rank, world, ctypes.cast(self._uid, ctypes.c_void_p) if self._uid else None)
+        h = ctypes.c_void_p()
+        rc = self.L.ngx_open(ctypes.byref(cfg), ctypes.byref(h))
+        if rc:
+            raise EngineError(rc, "ngx_open failed (no HIP device or RCCL init failed)")
+        self.h = h
+        self.rank, self.world = rank, world
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.ngx_close(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int, what: str):
+        if rc:
+            raise EngineError(rc, f"{what}: {self.L.ngx_last_error(self.h).decode()}")
+
+    # ---- schema + data
+    def add_space(self, space: int, num_parts: int):
+        self._check(self.L.ngx_add_space(self.h, space, num_parts), "add_space")
+
+    def add_schema(self, space, is_edge, sid, name, fields: Sequence[Tuple[str, int]], ver=0, ttl_col="", ttl_dur=0):
+        names = (ctypes.c_char_p * max(1, len(fields)))(*[f[0].encode() for f in fields])
+        types = (c_i32 * max(1, len(fields)))(*[f[1] for f in fields])
+        self._check(self.L.ngx_add_schema(self.h, space, 1 if is_edge else 0, sid, name.encode(), ver, len(fields),
+                                          names, types, ttl_col.encode(), ttl_dur), "add_schema")
+
+    def load_kv(self, space: int, keys, koff, vals, voff):
+        keys, vals = np.ascontiguousarray(keys, dtype=np.uint8), np.ascontiguousarray(vals, dtype=np.uint8)
+        koff, voff = np.ascontiguousarray(koff, dtype=np.uint64), np.ascontiguousarray(voff, dtype=np.uint64)
+        b = KVBatchC(len(koff) - 1, keys.ctypes.data, koff.ctypes.data, vals.ctypes.data, voff.ctypes.data)
+        self._check(self.L.ngx_load_kv(self.h, space, ctypes.byref(b)), "load_kv")
+
+    def load_batch(self, space: int, batch):
+        self.load_kv(space, *batch.arrays())
+
+    def commit(self, space: int):
+        self._check(self.L.ngx_commit(self.h, space), "commit")
+
+    def info(self, space: int) -> GraphInfo:
+        gi = GraphInfo()
+        self._check(self.L.ngx_graph_info_get(self.h, space, ctypes.byref(gi)), "graph_info")
+        return gi
+
+    # ---- GetNeighbors
+    def get_neighbors(self, space, parts: Sequence[Tuple[int, Sequence[int]]], edge_types: Optional[Sequence[int]],
+                      return_columns: Sequence[Tuple[int, int, str]], filter_bytes: bytes = b"",
+                      max_edges_per_vertex: int = 2**31 - 1, now_sec: int = 0) -> NeighborsResult:
+        pid = np.array([p for p, _ in parts], dtype=np.int32)
+        nv = np.array([len(v) for _, v in parts], dtype=np.uint32)
+        vids = np.array([x for _, v in parts for x in v], dtype=np.int64)
+        et = np.array(list(edge_types or []), dtype=np.int32)
+        cols = (PropDef * max(1, len(return_columns)))(*[PropDef(o, i, n.encode()) for o, i, n in return_columns])
+        req = GnRequest(space, len(parts), pid.ctypes.data_as(P(c_i32)), nv.ctypes.data_as(P(c_u32)),
+                        vids.ctypes.data_as(P(c_i64)), len(et), et.ctypes.data_as(P(c_i32)), filter_bytes,
+                        len(filter_bytes), len(return_columns), cols, max_edges_per_vertex, now_sec)
+        out = P(GnResult)()
+        rc = self.L.ngx_get_neighbors(self.h, ctypes.byref(req), ctypes.byref(out))
+        try:
+            r = out.contents
+            if rc and rc not in (NGX_OK,) and r.nfailed == 0:
+                raise EngineError(rc, self.L.ngx_last_error(self.h).decode())
+            failed = [(r.failed_codes[2 * i], r.failed_codes[2 * i + 1]) for i in range(r.nfailed)]
+            strings = ctypes.string_at(r.strings, r.strings_len) if r.strings_len else b""
+            nc = r.ncols
+            return NeighborsResult(
+                code=r.code, failed_codes=failed, total_edges=r.nedges,
+                edge_vertex=_arr(r.edge_vertex, r.nedges, np.uint32), edge_type=_arr(r.edge_type, r.nedges, np.int32),
+                edge_dst=_arr(r.edge_dst, r.nedges, np.int64),
+                edge_cells=_cells(r.edge_cells, r.nedges, nc, strings),
+                vertex_cells=_cells(r.vertex_cells, r.nvertices, nc, strings),
+                vertex_has_tag=_arr(r.vertex_has_tag, r.nvertices * nc, np.uint8))
+        finally:
+            self.L.ngx_gn_result_free(out)
+
+    # ---- GO
+    def go(self, space: int, s: Union[str, ngql.GoSentence], pushdown: bool = True, now_sec: int = 0,
+           raise_on_error: bool = False, rows: bool = True) -> GoResult:
+        if isinstance(s, str):
+            s = ngql.parse_go(s)
+        starts = np.array(s.vids, dtype=np.int64)
+        names = (ctypes.c_char_p * max(1, len(s.over)))(*[n.encode() for n, _ in s.over])
+        aliases = (ctypes.c_char_p * max(1, len(s.over)))(*[(a or "").encode() for _, a in s.over])
+        where = s.where.encode() if s.where is not None else b""
+        yb = [y.expr.encode() for y in s.yields]
+        yarr = (ctypes.c_char_p * max(1, len(yb)))(*yb)
+        ylen = (c_u32 * max(1, len(yb)))(*[len(y) for y in yb])
+        plan = GoPlan(space, s.record_from, s.record_to, len(starts), starts.ctypes.data_as(P(c_i64)), len(s.over),
+                      names, aliases, 1 if s.over_all else 0, s.direction, where if where else None, len(where),
+                      len(yb), yarr, ylen, 1 if s.distinct else 0, 1 if pushdown else 0, now_sec)
+        out = P(GoResultC)()
+        rc = self.L.ngx_go(self.h, ctypes.byref(plan), ctypes.byref(out))
+        try:
+            r = out.contents
+            err = self.L.ngx_last_error(self.h).decode() if rc else ""
+            if rc and (raise_on_error or rc in (E_DEVICE, E_UNSUPPORTED)):
+                raise EngineError(rc, err)
+            strings = ctypes.string_at(r.strings, r.strings_len) if r.strings_len else b""
+            n = r.nrows
+            res = GoResult(
+                ok=rc == 0, error=err, code=rc, col_types=[r.col_types[i] for i in range(r.ncols)],
+                rows=_cells(r.cells, n, r.ncols, strings) if rows else [],
+                src=_arr(r.row_src, n, np.int64), dst=_arr(r.row_dst, n, np.int64),
+                rank=_arr(r.row_rank, n, np.int64), etype=_arr(r.row_type, n, np.int32),
+                hop_frontier=[r.hop_frontier[i] for i in range(r.nhops)],
+                hop_edges=[r.hop_edges[i] for i in range(r.nhops)],
+                hop_next=[r.hop_next[i] for i in range(r.nhops)], device_ms=r.device_ms)
+            return res
+        finally:
+            self.L.ngx_go_result_free(out)
+
+    # ---- measurement
+    def set_profiling(self, on: bool):
+        self._check(self.L.ngx_set_profiling(self.h, 1 if on else 0), "set_profiling")
+
+    def kernel_stats(self) -> Dict[str, Tuple[int, float, int]]:
+        p = P(KernelStat)()
+        n = c_i32()
+        self._check(self.L.ngx_kernel_stats(self.h, ctypes.byref(p), ctypes.byref(n)), "kernel_stats")
+        return {p[i].name.decode(): (p[i].launches, p[i].total_ms, p[i].algo_bytes) for i in range(n.value)}
+
+
+def hash_string(s: str) -> int:
+    b = s.encode()
+    return lib().ngx_hash_string(b, len(b))

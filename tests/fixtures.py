@@ -43,6 +43,40 @@ class Dataset:
         orc.finalize()
         return orc
 
+    def load_engine(self, eng):
+        eng.add_space(self.space, self.num_parts)
+        for s in self.schemas:
+            eng.add_schema(self.space, s.is_edge, s.sid, s.name, s.fields, s.ver, s.ttl_col, s.ttl_dur)
+        eng.load_batch(self.space, self.batch)
+        eng.commit(self.space)
+        return eng
+
+
+class RmatDataset:
+    """RMAT space of bench.py (datagen.rmat): edge `e`(p0 INT, p1 INT), optional tag `vt`."""
+
+    def __init__(self, scale, ef=16, seed=42, num_parts=100, with_in=False, with_tag=False, threads=0):
+        from nebula_amd import datagen
+        self.space, self.num_parts, self.scale = datagen.RMAT_SPACE, num_parts, scale
+        self.rows = datagen.rmat(scale, ef, seed, num_parts, with_in, with_tag, threads=threads)
+        self.schemas = [SchemaDef(e, i, n, f) for e, i, n, f in datagen.rmat_schemas(with_tag)]
+
+    def load_oracle(self, orc, threads=8):
+        orc.add_space(self.space, self.num_parts)
+        for s in self.schemas:
+            orc.add_schema(self.space, s.is_edge, s.sid, s.name, s.fields, s.ver, s.ttl_col, s.ttl_dur)
+        orc.put_kv(self.space, *self.rows.arrays())
+        orc.finalize(threads)
+        return orc
+
+    def load_engine(self, eng):
+        eng.add_space(self.space, self.num_parts)
+        for s in self.schemas:
+            eng.add_schema(self.space, s.is_edge, s.sid, s.name, s.fields, s.ver, s.ttl_col, s.ttl_dur)
+        eng.load_kv(self.space, *self.rows.arrays())
+        eng.commit(self.space)
+        return eng
+
 
 # ----------------------------------------------------------------------------- NBA (GoTest)
 def nba() -> Dataset:
