@@ -43,7 +43,8 @@ def test_gotest_nba(nba, case, pushdown):
     ref = o.go(ds.space, s, pushdown=pushdown)
     assert ref.ok
     assert got == fixtures.normalize_cells(ref.rows)
-    assert r.col_types == ref.col_types
+    if ref.rows:                         # the reference sets column types only from result rows
+        assert r.col_types == ref.col_types
     if case.get("empty"):
         assert got == []
     else:
@@ -198,7 +199,8 @@ def test_rmat_go(rmat, qi, pushdown):
     assert got.ok == ref.ok, (got.error, ref.error)
     if not ref.ok:
         return
-    assert got.col_types == ref.col_types
+    if ref.rows:
+        assert got.col_types == ref.col_types
     a, b = fixtures.normalize_cells(got.rows), fixtures.normalize_cells(ref.rows)
     assert len(a) == len(b)
     assert a == b
