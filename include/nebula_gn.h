@@ -183,7 +183,17 @@ typedef struct {
     int32_t distinct;                  /* YIELD DISTINCT */
     int32_t filter_pushdown;           /* FLAGS_filter_pushdown */
     int64_t now_sec;
+    int32_t result_on_device;          /* 1: leave rows in HBM (dev_* below), no host cells / DISTINCT */
 } ngx_go_plan;
+
+/* Raw device value of one YIELD cell (result_on_device): type 1 int, 2 double (bits in x),
+ * 3 bool, 4 string (x = device pointer into the snapshot / program pool, len bytes), 0xFF none. */
+typedef struct {
+    int64_t x;
+    uint32_t len;
+    uint8_t type;
+    uint8_t pad[3];
+} ngx_dev_cell;
 
 typedef struct {
     int32_t code;                      /* NGX_OK or an error (message in ngx_last_error) */
@@ -203,6 +213,12 @@ typedef struct {
     const uint64_t* hop_edges;         /* edges scanned per hop (TEPS numerator) */
     const uint64_t* hop_next;          /* unique next-frontier vertices per hop (this shard) */
     double device_ms;                  /* HIP-event time from the first kernel to the last result write */
+    /* result_on_device: HBM arrays valid until the next call on the context (nrows entries) */
+    const int64_t* dev_src;
+    const int64_t* dev_dst;
+    const int64_t* dev_rank;
+    const int32_t* dev_type;
+    const ngx_dev_cell* dev_cells;     /* [row * ncols + col] */
 } ngx_go_result;
 
 int32_t ngx_go(ngx_ctx* ctx, const ngx_go_plan* plan, ngx_go_result** out);
@@ -218,6 +234,15 @@ typedef struct {
 } ngx_kernel_stat;
 int32_t ngx_set_profiling(ngx_ctx* ctx, int32_t on);
 int32_t ngx_kernel_stats(ngx_ctx* ctx, const ngx_kernel_stat** out, int32_t* n);
+
+/* Engine flags (the reference's gflags for this path):
+ *   "jit"  1 (default; env NGX_JIT=0 turns it off): compile each query's WHERE / YIELD into
+ *          final-hop kernels with hipRTC; 0: run the precompiled bytecode-interpreter kernels.
+ * Read-only counters for ngx_get_flag: "jit_compiled", "jit_hits", "jit_failed", "jit_compile_us". */
+int32_t ngx_set_flag(ngx_ctx* ctx, const char* name, int64_t value);
+int32_t ngx_get_flag(ngx_ctx* ctx, const char* name, int64_t* value);
+/* why the last query ran on the interpreter kernels instead of a generated one ("" if it did not) */
+const char* ngx_jit_note(ngx_ctx* ctx);
 
 /* libstdc++ std::hash<std::string>, the NBA fixture's vid function (TraverseTestBase.h:122-126) */
 int64_t ngx_hash_string(const char* s, uint64_t n);

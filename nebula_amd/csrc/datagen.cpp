@@ -186,7 +186,7 @@ inline uint64_t scramble(uint64_t v, int scale, uint64_t seed) {
 extern "C" {
 
 // RMAT (Graph500 A/B/C/D) with `ef * 2^scale` edges of one type `etype` carrying two INT props
-// p0 = h(src,dst) % 100 and p1 = h'(src,dst) % 1000000 (deterministic per (src,dst), so duplicate
+// p0 = h(src,dst) % 100 and p1 = h'(src,dst) as a full-range int64 (deterministic per (src,dst), so duplicate
 // generated edges write byte-identical rows). rank 0. with_in also writes the in-edge rows
 // (dst, -etype, rank, src), as InsertEdgeExecutor does. with_tag writes tag `tag` (v0 INT = vid % 1000,
 // name STRING = "v<vid>") for every vertex id.
@@ -206,7 +206,7 @@ int32_t ngd_rmat(int32_t scale, int32_t ef, double A, double B, double C, uint64
         uint64_t h = mix64((static_cast<uint64_t>(src) << 20) ^ static_cast<uint64_t>(dst) ^ seed);
         Row r;
         r.i64(static_cast<int64_t>(h % 100));
-        r.i64(static_cast<int64_t>((h >> 32) % 1000000));
+        r.i64(static_cast<int64_t>(mix64(h ^ 0x70f1)));
         if (g.owned(src)) { s.edge(g.partOf(src), src, etype, 0, dst, r); }
         if (with_in && g.owned(dst)) { s.edge(g.partOf(dst), dst, -etype, 0, src, r); }
     });
@@ -327,6 +327,36 @@ int32_t ngd_snb(int64_t np, int32_t knowsDeg, int64_t nposts, int32_t likesDeg, 
     });
     finish(g, out);
     return 0;
+}
+
+// GO FROM list for the RMAT configs: `k` vids drawn uniformly (with repetition) from the vertices
+// with at least one out-edge (SURVEY §8d "sampled uniformly from non-isolated vertices").
+int32_t ngd_rmat_seeds(int32_t scale, int32_t ef, double A, double B, double C, uint64_t seed, uint64_t sampleSeed,
+                       uint64_t k, int32_t threads, int64_t* out) {
+    if (scale < 1 || scale > 40) return -1;
+    uint64_t V = 1ULL << scale, E = static_cast<uint64_t>(ef) << scale;
+    std::vector<std::atomic<uint8_t>> has(V);
+    for (auto& h : has) h.store(0, std::memory_order_relaxed);
+    uint32_t a = static_cast<uint32_t>(A * 65536), ab = static_cast<uint32_t>((A + B) * 65536),
+             abc = static_cast<uint32_t>((A + B + C) * 65536);
+    int T = threads < 1 ? 1 : threads;
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++) {
+        th.emplace_back([&, t] {
+            for (uint64_t i = E * t / T; i < E * (t + 1) / T; i++) {
+                uint64_t su, du;
+                rmatEdge(seed, i, scale, a, ab, abc, su, du);
+                has[scramble(su, scale, seed)].store(1, std::memory_order_relaxed);
+            }
+        });
+    }
+    for (auto& x : th) x.join();
+    uint64_t found = 0;
+    for (uint64_t i = 0; found < k && i < 64 * k + V; i++) {
+        uint64_t v = draw(sampleSeed, 98, i) % V;
+        if (has[v].load(std::memory_order_relaxed)) out[found++] = static_cast<int64_t>(v);
+    }
+    return found == k ? 0 : -2;
 }
 
 // deterministic sample of `k` vids in [0, range) (the GO FROM list), with repetitions possible

@@ -13,9 +13,11 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <unordered_set>
 
 #include "exprc.h"
+#include "jit.h"
 #include "kernels.h"
 
 using namespace ngx;
@@ -95,6 +97,10 @@ struct ngx_ctx {
     DBuf oSrc, oDst, oRank, oType, oEntry, oCells, progBuf, sendBits, recvBits, vcells, misc;
     uint64_t visitedSize = 0;
     uint8_t epoch = 0;
+    // per-query kernels (hipRTC)
+    bool jitOn = true;
+    JitCache jit;
+    std::string jitNote;
     // profiling
     bool prof = false;
     struct Stat { std::string name; uint32_t launches = 0; double ms = 0; uint64_t bytes = 0; };
@@ -129,6 +135,9 @@ struct ngx_ctx {
         pending.push_back({k, {a, b}});
         stats[k].launches++;
         stats[k].bytes += algoBytes;
+    }
+    void addBytes(const char* name, uint64_t b) {
+        if (prof) stats[statIndex(name)].bytes += b;
     }
     void collectTimings() {
         if (!prof) return;
@@ -240,19 +249,23 @@ struct DevPrograms {
     const char* pool = nullptr;
     const int32_t* yOff = nullptr;
     const int32_t* ySlotType = nullptr;
+    const int32_t* yColType = nullptr;
 };
 
-DevPrograms uploadPrograms(ngx_ctx* c, const Programs& pr, const std::vector<int32_t>& ySlotType) {
+DevPrograms uploadPrograms(ngx_ctx* c, const Programs& pr, const std::vector<int32_t>& ySlotType,
+                           const std::vector<int32_t>& yColType = {}) {
     size_t codeBytes = pr.code.size() * sizeof(Insn);
     size_t yBytes = pr.yOff.size() * 4;
     size_t tBytes = ySlotType.size() * 4;
-    size_t poolOff = (codeBytes + yBytes + tBytes + 63) & ~size_t(63);
+    size_t cBytes = yColType.size() * 4;
+    size_t poolOff = (codeBytes + yBytes + tBytes + cBytes + 63) & ~size_t(63);
     size_t total = poolOff + pr.pool.size() + 64;
     char* base = c->progBuf.get<char>(total);
     std::vector<char> host(total, 0);
     std::memcpy(host.data(), pr.code.data(), codeBytes);
     std::memcpy(host.data() + codeBytes, pr.yOff.data(), yBytes);
     std::memcpy(host.data() + codeBytes + yBytes, ySlotType.data(), tBytes);
+    std::memcpy(host.data() + codeBytes + yBytes + tBytes, yColType.data(), cBytes);
     std::memcpy(host.data() + poolOff, pr.pool.data(), pr.pool.size());
     HIP_OK(hipMemcpyAsync(base, host.data(), total, hipMemcpyHostToDevice, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
@@ -260,6 +273,7 @@ DevPrograms uploadPrograms(ngx_ctx* c, const Programs& pr, const std::vector<int
     d.code = reinterpret_cast<const Insn*>(base);
     d.yOff = reinterpret_cast<const int32_t*>(base + codeBytes);
     d.ySlotType = reinterpret_cast<const int32_t*>(base + codeBytes + yBytes);
+    d.yColType = cBytes ? reinterpret_cast<const int32_t*>(base + codeBytes + yBytes + tBytes) : nullptr;
     d.pool = base + poolOff;
     return d;
 }
@@ -415,6 +429,7 @@ int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
     c->device = cfg->device;
     c->rank = cfg->rank;
     c->world = cfg->world < 1 ? 1 : cfg->world;
+    if (const char* j = std::getenv("NGX_JIT")) c->jitOn = std::string(j) != "0";
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return NGX_E_DEVICE;
     if (hipSetDevice(c->device) != hipSuccess) return NGX_E_DEVICE;
@@ -586,6 +601,27 @@ int32_t ngx_kernel_stats(ngx_ctx* c, const ngx_kernel_stat** out, int32_t* n) {
     *n = static_cast<int32_t>(c->statView.size());
     return NGX_OK;
 }
+
+int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
+    std::lock_guard<std::mutex> g(c->mu);
+    std::string n = name ? name : "";
+    if (n == "jit") { c->jitOn = value != 0; return NGX_OK; }
+    return fail(c, NGX_E_BAD_ARGUMENT, "unknown flag " + n);
+}
+
+int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
+    std::lock_guard<std::mutex> g(c->mu);
+    std::string n = name ? name : "";
+    if (n == "jit") *value = c->jitOn ? 1 : 0;
+    else if (n == "jit_compiled") *value = static_cast<int64_t>(c->jit.compiled);
+    else if (n == "jit_hits") *value = static_cast<int64_t>(c->jit.hits);
+    else if (n == "jit_failed") *value = static_cast<int64_t>(c->jit.failed);
+    else if (n == "jit_compile_us") *value = static_cast<int64_t>(c->jit.compileSeconds * 1e6);
+    else return fail(c, NGX_E_BAD_ARGUMENT, "unknown flag " + n);
+    return NGX_OK;
+}
+
+const char* ngx_jit_note(ngx_ctx* c) { return c ? c->jitNote.c_str() : ""; }
 
 int64_t ngx_hash_string(const char* s, uint64_t n) {
     return static_cast<int64_t>(std::hash<std::string>()(std::string(s, n)));
@@ -780,8 +816,47 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             return fail(c, NGX_E_UNSUPPORTED, "tag TTL is not evaluated on the device");
     }
     std::vector<int32_t> ySlotType(progs.yOff.size(), 0);
-    DevPrograms dp = uploadPrograms(c, progs, ySlotType);
+    DevPrograms dp = uploadPrograms(c, progs, ySlotType, gp.colTypes);
+    // WHERE fully pushed: for edges whose storage filter ran, graphd's re-evaluation is implied
+    bool wIsP = pushHere && gp.where && encodeExpr(*gp.pushed) == encodeExpr(*gp.where);
+    // per-query straight-line kernels (jit.cpp); the interpreter kernels otherwise
+    const JitKernels* jk = nullptr;
+    const JitKernels* jkNoP = nullptr;                       // record hops before the last (no pushdown)
+    if (c->jitOn) {
+        JitQuery jq;
+        jq.P = JitProgram{progs.P >= 0 ? progs.code.data() + progs.P : nullptr, progs.P >= 0};
+        jq.W = JitProgram{progs.W >= 0 ? progs.code.data() + progs.W : nullptr, progs.W >= 0};
+        for (int32_t off : progs.yOff) jq.Y.push_back(JitProgram{progs.code.data() + off, true});
+        jq.yColType = gp.colTypes;
+        std::string jerr;
+        std::string src = jitSource(sp, jq);
+        if (!src.empty()) jk = c->jit.get(src, jerr);
+        if (jk && jq.P.present && recordFrom < steps) {
+            jq.P = JitProgram{};
+            std::string src2 = jitSource(sp, jq);
+            if (!src2.empty()) jkNoP = c->jit.get(src2, jerr);
+            if (!jkNoP) jk = nullptr;
+        } else {
+            jkNoP = jk;
+        }
+        if (!jk) c->jitNote = jerr.empty() ? "jit: unsupported program" : jerr;
+    }
+    // algorithmic-byte model inputs: k_f prop columns read by the filter, k_y yielded
+    uint64_t kf = 0, ky = 0;
+    {
+        PropRefs wr, yr;
+        if (gp.where) collectRefs(*gp.where, wr);
+        for (auto& y : gp.yields) collectRefs(*y, yr);
+        auto count = [](const PropRefs& r) {
+            uint64_t n = 0;
+            for (auto& ap : r.alias) n += (ap.second != "_src" && ap.second != "_dst" && ap.second != "_rank" && ap.second != "_type");
+            return n + r.srcTag.size() + r.dstTag.size();
+        };
+        kf = count(wr);
+        ky = count(yr);
+    }
 
+    if (p.result_on_device && p.distinct) return fail(c, NGX_E_UNSUPPORTED, "YIELD DISTINCT needs host results");
     // ---- seeds (starts_), routed by ID_HASH; duplicates kept unless DISTINCT (:123-129)
     std::vector<int64_t> starts(p.starts, p.starts + p.nstarts);
     if (p.distinct) {
@@ -858,13 +933,22 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             a.yCode = dp.code;
             a.yOff = dp.yOff;
             a.ySlotType = nullptr;
+            a.yColType = dp.yColType;
+            a.wIsP = (isFinal && wIsP) ? 1u : 0u;
+            const JitKernels* kj = isFinal ? jk : jkNoP;
             uint64_t* chunkOff = c->chunkOff.get<uint64_t>(chunks + 1);
-            uint64_t* ctiles = c->tileSums.get<uint64_t>((std::max<uint64_t>(nEnt, chunks) + kTile - 1) / kTile + 1);
-            (void)ctiles;
+            uint64_t* ctiles = c->tileSums.get<uint64_t>((chunks + kTile - 1) / kTile + 1);
             uint64_t* rowsThisHop = counters + 1;
-            c->timed("final_eval", E * 8 * (1 + 1), [&] {
-                if (launchFinal(a, chunkOff, c->tileSums.get<uint64_t>((chunks + kTile - 1) / kTile + 1), rowsThisHop, c->stream))
+            c->timed("final_eval", E * 8 * (2 + kf), [&] {
+                if (kj) {
+                    void* args[] = {&a};
+                    HIP_OK(hipModuleLaunchKernel(kj->eval, static_cast<unsigned>(chunks), 1, 1, 256, 1, 1, 0, c->stream, args, nullptr));
+                } else if (launchFinalEval(a, c->stream)) {
                     throw Error{NGX_E_DEVICE, "final eval"};
+                }
+            });
+            c->timed("chunk_scan", chunks * 12, [&] {
+                if (launchChunkScan(a, chunkOff, ctiles, rowsThisHop, c->stream)) throw Error{NGX_E_DEVICE, "chunk scan"};
             });
             uint64_t nrows = readScalar(c, rowsThisHop);
             uint64_t cap = totalRows + nrows;
@@ -889,16 +973,23 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             a.oType = static_cast<int32_t*>(c->oType.p) + totalRows;
             a.oEntry = nullptr;
             a.oCells = static_cast<OutCell*>(c->oCells.p) + totalRows * a.nY;
-            c->timed("final_emit", nrows * (32 + 8ull * a.nY), [&] {
-                if (launchEmit(a, chunkOff, c->stream)) throw Error{NGX_E_DEVICE, "final emit"};
+            c->timed("final_emit", 0, [&] {
+                if (kj) {
+                    const uint64_t* co = chunkOff;
+                    void* args[] = {&a, &co};
+                    HIP_OK(hipModuleLaunchKernel(kj->emit, static_cast<unsigned>(chunks), 1, 1, 256, 1, 1, 0, c->stream, args, nullptr));
+                } else if (launchEmit(a, chunkOff, c->stream)) {
+                    throw Error{NGX_E_DEVICE, "final emit"};
+                }
             });
+            c->addBytes("final_emit", nrows * (24 + 8 * ky));
             totalRows += nrows;
         }
         if (isFinal) break;
         // ---- expand to the next frontier (set of distinct dsts)
         uint8_t ep = nextEpoch(c);
         if (E) {
-            c->timed("expand", E * 8 + nEnt * 24, [&] {
+            c->timed("expand", E * 8, [&] {
                 if (launchExpandMark(F, estart, nEnt, E, hs, c->visited.get<uint8_t>(d.vglobal), ep, c->stream))
                     throw Error{NGX_E_DEVICE, "expand"};
             });
@@ -906,11 +997,12 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         if (c->world > 1) c->timed("exchange", 0, [&] { exchangeFrontier(c, d, ep); });
         uint32_t* Fn = (F == c->F0.p) ? c->F1.get<uint32_t>(std::max<uint64_t>(d.V, 1)) : c->F0.get<uint32_t>(std::max<uint64_t>(d.V, 1));
         uint64_t* tiles2 = c->tileSums.get<uint64_t>((std::max<uint64_t>(d.V, 1) + kTile - 1) / kTile + 1);
-        c->timed("compact", d.V, [&] {
+        c->timed("compact", 0, [&] {
             if (launchCompact(c->visited.get<uint8_t>(d.vglobal), d.gbase, d.V, ep, Fn, tiles2, counters + 2, c->stream))
                 throw Error{NGX_E_DEVICE, "compact"};
         });
         nF = readScalar(c, counters + 2);
+        c->addBytes("compact", nF * 8);
         R.hopNext.push_back(nF);
         F = Fn;
         if (nF == 0 && c->world == 1) break;                    // GO_EXIT: empty frontier
@@ -921,13 +1013,23 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     HIP_OK(hipEventElapsedTime(&ms, t0, t1));
     c->collectTimings();
     R.r.device_ms = ms;
-    uint32_t flags[2];
-    HIP_OK(hipMemcpy(flags, errFlag, 8, hipMemcpyDeviceToHost));
+    uint32_t flags[3];
+    HIP_OK(hipMemcpy(flags, errFlag, 12, hipMemcpyDeviceToHost));
     if (flags[1]) return fail(c, NGX_E_UNSUPPORTED, "an expression needs a host-only construct (string building or parsing)");
     if (flags[0]) return fail(c, NGX_E_QUERY, "an expression of WHERE / YIELD failed to evaluate");
+    if (flags[2]) return fail(c, NGX_E_QUERY, "YIELD value does not match its column type (boost::get)");
 
-    // ---- results to the host
     int32_t nY = static_cast<int32_t>(progs.yOff.size());
+    if (p.result_on_device) {                                 // rows stay in HBM (valid until the next call)
+        R.r.nrows = totalRows;
+        R.r.dev_src = static_cast<const int64_t*>(c->oSrc.p);
+        R.r.dev_dst = static_cast<const int64_t*>(c->oDst.p);
+        R.r.dev_rank = static_cast<const int64_t*>(c->oRank.p);
+        R.r.dev_type = static_cast<const int32_t*>(c->oType.p);
+        R.r.dev_cells = static_cast<const ngx_dev_cell*>(c->oCells.p);
+        return NGX_OK;
+    }
+    // ---- results to the host
     R.src.resize(totalRows); R.dst.resize(totalRows); R.rank.resize(totalRows); R.type.resize(totalRows);
     std::vector<OutCell> raw(totalRows * nY);
     if (totalRows) {

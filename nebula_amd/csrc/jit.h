@@ -1,0 +1,53 @@
+// Per-query final-hop kernels: WHERE / YIELD bytecode -> straight-line HIP C++ -> hipRTC -> module.
+//
+// The generated evaluator calls the same op helpers as the interpreter (vm.h) with the opcodes,
+// column types and constants as literals, so the type dispatch and the operand stack fold away and
+// the evaluation stays in registers. Kernels are cached per generated source; a compile failure
+// falls back to the precompiled interpreter kernels (still on the device).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "ngx_internal.h"
+
+namespace ngx {
+
+struct JitKernels {
+    hipModule_t mod = nullptr;
+    hipFunction_t eval = nullptr;
+    hipFunction_t emit = nullptr;
+};
+
+// one compiled program segment of a query: code[off ...] up to OP_END
+struct JitProgram {
+    const Insn* code = nullptr;     // host copy
+    bool present = false;
+};
+
+struct JitQuery {
+    JitProgram P, W;
+    std::vector<JitProgram> Y;
+    std::vector<int32_t> yColType;  // calculateExprType per column
+};
+
+class JitCache {
+public:
+    ~JitCache();
+    // nullptr when compilation failed (err set); compiled kernels are cached by source
+    const JitKernels* get(const std::string& source, std::string& err);
+    uint64_t compiled = 0, hits = 0, failed = 0;
+    double compileSeconds = 0;
+
+private:
+    std::map<std::string, JitKernels> cache_;
+    std::map<std::string, std::string> failures_;
+};
+
+// C++ source of the evaluator struct + kernels for one query on one space snapshot
+std::string jitSource(const Space& sp, const JitQuery& q);
+
+}  // namespace ngx

@@ -3,68 +3,9 @@
 
 #include <hip/hip_runtime.h>
 
-#include "vm.h"
+#include "kargs.h"
 
 namespace ngx {
-
-// the edge-type slots one hop expands (by value in kernel arguments)
-struct HopSlots {
-    int32_t n;
-    int32_t slotIdx[kMaxSlots];         // index into the DSlot table
-    int32_t etype[kMaxSlots];
-    const uint64_t* off[kMaxSlots];
-    const uint32_t* dgid[kMaxSlots];
-    const int64_t* dst[kMaxSlots];
-    const int64_t* rank[kMaxSlots];
-};
-
-struct OutCell {                        // raw VM value of one YIELD / return column
-    int64_t x;
-    uint32_t len;
-    uint8_t t;                          // V_*; 0xFF: no value (column of another edge type / no tag row)
-    uint8_t pad[3];
-};
-
-struct FinalArgs {
-    const uint32_t* F;                  // frontier rows
-    const uint64_t* estart;             // exclusive prefix of entry degrees, [nEnt] = E
-    uint64_t nEnt;
-    uint64_t E;
-    HopSlots hs;
-    const int64_t* vid;                 // vertex table (src vid of an edge)
-    uint64_t V;
-    uint64_t gbase;
-    VmEnv env;
-    const Insn* P;                      // pushed storage filter, nullptr if none
-    const Insn* W;                      // graphd WHERE, nullptr if none
-    uint32_t propsMask;                 // hop slot s reads rows (not onlyStructure)
-    int32_t ttlCol[kMaxSlots];          // TTL column of hop slot s, -1 if none
-    int64_t ttlDur[kMaxSlots];
-    int64_t now;
-    uint64_t* mask;                     // pass bits, 64 words per 4096-edge chunk
-    uint32_t* chunkCount;
-    uint32_t* err;                      // graphd evaluation error flag
-    int32_t nY;
-    const Insn* yCode;
-    const int32_t* yOff;
-    const int32_t* ySlotType;           // 0 = any type; else the column belongs to this signed type
-    int64_t* oSrc;
-    int64_t* oDst;
-    int64_t* oRank;
-    int32_t* oType;
-    uint32_t* oEntry;                   // frontier index of each row (GetNeighbors), may be null
-    OutCell* oCells;
-};
-
-struct VertexCellArgs {
-    const uint32_t* rows;
-    uint64_t n;
-    int32_t ncols;
-    const int32_t* tagSlot;             // per column: tag slot, -1 for non-tag columns
-    const int32_t* col;
-    VmEnv env;
-    OutCell* out;
-};
 
 int launchLookup(const int32_t* qpart, const int64_t* qvid, uint64_t n, const int32_t* vpart, const int64_t* vid,
                  uint64_t V, uint32_t* out, hipStream_t s);
@@ -75,12 +16,14 @@ int launchExpandMark(const uint32_t* F, const uint64_t* estart, uint64_t nEnt, u
                      uint8_t* visited, uint8_t epoch, hipStream_t s);
 int launchCompact(const uint8_t* visited, uint64_t gbase, uint64_t V, uint8_t epoch, uint32_t* outF,
                   uint64_t* tileSums, uint64_t* count, hipStream_t s);
+// final hop: eval (interpreter kernel), scan of the per-chunk pass counts, or both
+int launchFinalEval(const FinalArgs& a, hipStream_t s);
+int launchChunkScan(const FinalArgs& a, uint64_t* chunkOff, uint64_t* tileSums, uint64_t* total, hipStream_t s);
 int launchFinal(const FinalArgs& a, uint64_t* chunkOff, uint64_t* tileSums, uint64_t* total, hipStream_t s);
 int launchEmit(const FinalArgs& a, const uint64_t* chunkOff, hipStream_t s);
 int launchVertexCells(const VertexCellArgs& a, hipStream_t s);
 int launchPack(const uint8_t* visited, uint8_t epoch, uint64_t lo, uint64_t n, uint64_t* bits, hipStream_t s);
 int launchMerge(const uint64_t* bits, uint64_t n, uint8_t* visited, uint64_t lo, uint8_t epoch, hipStream_t s);
 
-constexpr uint64_t kTile = 4096;        // edges per expansion workgroup / items per scan tile
 
 }  // namespace ngx

@@ -3,7 +3,9 @@
 // (exprc.cpp) and the device VM executes per edge (kernels.hip).
 #pragma once
 
+#ifndef __HIPCC_RTC__
 #include <cstdint>
+#endif
 
 namespace ngx {
 

@@ -2,9 +2,17 @@
 // restating the reference evaluation rules exactly (src/common/filter/Expressions.cpp:662-1228,
 // FunctionManager.cpp:20-555): no short circuit, error propagation left-first, implicit casts
 // bool < int < double, |l - r| < 1e-8 double equality, int64 overflow and division errors.
+//
+// Each operation is a __forceinline__ helper with the opcode as an argument, shared by the
+// interpreter below (vmEval, kernels.hip) and by the straight-line evaluators jit.cpp generates per
+// query (compiled with hipRTC): there the opcodes and column types are literals and the type
+// dispatch folds away.
 #pragma once
 
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
+#include <cmath>
+#endif
 
 #include "ngx_device.h"
 
@@ -148,6 +156,273 @@ __device__ __forceinline__ bool mulOverflow(int64_t lv, int64_t rv) {    // Expr
     return false;
 }
 
-__device__ Val vmEval(const Insn* code, const VmEnv& env, const EdgeCtx& ec);
+// ------------------------------------------------------------------------------ loads
+template <int CT>                       // column type known at compile time (JIT)
+__device__ __forceinline__ Val loadColT(const DCol& c, uint64_t i) {
+    if constexpr (CT == 2 || CT == 21 || CT == 3) return mkInt(static_cast<const int64_t*>(c.data)[i]);
+    else if constexpr (CT == 4 || CT == 5) return mkDbl(static_cast<const double*>(c.data)[i]);
+    else if constexpr (CT == 1) return mkBool(static_cast<const uint8_t*>(c.data)[i] != 0);
+    else if constexpr (CT == 6) {
+        uint64_t o = c.soff[i];
+        return Val{reinterpret_cast<int64_t>(c.sbytes + o), static_cast<uint32_t>(c.soff[i + 1] - o), V_STR};
+    } else return mkErr();
+}
+template <int CT>
+__device__ __forceinline__ Val defaultOfTypeT() {
+    if constexpr (CT == 1) return mkBool(false);
+    else if constexpr (CT == 4 || CT == 5) return mkDbl(0.0);
+    else if constexpr (CT == 6) return Val{0, 0, V_STR};
+    else return mkInt(0);
+}
+
+// OP_ECOL: edge column a of |type| b; mode bit0 mismatch -> dflt, bit1 missing field -> type default
+template <int CT>
+__device__ __forceinline__ Val opEcolT(const VmEnv& env, const EdgeCtx& ec, int32_t a, int32_t b, uint8_t mode, Val dflt) {
+    int32_t at = ec.etype < 0 ? -ec.etype : ec.etype;
+    if (at != b) return (mode & 1) ? dflt : mkErr();
+    const DCol& c = env.cols[env.slots[ec.slot].colBase + a];
+    if (c.valid != nullptr && c.valid[ec.pos] == 0) return (mode & 2) ? defaultOfTypeT<CT>() : mkErr();
+    return loadColT<CT>(c, ec.pos);
+}
+__device__ __forceinline__ Val opEcol(const VmEnv& env, const EdgeCtx& ec, int32_t a, int32_t b, uint8_t mode, Val dflt) {
+    int32_t at = ec.etype < 0 ? -ec.etype : ec.etype;
+    if (at != b) return (mode & 1) ? dflt : mkErr();
+    const DCol& c = env.cols[env.slots[ec.slot].colBase + a];
+    if (c.valid != nullptr && c.valid[ec.pos] == 0) return (mode & 2) ? defaultOfType(c.type) : mkErr();
+    return loadCol(c, ec.pos);
+}
+// OP_EKEY: key prop a (0 src, 1 dst, 2 rank, 3 type) of alias type b (0: any)
+__device__ __forceinline__ Val opEkey(const EdgeCtx& ec, int32_t a, int32_t b, uint8_t mode, Val dflt) {
+    int32_t at = ec.etype < 0 ? -ec.etype : ec.etype;
+    if (b != 0 && at != b) return (mode & 1) ? dflt : mkErr();
+    return mkInt(a == 0 ? ec.src : a == 1 ? ec.dst : a == 2 ? ec.rank : static_cast<int64_t>(ec.etype));
+}
+__device__ __forceinline__ Val opEdst(const EdgeCtx& ec, int32_t b) {
+    int32_t at = ec.etype < 0 ? -ec.etype : ec.etype;
+    return mkInt((b != 0 && at != b) ? 0 : ec.dst);
+}
+// OP_SRCTAG / OP_DSTTAG: column a of tag slot b for the src / dst row
+template <int CT>
+__device__ __forceinline__ Val opTagT(const VmEnv& env, uint32_t row, int32_t a, int32_t b, uint8_t mode, Val dflt) {
+    const DTag& t = env.tags[b];
+    if (row == kNoRow || t.present[row] == 0) return (mode & 1) ? dflt : mkErr();
+    const DCol& c = env.cols[t.colBase + a];
+    if (c.valid != nullptr && c.valid[row] == 0) return defaultOfTypeT<CT>();
+    return loadColT<CT>(c, row);
+}
+__device__ __forceinline__ Val opTag(const VmEnv& env, uint32_t row, int32_t a, int32_t b, uint8_t mode, Val dflt) {
+    const DTag& t = env.tags[b];
+    if (row == kNoRow || t.present[row] == 0) return (mode & 1) ? dflt : mkErr();
+    const DCol& c = env.cols[t.colBase + a];
+    if (c.valid != nullptr && c.valid[row] == 0) return defaultOfType(c.type);
+    return loadCol(c, row);
+}
+
+// ------------------------------------------------------------------------------ unary / cast
+__device__ __forceinline__ Val opNeg(Val v) {              // UnaryExpression NEGATE
+    if (v.t == V_INT) { v.x = static_cast<int64_t>(0ULL - static_cast<uint64_t>(v.x)); return v; }
+    if (v.t == V_DBL) return mkDbl(-dblOf(v));
+    return mkErr();
+}
+__device__ __forceinline__ Val opNot(Val v) { return v.t == V_ERR ? v : mkBool(!asBool(v)); }
+// TypeCastingExpression::eval; t1 = ColumnType (INT 0, STRING 1, DOUBLE 2, BOOL 3, TIMESTAMP 4)
+__device__ __forceinline__ Val opCast(Val v, uint8_t t1, const VmEnv& env) {
+    if (v.t == V_ERR) return v;
+    if (v.t == V_STR) {                                    // folly::to<int/double>(string): host only
+        if (t1 != 3) { atomicOr(env.unsupported, 1u); return mkErr(); }
+        return mkBool(asBool(v));
+    }
+    if (t1 == 0 || t1 == 4) return mkInt(toInt(v));
+    if (t1 == 2) return mkDbl(toDouble(v));
+    return mkBool(asBool(v));
+}
+
+// ------------------------------------------------------------------------------ arithmetic
+__device__ __forceinline__ Val opArith(uint8_t op, Val l, Val r, const VmEnv& env) {
+    if (l.t == V_ERR) return l;
+    if (r.t == V_ERR) return r;
+    if ((l.t == V_INT || l.t == V_DBL) && (r.t == V_INT || r.t == V_DBL)) {
+        if (l.t == V_DBL || r.t == V_DBL) {
+            double a = asDouble(l), b = asDouble(r);
+            switch (op) {
+                case OP_ADD: return mkDbl(a + b);
+                case OP_SUB: return mkDbl(a - b);
+                case OP_MUL: return mkDbl(a * b);
+                case OP_DIV: return fabs(b) < 1e-8 ? mkErr() : mkDbl(a / b);
+                case OP_MOD: return fabs(b) < 1e-8 ? mkErr() : mkDbl(fmod(a, b));
+                default: return mkInt(static_cast<int64_t>(round(a)) ^ static_cast<int64_t>(round(b)));
+            }
+        }
+        int64_t a = l.x, b = r.x;
+        switch (op) {
+            case OP_ADD: {
+                bool of = (a >= 0 && b >= 0) ? (INT64_MAX - a < b) : (a < 0 && b < 0) ? (INT64_MIN - a > b) : false;
+                return of ? mkErr() : mkInt(a + b);
+            }
+            case OP_SUB: {
+                bool of = (a > 0 && b < 0) ? (b == INT64_MIN || INT64_MAX - a < -b)
+                        : (a < 0 && b > 0) ? (INT64_MIN - a > -b) : false;
+                return of ? mkErr() : mkInt(a - b);
+            }
+            case OP_MUL:
+                return mulOverflow(a, b) ? mkErr()
+                     : mkInt(static_cast<int64_t>(static_cast<uint64_t>(a) * static_cast<uint64_t>(b)));
+            case OP_DIV: return (b == 0 || (a == INT64_MIN && b == -1)) ? mkErr() : mkInt(a / b);
+            case OP_MOD: return b == 0 ? mkErr() : (b == -1 ? mkInt(0) : mkInt(a % b));
+            default: return mkInt(a ^ b);
+        }
+    }
+    if (op == OP_ADD && l.t == V_STR && r.t == V_STR) atomicOr(env.unsupported, 1u);   // builds a string
+    return mkErr();
+}
+
+// ------------------------------------------------------------------------------ relational / logical
+__device__ __forceinline__ Val opRel(uint8_t op, Val l, Val r) {
+    if (l.t == V_ERR) return l;
+    if (r.t == V_ERR) return r;
+    if (op == OP_CONTAINS) return (l.t == V_STR && r.t == V_STR) ? mkBool(strContains(l, r)) : mkErr();
+    if ((l.t == V_STR) != (r.t == V_STR)) return mkErr();  // string vs non-string
+    int c;                                                 // -1 / 0 / 1, 2 = unordered (NaN)
+    bool eqOnly = false, eqv = false;
+    if (l.t == V_STR) {
+        c = strCmp(l, r);
+    } else if (l.t == V_DBL || r.t == V_DBL) {
+        double a = toDouble(l), b = toDouble(r);
+        c = a < b ? -1 : (a > b ? 1 : (a == b ? 0 : 2));
+        if (op == OP_EQ || op == OP_NE) { eqOnly = true; eqv = fabs(a - b) < 1e-8; }
+    } else if (l.t == V_INT || r.t == V_INT) {
+        int64_t a = toInt(l), b = toInt(r);
+        c = a < b ? -1 : (a > b ? 1 : 0);
+    } else {                                               // bool vs bool
+        c = l.x < r.x ? -1 : (l.x > r.x ? 1 : 0);
+    }
+    switch (op) {
+        case OP_LT: return mkBool(c == -1);
+        case OP_LE: return mkBool(c == -1 || c == 0);
+        case OP_GT: return mkBool(c == 1);
+        case OP_GE: return mkBool(c == 1 || c == 0);
+        case OP_EQ: return mkBool(eqOnly ? eqv : c == 0);
+        default: return mkBool(eqOnly ? !eqv : c != 0);
+    }
+}
+__device__ __forceinline__ Val opLogic(uint8_t op, Val l, Val r) {
+    if (l.t == V_ERR) return l;
+    if (r.t == V_ERR) return r;
+    bool a = asBool(l), b = asBool(r);
+    return mkBool(op == OP_AND ? (a && b) : op == OP_OR ? (a || b) : (a != b));
+}
+
+// ------------------------------------------------------------------------------ functions
+__device__ __forceinline__ Val opFunc(int32_t fid, const Val* args, int argc, const VmEnv& env) {
+    for (int k = 0; k < argc; k++) if (args[k].t == V_ERR) return args[k];
+    bool num1 = args[0].t == V_INT || args[0].t == V_DBL;
+    switch (fid) {
+        case F_ABS: return num1 ? mkDbl(fabs(asDouble(args[0]))) : mkErr();
+        case F_FLOOR: return num1 ? mkDbl(floor(asDouble(args[0]))) : mkErr();
+        case F_CEIL: return num1 ? mkDbl(ceil(asDouble(args[0]))) : mkErr();
+        case F_ROUND: return num1 ? mkDbl(round(asDouble(args[0]))) : mkErr();
+        case F_SQRT: return num1 ? mkDbl(sqrt(asDouble(args[0]))) : mkErr();
+        case F_CBRT: return num1 ? mkDbl(cbrt(asDouble(args[0]))) : mkErr();
+        case F_EXP: return num1 ? mkDbl(exp(asDouble(args[0]))) : mkErr();
+        case F_EXP2: return num1 ? mkDbl(exp2(asDouble(args[0]))) : mkErr();
+        case F_LOG: return num1 ? mkDbl(log(asDouble(args[0]))) : mkErr();
+        case F_LOG2: return num1 ? mkDbl(log2(asDouble(args[0]))) : mkErr();
+        case F_LOG10: return num1 ? mkDbl(log10(asDouble(args[0]))) : mkErr();
+        case F_SIN: return num1 ? mkDbl(sin(asDouble(args[0]))) : mkErr();
+        case F_ASIN: return num1 ? mkDbl(asin(asDouble(args[0]))) : mkErr();
+        case F_COS: return num1 ? mkDbl(cos(asDouble(args[0]))) : mkErr();
+        case F_ACOS: return num1 ? mkDbl(acos(asDouble(args[0]))) : mkErr();
+        case F_TAN: return num1 ? mkDbl(tan(asDouble(args[0]))) : mkErr();
+        case F_ATAN: return num1 ? mkDbl(atan(asDouble(args[0]))) : mkErr();
+        case F_HYPOT: case F_POW: {
+            bool num2 = args[1].t == V_INT || args[1].t == V_DBL;
+            if (!(num1 && num2)) return mkErr();
+            double a = asDouble(args[0]), b = asDouble(args[1]);
+            return mkDbl(fid == F_HYPOT ? hypot(a, b) : pow(a, b));
+        }
+        case F_LENGTH: return args[0].t == V_STR ? mkInt(args[0].len) : mkErr();
+        case F_STRCASECMP: {
+            if (!(args[0].t == V_STR && args[1].t == V_STR)) return mkErr();
+            const unsigned char* p = reinterpret_cast<const unsigned char*>(args[0].x);     // C strings: stop at NUL
+            const unsigned char* q = reinterpret_cast<const unsigned char*>(args[1].x);
+            for (uint32_t k = 0;; k++) {
+                int c1 = k < args[0].len ? p[k] : 0;
+                int c2 = k < args[1].len ? q[k] : 0;
+                if (c1 >= 'A' && c1 <= 'Z') c1 += 32;
+                if (c2 >= 'A' && c2 <= 'Z') c2 += 32;
+                if (c1 != c2 || c1 == 0) return mkInt(c1 - c2);
+            }
+        }
+        case F_HASH: {
+            const Val& a = args[0];
+            if (a.t == V_INT || a.t == V_BOOL) return mkInt(a.x);
+            if (a.t == V_DBL) {
+                double d = dblOf(a);
+                return mkInt(d != 0.0 ? static_cast<int64_t>(hashBytes(reinterpret_cast<const unsigned char*>(&d), 8)) : 0);
+            }
+            return mkInt(static_cast<int64_t>(hashBytes(reinterpret_cast<const unsigned char*>(a.x), a.len)));
+        }
+        case F_UDF_IS_IN: {                                // FunctionManager.cpp:467-513
+            const Val& c = args[0];
+            bool found = false;
+            for (int k = 1; k < argc && !found; k++) {
+                const Val& v = args[k];
+                if (c.t == V_INT) {
+                    if (v.t == V_STR) { atomicOr(env.unsupported, 1u); break; }
+                    found = toInt(v) == c.x;
+                } else if (c.t == V_DBL) {
+                    if (v.t == V_STR) { atomicOr(env.unsupported, 1u); break; }
+                    found = toDouble(v) == dblOf(c);
+                } else if (c.t == V_BOOL) {
+                    found = asBool(v) == (c.x != 0);
+                } else {
+                    if (v.t != V_STR) { atomicOr(env.unsupported, 1u); break; }   // toString
+                    found = strCmp(c, v) == 0;
+                }
+            }
+            return mkBool(found);
+        }
+        default: return mkErr();
+    }
+}
+
+// ------------------------------------------------------------------------------ interpreter
+static __device__ __noinline__ Val vmEval(const Insn* code, const VmEnv& env, const EdgeCtx& ec) {
+    Val st[kMaxStack];
+    int sp = 0;
+    for (int pc = 0;; pc++) {
+        const Insn in = code[pc];
+        switch (in.op) {
+            case OP_END: return sp > 0 ? st[sp - 1] : mkErr();
+            case OP_PUSH: st[sp++] = constVal(in.t1, in.imm, static_cast<uint32_t>(in.a), env.pool); break;
+            case OP_ERR: st[sp++] = mkErr(); break;
+            case OP_ECOL: st[sp++] = opEcol(env, ec, in.a, in.b, in.mode, constVal(in.t2, in.imm, 0, env.pool)); break;
+            case OP_EKEY: st[sp++] = opEkey(ec, in.a, in.b, in.mode, constVal(in.t2, in.imm, 0, env.pool)); break;
+            case OP_EDST: st[sp++] = opEdst(ec, in.b); break;
+            case OP_SRCTAG: case OP_DSTTAG:
+                st[sp++] = opTag(env, in.op == OP_SRCTAG ? ec.srow : ec.drow, in.a, in.b, in.mode,
+                                 constVal(in.t2, in.imm, 0, env.pool));
+                break;
+            case OP_PLUS: break;
+            case OP_NEG: st[sp - 1] = opNeg(st[sp - 1]); break;
+            case OP_NOT: st[sp - 1] = opNot(st[sp - 1]); break;
+            case OP_CAST: st[sp - 1] = opCast(st[sp - 1], in.t1, env); break;
+            case OP_ADD: case OP_SUB: case OP_MUL: case OP_DIV: case OP_MOD: case OP_AXOR:
+                sp--; st[sp - 1] = opArith(in.op, st[sp - 1], st[sp], env); break;
+            case OP_LT: case OP_LE: case OP_GT: case OP_GE: case OP_EQ: case OP_NE: case OP_CONTAINS:
+                sp--; st[sp - 1] = opRel(in.op, st[sp - 1], st[sp]); break;
+            case OP_AND: case OP_OR: case OP_LXOR:
+                sp--; st[sp - 1] = opLogic(in.op, st[sp - 1], st[sp]); break;
+            case OP_FUNC: {
+                int argc = in.b;
+                Val out = opFunc(in.a, &st[sp - argc], argc, env);
+                sp -= argc;
+                st[sp++] = out;
+                break;
+            }
+            default: return mkErr();
+        }
+    }
+}
 
 }  // namespace ngx

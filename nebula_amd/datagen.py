@@ -46,6 +46,8 @@ def lib():
         L.ngd_snb.restype = i32
         L.ngd_free.argtypes = [R]
         L.ngd_sample_vids.argtypes = [u64, u64, u64, ctypes.c_void_p]
+        L.ngd_rmat_seeds.argtypes = [i32, i32, dbl, dbl, dbl, u64, u64, u64, i32, ctypes.c_void_p]
+        L.ngd_rmat_seeds.restype = i32
         _lib = L
     return _lib
 
@@ -125,6 +127,17 @@ def snb(np_: int, knows_deg: int = 20, nposts: int = 0, likes_deg: int = 10, see
 def sample_vids(seed: int, rng: int, k: int) -> np.ndarray:
     out = np.zeros(k, dtype=np.int64)
     lib().ngd_sample_vids(seed, rng, k, out.ctypes.data)
+    return out
+
+
+def rmat_seeds(scale: int, k: int, ef: int = 16, seed: int = 42, sample_seed: int = 42, threads: int = 0,
+               abc=GRAPH500) -> np.ndarray:
+    """k vids sampled uniformly from the RMAT vertices that have out-edges."""
+    out = np.zeros(k, dtype=np.int64)
+    rc = lib().ngd_rmat_seeds(scale, ef, abc[0], abc[1], abc[2], seed, sample_seed, k, _threads(threads),
+                              out.ctypes.data)
+    if rc:
+        raise ValueError("could not sample seeds")
     return out
 
 

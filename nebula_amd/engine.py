@@ -88,7 +88,7 @@ class GoPlan(ctypes.Structure):
                 ("over_aliases", P(ctypes.c_char_p)), ("over_all", c_i32), ("direction", c_i32),
                 ("where", ctypes.c_char_p), ("where_len", c_u32), ("nyields", c_i32),
                 ("yields", P(ctypes.c_char_p)), ("yield_lens", P(c_u32)), ("distinct", c_i32),
-                ("filter_pushdown", c_i32), ("now_sec", c_i64)]
+                ("filter_pushdown", c_i32), ("now_sec", c_i64), ("result_on_device", c_i32)]
 
 
 class GoResultC(ctypes.Structure):
@@ -96,7 +96,8 @@ class GoResultC(ctypes.Structure):
                 ("row_src", P(c_i64)), ("row_dst", P(c_i64)), ("row_rank", P(c_i64)), ("row_type", P(c_i32)),
                 ("strings", ctypes.c_void_p), ("strings_len", c_u64), ("nhops", c_i32),
                 ("hop_frontier", P(c_u64)), ("hop_edges", P(c_u64)), ("hop_next", P(c_u64)),
-                ("device_ms", c_dbl)]
+                ("device_ms", c_dbl), ("dev_src", ctypes.c_void_p), ("dev_dst", ctypes.c_void_p),
+                ("dev_rank", ctypes.c_void_p), ("dev_type", ctypes.c_void_p), ("dev_cells", ctypes.c_void_p)]
 
 
 class KernelStat(ctypes.Structure):
@@ -121,6 +122,9 @@ SIGNATURES = {
     "ngx_go_result_free": (None, [P(GoResultC)]),
     "ngx_set_profiling": (c_i32, [ctypes.c_void_p, c_i32]),
     "ngx_kernel_stats": (c_i32, [ctypes.c_void_p, P(P(KernelStat)), P(c_i32)]),
+    "ngx_set_flag": (c_i32, [ctypes.c_void_p, ctypes.c_char_p, c_i64]),
+    "ngx_get_flag": (c_i32, [ctypes.c_void_p, ctypes.c_char_p, P(c_i64)]),
+    "ngx_jit_note": (ctypes.c_char_p, [ctypes.c_void_p]),
     "ngx_hash_string": (c_i64, [ctypes.c_char_p, c_u64]),
 }
 
@@ -189,6 +193,7 @@ class GoResult:
     hop_edges: List[int] = field(default_factory=list)
     hop_next: List[int] = field(default_factory=list)
     device_ms: float = 0.0
+    nrows: int = 0
 
 
 @dataclass
@@ -298,7 +303,9 @@ class Engine:
 
     # ---- GO
     def go(self, space: int, s: Union[str, ngql.GoSentence], pushdown: bool = True, now_sec: int = 0,
-           raise_on_error: bool = False, rows: bool = True) -> GoResult:
+           raise_on_error: bool = False, rows: bool = True, on_device: bool = False) -> GoResult:
+        """Run one GO. rows=False skips decoding cells into Python tuples; on_device=True leaves the
+        result rows in HBM (GoResult.nrows and the statistics only)."""
         if isinstance(s, str):
             s = ngql.parse_go(s)
         starts = np.array(s.vids, dtype=np.int64)
@@ -310,7 +317,8 @@ class Engine:
         ylen = (c_u32 * max(1, len(yb)))(*[len(y) for y in yb])
         plan = GoPlan(space, s.record_from, s.record_to, len(starts), starts.ctypes.data_as(P(c_i64)), len(s.over),
                       names, aliases, 1 if s.over_all else 0, s.direction, where if where else None, len(where),
-                      len(yb), yarr, ylen, 1 if s.distinct else 0, 1 if pushdown else 0, now_sec)
+                      len(yb), yarr, ylen, 1 if s.distinct else 0, 1 if pushdown else 0, now_sec,
+                      1 if on_device else 0)
         out = P(GoResultC)()
         rc = self.L.ngx_go(self.h, ctypes.byref(plan), ctypes.byref(out))
         try:
@@ -320,6 +328,11 @@ class Engine:
                 raise EngineError(rc, err)
             strings = ctypes.string_at(r.strings, r.strings_len) if r.strings_len else b""
             n = r.nrows
+            if on_device:
+                return GoResult(ok=rc == 0, error=err, code=rc, col_types=[r.col_types[i] for i in range(r.ncols)],
+                                rows=[], nrows=n, hop_frontier=[r.hop_frontier[i] for i in range(r.nhops)],
+                                hop_edges=[r.hop_edges[i] for i in range(r.nhops)],
+                                hop_next=[r.hop_next[i] for i in range(r.nhops)], device_ms=r.device_ms)
             res = GoResult(
                 ok=rc == 0, error=err, code=rc, col_types=[r.col_types[i] for i in range(r.ncols)],
                 rows=_cells(r.cells, n, r.ncols, strings) if rows else [],
@@ -327,10 +340,22 @@ class Engine:
                 rank=_arr(r.row_rank, n, np.int64), etype=_arr(r.row_type, n, np.int32),
                 hop_frontier=[r.hop_frontier[i] for i in range(r.nhops)],
                 hop_edges=[r.hop_edges[i] for i in range(r.nhops)],
-                hop_next=[r.hop_next[i] for i in range(r.nhops)], device_ms=r.device_ms)
+                hop_next=[r.hop_next[i] for i in range(r.nhops)], device_ms=r.device_ms, nrows=n)
             return res
         finally:
             self.L.ngx_go_result_free(out)
+
+    # ---- flags
+    def set_flag(self, name: str, value: int):
+        self._check(self.L.ngx_set_flag(self.h, name.encode(), int(value)), "set_flag")
+
+    def get_flag(self, name: str) -> int:
+        v = c_i64()
+        self._check(self.L.ngx_get_flag(self.h, name.encode(), ctypes.byref(v)), "get_flag")
+        return v.value
+
+    def jit_note(self) -> str:
+        return self.L.ngx_jit_note(self.h).decode()
 
     # ---- measurement
     def set_profiling(self, on: bool):

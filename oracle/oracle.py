@@ -211,6 +211,8 @@ class GoResult:
     rows: List[tuple]
     hop_frontier: List[int] = field(default_factory=list)
     hop_scanned: List[int] = field(default_factory=list)
+    seconds: float = 0.0                 # wall time of the restated GoExecutor run (no serialisation)
+    nrows: int = 0
 
 
 def _cell(r: _Rd):
@@ -320,7 +322,7 @@ class Oracle:
             verts.append({"vid": vid, "tags": tags, "edges": edata})
         return NeighborsResponse(failed, vs, es, verts, r.get("i"))
 
-    def go(self, space: int, s, pushdown=True) -> GoResult:
+    def go(self, space: int, s, pushdown=True, rows=True) -> GoResult:
         """Run a parsed nebula_amd.ngql.GoSentence through the restated GoExecutor."""
         b = struct.pack("<IIi", s.record_from, s.record_to, len(s.vids)) + struct.pack(f"<{len(s.vids)}q", *s.vids)
         b += struct.pack("<i", len(s.over))
@@ -331,17 +333,17 @@ class Oracle:
         b += struct.pack("<Bi", 1 if s.distinct else 0, len(s.yields))
         for y in s.yields:
             b += _s(y.expr.encode()) + _s(y.alias)
-        b += struct.pack("<B", 1 if pushdown else 0)
+        b += struct.pack("<BB", 1 if pushdown else 0, 0 if rows else 1)
         r = _Rd(_call(self.L.orc_go, self.h, space, b, len(b)))
         ok = r.get("B") == 1
         err = r.str().decode()
         ncol = r.get("i")
         types = [r.get("i") for _ in range(ncol)]
         nrows = r.get("q")
-        rows = [tuple(_cell(r) for _ in range(ncol)) for _ in range(nrows)]
+        out = [tuple(_cell(r) for _ in range(ncol)) for _ in range(nrows)] if rows else []
         hops = r.get("i")
         fr, sc = [], []
         for _ in range(hops):
             fr.append(r.get("q"))
             sc.append(r.get("q"))
-        return GoResult(ok, err, types, rows, fr, sc)
+        return GoResult(ok, err, types, out, fr, sc, r.get("d"), nrows)

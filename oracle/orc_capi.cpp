@@ -1,3 +1,4 @@
+#include <chrono>
 // ORACLE — TEST INFRASTRUCTURE ONLY (see orc_core.h header).
 // extern "C" surface used by oracle/oracle.py (ctypes). Requests arrive as little-endian blobs
 // built by the Python side; responses are returned as blobs the Python side decodes. Response
@@ -213,13 +214,17 @@ char* orc_go(void* e, int32_t space, const uint8_t* blob, uint64_t len, uint64_t
     for (int32_t i = 0; i < ny; i++) { auto x = r.str(); auto a = r.str(); s.yields.push_back({x, a}); }
     GoFlags f;
     f.filter_pushdown = r.get<uint8_t>() != 0;
+    bool countOnly = r.p < r.e && r.get<uint8_t>() != 0;
+    auto t0 = std::chrono::steady_clock::now();
     auto res = runGo(*eng, space, s, f);
+    double seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     Writer w;
     w.put<uint8_t>(res.ok ? 1 : 0);
     w.str(res.error);
     w.put<int32_t>(static_cast<int32_t>(res.colTypes.size()));
     for (auto t : res.colTypes) w.put<int32_t>(t);
     w.put<int64_t>(static_cast<int64_t>(res.rows.size()));
+    if (countOnly) res.rows.clear();
     for (auto& row : res.rows) {
         for (size_t c = 0; c < row.size(); c++) {
             cell(w, c < res.colTypes.size() ? res.colTypes[c] : UNKNOWN, row[c]);
@@ -230,6 +235,7 @@ char* orc_go(void* e, int32_t space, const uint8_t* blob, uint64_t len, uint64_t
         w.put<int64_t>(res.hopFrontier[i]);
         w.put<int64_t>(res.hopScanned[i]);
     }
+    w.put<double>(seconds);
     return toHeap(w.b, outLen);
 }
 

@@ -21,14 +21,29 @@ from tests.golden.gotest_cases import CASES
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def nba():
+def _engine(mode):
+    """An engine on device 0 running the final hop through per-query hipRTC kernels ("jit") or the
+    precompiled bytecode interpreter ("vm")."""
+    e = engine.Engine(0)
+    e.set_flag("jit", 1 if mode == "jit" else 0)
+    return e
+
+
+def _check_jit(e, mode):
+    if mode == "jit":
+        assert e.get_flag("jit_failed") == 0, e.jit_note()
+        assert e.jit_note() == ""
+
+
+@pytest.fixture(scope="module", params=["jit", "vm"])
+def nba(request):
     ds = fixtures.nba()
     o = oracle.Oracle()
     ds.load_oracle(o)
-    e = engine.Engine(0)
+    e = _engine(request.param)
     ds.load_engine(e)
     yield ds, o, e
+    _check_jit(e, request.param)
     e.close()
 
 
@@ -57,7 +72,7 @@ def qb():
     ds = fixtures.querybound()
     o = oracle.Oracle()
     ds.load_oracle(o)
-    e = engine.Engine(0)
+    e = _engine("vm")
     ds.load_engine(e)
     yield o, e
     e.close()
@@ -175,15 +190,16 @@ RMAT_QUERIES = [
 ]
 
 
-@pytest.fixture(scope="module")
-def rmat():
+@pytest.fixture(scope="module", params=["jit", "vm"])
+def rmat(request):
     ds = fixtures.RmatDataset(12, with_in=True, with_tag=True)
     o = oracle.Oracle()
     o.set_flags(threads=8)
     ds.load_oracle(o)
-    e = engine.Engine(0)
+    e = _engine(request.param)
     ds.load_engine(e)
     yield ds, o, e
+    _check_jit(e, request.param)
     e.close()
 
 
@@ -206,6 +222,16 @@ def test_rmat_go(rmat, qi, pushdown):
     assert a == b
     # TEPS numerator: edges scanned per hop agree with the restated storage scan
     assert got.hop_edges[:len(ref.hop_scanned)] == ref.hop_scanned[:len(got.hop_edges)]
+
+
+def test_rmat_device_results(rmat):
+    """result_on_device leaves the rows in HBM: same row count and hop statistics as the host path."""
+    ds, o, e = rmat
+    seeds = datagen.sample_vids(77, 1 << ds.scale, 40)
+    s = ngql.parse_go(RMAT_QUERIES[0].replace("{S}", ", ".join(str(int(v)) for v in seeds)))
+    host = e.go(ds.space, s)
+    dev = e.go(ds.space, s, on_device=True)
+    assert dev.ok and dev.nrows == len(host.rows) and dev.hop_edges == host.hop_edges
 
 
 def test_rmat_empty_and_missing_seeds(rmat):
