@@ -90,8 +90,8 @@ def main():
 
     plans = [sentence(i, args.seeds) for i in range(args.warmup + args.steps)]
 
-    def step(s):
-        r = eng.go(datagen.RMAT_SPACE, s, rows=False)
+    def step(s, on_device=True):
+        r = eng.go(datagen.RMAT_SPACE, s, rows=False, on_device=on_device)
         if not r.ok:
             raise RuntimeError(r.error)
         return r
@@ -114,7 +114,7 @@ def main():
     for i in range(args.steps):
         r = step(plans[args.warmup + i])
         edges += sum(r.hop_edges)
-        result_rows += len(r.src)
+        result_rows += r.nrows
         dev_ms += r.device_ms
         hop_edges = r.hop_edges
     torch.cuda.synchronize()
@@ -122,6 +122,16 @@ def main():
     elapsed = time.perf_counter() - t_start
     stats = eng.kernel_stats()
     eng.set_profiling(False)
+    # the same steps with the result rows and typed cells delivered to host memory (reported only)
+    host_steps = min(2, args.steps)
+    barrier()
+    t_h = time.perf_counter()
+    for i in range(host_steps):
+        step(plans[args.warmup + i], on_device=False)
+    barrier()
+    host_ms = (time.perf_counter() - t_h) * 1e3 / max(host_steps, 1)
+    jit = {"compiled": eng.get_flag("jit_compiled"), "failed": eng.get_flag("jit_failed"),
+           "compile_ms": eng.get_flag("jit_compile_us") / 1e3, "note": eng.jit_note()}
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -175,6 +185,10 @@ def main():
             "rows_per_step": result_rows // args.steps,
             "hop_edges_last_step": hop_edges,
             "device_ms_per_step": round(dev_ms / args.steps, 3),
+            "ms_per_step_host_rows": round(host_ms, 3),
+            "timed_region": "seeds on host -> result rows + YIELD cells in HBM (result_on_device); "
+                            "ms_per_step_host_rows adds D2H and host cell conversion",
+            "jit": jit,
             "path_roofline": {"algo_bytes": all_bytes, "kernel_ms": round(all_ms, 3),
                               "frac": round(all_bytes / (all_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if all_ms else None},
             "kernels": {k: {"launches": v[0], "ms": round(v[1], 3), "algo_bytes": v[2]} for k, v in stats.items()},
