@@ -186,14 +186,19 @@ typedef struct {
     int32_t result_on_device;          /* 1: leave rows in HBM (dev_* below), no host cells / DISTINCT */
 } ngx_go_plan;
 
-/* Raw device value of one YIELD cell (result_on_device): type 1 int, 2 double (bits in x),
- * 3 bool, 4 string (x = device pointer into the snapshot / program pool, len bytes), 0xFF none. */
+/* One YIELD column of a device-resident result (result_on_device), columnar in HBM, nrows entries:
+ *   x     value bits per row: int, double bits, bool 0/1, or a device pointer to string bytes
+ *         (into the snapshot or the query's constant pool)
+ *   len   string byte lengths; NULL when the column holds no strings (its static type is not STRING
+ *         and not UNKNOWN)
+ *   type  per-row value type (1 int, 2 double, 3 bool, 4 string); NULL when every row has the
+ *         column's static type col_types[c] (a row of another type fails the query, as boost::get
+ *         in GoExecutor::toThriftResponse does), i.e. non-NULL only for UNKNOWN-typed columns */
 typedef struct {
-    int64_t x;
-    uint32_t len;
-    uint8_t type;
-    uint8_t pad[3];
-} ngx_dev_cell;
+    const int64_t* x;
+    const uint32_t* len;
+    const uint8_t* type;
+} ngx_dev_column;
 
 typedef struct {
     int32_t code;                      /* NGX_OK or an error (message in ngx_last_error) */
@@ -218,11 +223,15 @@ typedef struct {
     const int64_t* dev_dst;
     const int64_t* dev_rank;
     const int32_t* dev_type;
-    const ngx_dev_cell* dev_cells;     /* [row * ncols + col] */
+    const ngx_dev_column* dev_cols;    /* ncols columns */
 } ngx_go_result;
 
 int32_t ngx_go(ngx_ctx* ctx, const ngx_go_plan* plan, ngx_go_result** out);
 void ngx_go_result_free(ngx_go_result* r);
+
+/* Copy `bytes` from device memory of this context (e.g. a result_on_device array) to host memory,
+ * ordered after the context's work. */
+int32_t ngx_device_to_host(ngx_ctx* ctx, void* dst, const void* src, uint64_t bytes);
 
 /* ---------------------------------------------------------------- measurement hooks */
 /* Per-kernel device times of the last ngx_go (HIP events on the engine stream), for bench.py. */

@@ -93,8 +93,11 @@ struct ngx_ctx {
     std::string lastError;
     std::mutex mu;
     // scratch
-    DBuf visited, F0, F1, estart, tileSums, counters, mask, chunkCount, chunkOff, seedPart, seedVid;
-    DBuf oSrc, oDst, oRank, oType, oEntry, oCells, progBuf, sendBits, recvBits, vcells, misc;
+    DBuf visited, F0, F1, estart, chunkFirst, tileSums, counters, lbStatus, seedPart, seedVid;
+    DBuf oSrc, oDst, oRank, oType, oEntry, progBuf, sendBits, recvBits, vcells, misc, oColDesc;
+    struct ColBuf { DBuf x, len, t; };
+    std::vector<ColBuf> oCols;                          // result columns (columnar, HBM)
+    std::vector<OutCol> oColView;                       // their device pointers, as uploaded to oColDesc
     uint64_t visitedSize = 0;
     uint8_t epoch = 0;
     // per-query kernels (hipRTC)
@@ -368,9 +371,12 @@ T readScalar(ngx_ctx* c, const T* dev) {
     return v;
 }
 
+struct ColSpec { bool len, t; };
+
 // Result holders: the C structs point into these vectors
 struct GoResultHolder {
     ngx_go_result r{};
+    std::vector<ngx_dev_column> devCols;
     std::vector<int32_t> colTypes;
     std::vector<ngx_cell> cells;
     std::vector<int64_t> src, dst, rank;
@@ -405,6 +411,8 @@ HopSlots makeHopSlots(const Space& sp, const DeviceGraph& d, const std::vector<i
         hs.dgid[hs.n] = ds.dgid;
         hs.dst[hs.n] = ds.dst;
         hs.rank[hs.n] = ds.rank;
+        hs.eflags[hs.n] = ds.hasFlags ? ds.eflags : nullptr;
+        hs.colBase[hs.n] = ds.colBase;
         hs.n++;
         hopTypes.push_back(t);
     }
@@ -451,9 +459,11 @@ void ngx_close(ngx_ctx* c) {
         (void)hipSetDevice(c->device);
         (void)hipStreamSynchronize(c->stream);
         c->spaces.clear();
-        for (DBuf* b : {&c->visited, &c->F0, &c->F1, &c->estart, &c->tileSums, &c->counters, &c->mask, &c->chunkCount,
-                        &c->chunkOff, &c->seedPart, &c->seedVid, &c->oSrc, &c->oDst, &c->oRank, &c->oType, &c->oEntry,
-                        &c->oCells, &c->progBuf, &c->sendBits, &c->recvBits, &c->vcells, &c->misc}) b->release();
+        for (DBuf* b : {&c->visited, &c->F0, &c->F1, &c->estart, &c->tileSums, &c->counters, &c->lbStatus,
+                        &c->seedPart, &c->seedVid, &c->oSrc, &c->oDst, &c->oRank, &c->oType, &c->oEntry,
+                        &c->chunkFirst, &c->oColDesc, &c->progBuf, &c->sendBits, &c->recvBits, &c->vcells,
+                        &c->misc}) b->release();
+        for (auto& cb : c->oCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         for (auto e : c->eventPool) (void)hipEventDestroy(e);
         if (c->comm) ncclCommDestroy(c->comm);
         (void)hipStreamDestroy(c->stream);
@@ -583,6 +593,21 @@ int32_t ngx_graph_info_get(ngx_ctx* c, int32_t space, ngx_graph_info* out) {
     out->device_bytes = sp->dev->bytes;
     out->slots = static_cast<int32_t>(sp->dev->slots.size());
     out->tags = static_cast<int32_t>(sp->dev->tags.size());
+    return NGX_OK;
+}
+
+int32_t ngx_device_to_host(ngx_ctx* c, void* dst, const void* src, uint64_t bytes) {
+    if (!c || (bytes && (!dst || !src))) return NGX_E_BAD_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    try {
+        HIP_OK(hipSetDevice(c->device));
+        if (bytes) {
+            HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+            HIP_OK(hipStreamSynchronize(c->stream));
+        }
+    } catch (const Error& e) {
+        return fail(c, e.code, e.msg);
+    }
     return NGX_OK;
 }
 
@@ -753,6 +778,77 @@ void exchangeFrontier(ngx_ctx* c, const DeviceGraph& d, uint8_t epoch) {
     }
 }
 
+// grow a device buffer to `bytes`, keeping its first `keep` bytes
+void growKeep(ngx_ctx* c, DBuf& b, size_t bytes, size_t keep) {
+    bytes = std::max<size_t>(bytes, 64);
+    if (b.cap >= bytes) return;
+    if (keep == 0 || b.p == nullptr) { b.get<char>(bytes); return; }
+    DBuf nb;
+    nb.get<char>(bytes);
+    HIP_OK(hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    b.release();
+    b = nb;
+}
+
+// the final kernel's look-back words (ticket + one status per chunk), zeroed on the stream
+uint64_t* zeroedLookBack(ngx_ctx* c, uint64_t chunks) {
+    size_t bytes = ((chunks + 1) * 8 + 15) & ~size_t(15);
+    uint64_t* p = c->lbStatus.get<uint64_t>(bytes / 8);
+    HIP_OK(hipMemsetAsync(p, 0, bytes, c->stream));
+    return p;
+}
+
+// size the result columns for `cap` rows (keeping `keep`) and upload their descriptors
+const OutCol* prepareCols(ngx_ctx* c, const std::vector<ColSpec>& spec, uint64_t cap, uint64_t keep) {
+    if (c->oCols.size() < spec.size()) c->oCols.resize(spec.size());
+    c->oColView.assign(spec.size(), OutCol{nullptr, nullptr, nullptr});
+    for (size_t y = 0; y < spec.size(); y++) {
+        auto& cb = c->oCols[y];
+        growKeep(c, cb.x, cap * 8, keep * 8);
+        c->oColView[y].x = static_cast<int64_t*>(cb.x.p);
+        if (spec[y].len) { growKeep(c, cb.len, cap * 4, keep * 4); c->oColView[y].len = static_cast<uint32_t*>(cb.len.p); }
+        if (spec[y].t) { growKeep(c, cb.t, cap, keep); c->oColView[y].t = static_cast<uint8_t*>(cb.t.p); }
+    }
+    OutCol* dev = c->oColDesc.get<OutCol>(std::max<size_t>(spec.size(), 1));
+    if (!spec.empty()) {
+        HIP_OK(hipMemcpyAsync(dev, c->oColView.data(), spec.size() * sizeof(OutCol), hipMemcpyHostToDevice, c->stream));
+    }
+    return dev;
+}
+
+// result columns rows [first, first + n) -> host OutCells (row-major); a typed column's rows carry its static type
+std::vector<OutCell> downloadCells(ngx_ctx* c, const std::vector<ColSpec>& spec, const std::vector<int32_t>& colTypes,
+                                   uint64_t n, uint64_t first) {
+    size_t nY = spec.size();
+    std::vector<OutCell> raw(n * nY);
+    std::vector<int64_t> x(n);
+    std::vector<uint32_t> len(n);
+    std::vector<uint8_t> t(n);
+    for (size_t y = 0; y < nY; y++) {
+        const OutCol& v = c->oColView[y];
+        HIP_OK(hipMemcpyAsync(x.data(), v.x + first, n * 8, hipMemcpyDeviceToHost, c->stream));
+        if (v.len) HIP_OK(hipMemcpyAsync(len.data(), v.len + first, n * 4, hipMemcpyDeviceToHost, c->stream));
+        if (v.t) HIP_OK(hipMemcpyAsync(t.data(), v.t + first, n, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipStreamSynchronize(c->stream));
+        uint8_t st = V_ERR;
+        switch (y < colTypes.size() ? colTypes[y] : T_UNKNOWN) {
+            case T_BOOL: st = V_BOOL; break;
+            case T_INT: case T_VID: case T_TIMESTAMP: st = V_INT; break;
+            case T_FLOAT: case T_DOUBLE: st = V_DBL; break;
+            case T_STRING: st = V_STR; break;
+            default: break;
+        }
+        for (uint64_t r = 0; r < n; r++) {
+            OutCell& o = raw[r * nY + y];
+            o.x = x[r];
+            o.len = v.len ? len[r] : 0;
+            o.t = v.t ? t[r] : st;
+        }
+    }
+    return raw;
+}
+
 int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     DeviceGraph& d = *sp.dev;
     GoPlan gp;
@@ -819,11 +915,15 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     DevPrograms dp = uploadPrograms(c, progs, ySlotType, gp.colTypes);
     // WHERE fully pushed: for edges whose storage filter ran, graphd's re-evaluation is implied
     bool wIsP = pushHere && gp.where && encodeExpr(*gp.pushed) == encodeExpr(*gp.where);
+    std::vector<int32_t> hopTypes;
+    HopSlots hs = makeHopSlots(sp, d, gp.edgeTypes, hopTypes);
     // per-query straight-line kernels (jit.cpp); the interpreter kernels otherwise
     const JitKernels* jk = nullptr;
     const JitKernels* jkNoP = nullptr;                       // record hops before the last (no pushdown)
+    c->jitNote.clear();
     if (c->jitOn) {
         JitQuery jq;
+        jq.oneSlot = hs.n == 1;
         jq.P = JitProgram{progs.P >= 0 ? progs.code.data() + progs.P : nullptr, progs.P >= 0};
         jq.W = JitProgram{progs.W >= 0 ? progs.code.data() + progs.W : nullptr, progs.W >= 0};
         for (int32_t off : progs.yOff) jq.Y.push_back(JitProgram{progs.code.data() + off, true});
@@ -889,8 +989,10 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     uint32_t* errFlag = reinterpret_cast<uint32_t*>(counters + 4);
     HIP_OK(hipMemsetAsync(counters, 0, 64, c->stream));
     uint64_t totalRows = 0;
-    std::vector<int32_t> hopTypes;
-    HopSlots hs = makeHopSlots(sp, d, gp.edgeTypes, hopTypes);
+    // result columns: value bits always; lengths when strings can appear; per-row types when the
+    // column's static type is unknown
+    std::vector<ColSpec> colSpec;
+    for (int32_t ct : gp.colTypes) colSpec.push_back(ColSpec{ct == T_UNKNOWN || ct == T_STRING, ct == T_UNKNOWN});
 
     for (uint32_t h = 1; h <= steps; h++) {
         bool isRecord = h >= recordFrom;
@@ -907,9 +1009,16 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         }
         R.hopFrontier.push_back(nF);
         R.hopEdges.push_back(E);
+        uint64_t chunks = (E + kChunk - 1) / kChunk;
+        uint64_t* chunkFirst = c->chunkFirst.get<uint64_t>(std::max<uint64_t>(chunks, 1));
+        if (E) {
+            c->timed("chunk_first", nEnt * 16, [&] {
+                if (launchChunkFirst(estart, nEnt, chunkFirst, c->stream)) throw Error{NGX_E_DEVICE, "chunk first"};
+            });
+        }
         if (isRecord && E) {
             FinalArgs a{};
-            a.F = F; a.estart = estart; a.nEnt = nEnt; a.E = E; a.hs = hs;
+            a.F = F; a.estart = estart; a.chunkFirst = chunkFirst; a.nEnt = nEnt; a.E = E; a.hs = hs;
             a.vid = d.vid; a.V = d.V; a.gbase = d.gbase;
             a.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1};
             a.P = (isFinal && progs.P >= 0) ? dp.code + progs.P : nullptr;
@@ -925,9 +1034,6 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
                 }
             }
             a.now = p.now_sec;
-            uint64_t chunks = (E + kTile - 1) / kTile;
-            a.mask = c->mask.get<uint64_t>(chunks * (kTile / 64));
-            a.chunkCount = c->chunkCount.get<uint32_t>(chunks);
             a.err = errFlag;
             a.nY = static_cast<int32_t>(progs.yOff.size());
             a.yCode = dp.code;
@@ -936,53 +1042,30 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             a.yColType = dp.yColType;
             a.wIsP = (isFinal && wIsP) ? 1u : 0u;
             const JitKernels* kj = isFinal ? jk : jkNoP;
-            uint64_t* chunkOff = c->chunkOff.get<uint64_t>(chunks + 1);
-            uint64_t* ctiles = c->tileSums.get<uint64_t>((chunks + kTile - 1) / kTile + 1);
-            uint64_t* rowsThisHop = counters + 1;
-            c->timed("final_eval", E * 8 * (2 + kf), [&] {
+            // outputs sized for every edge passing (rows are written in the same launch)
+            uint64_t cap = totalRows + E;
+            growKeep(c, c->oSrc, cap * 8, totalRows * 8);
+            growKeep(c, c->oDst, cap * 8, totalRows * 8);
+            growKeep(c, c->oRank, cap * 8, totalRows * 8);
+            growKeep(c, c->oType, cap * 4, totalRows * 4);
+            a.oCols = prepareCols(c, colSpec, cap, totalRows);
+            a.oBase = totalRows;
+            a.oSrc = static_cast<int64_t*>(c->oSrc.p);
+            a.oDst = static_cast<int64_t*>(c->oDst.p);
+            a.oRank = static_cast<int64_t*>(c->oRank.p);
+            a.oType = static_cast<int32_t*>(c->oType.p);
+            a.oEntry = nullptr;
+            a.lbStatus = zeroedLookBack(c, chunks);
+            c->timed("final", E * 8 * (2 + kf), [&] {
                 if (kj) {
                     void* args[] = {&a};
-                    HIP_OK(hipModuleLaunchKernel(kj->eval, static_cast<unsigned>(chunks), 1, 1, 256, 1, 1, 0, c->stream, args, nullptr));
-                } else if (launchFinalEval(a, c->stream)) {
-                    throw Error{NGX_E_DEVICE, "final eval"};
+                    HIP_OK(hipModuleLaunchKernel(kj->final, static_cast<unsigned>(chunks), 1, 1, 256, 1, 1, 0, c->stream, args, nullptr));
+                } else if (launchFinal(a, c->stream)) {
+                    throw Error{NGX_E_DEVICE, "final"};
                 }
             });
-            c->timed("chunk_scan", chunks * 12, [&] {
-                if (launchChunkScan(a, chunkOff, ctiles, rowsThisHop, c->stream)) throw Error{NGX_E_DEVICE, "chunk scan"};
-            });
-            uint64_t nrows = readScalar(c, rowsThisHop);
-            uint64_t cap = totalRows + nrows;
-            // grow outputs preserving earlier record hops
-            auto grow = [&](DBuf& b, size_t elem) {
-                if (b.cap < std::max<size_t>(cap * elem, 64) && totalRows) {
-                    DBuf nb;
-                    nb.get<char>(cap * elem);
-                    HIP_OK(hipMemcpyAsync(nb.p, b.p, totalRows * elem, hipMemcpyDeviceToDevice, c->stream));
-                    HIP_OK(hipStreamSynchronize(c->stream));
-                    b.release();
-                    b = nb;
-                } else {
-                    b.get<char>(std::max<size_t>(cap * elem, 64));
-                }
-            };
-            grow(c->oSrc, 8); grow(c->oDst, 8); grow(c->oRank, 8); grow(c->oType, 4);
-            grow(c->oCells, sizeof(OutCell) * std::max<size_t>(a.nY, 1));
-            a.oSrc = static_cast<int64_t*>(c->oSrc.p) + totalRows;
-            a.oDst = static_cast<int64_t*>(c->oDst.p) + totalRows;
-            a.oRank = static_cast<int64_t*>(c->oRank.p) + totalRows;
-            a.oType = static_cast<int32_t*>(c->oType.p) + totalRows;
-            a.oEntry = nullptr;
-            a.oCells = static_cast<OutCell*>(c->oCells.p) + totalRows * a.nY;
-            c->timed("final_emit", 0, [&] {
-                if (kj) {
-                    const uint64_t* co = chunkOff;
-                    void* args[] = {&a, &co};
-                    HIP_OK(hipModuleLaunchKernel(kj->emit, static_cast<unsigned>(chunks), 1, 1, 256, 1, 1, 0, c->stream, args, nullptr));
-                } else if (launchEmit(a, chunkOff, c->stream)) {
-                    throw Error{NGX_E_DEVICE, "final emit"};
-                }
-            });
-            c->addBytes("final_emit", nrows * (24 + 8 * ky));
+            uint64_t nrows = readScalar(c, a.lbStatus);      // GO: rows reserved by atomicAdd
+            c->addBytes("final", nrows * (24 + 8 * ky));
             totalRows += nrows;
         }
         if (isFinal) break;
@@ -990,7 +1073,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         uint8_t ep = nextEpoch(c);
         if (E) {
             c->timed("expand", E * 8, [&] {
-                if (launchExpandMark(F, estart, nEnt, E, hs, c->visited.get<uint8_t>(d.vglobal), ep, c->stream))
+                if (launchExpandMark(F, estart, chunkFirst, nEnt, E, hs, c->visited.get<uint8_t>(d.vglobal), ep, c->stream))
                     throw Error{NGX_E_DEVICE, "expand"};
             });
         }
@@ -1013,8 +1096,9 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     HIP_OK(hipEventElapsedTime(&ms, t0, t1));
     c->collectTimings();
     R.r.device_ms = ms;
-    uint32_t flags[3];
-    HIP_OK(hipMemcpy(flags, errFlag, 12, hipMemcpyDeviceToHost));
+    uint32_t flags[4];
+    HIP_OK(hipMemcpy(flags, errFlag, 16, hipMemcpyDeviceToHost));
+    if (flags[3]) return fail(c, NGX_E_DEVICE, "final-hop look-back did not complete (device fault)");
     if (flags[1]) return fail(c, NGX_E_UNSUPPORTED, "an expression needs a host-only construct (string building or parsing)");
     if (flags[0]) return fail(c, NGX_E_QUERY, "an expression of WHERE / YIELD failed to evaluate");
     if (flags[2]) return fail(c, NGX_E_QUERY, "YIELD value does not match its column type (boost::get)");
@@ -1026,19 +1110,24 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         R.r.dev_dst = static_cast<const int64_t*>(c->oDst.p);
         R.r.dev_rank = static_cast<const int64_t*>(c->oRank.p);
         R.r.dev_type = static_cast<const int32_t*>(c->oType.p);
-        R.r.dev_cells = static_cast<const ngx_dev_cell*>(c->oCells.p);
+        R.devCols.clear();
+        for (int32_t y = 0; y < nY; y++) {
+            bool have = y < static_cast<int32_t>(c->oColView.size()) && totalRows;
+            R.devCols.push_back(ngx_dev_column{have ? c->oColView[y].x : nullptr, have ? c->oColView[y].len : nullptr,
+                                               have ? c->oColView[y].t : nullptr});
+        }
+        R.r.dev_cols = R.devCols.data();
         return NGX_OK;
     }
     // ---- results to the host
     R.src.resize(totalRows); R.dst.resize(totalRows); R.rank.resize(totalRows); R.type.resize(totalRows);
-    std::vector<OutCell> raw(totalRows * nY);
+    std::vector<OutCell> raw;
     if (totalRows) {
         HIP_OK(hipMemcpyAsync(R.src.data(), c->oSrc.p, totalRows * 8, hipMemcpyDeviceToHost, c->stream));
         HIP_OK(hipMemcpyAsync(R.dst.data(), c->oDst.p, totalRows * 8, hipMemcpyDeviceToHost, c->stream));
         HIP_OK(hipMemcpyAsync(R.rank.data(), c->oRank.p, totalRows * 8, hipMemcpyDeviceToHost, c->stream));
         HIP_OK(hipMemcpyAsync(R.type.data(), c->oType.p, totalRows * 4, hipMemcpyDeviceToHost, c->stream));
-        if (nY) HIP_OK(hipMemcpyAsync(raw.data(), c->oCells.p, raw.size() * sizeof(OutCell), hipMemcpyDeviceToHost, c->stream));
-        HIP_OK(hipStreamSynchronize(c->stream));
+        raw = downloadCells(c, colSpec, gp.colTypes, totalRows, 0);
     }
     R.cells.resize(totalRows * nY);
     for (uint64_t r = 0; r < totalRows; r++) {
@@ -1230,8 +1319,11 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
     int32_t nY = q.ncols;
     std::vector<OutCell> raw;
     if (E) {
+        uint64_t chunks = (E + kChunk - 1) / kChunk;
+        uint64_t* chunkFirst = c->chunkFirst.get<uint64_t>(chunks);
+        if (launchChunkFirst(estart, nEnt, chunkFirst, c->stream)) throw Error{NGX_E_DEVICE, "chunk first"};
         FinalArgs a{};
-        a.F = F; a.estart = estart; a.nEnt = nEnt; a.E = E; a.hs = hs;
+        a.F = F; a.estart = estart; a.chunkFirst = chunkFirst; a.nEnt = nEnt; a.E = E; a.hs = hs;
         a.vid = d.vid; a.V = d.V; a.gbase = d.gbase;
         a.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1};
         a.P = progs.P >= 0 ? dp.code + progs.P : nullptr;
@@ -1248,34 +1340,30 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
             }
         }
         a.now = q.now_sec;
-        uint64_t chunks = (E + kTile - 1) / kTile;
-        a.mask = c->mask.get<uint64_t>(chunks * (kTile / 64));
-        a.chunkCount = c->chunkCount.get<uint32_t>(chunks);
         a.err = errFlag;
         a.nY = nY;
         a.yCode = dp.code;
         a.yOff = dp.yOff;
         a.ySlotType = dp.ySlotType;
-        uint64_t* chunkOff = c->chunkOff.get<uint64_t>(chunks + 1);
-        if (launchFinal(a, chunkOff, c->tileSums.get<uint64_t>((chunks + kTile - 1) / kTile + 1), counters + 1, c->stream))
-            throw Error{NGX_E_DEVICE, "final"};
-        nrows = readScalar(c, counters + 1);
-        a.oSrc = c->oSrc.get<int64_t>(nrows);
-        a.oDst = c->oDst.get<int64_t>(nrows);
-        a.oRank = c->oRank.get<int64_t>(nrows);
-        a.oType = c->oType.get<int32_t>(nrows);
-        a.oEntry = c->oEntry.get<uint32_t>(nrows);
-        a.oCells = c->oCells.get<OutCell>(std::max<uint64_t>(nrows * std::max(nY, 1), 1));
-        if (launchEmit(a, chunkOff, c->stream)) throw Error{NGX_E_DEVICE, "emit"};
+        a.oBase = 0;
+        a.oSrc = c->oSrc.get<int64_t>(E);
+        a.oDst = c->oDst.get<int64_t>(E);
+        a.oRank = c->oRank.get<int64_t>(E);
+        a.oType = c->oType.get<int32_t>(E);
+        a.oEntry = c->oEntry.get<uint32_t>(E);
+        std::vector<ColSpec> spec(nY, ColSpec{true, true});   // raw value cells: every column typed per row
+        a.oCols = prepareCols(c, spec, E, 0);
+        a.lbStatus = zeroedLookBack(c, chunks);
+        if (launchFinal(a, c->stream)) throw Error{NGX_E_DEVICE, "final"};
+        nrows = readScalar(c, a.lbStatus + chunks) & ((1ULL << 62) - 1);
         R.edgeVertex.resize(nrows);
         R.edgeType.resize(nrows);
         R.edgeDst.resize(nrows);
-        raw.resize(nrows * nY);
         if (nrows) {
             HIP_OK(hipMemcpyAsync(R.edgeVertex.data(), a.oEntry, nrows * 4, hipMemcpyDeviceToHost, c->stream));
             HIP_OK(hipMemcpyAsync(R.edgeType.data(), a.oType, nrows * 4, hipMemcpyDeviceToHost, c->stream));
             HIP_OK(hipMemcpyAsync(R.edgeDst.data(), a.oDst, nrows * 8, hipMemcpyDeviceToHost, c->stream));
-            if (nY) HIP_OK(hipMemcpyAsync(raw.data(), a.oCells, raw.size() * sizeof(OutCell), hipMemcpyDeviceToHost, c->stream));
+            raw = downloadCells(c, spec, std::vector<int32_t>(nY, T_UNKNOWN), nrows, 0);
         }
     }
     // per-vertex tag columns
@@ -1300,6 +1388,10 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
         HIP_OK(hipMemcpyAsync(vraw.data(), va.out, nF * nY * sizeof(OutCell), hipMemcpyDeviceToHost, c->stream));
     }
     HIP_OK(hipStreamSynchronize(c->stream));
+    uint32_t flags[4];
+    HIP_OK(hipMemcpy(flags, errFlag, 16, hipMemcpyDeviceToHost));
+    if (flags[3]) throw Error{NGX_E_DEVICE, "final-hop look-back did not complete (device fault)"};
+    if (flags[1]) throw Error{NGX_E_UNSUPPORTED, "a return column needs a host-only construct"};
     R.edgeCells.resize(nrows * nY);
     for (uint64_t i = 0; i < nrows * nY; i++) rawCell(raw[i], R.edgeCells[i], R.strings, d, dp, progs.pool);
     R.vertexCells.resize(nF * nY);

@@ -18,8 +18,7 @@ namespace ngx {
 
 struct JitKernels {
     hipModule_t mod = nullptr;
-    hipFunction_t eval = nullptr;
-    hipFunction_t emit = nullptr;
+    hipFunction_t final = nullptr;      // the fused final-hop kernel (final_kernels.h finalBody)
 };
 
 // one compiled program segment of a query: code[off ...] up to OP_END
@@ -32,6 +31,7 @@ struct JitQuery {
     JitProgram P, W;
     std::vector<JitProgram> Y;
     std::vector<int32_t> yColType;  // calculateExprType per column
+    bool oneSlot = false;           // the hop expands a single edge-type slot (ONE kernels)
 };
 
 class JitCache {

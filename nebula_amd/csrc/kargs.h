@@ -15,6 +15,8 @@ struct HopSlots {
     const uint32_t* dgid[kMaxSlots];
     const int64_t* dst[kMaxSlots];
     const int64_t* rank[kMaxSlots];
+    const uint8_t* eflags[kMaxSlots];   // per-edge EF_* flags, nullptr when the slot has none
+    int32_t colBase[kMaxSlots];         // first DCol of the slot in the column table
 };
 
 struct OutCell {                        // raw VM value of one YIELD / return column
@@ -24,9 +26,17 @@ struct OutCell {                        // raw VM value of one YIELD / return co
     uint8_t pad[3];
 };
 
+// One YIELD / return column of the result, columnar in HBM (row o at index oBase + o).
+struct OutCol {
+    int64_t* x;                         // value bits: int, double bits, bool 0/1, string device pointer
+    uint32_t* len;                      // string lengths; nullptr when the column holds no strings
+    uint8_t* t;                         // V_* (0xFF none) per row; nullptr when every row has the column's static type
+};
+
 struct FinalArgs {
     const uint32_t* F;                  // frontier rows
     const uint64_t* estart;             // exclusive prefix of entry degrees, [nEnt] = E
+    const uint64_t* chunkFirst;         // entry holding the first edge of each CE-edge chunk
     uint64_t nEnt;
     uint64_t E;
     HopSlots hs;
@@ -40,21 +50,22 @@ struct FinalArgs {
     int32_t ttlCol[kMaxSlots];          // TTL column of hop slot s, -1 if none
     int64_t ttlDur[kMaxSlots];
     int64_t now;
-    uint64_t* mask;                     // pass bits, 64 words per 4096-edge chunk
-    uint32_t* chunkCount;
-    uint32_t* err;                      // [0] graphd evaluation error, [1] host-only construct, [2] YIELD type mismatch
+    uint64_t* lbStatus;                 // [0] chunk ticket, [1 + c] look-back status of chunk c (zeroed per launch)
+    uint32_t* err;                      // [0] graphd evaluation error, [1] host-only construct, [2] YIELD type
+                                        // mismatch, [3] look-back spin limit (device fault)
     int32_t nY;
     const Insn* yCode;
     const int32_t* yOff;
     const int32_t* ySlotType;           // 0 = any type; else the column belongs to this signed type
     const int32_t* yColType;            // calculateExprType per column (0 UNKNOWN: any value type), may be null
     uint32_t wIsP;                      // WHERE == pushed filter: W is implied by P where P was evaluated
+    uint64_t oBase;                     // first output row of this launch (earlier record hops before it)
     int64_t* oSrc;
     int64_t* oDst;
     int64_t* oRank;
     int32_t* oType;
     uint32_t* oEntry;                   // frontier index of each row (GetNeighbors), may be null
-    OutCell* oCells;
+    const OutCol* oCols;                // nY columns (device array)
 };
 
 struct VertexCellArgs {
@@ -67,6 +78,7 @@ struct VertexCellArgs {
     OutCell* out;
 };
 
-constexpr uint64_t kTile = 4096;        // edges per expansion workgroup / items per scan tile
+constexpr uint64_t kTile = 4096;        // items per scan tile
+constexpr uint64_t kChunk = 2048;       // edges per edge-balanced workgroup (expansion, final hop)
 
 }  // namespace ngx

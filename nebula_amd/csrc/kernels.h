@@ -12,15 +12,16 @@ int launchLookup(const int32_t* qpart, const int64_t* qvid, uint64_t n, const in
 // estart must hold nEnt + 1 entries; estart[nEnt] receives E
 int launchDegreeScan(const uint32_t* F, uint64_t nEnt, const HopSlots& hs, uint64_t* estart, uint64_t* tileSums,
                      hipStream_t s);
-int launchExpandMark(const uint32_t* F, const uint64_t* estart, uint64_t nEnt, uint64_t E, const HopSlots& hs,
-                     uint8_t* visited, uint8_t epoch, hipStream_t s);
+// chunkFirst must hold ceil(E / kChunk) entries (estart[nEnt] = E)
+int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst, hipStream_t s);
+int launchExpandMark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst, uint64_t nEnt, uint64_t E,
+                     const HopSlots& hs, uint8_t* visited, uint8_t epoch, hipStream_t s);
 int launchCompact(const uint8_t* visited, uint64_t gbase, uint64_t V, uint8_t epoch, uint32_t* outF,
                   uint64_t* tileSums, uint64_t* count, hipStream_t s);
-// final hop: eval (interpreter kernel), scan of the per-chunk pass counts, or both
-int launchFinalEval(const FinalArgs& a, hipStream_t s);
-int launchChunkScan(const FinalArgs& a, uint64_t* chunkOff, uint64_t* tileSums, uint64_t* total, hipStream_t s);
-int launchFinal(const FinalArgs& a, uint64_t* chunkOff, uint64_t* tileSums, uint64_t* total, hipStream_t s);
-int launchEmit(const FinalArgs& a, const uint64_t* chunkOff, hipStream_t s);
+// final hop, one pass (interpreter kernel): a.lbStatus zeroed, ceil(E / kChunk) + 1 words; outputs
+// sized for a.oBase + a.E rows. a.oEntry set (GetNeighbors): rows in edge order, rows written = the
+// inclusive status of the last chunk; else (GO) chunks in completion order, rows written = lbStatus[0]
+int launchFinal(const FinalArgs& a, hipStream_t s);
 int launchVertexCells(const VertexCellArgs& a, hipStream_t s);
 int launchPack(const uint8_t* visited, uint8_t epoch, uint64_t lo, uint64_t n, uint64_t* bits, hipStream_t s);
 int launchMerge(const uint64_t* bits, uint64_t n, uint8_t* visited, uint64_t lo, uint8_t epoch, hipStream_t s);

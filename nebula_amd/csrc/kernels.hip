@@ -3,17 +3,18 @@
 //  * k_lookup           seed (part, vid) -> vertex row, binary search of the sorted vertex table
 //  * tile scans         3-phase reduce-then-scan (tile = 256 threads x 16 items) used for entry
 //                       degrees (CSR offsets of the frontier) and for frontier compaction
-//  * k_expand_mark      intermediate hop: edge-balanced expansion. A workgroup owns 4096 consecutive
+//  * k_chunk_first      per 2048-edge chunk of a hop: the frontier entry holding its first edge
+//  * k_expand_mark      intermediate hop: edge-balanced expansion. A workgroup owns 2048 consecutive
 //                       frontier edges whatever their vertices' degrees (a supernode spreads over
-//                       many workgroups, a thread never loops over a whole adjacency); the edge ->
-//                       frontier-entry map is built in LDS (atomicMax scatter + max-scan); each
+//                       many workgroups, a thread never loops over a whole adjacency); the entry
+//                       records of the chunk are staged in LDS (final_kernels.h buildMap); each
 //                       edge reads one 4-byte destination row id (coalesced) and marks the
 //                       destination in an epoch byte array = the hop's frontier dedup
 //  * k_compact          visited[row] == epoch -> next frontier (ballot-free tile compaction)
-//  * k_final_eval       last hop: storage filter (pushdown) + graphd WHERE through the bytecode VM,
-//                       wave-ballot pass masks + per-chunk pass counts
-//  * k_final_emit       last hop: YIELD columns for passing edges, written densely at
-//                       chunk offset + ballot prefix (deterministic order)
+//  * k_final            last hop in one pass: storage filter (pushdown) + graphd WHERE through the
+//                       bytecode VM, wave-ballot pass masks, decoupled look-back over the chunks'
+//                       pass counts, rows + columnar YIELD cells of passing edges written densely
+//                       (deterministic order)
 //  * k_pack / k_merge   multi-GPU frontier exchange: epoch marks -> per-peer bitmaps and back
 #include <hip/hip_runtime.h>
 
@@ -41,10 +42,6 @@ struct FlagIn {                  // visited[gbase + r] == epoch
     uint64_t gbase;
     uint8_t epoch;
     __device__ __forceinline__ uint64_t operator()(uint64_t r) const { return visited[gbase + r] == epoch ? 1 : 0; }
-};
-struct CountIn {                 // plain uint32 counts
-    const uint32_t* c;
-    __device__ __forceinline__ uint64_t operator()(uint64_t i) const { return c[i]; }
 };
 struct WriteEstart {
     uint64_t* estart;
@@ -135,24 +132,42 @@ __global__ void k_lookup(const int32_t* qpart, const int64_t* qvid, uint64_t n, 
     out[i] = (lo < V && vpart[lo] == p && vid[lo] == v) ? static_cast<uint32_t>(lo) : kNoRow;
 }
 
+// ------------------------------------------------------------------------------ chunk -> first entry
+// chunkFirst[c] = the entry holding edge c * CE (the only entry with estart[i] <= c*CE < estart[i+1])
+__global__ void k_chunk_first(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst) {
+    uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= nEnt) return;
+    uint64_t s = estart[i], t = estart[i + 1];
+    for (uint64_t c = (s + CE - 1) / CE; c * CE < t; c++) chunkFirst[c] = i;
+}
+
 // ------------------------------------------------------------------------------ intermediate hop
-__global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uint64_t* estart, uint64_t nEnt,
-                                                    uint64_t E, HopSlots hs, uint8_t* visited, uint8_t epoch) {
-    __shared__ uint32_t smap[TILE];
-    __shared__ uint64_t sLo;
-    uint64_t base = static_cast<uint64_t>(blockIdx.x) * TILE;
-    uint32_t cnt = static_cast<uint32_t>(E - base < TILE ? E - base : TILE);
-    uint64_t lo = mapChunk(estart, nEnt, base, cnt, smap, &sLo);
-#pragma unroll 4
-    for (int k = 0; k < ITEMS; k++) {
+// Edge-balanced expansion: every edge of the hop reads its 4-byte destination row and stores the
+// hop's epoch into visited[] (the frontier dedup of GoExecutor::getDstIdsFromResp, a set of dsts).
+// The store is unconditional: a byte store needs no read and duplicates write the same value.
+template <bool ONE>
+__global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst,
+                                                    uint64_t nEnt, uint64_t E, HopSlots hs, uint8_t* visited,
+                                                    uint8_t epoch) {
+    __shared__ ChunkMap<false> m;
+    const uint64_t base = static_cast<uint64_t>(blockIdx.x) * CE;
+    const uint32_t cnt = static_cast<uint32_t>(E - base < CE ? E - base : CE);
+    buildMap<ONE, false>(estart, chunkFirst, nEnt, blockIdx.x, gridDim.x, base, cnt, F, hs, m);
+    uint32_t g[CITEMS];
+#pragma unroll
+    for (int k = 0; k < CITEMS; k++) {
         uint32_t p = threadIdx.x + k * WG;
-        if (p >= cnt) break;
-        uint64_t ent = lo + smap[p];
-        int s = static_cast<int>(ent % hs.n);
-        uint32_t r = F[ent / hs.n];
-        uint64_t pos = hs.off[s][r] + (base + p - estart[ent]);
-        uint32_t g = hs.dgid[s][pos];
-        if (g != kNoRow && visited[g] != epoch) visited[g] = epoch;
+        g[k] = kNoRow;
+        if (p < cnt) {
+            uint32_t q = m.at[p];
+            int s = ONE ? 0 : m.slot[q];
+            uint64_t pos = static_cast<uint64_t>(static_cast<int64_t>(base + p) + m.pb[q]);
+            g[k] = hs.dgid[s][pos];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < CITEMS; k++) {
+        if (g[k] != kNoRow) visited[g[k]] = epoch;
     }
 }
 
@@ -162,24 +177,26 @@ struct VmEv {
     static __device__ __forceinline__ bool hasW(const FinalArgs& a) { return a.W != nullptr; }
     static __device__ __forceinline__ Val P(const FinalArgs& a, const EdgeCtx& ec) { return vmEval(a.P, a.env, ec); }
     static __device__ __forceinline__ Val W(const FinalArgs& a, const EdgeCtx& ec) { return vmEval(a.W, a.env, ec); }
-    static __device__ __forceinline__ void Y(const FinalArgs& a, const EdgeCtx& ec, uint64_t o) {
+    static __device__ __forceinline__ void Y(const FinalArgs& a, const EdgeCtx& ec, uint64_t o, uint32_t& errs) {
         for (int y = 0; y < a.nY; y++) {
-            OutCell c;
+            const OutCol& oc = a.oCols[y];
+            Val v;
             if (a.ySlotType != nullptr && a.ySlotType[y] != 0 && a.ySlotType[y] != ec.etype) {
-                c.t = 0xFF; c.len = 0; c.x = 0;              // column of another edge type (GetNeighbors)
+                v.t = 0xFF; v.len = 0; v.x = 0;              // column of another edge type (GetNeighbors)
             } else {
-                Val v = vmEval(a.yCode + a.yOff[y], a.env, ec);
-                if (v.t == V_ERR) atomicOr(a.err, 1u);
-                else if (a.yColType != nullptr && !cellTypeOk(a.yColType[y], v.t)) atomicOr(a.err + 2, 1u);
-                c.t = v.t; c.len = v.len; c.x = v.x;
+                v = vmEval(a.yCode + a.yOff[y], a.env, ec);
+                if (v.t == V_ERR) errs |= 1u;
+                else if (a.yColType != nullptr && !cellTypeOk(a.yColType[y], v.t)) errs |= 4u;
             }
-            a.oCells[o * a.nY + y] = c;
+            oc.x[o] = v.x;
+            if (oc.len) oc.len[o] = v.len;
+            if (oc.t) oc.t[o] = v.t;
         }
     }
 };
 
-__global__ __launch_bounds__(WG) void k_final_eval(FinalArgs a) { finalEvalBody<VmEv>(a); }
-__global__ __launch_bounds__(WG) void k_final_emit(FinalArgs a, const uint64_t* chunkOff) { finalEmitBody<VmEv>(a, chunkOff); }
+template <bool ONE, bool FIDX>
+__global__ __launch_bounds__(WG) void k_final(FinalArgs a) { finalBody<VmEv, ONE, FIDX, FIDX>(a); }
 
 // ------------------------------------------------------------------------------ vertex cells
 __global__ void k_vertex_cells(VertexCellArgs a) {
@@ -233,11 +250,18 @@ int launchDegreeScan(const uint32_t* F, uint64_t nEnt, const HopSlots& hs, uint6
     return scan3(DegreeIn{F, hs}, nEnt, WriteEstart{estart}, tileSums, estart + nEnt, s);
 }
 
-int launchExpandMark(const uint32_t* F, const uint64_t* estart, uint64_t nEnt, uint64_t E, const HopSlots& hs,
-                     uint8_t* visited, uint8_t epoch, hipStream_t s) {
+int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst, hipStream_t s) {
+    if (nEnt == 0) return 0;
+    hipLaunchKernelGGL(k_chunk_first, dim3(static_cast<unsigned>((nEnt + 255) / 256)), dim3(256), 0, s, estart, nEnt, chunkFirst);
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchExpandMark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst, uint64_t nEnt, uint64_t E,
+                     const HopSlots& hs, uint8_t* visited, uint8_t epoch, hipStream_t s) {
     if (E == 0) return 0;
-    uint64_t chunks = (E + TILE - 1) / TILE;
-    hipLaunchKernelGGL(k_expand_mark, dim3(static_cast<unsigned>(chunks)), dim3(WG), 0, s, F, estart, nEnt, E, hs, visited, epoch);
+    dim3 grid(static_cast<unsigned>((E + CE - 1) / CE));
+    if (hs.n == 1) hipLaunchKernelGGL(k_expand_mark<true>, grid, dim3(WG), 0, s, F, estart, chunkFirst, nEnt, E, hs, visited, epoch);
+    else hipLaunchKernelGGL(k_expand_mark<false>, grid, dim3(WG), 0, s, F, estart, chunkFirst, nEnt, E, hs, visited, epoch);
     return static_cast<int>(hipGetLastError());
 }
 
@@ -246,29 +270,16 @@ int launchCompact(const uint8_t* visited, uint64_t gbase, uint64_t V, uint8_t ep
     return scan3(FlagIn{visited, gbase, epoch}, V, WriteCompact{outF}, tileSums, count, s);
 }
 
-int launchFinalEval(const FinalArgs& a, hipStream_t s) {
+int launchFinal(const FinalArgs& a, hipStream_t s) {
     if (a.E == 0) return 0;
-    uint64_t chunks = (a.E + TILE - 1) / TILE;
-    hipLaunchKernelGGL(k_final_eval, dim3(static_cast<unsigned>(chunks)), dim3(WG), 0, s, a);
-    return static_cast<int>(hipGetLastError());
-}
-
-int launchChunkScan(const FinalArgs& a, uint64_t* chunkOff, uint64_t* tileSums, uint64_t* total, hipStream_t s) {
-    if (a.E == 0) { (void)hipMemsetAsync(total, 0, 8, s); return 0; }
-    uint64_t chunks = (a.E + TILE - 1) / TILE;
-    return scan3(CountIn{a.chunkCount}, chunks, WriteEstart{chunkOff}, tileSums, total, s);
-}
-
-int launchFinal(const FinalArgs& a, uint64_t* chunkOff, uint64_t* tileSums, uint64_t* total, hipStream_t s) {
-    if (a.E == 0) { (void)hipMemsetAsync(total, 0, 8, s); return 0; }
-    int rc = launchFinalEval(a, s);
-    return rc ? rc : launchChunkScan(a, chunkOff, tileSums, total, s);
-}
-
-int launchEmit(const FinalArgs& a, const uint64_t* chunkOff, hipStream_t s) {
-    if (a.E == 0) return 0;
-    uint64_t chunks = (a.E + TILE - 1) / TILE;
-    hipLaunchKernelGGL(k_final_emit, dim3(static_cast<unsigned>(chunks)), dim3(WG), 0, s, a, chunkOff);
+    dim3 grid(static_cast<unsigned>((a.E + CE - 1) / CE));
+    if (a.oEntry != nullptr) {
+        if (a.hs.n == 1) hipLaunchKernelGGL((k_final<true, true>), grid, dim3(WG), 0, s, a);
+        else hipLaunchKernelGGL((k_final<false, true>), grid, dim3(WG), 0, s, a);
+    } else {
+        if (a.hs.n == 1) hipLaunchKernelGGL((k_final<true, false>), grid, dim3(WG), 0, s, a);
+        else hipLaunchKernelGGL((k_final<false, false>), grid, dim3(WG), 0, s, a);
+    }
     return static_cast<int>(hipGetLastError());
 }
 

@@ -27,6 +27,7 @@ struct Val {
 struct EdgeCtx {
     int32_t slot;
     int32_t etype;
+    const DCol* cols;   // first column of the slot's edge schema
     uint64_t pos;       // edge index inside the slot arrays
     uint32_t srow;      // local row of the source vertex
     uint32_t drow;      // local row of the destination (kNoRow when not on this shard)
@@ -180,14 +181,14 @@ template <int CT>
 __device__ __forceinline__ Val opEcolT(const VmEnv& env, const EdgeCtx& ec, int32_t a, int32_t b, uint8_t mode, Val dflt) {
     int32_t at = ec.etype < 0 ? -ec.etype : ec.etype;
     if (at != b) return (mode & 1) ? dflt : mkErr();
-    const DCol& c = env.cols[env.slots[ec.slot].colBase + a];
+    const DCol& c = ec.cols[a];
     if (c.valid != nullptr && c.valid[ec.pos] == 0) return (mode & 2) ? defaultOfTypeT<CT>() : mkErr();
     return loadColT<CT>(c, ec.pos);
 }
 __device__ __forceinline__ Val opEcol(const VmEnv& env, const EdgeCtx& ec, int32_t a, int32_t b, uint8_t mode, Val dflt) {
     int32_t at = ec.etype < 0 ? -ec.etype : ec.etype;
     if (at != b) return (mode & 1) ? dflt : mkErr();
-    const DCol& c = env.cols[env.slots[ec.slot].colBase + a];
+    const DCol& c = ec.cols[a];
     if (c.valid != nullptr && c.valid[ec.pos] == 0) return (mode & 2) ? defaultOfType(c.type) : mkErr();
     return loadCol(c, ec.pos);
 }

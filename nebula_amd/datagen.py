@@ -147,3 +147,27 @@ def rmat_schemas(with_tag: bool = False):
     if with_tag:
         s.append((False, RMAT_TAG, RMAT_TAG_NAME, RMAT_TAG_FIELDS))
     return s
+
+
+# power-law space (C4): one edge type with an INT and a DOUBLE prop, no tags
+PL_SPACE, PL_EDGE, PL_EDGE_NAME = 2, 1, "pl"
+PL_EDGE_FIELDS = [("w", 2), ("score", 5)]
+
+
+def powerlaw_schemas():
+    return [(True, PL_EDGE, PL_EDGE_NAME, PL_EDGE_FIELDS)]
+
+
+# LDBC-SNB-like space (C5)
+SNB_SPACE = 3
+
+
+def snb_schemas(ids: SnbIds = SnbIds()):
+    """(is_edge, id, name, fields) of the SNB-like space, field order as ngd_snb writes the rows."""
+    return [
+        (False, ids.person, "person", [("firstName", 6), ("age", 2), ("gender", 6)]),
+        (False, ids.post, "post", [("content", 6), ("length", 2), ("lang", 6)]),
+        (True, ids.knows, "knows", [("creationDate", 2), ("weight", 5)]),
+        (True, ids.likes, "likes", [("creationDate", 2)]),
+        (True, ids.has_creator, "hasCreator", [("creationDate", 2)]),
+    ]

@@ -97,7 +97,7 @@ class GoResultC(ctypes.Structure):
                 ("strings", ctypes.c_void_p), ("strings_len", c_u64), ("nhops", c_i32),
                 ("hop_frontier", P(c_u64)), ("hop_edges", P(c_u64)), ("hop_next", P(c_u64)),
                 ("device_ms", c_dbl), ("dev_src", ctypes.c_void_p), ("dev_dst", ctypes.c_void_p),
-                ("dev_rank", ctypes.c_void_p), ("dev_type", ctypes.c_void_p), ("dev_cells", ctypes.c_void_p)]
+                ("dev_rank", ctypes.c_void_p), ("dev_type", ctypes.c_void_p), ("dev_cols", ctypes.c_void_p)]
 
 
 class KernelStat(ctypes.Structure):
@@ -126,7 +126,12 @@ SIGNATURES = {
     "ngx_get_flag": (c_i32, [ctypes.c_void_p, ctypes.c_char_p, P(c_i64)]),
     "ngx_jit_note": (ctypes.c_char_p, [ctypes.c_void_p]),
     "ngx_hash_string": (c_i64, [ctypes.c_char_p, c_u64]),
+    "ngx_device_to_host": (c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_u64]),
 }
+
+
+class DevColumn(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_void_p), ("len", ctypes.c_void_p), ("type", ctypes.c_void_p)]
 
 _lib = None
 
@@ -194,6 +199,8 @@ class GoResult:
     hop_next: List[int] = field(default_factory=list)
     device_ms: float = 0.0
     nrows: int = 0
+    # on_device + fetch: the HBM result copied back as arrays (x, len or None, type or None) per column
+    dev_cols: List[tuple] = field(default_factory=list)
 
 
 @dataclass
@@ -303,9 +310,10 @@ class Engine:
 
     # ---- GO
     def go(self, space: int, s: Union[str, ngql.GoSentence], pushdown: bool = True, now_sec: int = 0,
-           raise_on_error: bool = False, rows: bool = True, on_device: bool = False) -> GoResult:
+           raise_on_error: bool = False, rows: bool = True, on_device: bool = False, fetch: bool = False) -> GoResult:
         """Run one GO. rows=False skips decoding cells into Python tuples; on_device=True leaves the
-        result rows in HBM (GoResult.nrows and the statistics only)."""
+        result rows in HBM (GoResult.nrows and the statistics only); with fetch=True the HBM arrays
+        (src/dst/rank/type and the columnar YIELD columns) are copied back into the result."""
         if isinstance(s, str):
             s = ngql.parse_go(s)
         starts = np.array(s.vids, dtype=np.int64)
@@ -329,10 +337,22 @@ class Engine:
             strings = ctypes.string_at(r.strings, r.strings_len) if r.strings_len else b""
             n = r.nrows
             if on_device:
-                return GoResult(ok=rc == 0, error=err, code=rc, col_types=[r.col_types[i] for i in range(r.ncols)],
-                                rows=[], nrows=n, hop_frontier=[r.hop_frontier[i] for i in range(r.nhops)],
-                                hop_edges=[r.hop_edges[i] for i in range(r.nhops)],
-                                hop_next=[r.hop_next[i] for i in range(r.nhops)], device_ms=r.device_ms)
+                res = GoResult(ok=rc == 0, error=err, code=rc, col_types=[r.col_types[i] for i in range(r.ncols)],
+                               rows=[], nrows=n, hop_frontier=[r.hop_frontier[i] for i in range(r.nhops)],
+                               hop_edges=[r.hop_edges[i] for i in range(r.nhops)],
+                               hop_next=[r.hop_next[i] for i in range(r.nhops)], device_ms=r.device_ms)
+                if fetch and rc == 0:
+                    res.src = self._d2h(r.dev_src, n, np.int64)
+                    res.dst = self._d2h(r.dev_dst, n, np.int64)
+                    res.rank = self._d2h(r.dev_rank, n, np.int64)
+                    res.etype = self._d2h(r.dev_type, n, np.int32)
+                    cols = ctypes.cast(r.dev_cols, P(DevColumn)) if r.dev_cols else None
+                    for c in range(r.ncols):
+                        dc = cols[c]
+                        res.dev_cols.append((self._d2h(dc.x, n, np.int64),
+                                             self._d2h(dc.len, n, np.uint32) if dc.len else None,
+                                             self._d2h(dc.type, n, np.uint8) if dc.type else None))
+                return res
             res = GoResult(
                 ok=rc == 0, error=err, code=rc, col_types=[r.col_types[i] for i in range(r.ncols)],
                 rows=_cells(r.cells, n, r.ncols, strings) if rows else [],
@@ -344,6 +364,12 @@ class Engine:
             return res
         finally:
             self.L.ngx_go_result_free(out)
+
+    def _d2h(self, ptr, n, dtype):
+        out = np.zeros(n, dtype=dtype)
+        if n and ptr:
+            self._check(self.L.ngx_device_to_host(self.h, out.ctypes.data, ptr, out.nbytes), "device_to_host")
+        return out
 
     # ---- flags
     def set_flag(self, name: str, value: int):

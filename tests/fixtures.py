@@ -52,14 +52,12 @@ class Dataset:
         return eng
 
 
-class RmatDataset:
-    """RMAT space of bench.py (datagen.rmat): edge `e`(p0 INT, p1 INT), optional tag `vt`."""
+class GenDataset:
+    """A generated space (datagen Rows + schemas) loadable into the oracle and the engine."""
 
-    def __init__(self, scale, ef=16, seed=42, num_parts=100, with_in=False, with_tag=False, threads=0):
-        from nebula_amd import datagen
-        self.space, self.num_parts, self.scale = datagen.RMAT_SPACE, num_parts, scale
-        self.rows = datagen.rmat(scale, ef, seed, num_parts, with_in, with_tag, threads=threads)
-        self.schemas = [SchemaDef(e, i, n, f) for e, i, n, f in datagen.rmat_schemas(with_tag)]
+    def __init__(self, space, num_parts, rows, schemas):
+        self.space, self.num_parts, self.rows = space, num_parts, rows
+        self.schemas = [SchemaDef(e, i, n, f) for e, i, n, f in schemas]
 
     def load_oracle(self, orc, threads=8):
         orc.add_space(self.space, self.num_parts)
@@ -76,6 +74,35 @@ class RmatDataset:
         eng.load_kv(self.space, *self.rows.arrays())
         eng.commit(self.space)
         return eng
+
+
+class RmatDataset(GenDataset):
+    """RMAT space of bench.py (datagen.rmat): edge `e`(p0 INT, p1 INT), optional tag `vt`."""
+
+    def __init__(self, scale, ef=16, seed=42, num_parts=100, with_in=False, with_tag=False, threads=0):
+        from nebula_amd import datagen
+        super().__init__(datagen.RMAT_SPACE, num_parts,
+                         datagen.rmat(scale, ef, seed, num_parts, with_in, with_tag, threads=threads),
+                         datagen.rmat_schemas(with_tag))
+        self.scale = scale
+
+
+def powerlaw_dataset(n, ef=8, nsuper=4, superdeg=20000, seed=42, num_parts=100, threads=0):
+    """C4 shape: power-law graph with `nsuper` supernodes of in-degree `superdeg` (out + in rows)."""
+    from nebula_amd import datagen
+    rows = datagen.powerlaw(n, ef, 2.0, nsuper, superdeg, seed, num_parts, datagen.PL_EDGE, threads=threads)
+    ds = GenDataset(datagen.PL_SPACE, num_parts, rows, datagen.powerlaw_schemas())
+    ds.n = n
+    return ds
+
+
+def snb_dataset(np_, knows_deg=20, likes_deg=10, seed=42, num_parts=100, threads=0):
+    """C5 shape: LDBC-SNB-like persons/posts with knows/likes/hasCreator (string + int props)."""
+    from nebula_amd import datagen
+    rows = datagen.snb(np_, knows_deg, 0, likes_deg, seed, num_parts, threads=threads)
+    ds = GenDataset(datagen.SNB_SPACE, num_parts, rows, datagen.snb_schemas())
+    ds.np = np_
+    return ds
 
 
 # ----------------------------------------------------------------------------- NBA (GoTest)

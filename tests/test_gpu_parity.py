@@ -249,3 +249,141 @@ def test_rmat_query_error_matches(rmat):
     ref = o.go(ds.space, s)
     got = e.go(ds.space, s)
     assert got.ok == ref.ok
+
+
+def test_rmat_device_results_values(rmat):
+    """result_on_device leaves the rows in HBM, columnar: the arrays copied back hold the same rows as
+    the host result (compared sorted: GO rows come in chunk-completion order, as the reference's come
+    in response order), typed int columns carry no per-row type array, strings carry lengths."""
+    ds, o, e = rmat
+    seeds = datagen.sample_vids(78, 1 << ds.scale, 60)
+    q = ("GO 2 STEPS FROM " + ", ".join(str(int(v)) for v in seeds) +
+         " OVER e WHERE e.p0 < 50 YIELD e._dst, e._rank, e.p0, e.p1, $^.vt.name")
+    s = ngql.parse_go(q)
+    host = e.go(ds.space, s)
+    dev = e.go(ds.space, s, on_device=True, fetch=True)
+    assert host.ok and dev.ok and dev.nrows == len(host.rows) > 0
+    for c in range(4):
+        x, ln, t = dev.dev_cols[c]
+        assert ln is None and t is None
+    x, ln, t = dev.dev_cols[4]
+    assert ln is not None and t is None
+    got = sorted(zip(dev.src.tolist(), dev.dst.tolist(), dev.rank.tolist(),
+                     *[dev.dev_cols[c][0].tolist() for c in range(4)], dev.dev_cols[4][1].tolist()))
+    ref = sorted(zip(host.src.tolist(), host.dst.tolist(), host.rank.tolist(),
+                     *[[r[c][1] for r in host.rows] for c in range(4)],
+                     [len(r[4][1].encode()) for r in host.rows]))
+    assert got == ref
+
+
+# --------------------------------------------------------------------------- larger RMAT (C2 shape)
+@pytest.fixture(scope="module", params=["jit", "vm"])
+def rmat16(request):
+    ds = fixtures.RmatDataset(16, threads=8)
+    o = oracle.Oracle()
+    o.set_flags(threads=8)
+    ds.load_oracle(o)
+    e = _engine(request.param)
+    ds.load_engine(e)
+    yield ds, o, e
+    _check_jit(e, request.param)
+    e.close()
+
+
+@pytest.mark.parametrize("sel", [10, 50, 90])
+def test_rmat16_bench_query(rmat16, sel):
+    """The bench query (BASELINE configs[1] shape) at scale 16: GO 3 STEPS from 200 vids WHERE
+    e.p0 < sel: rows and per-hop scanned edges equal the oracle's; hubs span many 2048-edge chunks."""
+    ds, o, e = rmat16
+    seeds = datagen.rmat_seeds(16, 200, 16, 42, 7 + sel, threads=8)
+    q = (f"GO 3 STEPS FROM {', '.join(str(int(v)) for v in seeds)} OVER e WHERE e.p0 < {sel} "
+         "YIELD e._dst, e._rank, e.p0, e.p1")
+    s = ngql.parse_go(q)
+    ref = o.go(ds.space, s)
+    got = e.go(ds.space, s)
+    assert ref.ok and got.ok, (got.error, ref.error)
+    assert got.hop_edges == ref.hop_scanned
+    assert fixtures.normalize_cells(got.rows) == fixtures.normalize_cells(ref.rows)
+
+
+# --------------------------------------------------------------------------- C4: power law + supernodes
+PL_QUERIES = [
+    "GO 2 STEPS FROM {S} OVER pl REVERSELY YIELD pl._dst, pl.w, pl.score",
+    "GO 2 STEPS FROM {S} OVER pl REVERSELY WHERE pl.w < 30 && pl.score > 0.25 YIELD pl._dst, pl._src, pl.score",
+    "GO 2 STEPS FROM {S} OVER pl WHERE pl.score * 100.0 > pl.w YIELD pl._dst, pl.w + 1",
+    "GO 1 TO 2 STEPS FROM {S} OVER pl BIDIRECT WHERE pl.w == 7 YIELD pl._dst, pl._src, pl.w",
+]
+
+
+@pytest.fixture(scope="module", params=["jit", "vm"])
+def plaw(request):
+    ds = fixtures.powerlaw_dataset(50000, superdeg=30000, threads=8)
+    o = oracle.Oracle()
+    o.set_flags(threads=8)
+    ds.load_oracle(o)
+    e = _engine(request.param)
+    ds.load_engine(e)
+    yield ds, o, e
+    _check_jit(e, request.param)
+    e.close()
+
+
+@pytest.mark.parametrize("qi", range(len(PL_QUERIES)))
+def test_powerlaw_supernodes(plaw, qi):
+    """C4 shape: seeds include the supernodes (in-degree 30000 = 15 chunks of 2048 edges each), so
+    one frontier entry spans many workgroups; REVERSELY has no pushdown (GoExecutor.cpp:528-533)."""
+    ds, o, e = plaw
+    seeds = [0, 7919, 15838, 23757] + [int(v) for v in datagen.sample_vids(300 + qi, ds.n, 20)]
+    q = PL_QUERIES[qi].replace("{S}", ", ".join(str(v) for v in seeds))
+    s = ngql.parse_go(q)
+    ref = o.go(ds.space, s)
+    got = e.go(ds.space, s)
+    assert ref.ok and got.ok, (got.error, ref.error)
+    assert got.hop_edges[:len(ref.hop_scanned)] == ref.hop_scanned[:len(got.hop_edges)]
+    assert fixtures.normalize_cells(got.rows) == fixtures.normalize_cells(ref.rows)
+
+
+# --------------------------------------------------------------------------- C5: SNB-like, strings
+SNB_QUERIES = [
+    "GO 4 STEPS FROM {S} OVER knows WHERE knows.creationDate > 1400000000 && $^.person.gender == \"female\" "
+    "YIELD knows._dst, knows.weight, $^.person.firstName, $$.person.age",
+    "GO 2 STEPS FROM {S} OVER knows, likes WHERE likes.creationDate > 1300000000 || knows.weight > 5.0 "
+    "YIELD knows._dst, likes._dst, likes.creationDate, knows.weight",
+    "GO 1 STEPS FROM {S} OVER likes WHERE $$.post.lang == \"en\" && $$.post.length > 40 "
+    "YIELD likes._dst, $$.post.content, $$.post.lang",
+    "GO 2 STEPS FROM {S} OVER hasCreator, likes REVERSELY WHERE likes.creationDate > 1400000000 "
+    "YIELD hasCreator._dst, likes._dst, likes.creationDate",
+    "GO 3 STEPS FROM {S} OVER * WHERE $^.person.firstName CONTAINS \"a\" YIELD knows._dst, likes._dst, hasCreator._dst",
+]
+
+
+@pytest.fixture(scope="module", params=["jit", "vm"])
+def snb(request):
+    ds = fixtures.snb_dataset(5000, threads=8)
+    o = oracle.Oracle()
+    o.set_flags(threads=8)
+    ds.load_oracle(o)
+    e = _engine(request.param)
+    ds.load_engine(e)
+    yield ds, o, e
+    _check_jit(e, request.param)
+    e.close()
+
+
+@pytest.mark.parametrize("pushdown", [True, False])
+@pytest.mark.parametrize("qi", range(len(SNB_QUERIES)))
+def test_snb_compound(snb, qi, pushdown):
+    """C5 shape: multi-edge-type schema with string + int props, a batch of person seeds, compound
+    WHERE over edge, $^ and $$ props, multi-column YIELD (strings returned through the columnar
+    result)."""
+    ds, o, e = snb
+    seeds = [int(v) for v in datagen.sample_vids(500 + qi, ds.np, 400)]
+    q = SNB_QUERIES[qi].replace("{S}", ", ".join(str(v) for v in seeds))
+    s = ngql.parse_go(q)
+    ref = o.go(ds.space, s, pushdown=pushdown)
+    got = e.go(ds.space, s, pushdown=pushdown)
+    assert got.ok == ref.ok, (got.error, ref.error)
+    if not ref.ok:
+        return
+    assert got.col_types == ref.col_types
+    assert fixtures.normalize_cells(got.rows) == fixtures.normalize_cells(ref.rows)
