@@ -31,6 +31,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
     ap.add_argument("--dominant", default="", help="kernel name substring whose traffic bench.py reads")
+    ap.add_argument("--kernel-class", default="final",
+                    help="bench.py's name for the dominant kernel (its roofline.kernel); written as kernel_class")
     args = ap.parse_args()
     src = os.path.join(ROOT, "gpurun_out", "prof", args.tag)
     dst = os.path.join(ROOT, "profiles")
@@ -80,10 +82,13 @@ def main():
         dom = [r for r in rows if args.dominant in r["kernel"]]
         if dom:
             d = dom[0]
-            traffic["kernel_class"] = args.dominant
+            traffic["kernel_class"] = args.kernel_class
+            traffic["kernel_name"] = d["kernel"]
             if d["fetch_bytes_x2"] is not None and d["write_bytes"] is not None:
                 traffic["bytes_per_launch"] = d["fetch_bytes_x2"] + d["write_bytes"]
     json.dump(traffic, open(os.path.join(dst, f"{args.tag}_traffic.json"), "w"), indent=1)
+    if "bytes_per_launch" in traffic:        # the file bench.py reads by default
+        json.dump(traffic, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
     print(open(os.path.join(dst, f"{args.tag}_summary.md")).read())
 
 
