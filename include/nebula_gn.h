@@ -57,11 +57,23 @@ extern "C" {
 
 typedef struct ngx_ctx ngx_ctx;
 
+/* Host-side collective for world > 1 in place of RCCL (rehearsal hook: ranks that share one GPU,
+ * e.g. torch.distributed gloo in the multi-shard tests). `bytes` is the block size per rank:
+ *   NGX_XCHG_ALLGATHER: send = 1 block, recv = world blocks in rank order;
+ *   NGX_XCHG_ALLTOALL:  send = world blocks (block q goes to rank q), recv = world blocks (block q
+ *                       came from rank q); the rank's own block is ignored.
+ * Returns 0 on success. Every rank calls it the same number of times with the same op and bytes. */
+#define NGX_XCHG_ALLGATHER 0
+#define NGX_XCHG_ALLTOALL 1
+typedef int32_t (*ngx_exchange_fn)(void* user, int32_t op, const void* send, void* recv, uint64_t bytes);
+
 typedef struct {
     int32_t device;               /* HIP device ordinal */
     int32_t rank;                 /* this shard (GPU) 0..world-1 */
     int32_t world;                /* shards on the node; part p lives on shard p % world */
-    const void* nccl_unique_id;   /* 128-byte ncclUniqueId when world > 1 */
+    const void* nccl_unique_id;   /* 128-byte ncclUniqueId when world > 1 and no host exchange */
+    ngx_exchange_fn exchange;     /* optional: host collective instead of RCCL (may be NULL) */
+    void* exchange_user;
 } ngx_config;
 
 int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out);

@@ -89,6 +89,8 @@ struct ngx_ctx {
     int32_t device = 0, rank = 0, world = 1;
     hipStream_t stream = nullptr;
     ncclComm_t comm = nullptr;
+    ngx_exchange_fn xchg = nullptr;                    // host collective instead of RCCL (tests)
+    void* xchgUser = nullptr;
     std::map<int32_t, std::unique_ptr<Space>> spaces;
     std::string lastError;
     std::mutex mu;
@@ -419,6 +421,23 @@ HopSlots makeHopSlots(const Space& sp, const DeviceGraph& d, const std::vector<i
     return hs;
 }
 
+// host collective (ngx_config.exchange): device blocks staged through host memory
+void hostExchange(ngx_ctx* c, int32_t op, const void* dsend, void* drecv, uint64_t bytes) {
+    uint64_t sendBytes = op == NGX_XCHG_ALLGATHER ? bytes : bytes * c->world;
+    std::vector<uint8_t> hs(sendBytes), hr(bytes * c->world);
+    HIP_OK(hipMemcpyAsync(hs.data(), dsend, sendBytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    if (c->xchg(c->xchgUser, op, hs.data(), hr.data(), bytes) != 0) throw Error{NGX_E_DEVICE, "host exchange failed"};
+    HIP_OK(hipMemcpyAsync(drecv, hr.data(), hr.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+}
+
+// all-gather of `bytes` per rank (rank order) over RCCL or the host exchange
+void allGather(ngx_ctx* c, const void* dsend, void* drecv, uint64_t bytes) {
+    if (c->xchg) hostExchange(c, NGX_XCHG_ALLGATHER, dsend, drecv, bytes);
+    else NCCL_OK(ncclAllGather(dsend, drecv, bytes, ncclUint8, c->comm, c->stream));
+}
+
 }  // namespace
 
 // ============================================================================ C ABI
@@ -442,7 +461,9 @@ int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return NGX_E_DEVICE;
     if (hipSetDevice(c->device) != hipSuccess) return NGX_E_DEVICE;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return NGX_E_DEVICE;
-    if (c->world > 1) {
+    c->xchg = cfg->exchange;
+    c->xchgUser = cfg->exchange_user;
+    if (c->world > 1 && !c->xchg) {
         if (!cfg->nccl_unique_id) return NGX_E_BAD_ARGUMENT;
         ncclUniqueId id;
         std::memcpy(&id, cfg->nccl_unique_id, sizeof(id));
@@ -551,7 +572,7 @@ int32_t ngx_commit(ngx_ctx* c, int32_t space) {
             uint64_t* dcnt = c->misc.get<uint64_t>(c->world * 2);
             uint64_t myCount = mine.size();
             HIP_OK(hipMemcpyAsync(dcnt + c->world, &myCount, 8, hipMemcpyHostToDevice, c->stream));
-            NCCL_OK(ncclAllGather(dcnt + c->world, dcnt, 1, ncclUint64, c->comm, c->stream));
+            allGather(c, dcnt + c->world, dcnt, 8);
             std::vector<uint64_t> counts(c->world);
             HIP_OK(hipMemcpyAsync(counts.data(), dcnt, 8 * c->world, hipMemcpyDeviceToHost, c->stream));
             HIP_OK(hipStreamSynchronize(c->stream));
@@ -561,7 +582,7 @@ int32_t ngx_commit(ngx_ctx* c, int32_t space) {
             int64_t* sendb = c->sendBits.get<int64_t>(std::max<uint64_t>(maxc * 2, 2));
             int64_t* recvb = c->recvBits.get<int64_t>(std::max<uint64_t>(maxc * 2 * c->world, 2));
             HIP_OK(hipMemcpyAsync(sendb, packed.data(), maxc * 16, hipMemcpyHostToDevice, c->stream));
-            NCCL_OK(ncclAllGather(sendb, recvb, maxc * 2, ncclInt64, c->comm, c->stream));
+            allGather(c, sendb, recvb, maxc * 16);
             std::vector<int64_t> all(maxc * 2 * c->world);
             HIP_OK(hipMemcpyAsync(all.data(), recvb, all.size() * 8, hipMemcpyDeviceToHost, c->stream));
             HIP_OK(hipStreamSynchronize(c->stream));
@@ -763,14 +784,18 @@ void exchangeFrontier(ngx_ctx* c, const DeviceGraph& d, uint8_t epoch) {
         uint64_t n = sb[q + 1] - sb[q];
         if (launchPack(c->visited.get<uint8_t>(d.vglobal), epoch, sb[q], n, send + q * maxWords, c->stream)) throw Error{NGX_E_DEVICE, "pack"};
     }
-    NCCL_OK(ncclGroupStart());
-    for (int q = 0; q < W; q++) {
-        if (q == c->rank) continue;
-        uint64_t nq = (sb[q + 1] - sb[q] + 63) / 64;
-        if (nq) NCCL_OK(ncclSend(send + q * maxWords, nq * 8, ncclUint8, q, c->comm, c->stream));
-        if (myWords) NCCL_OK(ncclRecv(recv + q * maxWords, myWords * 8, ncclUint8, q, c->comm, c->stream));
+    if (c->xchg) {
+        hostExchange(c, NGX_XCHG_ALLTOALL, send, recv, maxWords * 8);
+    } else {
+        NCCL_OK(ncclGroupStart());
+        for (int q = 0; q < W; q++) {
+            if (q == c->rank) continue;
+            uint64_t nq = (sb[q + 1] - sb[q] + 63) / 64;
+            if (nq) NCCL_OK(ncclSend(send + q * maxWords, nq * 8, ncclUint8, q, c->comm, c->stream));
+            if (myWords) NCCL_OK(ncclRecv(recv + q * maxWords, myWords * 8, ncclUint8, q, c->comm, c->stream));
+        }
+        NCCL_OK(ncclGroupEnd());
     }
-    NCCL_OK(ncclGroupEnd());
     for (int q = 0; q < W; q++) {
         if (q == c->rank) continue;
         if (launchMerge(recv + q * maxWords, myRows, c->visited.get<uint8_t>(d.vglobal), sb[c->rank], epoch, c->stream))
@@ -799,12 +824,37 @@ uint64_t* zeroedLookBack(ngx_ctx* c, uint64_t chunks) {
     return p;
 }
 
-// size the result columns for `cap` rows (keeping `keep`) and upload their descriptors
-const OutCol* prepareCols(ngx_ctx* c, const std::vector<ColSpec>& spec, uint64_t cap, uint64_t keep) {
+// YIELD columns that are exactly an edge key prop of every edge the hop expands (`e._dst`,
+// `e._src`, `e._rank` of the only OVER type, typed INT/VID): their cells equal the oSrc/oDst/oRank
+// row, so the column aliases that array instead of storing the same 8 B per row again.
+std::vector<int32_t> keyAliases(const Programs& progs, const std::vector<int32_t>& colTypes, const HopSlots& hs) {
+    std::vector<int32_t> k(progs.yOff.size(), -1);
+    for (size_t y = 0; y < progs.yOff.size(); y++) {
+        const Insn* code = progs.code.data() + progs.yOff[y];
+        int32_t ct = y < colTypes.size() ? colTypes[y] : T_UNKNOWN;
+        if (code[1].op != OP_END || !(ct == T_INT || ct == T_VID || ct == T_TIMESTAMP)) continue;
+        int32_t key = code[0].op == OP_EDST ? 1 : (code[0].op == OP_EKEY && code[0].a >= 0 && code[0].a <= 2) ? code[0].a : -1;
+        if (key < 0) continue;
+        bool all = true;
+        for (int s = 0; s < hs.n; s++) all = all && (code[0].b == 0 || std::abs(hs.etype[s]) == code[0].b);
+        if (all) k[y] = key;
+    }
+    return k;
+}
+
+// size the result columns for `cap` rows (keeping `keep`) and upload their descriptors; aliased
+// key columns (keyAliases) point at oSrc/oDst/oRank, which must already be sized
+const OutCol* prepareCols(ngx_ctx* c, const std::vector<ColSpec>& spec, uint64_t cap, uint64_t keep,
+                          const std::vector<int32_t>& alias = {}) {
     if (c->oCols.size() < spec.size()) c->oCols.resize(spec.size());
     c->oColView.assign(spec.size(), OutCol{nullptr, nullptr, nullptr});
     for (size_t y = 0; y < spec.size(); y++) {
         auto& cb = c->oCols[y];
+        if (y < alias.size() && alias[y] >= 0) {
+            DBuf& kb = alias[y] == 0 ? c->oSrc : alias[y] == 1 ? c->oDst : c->oRank;
+            c->oColView[y].x = static_cast<int64_t*>(kb.p);
+            continue;
+        }
         growKeep(c, cb.x, cap * 8, keep * 8);
         c->oColView[y].x = static_cast<int64_t*>(cb.x.p);
         if (spec[y].len) { growKeep(c, cb.len, cap * 4, keep * 4); c->oColView[y].len = static_cast<uint32_t*>(cb.len.p); }
@@ -917,6 +967,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     bool wIsP = pushHere && gp.where && encodeExpr(*gp.pushed) == encodeExpr(*gp.where);
     std::vector<int32_t> hopTypes;
     HopSlots hs = makeHopSlots(sp, d, gp.edgeTypes, hopTypes);
+    const std::vector<int32_t> yAlias = keyAliases(progs, gp.colTypes, hs);
     // per-query straight-line kernels (jit.cpp); the interpreter kernels otherwise
     const JitKernels* jk = nullptr;
     const JitKernels* jkNoP = nullptr;                       // record hops before the last (no pushdown)
@@ -928,6 +979,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         jq.W = JitProgram{progs.W >= 0 ? progs.code.data() + progs.W : nullptr, progs.W >= 0};
         for (int32_t off : progs.yOff) jq.Y.push_back(JitProgram{progs.code.data() + off, true});
         jq.yColType = gp.colTypes;
+        jq.yKey = yAlias;
         std::string jerr;
         std::string src = jitSource(sp, jq);
         if (!src.empty()) jk = c->jit.get(src, jerr);
@@ -1048,7 +1100,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             growKeep(c, c->oDst, cap * 8, totalRows * 8);
             growKeep(c, c->oRank, cap * 8, totalRows * 8);
             growKeep(c, c->oType, cap * 4, totalRows * 4);
-            a.oCols = prepareCols(c, colSpec, cap, totalRows);
+            a.oCols = prepareCols(c, colSpec, cap, totalRows, yAlias);
             a.oBase = totalRows;
             a.oSrc = static_cast<int64_t*>(c->oSrc.p);
             a.oDst = static_cast<int64_t*>(c->oDst.p);

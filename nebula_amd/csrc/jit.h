@@ -31,6 +31,8 @@ struct JitQuery {
     JitProgram P, W;
     std::vector<JitProgram> Y;
     std::vector<int32_t> yColType;  // calculateExprType per column
+    std::vector<int32_t> yKey;      // >= 0: column is the edge's key prop (0 src, 1 dst, 2 rank), written
+                                    // once as oSrc/oDst/oRank and aliased, not stored again (engine.cpp keyAliases)
     bool oneSlot = false;           // the hop expands a single edge-type slot (ONE kernels)
 };
 
