@@ -44,7 +44,8 @@ P = ctypes.POINTER
 
 
 class Config(ctypes.Structure):
-    _fields_ = [("device", c_i32), ("rank", c_i32), ("world", c_i32), ("nccl_unique_id", ctypes.c_void_p)]
+    _fields_ = [("device", c_i32), ("rank", c_i32), ("world", c_i32), ("nccl_unique_id", ctypes.c_void_p),
+                ("exchange", ctypes.c_void_p), ("exchange_user", ctypes.c_void_p)]
 
 
 class KVBatchC(ctypes.Structure):
@@ -151,6 +152,36 @@ def lib():
     return _lib
 
 
+XCHG_ALLGATHER, XCHG_ALLTOALL = 0, 1
+ExchangeFn = ctypes.CFUNCTYPE(c_i32, ctypes.c_void_p, c_i32, ctypes.c_void_p, ctypes.c_void_p, c_u64)
+
+
+def dist_exchange(group=None):
+    """Host collective for ngx_config.exchange over torch.distributed (gloo): lets world > 1 shards
+    share one GPU (multi-shard tests) where RCCL needs one GPU per rank. Semantics: nebula_gn.h."""
+    import torch
+    import torch.distributed as dist
+
+    def fn(user, op, send, recv, nbytes):
+        try:
+            w, me = dist.get_world_size(group), dist.get_rank(group)
+            n_send = nbytes if op == XCHG_ALLGATHER else nbytes * w
+            sb = torch.frombuffer(bytearray(ctypes.string_at(send, n_send)), dtype=torch.uint8) if n_send else \
+                torch.zeros(0, dtype=torch.uint8)
+            got = [torch.empty(n_send, dtype=torch.uint8) for _ in range(w)]
+            dist.all_gather(got, sb, group=group)     # gloo has no all_to_all: gather and pick blocks
+            if op == XCHG_ALLTOALL:
+                got = [g[me * nbytes:(me + 1) * nbytes] for g in got]
+            out = torch.cat(got).numpy()
+            if out.size:
+                ctypes.memmove(recv, out.ctypes.data, out.size)
+            return 0
+        except Exception:                          # never raise through the C ABI
+            return 1
+
+    return ExchangeFn(fn)
+
+
 def unique_id() -> bytes:
     buf = ctypes.create_string_buffer(128)
     rc = lib().ngx_get_unique_id(buf)
@@ -224,10 +255,15 @@ def _arr(ptr, n, dtype):
 
 # ----------------------------------------------------------------------------- engine
 class Engine:
-    def __init__(self, device: int = 0, rank: int = 0, world: int = 1, nccl_id: Optional[bytes] = None):
+    def __init__(self, device: int = 0, rank: int = 0, world: int = 1, nccl_id: Optional[bytes] = None,
+                 exchange=None):
+        """world > 1: one shard per rank over RCCL (nccl_id from unique_id() on rank 0), or over a host
+        collective `exchange` (dist_exchange()) when the ranks share a GPU."""
         self.L = lib()
         self._uid = ctypes.create_string_buffer(nccl_id, 128) if nccl_id else None
-        cfg = Config(device, rank, world, ctypes.cast(self._uid, ctypes.c_void_p) if self._uid else None)
+        self._xchg = exchange                      # keep the ctypes callback alive with the context
+        cfg = Config(device, rank, world, ctypes.cast(self._uid, ctypes.c_void_p) if self._uid else None,
+                     ctypes.cast(exchange, ctypes.c_void_p) if exchange else None, None)
         h = ctypes.c_void_p()
         rc = self.L.ngx_open(ctypes.byref(cfg), ctypes.byref(h))
         if rc:
