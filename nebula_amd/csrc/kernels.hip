@@ -173,6 +173,9 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
 
 // ------------------------------------------------------------------------------ final hop (interpreter)
 struct VmEv {
+    static constexpr int kEager = -1;                 // YIELD evaluated in the write pass
+    static __device__ __forceinline__ void YV(const FinalArgs&, const EdgeCtx&, Val*) {}
+    static __device__ __forceinline__ void YS(const FinalArgs&, const Val*, uint64_t, uint32_t&) {}
     static __device__ __forceinline__ bool hasP(const FinalArgs& a) { return a.P != nullptr; }
     static __device__ __forceinline__ bool hasW(const FinalArgs& a) { return a.W != nullptr; }
     static __device__ __forceinline__ Val P(const FinalArgs& a, const EdgeCtx& ec) { return vmEval(a.P, a.env, ec); }
