@@ -39,6 +39,9 @@ def parse():
     p.add_argument("--parts", type=int, default=100)
     p.add_argument("--cpu-budget", type=float, default=10.0, help="target seconds of oracle work (0: skip)")
     p.add_argument("--threads", type=int, default=16, help="host threads for datagen / oracle")
+    p.add_argument("--host-exchange", action="store_true",
+                   help="rehearsal of the N > 1 path on one GPU: every rank on device 0, frontier exchange "
+                        "through the host collective (gloo) instead of RCCL")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch of the dominant kernel (from profiles/)")
     return p.parse_args()
@@ -58,19 +61,23 @@ def main():
     import torch.distributed as dist
     from nebula_amd import datagen, engine, ngql
 
-    torch.cuda.set_device(local)
-    uid = None
+    device = 0 if args.host_exchange else local
+    torch.cuda.set_device(device)
+    uid, xchg = None, None
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        obj = [engine.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        uid = obj[0]
+        if args.host_exchange:
+            xchg = engine.dist_exchange()
+        else:
+            obj = [engine.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            uid = obj[0]
 
     t0 = time.time()
     rows = datagen.rmat(scale, args.ef, 42, args.parts, with_in=False, with_tag=False, rank=rank, world=world,
                         threads=args.threads)
     log(f"[rank {rank}] generated {rows.n} rows of RMAT scale {scale} in {time.time() - t0:.1f}s")
-    eng = engine.Engine(local, rank, world, uid)
+    eng = engine.Engine(device, rank, world, uid, exchange=xchg)
     eng.add_space(datagen.RMAT_SPACE, args.parts)
     for is_edge, sid, name, fields in datagen.rmat_schemas():
         eng.add_schema(datagen.RMAT_SPACE, is_edge, sid, name, fields)
@@ -178,7 +185,9 @@ def main():
                                    f"{args.parts} parts, GO 3 STEPS from {args.seeds} vids WHERE e.p0 < 50",
                        "scale": scale, "edge_factor": args.ef, "parts": args.parts, "seeds": args.seeds,
                        "query": QUERY.replace("{S}", f"<{args.seeds} vids>"),
-                       "parallelism": f"{world} shard(s), part % {world}, RCCL bitmap all-to-all per hop"},
+                       "parallelism": f"{world} shard(s), part % {world}, "
+                                      + ("host (gloo) exchange, all shards on GPU 0 (rehearsal)" if args.host_exchange
+                                         else "RCCL bitmap all-to-all per hop")},
             "roofline": roof,
             "cpu_baseline": cpu,
             "edges_per_step": edges // args.steps,
