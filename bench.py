@@ -138,7 +138,8 @@ def main():
     barrier()
     host_ms = (time.perf_counter() - t_h) * 1e3 / max(host_steps, 1)
     jit = {"compiled": eng.get_flag("jit_compiled"), "failed": eng.get_flag("jit_failed"),
-           "compile_ms": eng.get_flag("jit_compile_us") / 1e3, "note": eng.jit_note()}
+           "compile_ms": eng.get_flag("jit_compile_us") / 1e3, "vgprs": eng.get_flag("jit_vgprs"),
+           "scratch_bytes": eng.get_flag("jit_scratch"), "note": eng.jit_note()}
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)

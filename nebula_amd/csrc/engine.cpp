@@ -663,6 +663,8 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "jit_hits") *value = static_cast<int64_t>(c->jit.hits);
     else if (n == "jit_failed") *value = static_cast<int64_t>(c->jit.failed);
     else if (n == "jit_compile_us") *value = static_cast<int64_t>(c->jit.compileSeconds * 1e6);
+    else if (n == "jit_vgprs") *value = c->jit.lastRegs;          // registers / scratch of the last compiled
+    else if (n == "jit_scratch") *value = c->jit.lastScratch;     // final-hop kernel (occupancy check)
     else return fail(c, NGX_E_BAD_ARGUMENT, "unknown flag " + n);
     return NGX_OK;
 }
@@ -975,6 +977,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     if (c->jitOn) {
         JitQuery jq;
         jq.oneSlot = hs.n == 1;
+        jq.pos32 = true;
+        for (int s = 0; s < hs.n; s++) jq.pos32 = jq.pos32 && sp.host->slots[hs.slotIdx[s]].dst.size() < (1ULL << 32);
         jq.P = JitProgram{progs.P >= 0 ? progs.code.data() + progs.P : nullptr, progs.P >= 0};
         jq.W = JitProgram{progs.W >= 0 ? progs.code.data() + progs.W : nullptr, progs.W >= 0};
         for (int32_t off : progs.yOff) jq.Y.push_back(JitProgram{progs.code.data() + off, true});

@@ -34,6 +34,7 @@ struct JitQuery {
     std::vector<int32_t> yKey;      // >= 0: column is the edge's key prop (0 src, 1 dst, 2 rank), written
                                     // once as oSrc/oDst/oRank and aliased, not stored again (engine.cpp keyAliases)
     bool oneSlot = false;           // the hop expands a single edge-type slot (ONE kernels)
+    bool pos32 = false;             // every CSR position of the hop's slots fits 32 bits (ChunkMap P32)
 };
 
 class JitCache {
@@ -43,6 +44,7 @@ public:
     const JitKernels* get(const std::string& source, std::string& err);
     uint64_t compiled = 0, hits = 0, failed = 0;
     double compileSeconds = 0;
+    int64_t lastRegs = -1, lastScratch = -1;    // hipFuncGetAttribute of the last compiled kernel
 
 private:
     std::map<std::string, JitKernels> cache_;

@@ -149,7 +149,7 @@ template <bool ONE>
 __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst,
                                                     uint64_t nEnt, uint64_t E, HopSlots hs, uint8_t* visited,
                                                     uint8_t epoch) {
-    __shared__ ChunkMap<false> m;
+    __shared__ ChunkMap<ONE, false> m;
     const uint64_t base = static_cast<uint64_t>(blockIdx.x) * CE;
     const uint32_t cnt = static_cast<uint32_t>(E - base < CE ? E - base : CE);
     buildMap<ONE, false>(estart, chunkFirst, nEnt, blockIdx.x, gridDim.x, base, cnt, F, hs, m);
@@ -174,6 +174,7 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
 // ------------------------------------------------------------------------------ final hop (interpreter)
 struct VmEv {
     static constexpr int kEager = -1;                 // YIELD evaluated in the write pass
+    static constexpr bool kPos32 = false;             // 64-bit CSR positions in the chunk map
     static __device__ __forceinline__ void YV(const FinalArgs&, const EdgeCtx&, Val*) {}
     static __device__ __forceinline__ void YS(const FinalArgs&, const Val*, uint64_t, uint32_t&) {}
     static __device__ __forceinline__ bool hasP(const FinalArgs& a) { return a.P != nullptr; }
