@@ -1050,6 +1050,13 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     std::vector<ColSpec> colSpec;
     for (int32_t ct : gp.colTypes) colSpec.push_back(ColSpec{ct == T_UNKNOWN || ct == T_STRING, ct == T_UNKNOWN});
 
+    // the compaction after an intermediate hop also writes the next hop's estart[] and E (fused
+    // scan) when the packed (|F|, E) total fits; the slot totals bound E
+    uint64_t slotEdges = 0;
+    for (int s = 0; s < hs.n; s++) slotEdges += sp.host->slots[hs.slotIdx[s]].dst.size();
+    const bool fuseDeg = d.V < (1ULL << (64 - kFdShift)) && slotEdges <= kFdMask && hs.n > 0;
+    bool haveEstart = false;                                   // estart[] / E of this hop already built
+    uint64_t fusedE = 0;
     for (uint32_t h = 1; h <= steps; h++) {
         bool isRecord = h >= recordFrom;
         bool isFinal = h == steps;
@@ -1057,12 +1064,15 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         uint64_t* estart = c->estart.get<uint64_t>(nEnt + 1);
         uint64_t* tiles = c->tileSums.get<uint64_t>((std::max<uint64_t>(nEnt, 1) + kTile - 1) / kTile + 1);
         uint64_t E = 0;
-        if (nEnt) {
+        if (haveEstart) {
+            E = nEnt ? fusedE : 0;
+        } else if (nEnt) {
             c->timed("degree_scan", nEnt * 24, [&] {
                 if (launchDegreeScan(F, nEnt, hs, estart, tiles, c->stream)) throw Error{NGX_E_DEVICE, "degree scan"};
             });
             E = readScalar(c, estart + nEnt);
         }
+        haveEstart = false;
         R.hopFrontier.push_back(nF);
         R.hopEdges.push_back(E);
         uint64_t chunks = (E + kChunk - 1) / kChunk;
@@ -1136,12 +1146,27 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         if (c->world > 1) c->timed("exchange", 0, [&] { exchangeFrontier(c, d, ep); });
         uint32_t* Fn = (F == c->F0.p) ? c->F1.get<uint32_t>(std::max<uint64_t>(d.V, 1)) : c->F0.get<uint32_t>(std::max<uint64_t>(d.V, 1));
         uint64_t* tiles2 = c->tileSums.get<uint64_t>((std::max<uint64_t>(d.V, 1) + kTile - 1) / kTile + 1);
-        c->timed("compact", 0, [&] {
-            if (launchCompact(c->visited.get<uint8_t>(d.vglobal), d.gbase, d.V, ep, Fn, tiles2, counters + 2, c->stream))
-                throw Error{NGX_E_DEVICE, "compact"};
-        });
-        nF = readScalar(c, counters + 2);
-        c->addBytes("compact", nF * 8);
+        if (fuseDeg) {
+            // estart sized for any next frontier (every row of the shard) so the next hop's get() keeps it
+            uint64_t* est = c->estart.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
+            c->timed("compact_degrees", 0, [&] {
+                if (launchCompactDegrees(c->visited.get<uint8_t>(d.vglobal), d.gbase, d.V, ep, hs, Fn, est, tiles2,
+                                         counters + 2, c->stream))
+                    throw Error{NGX_E_DEVICE, "compact"};
+            });
+            uint64_t packed = readScalar(c, counters + 2);
+            nF = packed >> kFdShift;
+            fusedE = packed & kFdMask;
+            haveEstart = true;
+            c->addBytes("compact_degrees", nF * 8 + nF * static_cast<uint64_t>(hs.n) * 24);
+        } else {
+            c->timed("compact", 0, [&] {
+                if (launchCompact(c->visited.get<uint8_t>(d.vglobal), d.gbase, d.V, ep, Fn, tiles2, counters + 2, c->stream))
+                    throw Error{NGX_E_DEVICE, "compact"};
+            });
+            nF = readScalar(c, counters + 2);
+            c->addBytes("compact", nF * 8);
+        }
         R.hopNext.push_back(nF);
         F = Fn;
         if (nF == 0 && c->world == 1) break;                    // GO_EXIT: empty frontier

@@ -18,6 +18,13 @@ int launchExpandMark(const uint32_t* F, const uint64_t* estart, const uint64_t* 
                      const HopSlots& hs, uint8_t* visited, uint8_t epoch, hipStream_t s);
 int launchCompact(const uint8_t* visited, uint64_t gbase, uint64_t V, uint8_t epoch, uint32_t* outF,
                   uint64_t* tileSums, uint64_t* count, hipStream_t s);
+// fused compaction + next-hop degree scan (kernels.hip FlagDegIn): outF gets the next frontier,
+// estart its entries' edge offsets (|F| * hs.n + 1 entries, the last = E), *packedTotal = |F| << kFdShift | E.
+// Requires V < 2^(64 - kFdShift) and the slots' total edges < 2^kFdShift.
+constexpr int kFdShift = 36;
+constexpr uint64_t kFdMask = (1ULL << kFdShift) - 1;
+int launchCompactDegrees(const uint8_t* visited, uint64_t gbase, uint64_t V, uint8_t epoch, const HopSlots& hs,
+                         uint32_t* outF, uint64_t* estart, uint64_t* tileSums, uint64_t* packedTotal, hipStream_t s);
 // final hop, one pass (interpreter kernel): a.lbStatus zeroed, ceil(E / kChunk) + 1 words; outputs
 // sized for a.oBase + a.E rows. a.oEntry set (GetNeighbors): rows in edge order, rows written = the
 // inclusive status of the last chunk; else (GO) chunks in completion order, rows written = lbStatus[0]

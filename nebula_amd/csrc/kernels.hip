@@ -52,6 +52,38 @@ struct WriteCompact {
     __device__ __forceinline__ void operator()(uint64_t i, uint64_t v, uint64_t pre) const { if (v) out[pre] = static_cast<uint32_t>(i); }
 };
 
+// Fused compaction + next-hop degree scan: one scan over the shard's rows of the pair
+// (1 if visited[row] == epoch, the row's degree over the hop's slots), packed as count << kFdShift | degree
+// (host guarantees V < 2^(64 - kFdShift) rows and E < 2^kFdShift edges). The write phase stores the
+// next frontier row AND its entries' estart, so the next hop needs no separate degree scan and the
+// host reads |F| and E together in one round trip.
+struct FlagDegIn {
+    const uint8_t* visited;
+    uint64_t gbase;
+    uint8_t epoch;
+    HopSlots hs;
+    __device__ __forceinline__ uint64_t operator()(uint64_t r) const {
+        if (visited[gbase + r] != epoch) return 0;
+        uint64_t d = 0;
+        for (int s = 0; s < hs.n; s++) d += hs.off[s][r + 1] - hs.off[s][r];
+        return (1ULL << kFdShift) | d;
+    }
+};
+struct WriteCompactEstart {
+    uint32_t* out;
+    uint64_t* estart;
+    HopSlots hs;
+    __device__ __forceinline__ void operator()(uint64_t r, uint64_t v, uint64_t pre) const {
+        if (!v) return;
+        uint64_t f = pre >> kFdShift, e = pre & kFdMask;
+        out[f] = static_cast<uint32_t>(r);
+        for (int s = 0; s < hs.n; s++) {
+            estart[f * hs.n + s] = e;
+            e += hs.off[s][r + 1] - hs.off[s][r];
+        }
+    }
+};
+
 template <class In>
 __global__ __launch_bounds__(WG) void k_tile_reduce(In in, uint64_t n, uint64_t* tileSums) {
     __shared__ uint64_t sm[NW + 1];
@@ -63,7 +95,8 @@ __global__ __launch_bounds__(WG) void k_tile_reduce(In in, uint64_t n, uint64_t*
     if (threadIdx.x == 0) tileSums[blockIdx.x] = t;
 }
 
-__global__ __launch_bounds__(1024) void k_scan_tiles(uint64_t* sums, uint64_t nt, uint64_t* total) {
+// tail != nullptr (fused compaction): also writes estart[|F| * ns] = E from the packed total
+__global__ __launch_bounds__(1024) void k_scan_tiles(uint64_t* sums, uint64_t nt, uint64_t* total, uint64_t* tail, int ns) {
     __shared__ uint64_t sm[1024 / 64 + 1];
     uint64_t per = (nt + 1023) / 1024;
     uint64_t lo = threadIdx.x * per, hi = lo + per < nt ? lo + per : nt;
@@ -86,7 +119,10 @@ __global__ __launch_bounds__(1024) void k_scan_tiles(uint64_t* sums, uint64_t nt
     __syncthreads();
     uint64_t pre = sm[wid] + x - s;
     for (uint64_t i = lo; i < hi; i++) { uint64_t t = sums[i]; sums[i] = pre; pre += t; }
-    if (threadIdx.x == 0) *total = sm[16];
+    if (threadIdx.x == 0) {
+        *total = sm[16];
+        if (tail) tail[(sm[16] >> kFdShift) * static_cast<uint64_t>(ns)] = sm[16] & kFdMask;
+    }
 }
 
 template <class In, class Out>
@@ -107,11 +143,16 @@ __global__ __launch_bounds__(WG) void k_tile_scan(In in, uint64_t n, const uint6
 }
 
 template <class In, class Out>
-static int scan3(In in, uint64_t n, Out out, uint64_t* tileSums, uint64_t* total, hipStream_t s) {
+static int scan3(In in, uint64_t n, Out out, uint64_t* tileSums, uint64_t* total, hipStream_t s,
+                 uint64_t* tail = nullptr, int ns = 0) {
     uint64_t nt = (n + TILE - 1) / TILE;
-    if (nt == 0) { (void)hipMemsetAsync(total, 0, 8, s); return 0; }
+    if (nt == 0) {
+        (void)hipMemsetAsync(total, 0, 8, s);
+        if (tail) (void)hipMemsetAsync(tail, 0, 8, s);
+        return 0;
+    }
     hipLaunchKernelGGL(k_tile_reduce<In>, dim3(static_cast<unsigned>(nt)), dim3(WG), 0, s, in, n, tileSums);
-    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, s, tileSums, nt, total);
+    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, s, tileSums, nt, total, tail, ns);
     hipLaunchKernelGGL((k_tile_scan<In, Out>), dim3(static_cast<unsigned>(nt)), dim3(WG), 0, s, in, n, tileSums, out);
     return static_cast<int>(hipGetLastError());
 }
@@ -272,6 +313,12 @@ int launchExpandMark(const uint32_t* F, const uint64_t* estart, const uint64_t* 
 int launchCompact(const uint8_t* visited, uint64_t gbase, uint64_t V, uint8_t epoch, uint32_t* outF, uint64_t* tileSums,
                   uint64_t* count, hipStream_t s) {
     return scan3(FlagIn{visited, gbase, epoch}, V, WriteCompact{outF}, tileSums, count, s);
+}
+
+int launchCompactDegrees(const uint8_t* visited, uint64_t gbase, uint64_t V, uint8_t epoch, const HopSlots& hs,
+                         uint32_t* outF, uint64_t* estart, uint64_t* tileSums, uint64_t* packedTotal, hipStream_t s) {
+    return scan3(FlagDegIn{visited, gbase, epoch, hs}, V, WriteCompactEstart{outF, estart, hs}, tileSums, packedTotal,
+                 s, estart, hs.n);
 }
 
 int launchFinal(const FinalArgs& a, hipStream_t s) {
