@@ -1053,7 +1053,12 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     // the compaction after an intermediate hop also writes the next hop's estart[] and E (fused
     // scan) when the packed (|F|, E) total fits; the slot totals bound E
     uint64_t slotEdges = 0;
-    for (int s = 0; s < hs.n; s++) slotEdges += sp.host->slots[hs.slotIdx[s]].dst.size();
+    bool pos32 = true;                                         // every CSR position fits 32 bits
+    for (int s = 0; s < hs.n; s++) {
+        uint64_t es = sp.host->slots[hs.slotIdx[s]].dst.size();
+        slotEdges += es;
+        pos32 = pos32 && es < (1ULL << 32);
+    }
     const bool fuseDeg = d.V < (1ULL << (64 - kFdShift)) && slotEdges <= kFdMask && hs.n > 0;
     bool haveEstart = false;                                   // estart[] / E of this hop already built
     uint64_t fusedE = 0;
@@ -1139,7 +1144,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         uint8_t ep = nextEpoch(c);
         if (E) {
             c->timed("expand", E * 8, [&] {
-                if (launchExpandMark(F, estart, chunkFirst, nEnt, E, hs, c->visited.get<uint8_t>(d.vglobal), ep, c->stream))
+                if (launchExpandMark(F, estart, chunkFirst, nEnt, E, hs, c->visited.get<uint8_t>(d.vglobal), ep, pos32, c->stream))
                     throw Error{NGX_E_DEVICE, "expand"};
             });
         }

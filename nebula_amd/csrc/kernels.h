@@ -15,7 +15,7 @@ int launchDegreeScan(const uint32_t* F, uint64_t nEnt, const HopSlots& hs, uint6
 // chunkFirst must hold ceil(E / kChunk) entries (estart[nEnt] = E)
 int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst, hipStream_t s);
 int launchExpandMark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst, uint64_t nEnt, uint64_t E,
-                     const HopSlots& hs, uint8_t* visited, uint8_t epoch, hipStream_t s);
+                     const HopSlots& hs, uint8_t* visited, uint8_t epoch, bool pos32, hipStream_t s);
 int launchCompact(const uint8_t* visited, uint64_t gbase, uint64_t V, uint8_t epoch, uint32_t* outF,
                   uint64_t* tileSums, uint64_t* count, hipStream_t s);
 // fused compaction + next-hop degree scan (kernels.hip FlagDegIn): outF gets the next frontier,

@@ -186,14 +186,15 @@ __global__ void k_chunk_first(const uint64_t* estart, uint64_t nEnt, uint64_t* c
 // Edge-balanced expansion: every edge of the hop reads its 4-byte destination row and stores the
 // hop's epoch into visited[] (the frontier dedup of GoExecutor::getDstIdsFromResp, a set of dsts).
 // The store is unconditional: a byte store needs no read and duplicates write the same value.
-template <bool ONE>
+// P32: CSR positions fit 32 bits (20 KiB chunk map instead of 28, see ChunkMap)
+template <bool ONE, bool P32>
 __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst,
                                                     uint64_t nEnt, uint64_t E, HopSlots hs, uint8_t* visited,
                                                     uint8_t epoch) {
-    __shared__ ChunkMap<ONE, false> m;
+    __shared__ ChunkMap<ONE, false, P32> m;
     const uint64_t base = static_cast<uint64_t>(blockIdx.x) * CE;
     const uint32_t cnt = static_cast<uint32_t>(E - base < CE ? E - base : CE);
-    buildMap<ONE, false>(estart, chunkFirst, nEnt, blockIdx.x, gridDim.x, base, cnt, F, hs, m);
+    buildMap<ONE, false, P32>(estart, chunkFirst, nEnt, blockIdx.x, gridDim.x, base, cnt, F, hs, m);
     uint32_t g[CITEMS];
 #pragma unroll
     for (int k = 0; k < CITEMS; k++) {
@@ -202,7 +203,8 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
         if (p < cnt) {
             uint32_t q = m.at[p];
             int s = ONE ? 0 : m.slot[q];
-            uint64_t pos = static_cast<uint64_t>(static_cast<int64_t>(base + p) + m.pb[q]);
+            uint64_t pos = P32 ? static_cast<uint64_t>(static_cast<uint32_t>(base + p) + static_cast<uint32_t>(m.pb[q]))
+                               : static_cast<uint64_t>(static_cast<int64_t>(base + p) + static_cast<int64_t>(m.pb[q]));
             g[k] = hs.dgid[s][pos];
         }
     }
@@ -302,11 +304,13 @@ int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst
 }
 
 int launchExpandMark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst, uint64_t nEnt, uint64_t E,
-                     const HopSlots& hs, uint8_t* visited, uint8_t epoch, hipStream_t s) {
+                     const HopSlots& hs, uint8_t* visited, uint8_t epoch, bool pos32, hipStream_t s) {
     if (E == 0) return 0;
     dim3 grid(static_cast<unsigned>((E + CE - 1) / CE));
-    if (hs.n == 1) hipLaunchKernelGGL(k_expand_mark<true>, grid, dim3(WG), 0, s, F, estart, chunkFirst, nEnt, E, hs, visited, epoch);
-    else hipLaunchKernelGGL(k_expand_mark<false>, grid, dim3(WG), 0, s, F, estart, chunkFirst, nEnt, E, hs, visited, epoch);
+    if (hs.n == 1 && pos32) hipLaunchKernelGGL((k_expand_mark<true, true>), grid, dim3(WG), 0, s, F, estart, chunkFirst, nEnt, E, hs, visited, epoch);
+    else if (hs.n == 1) hipLaunchKernelGGL((k_expand_mark<true, false>), grid, dim3(WG), 0, s, F, estart, chunkFirst, nEnt, E, hs, visited, epoch);
+    else if (pos32) hipLaunchKernelGGL((k_expand_mark<false, true>), grid, dim3(WG), 0, s, F, estart, chunkFirst, nEnt, E, hs, visited, epoch);
+    else hipLaunchKernelGGL((k_expand_mark<false, false>), grid, dim3(WG), 0, s, F, estart, chunkFirst, nEnt, E, hs, visited, epoch);
     return static_cast<int>(hipGetLastError());
 }
 
