@@ -90,6 +90,9 @@ struct ngx_ctx {
     hipStream_t stream = nullptr;
     ncclComm_t comm = nullptr;
     ngx_exchange_fn xchg = nullptr;                    // host collective instead of RCCL (tests)
+    uint64_t* pin = nullptr;                           // host-mapped [value, seq]: scan totals published by
+    uint64_t* pinDev = nullptr;                        // k_scan_tiles (kernels.h Publish)
+    uint64_t pinSeq = 0;
     void* xchgUser = nullptr;
     std::map<int32_t, std::unique_ptr<Space>> spaces;
     std::string lastError;
@@ -373,6 +376,27 @@ T readScalar(ngx_ctx* c, const T* dev) {
     return v;
 }
 
+// next publication slot for a scan total (none when the mapped buffer is unavailable)
+Publish nextPub(ngx_ctx* c) {
+    if (!c->pinDev) return Publish{nullptr, 0};
+    return Publish{c->pinDev, ++c->pinSeq};
+}
+
+// the published scan total: poll the host-mapped slot (no stream round trip); after ~50 ms block on
+// the stream, and read the device copy if the slot still disagrees
+uint64_t awaitPub(ngx_ctx* c, const Publish& p, const uint64_t* devCopy) {
+    if (!p.slot) return readScalar(c, devCopy);
+    auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0;; i++) {
+        if (__atomic_load_n(&c->pin[1], __ATOMIC_ACQUIRE) == p.seq) return __atomic_load_n(&c->pin[0], __ATOMIC_RELAXED);
+        __builtin_ia32_pause();
+        if ((i & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
+    }
+    HIP_OK(hipStreamSynchronize(c->stream));
+    if (__atomic_load_n(&c->pin[1], __ATOMIC_ACQUIRE) == p.seq) return __atomic_load_n(&c->pin[0], __ATOMIC_RELAXED);
+    return readScalar(c, devCopy);
+}
+
 struct ColSpec { bool len, t; };
 
 // Result holders: the C structs point into these vectors
@@ -461,6 +485,12 @@ int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return NGX_E_DEVICE;
     if (hipSetDevice(c->device) != hipSuccess) return NGX_E_DEVICE;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return NGX_E_DEVICE;
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->pin), 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+        std::memset(c->pin, 0, 64);
+        if (hipHostGetDevicePointer(reinterpret_cast<void**>(&c->pinDev), c->pin, 0) != hipSuccess) c->pinDev = nullptr;
+    } else {
+        c->pin = nullptr;
+    }
     c->xchg = cfg->exchange;
     c->xchgUser = cfg->exchange_user;
     if (c->world > 1 && !c->xchg) {
@@ -487,6 +517,7 @@ void ngx_close(ngx_ctx* c) {
         for (auto& cb : c->oCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         for (auto e : c->eventPool) (void)hipEventDestroy(e);
         if (c->comm) ncclCommDestroy(c->comm);
+        if (c->pin) (void)hipHostFree(c->pin);
         (void)hipStreamDestroy(c->stream);
     }
     delete c;
@@ -1072,10 +1103,11 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         if (haveEstart) {
             E = nEnt ? fusedE : 0;
         } else if (nEnt) {
+            Publish pub = nextPub(c);
             c->timed("degree_scan", nEnt * 24, [&] {
-                if (launchDegreeScan(F, nEnt, hs, estart, tiles, c->stream)) throw Error{NGX_E_DEVICE, "degree scan"};
+                if (launchDegreeScan(F, nEnt, hs, estart, tiles, c->stream, pub)) throw Error{NGX_E_DEVICE, "degree scan"};
             });
-            E = readScalar(c, estart + nEnt);
+            E = awaitPub(c, pub, estart + nEnt);
         }
         haveEstart = false;
         R.hopFrontier.push_back(nF);
@@ -1154,12 +1186,13 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         if (fuseDeg) {
             // estart sized for any next frontier (every row of the shard) so the next hop's get() keeps it
             uint64_t* est = c->estart.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
+            Publish pub = nextPub(c);
             c->timed("compact_degrees", 0, [&] {
                 if (launchCompactDegrees(c->visited.get<uint8_t>(d.vglobal), d.gbase, d.V, ep, hs, Fn, est, tiles2,
-                                         counters + 2, c->stream))
+                                         counters + 2, c->stream, pub))
                     throw Error{NGX_E_DEVICE, "compact"};
             });
-            uint64_t packed = readScalar(c, counters + 2);
+            uint64_t packed = awaitPub(c, pub, counters + 2);
             nF = packed >> kFdShift;
             fusedE = packed & kFdMask;
             haveEstart = true;

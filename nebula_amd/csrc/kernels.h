@@ -7,11 +7,17 @@
 
 namespace ngx {
 
+// host-mapped publication slot of a scan total: slot[0] = value, slot[1] = seq (written last)
+struct Publish {
+    uint64_t* slot;
+    uint64_t seq;
+};
+
 int launchLookup(const int32_t* qpart, const int64_t* qvid, uint64_t n, const int32_t* vpart, const int64_t* vid,
                  uint64_t V, uint32_t* out, hipStream_t s);
 // estart must hold nEnt + 1 entries; estart[nEnt] receives E
 int launchDegreeScan(const uint32_t* F, uint64_t nEnt, const HopSlots& hs, uint64_t* estart, uint64_t* tileSums,
-                     hipStream_t s);
+                     hipStream_t s, Publish pub = Publish{nullptr, 0});
 // chunkFirst must hold ceil(E / kChunk) entries (estart[nEnt] = E)
 int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst, hipStream_t s);
 int launchExpandMark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst, uint64_t nEnt, uint64_t E,
@@ -24,7 +30,8 @@ int launchCompact(const uint8_t* visited, uint64_t gbase, uint64_t V, uint8_t ep
 constexpr int kFdShift = 36;
 constexpr uint64_t kFdMask = (1ULL << kFdShift) - 1;
 int launchCompactDegrees(const uint8_t* visited, uint64_t gbase, uint64_t V, uint8_t epoch, const HopSlots& hs,
-                         uint32_t* outF, uint64_t* estart, uint64_t* tileSums, uint64_t* packedTotal, hipStream_t s);
+                         uint32_t* outF, uint64_t* estart, uint64_t* tileSums, uint64_t* packedTotal, hipStream_t s,
+                         Publish pub = Publish{nullptr, 0});
 // final hop, one pass (interpreter kernel): a.lbStatus zeroed, ceil(E / kChunk) + 1 words; outputs
 // sized for a.oBase + a.E rows. a.oEntry set (GetNeighbors): rows in edge order, rows written = the
 // inclusive status of the last chunk; else (GO) chunks in completion order, rows written = lbStatus[0]

@@ -96,7 +96,10 @@ __global__ __launch_bounds__(WG) void k_tile_reduce(In in, uint64_t n, uint64_t*
 }
 
 // tail != nullptr (fused compaction): also writes estart[|F| * ns] = E from the packed total
-__global__ __launch_bounds__(1024) void k_scan_tiles(uint64_t* sums, uint64_t nt, uint64_t* total, uint64_t* tail, int ns) {
+// pub.slot != nullptr: the total is also published to host-mapped memory (value, then the sequence
+// number with a system-scope release store), so the host learns it while the scan's last phase runs
+__global__ __launch_bounds__(1024) void k_scan_tiles(uint64_t* sums, uint64_t nt, uint64_t* total, uint64_t* tail, int ns,
+                                                     Publish pub) {
     __shared__ uint64_t sm[1024 / 64 + 1];
     uint64_t per = (nt + 1023) / 1024;
     uint64_t lo = threadIdx.x * per, hi = lo + per < nt ? lo + per : nt;
@@ -122,6 +125,10 @@ __global__ __launch_bounds__(1024) void k_scan_tiles(uint64_t* sums, uint64_t nt
     if (threadIdx.x == 0) {
         *total = sm[16];
         if (tail) tail[(sm[16] >> kFdShift) * static_cast<uint64_t>(ns)] = sm[16] & kFdMask;
+        if (pub.slot) {
+            __hip_atomic_store(pub.slot, sm[16], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(pub.slot + 1, pub.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -144,15 +151,14 @@ __global__ __launch_bounds__(WG) void k_tile_scan(In in, uint64_t n, const uint6
 
 template <class In, class Out>
 static int scan3(In in, uint64_t n, Out out, uint64_t* tileSums, uint64_t* total, hipStream_t s,
-                 uint64_t* tail = nullptr, int ns = 0) {
+                 uint64_t* tail = nullptr, int ns = 0, Publish pub = Publish{nullptr, 0}) {
     uint64_t nt = (n + TILE - 1) / TILE;
-    if (nt == 0) {
-        (void)hipMemsetAsync(total, 0, 8, s);
-        if (tail) (void)hipMemsetAsync(tail, 0, 8, s);
-        return 0;
+    if (nt == 0) {                       // empty input: the 1-tile scan of nothing publishes 0 below
+        nt = 1;
+        n = 0;
     }
     hipLaunchKernelGGL(k_tile_reduce<In>, dim3(static_cast<unsigned>(nt)), dim3(WG), 0, s, in, n, tileSums);
-    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, s, tileSums, nt, total, tail, ns);
+    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, s, tileSums, nt, total, tail, ns, pub);
     hipLaunchKernelGGL((k_tile_scan<In, Out>), dim3(static_cast<unsigned>(nt)), dim3(WG), 0, s, in, n, tileSums, out);
     return static_cast<int>(hipGetLastError());
 }
@@ -293,8 +299,8 @@ int launchLookup(const int32_t* qpart, const int64_t* qvid, uint64_t n, const in
 }
 
 int launchDegreeScan(const uint32_t* F, uint64_t nEnt, const HopSlots& hs, uint64_t* estart, uint64_t* tileSums,
-                     hipStream_t s) {
-    return scan3(DegreeIn{F, hs}, nEnt, WriteEstart{estart}, tileSums, estart + nEnt, s);
+                     hipStream_t s, Publish pub) {
+    return scan3(DegreeIn{F, hs}, nEnt, WriteEstart{estart}, tileSums, estart + nEnt, s, nullptr, 0, pub);
 }
 
 int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst, hipStream_t s) {
@@ -320,9 +326,10 @@ int launchCompact(const uint8_t* visited, uint64_t gbase, uint64_t V, uint8_t ep
 }
 
 int launchCompactDegrees(const uint8_t* visited, uint64_t gbase, uint64_t V, uint8_t epoch, const HopSlots& hs,
-                         uint32_t* outF, uint64_t* estart, uint64_t* tileSums, uint64_t* packedTotal, hipStream_t s) {
+                         uint32_t* outF, uint64_t* estart, uint64_t* tileSums, uint64_t* packedTotal, hipStream_t s,
+                         Publish pub) {
     return scan3(FlagDegIn{visited, gbase, epoch, hs}, V, WriteCompactEstart{outF, estart, hs}, tileSums, packedTotal,
-                 s, estart, hs.n);
+                 s, estart, hs.n, pub);
 }
 
 int launchFinal(const FinalArgs& a, hipStream_t s) {
