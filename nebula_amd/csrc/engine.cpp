@@ -32,6 +32,7 @@ struct DeviceGraph {
     std::vector<uint64_t> shardBase;
     int32_t* vpart = nullptr;
     int64_t* vid = nullptr;
+    VIndex vindex{nullptr, 0};                          // (part, vid) -> row hash index (seed lookup)
     std::vector<DSlot> slots;
     std::vector<DTag> tags;
     std::vector<DCol> cols;
@@ -202,6 +203,17 @@ std::unique_ptr<DeviceGraph> upload(HostGraph& g) {
     d->shardBase = g.shardBase;
     d->vpart = d->upload(g.vpart.data(), d->V);
     d->vid = d->upload(g.vid.data(), d->V);
+    {
+        uint64_t cap = 1024;
+        while (cap < 2 * d->V) cap <<= 1;
+        std::vector<VIndexSlot> t(cap, VIndexSlot{0, 0, kNoRow});
+        for (uint64_t r = 0; r < d->V; r++) {
+            uint64_t h = vindexHash(g.vpart[r], g.vid[r]) & (cap - 1);
+            while (t[h].row != kNoRow) h = (h + 1) & (cap - 1);
+            t[h] = VIndexSlot{g.vid[r], g.vpart[r], static_cast<uint32_t>(r)};
+        }
+        d->vindex = VIndex{d->upload(t.data(), cap), cap - 1};
+    }
     for (auto& s : g.slots) {
         DSlot ds{};
         ds.etype = s.etype;
@@ -1063,14 +1075,28 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     HIP_OK(hipEventRecord(t0, c->stream));
     uint64_t nF = svids.size();
     uint32_t* F = c->F0.get<uint32_t>(std::max<uint64_t>(nF, 1));
+    bool haveEstart = false;                                   // estart[] / E of the next hop already built
+    uint64_t fusedE = 0;
     if (nF) {
         int32_t* dp_ = c->seedPart.get<int32_t>(nF);
         int64_t* dv = c->seedVid.get<int64_t>(nF);
         HIP_OK(hipMemcpyAsync(dp_, sparts.data(), nF * 4, hipMemcpyHostToDevice, c->stream));
         HIP_OK(hipMemcpyAsync(dv, svids.data(), nF * 8, hipMemcpyHostToDevice, c->stream));
-        c->timed("lookup", nF * 12, [&] {
-            if (launchLookup(dp_, dv, nF, d.vpart, d.vid, d.V, F, c->stream)) throw Error{NGX_E_DEVICE, "lookup"};
-        });
+        const uint64_t nEnt0 = nF * static_cast<uint64_t>(hs.n);
+        if (hs.n > 0 && nF <= kSeedFuseMax && nEnt0 <= kSeedFuseMax && d.vindex.slots) {
+            // lookup + degrees + scan of the seed hop in one workgroup; E published (no stream round trip)
+            uint64_t* est0 = c->estart.get<uint64_t>(nEnt0 + 1);
+            Publish pub = nextPub(c);
+            c->timed("seed", nF * 12 + nEnt0 * 24, [&] {
+                if (launchSeedFrontier(dp_, dv, nF, d.vindex, hs, F, est0, pub, c->stream)) throw Error{NGX_E_DEVICE, "seed"};
+            });
+            fusedE = awaitPub(c, pub, est0 + nEnt0);
+            haveEstart = true;
+        } else {
+            c->timed("lookup", nF * 12, [&] {
+                if (launchLookup(dp_, dv, nF, d.vpart, d.vid, d.V, F, c->stream)) throw Error{NGX_E_DEVICE, "lookup"};
+            });
+        }
     }
     uint64_t* counters = c->counters.get<uint64_t>(8);
     uint32_t* errFlag = reinterpret_cast<uint32_t*>(counters + 4);
@@ -1091,8 +1117,6 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         pos32 = pos32 && es < (1ULL << 32);
     }
     const bool fuseDeg = d.V < (1ULL << (64 - kFdShift)) && slotEdges <= kFdMask && hs.n > 0;
-    bool haveEstart = false;                                   // estart[] / E of this hop already built
-    uint64_t fusedE = 0;
     for (uint32_t h = 1; h <= steps; h++) {
         bool isRecord = h >= recordFrom;
         bool isFinal = h == steps;

@@ -13,6 +13,30 @@ struct Publish {
     uint64_t seq;
 };
 
+// (part, vid) -> shard vertex row: open-addressing table (linear probing, power-of-two capacity
+// >= 2V, built at commit) so a seed lookup is ~1 probe instead of a binary search over V rows
+struct VIndexSlot {
+    int64_t vid;
+    int32_t part;
+    uint32_t row;                       // kNoRow: empty
+};
+struct VIndex {
+    const VIndexSlot* slots;
+    uint64_t mask;                      // capacity - 1
+};
+__host__ __device__ inline uint64_t vindexHash(int32_t part, int64_t vid) {
+    uint64_t h = static_cast<uint64_t>(vid) * 0x9E3779B97F4A7C15ULL ^ static_cast<uint64_t>(static_cast<uint32_t>(part)) * 0xC2B2AE3D27D4EB4FULL;
+    h ^= h >> 29;
+    h *= 0xBF58476D1CE4E5B9ULL;
+    return h ^ (h >> 32);
+}
+
+// seed hop in ONE single-workgroup launch (n seeds, n * hs.n <= kSeedFuseMax entries): lookup through
+// the index -> F, entry degrees -> estart (n * hs.n + 1 entries, the last = E), E published
+constexpr uint64_t kSeedFuseMax = 4096;
+int launchSeedFrontier(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, const HopSlots& hs,
+                       uint32_t* F, uint64_t* estart, Publish pub, hipStream_t s);
+
 int launchLookup(const int32_t* qpart, const int64_t* qvid, uint64_t n, const int32_t* vpart, const int64_t* vid,
                  uint64_t V, uint32_t* out, hipStream_t s);
 // estart must hold nEnt + 1 entries; estart[nEnt] receives E

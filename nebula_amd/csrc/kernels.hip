@@ -179,6 +179,73 @@ __global__ void k_lookup(const int32_t* qpart, const int64_t* qvid, uint64_t n, 
     out[i] = (lo < V && vpart[lo] == p && vid[lo] == v) ? static_cast<uint32_t>(lo) : kNoRow;
 }
 
+__device__ __forceinline__ uint32_t vindexFind(const VIndex& idx, int32_t part, int64_t vid) {
+    uint64_t h = vindexHash(part, vid) & idx.mask;
+    for (uint64_t probe = 0; probe <= idx.mask; probe++) {
+        const VIndexSlot& sl = idx.slots[h];
+        if (sl.row == kNoRow) return kNoRow;
+        if (sl.vid == vid && sl.part == part) return sl.row;
+        h = (h + 1) & idx.mask;
+    }
+    return kNoRow;
+}
+
+// 1024 threads; thread t owns seeds [t*per, t*per + per) and their entries (contiguous)
+__global__ __launch_bounds__(1024) void k_seed_frontier(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx,
+                                                        HopSlots hs, uint32_t* F, uint64_t* estart, Publish pub) {
+    __shared__ uint64_t sm[1024 / 64 + 1];
+    constexpr int kPer = static_cast<int>(kSeedFuseMax / 1024);
+    const uint64_t per = (n + 1023) / 1024;
+    const uint64_t lo = threadIdx.x * per;
+    uint32_t rows[kPer];
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        rows[k] = kNoRow;
+        uint64_t i = lo + k;
+        if (k < static_cast<int>(per) && i < n) {
+            rows[k] = vindexFind(idx, qpart[i], qvid[i]);
+            F[i] = rows[k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        if (rows[k] == kNoRow) continue;
+        for (int s = 0; s < hs.n; s++) sum += hs.off[s][rows[k] + 1] - hs.off[s][rows[k]];
+    }
+    int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint64_t x = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+        uint64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sm[wid] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t acc = 0;
+        for (int w = 0; w < 16; w++) { uint64_t t = sm[w]; sm[w] = acc; acc += t; }
+        sm[16] = acc;
+    }
+    __syncthreads();
+    uint64_t pre = sm[wid] + x - sum;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        uint64_t i = lo + k;
+        if (k >= static_cast<int>(per) || i >= n) continue;
+        for (int s = 0; s < hs.n; s++) {
+            estart[i * hs.n + s] = pre;
+            if (rows[k] != kNoRow) pre += hs.off[s][rows[k] + 1] - hs.off[s][rows[k]];
+        }
+    }
+    if (threadIdx.x == 0) {
+        estart[n * hs.n] = sm[16];
+        if (pub.slot) {
+            __hip_atomic_store(pub.slot, sm[16], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(pub.slot + 1, pub.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------ chunk -> first entry
 // chunkFirst[c] = the entry holding edge c * CE (the only entry with estart[i] <= c*CE < estart[i+1])
 __global__ void k_chunk_first(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst) {
@@ -301,6 +368,13 @@ int launchLookup(const int32_t* qpart, const int64_t* qvid, uint64_t n, const in
 int launchDegreeScan(const uint32_t* F, uint64_t nEnt, const HopSlots& hs, uint64_t* estart, uint64_t* tileSums,
                      hipStream_t s, Publish pub) {
     return scan3(DegreeIn{F, hs}, nEnt, WriteEstart{estart}, tileSums, estart + nEnt, s, nullptr, 0, pub);
+}
+
+int launchSeedFrontier(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, const HopSlots& hs,
+                       uint32_t* F, uint64_t* estart, Publish pub, hipStream_t s) {
+    if (n * static_cast<uint64_t>(hs.n) > kSeedFuseMax || n > kSeedFuseMax || idx.slots == nullptr) return 1;
+    hipLaunchKernelGGL(k_seed_frontier, dim3(1), dim3(1024), 0, s, qpart, qvid, n, idx, hs, F, estart, pub);
+    return static_cast<int>(hipGetLastError());
 }
 
 int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst, hipStream_t s) {
