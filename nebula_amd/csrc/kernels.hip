@@ -265,6 +265,11 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
                                                     uint64_t nEnt, uint64_t E, HopSlots hs, uint8_t* visited,
                                                     uint8_t epoch) {
     __shared__ ChunkMap<ONE, false, P32> m;
+    // direct-mapped LDS filter of the rows this workgroup already marked: a repeated destination
+    // (hubs of a power-law graph) costs an LDS probe instead of another L2 byte-store transaction
+    constexpr int kSeenBits = 11;
+    __shared__ uint32_t seen[1 << kSeenBits];
+    for (int p = threadIdx.x; p < (1 << kSeenBits); p += WG) seen[p] = kNoRow;
     const uint64_t base = static_cast<uint64_t>(blockIdx.x) * CE;
     const uint32_t cnt = static_cast<uint32_t>(E - base < CE ? E - base : CE);
     buildMap<ONE, false, P32>(estart, chunkFirst, nEnt, blockIdx.x, gridDim.x, base, cnt, F, hs, m);
@@ -283,7 +288,11 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
     }
 #pragma unroll
     for (int k = 0; k < CITEMS; k++) {
-        if (g[k] != kNoRow) visited[g[k]] = epoch;
+        if (g[k] == kNoRow) continue;
+        uint32_t h = (g[k] * 2654435761u) >> (32 - kSeenBits);
+        if (seen[h] == g[k]) continue;                  // marked by this workgroup already (its store is issued)
+        seen[h] = g[k];
+        visited[g[k]] = epoch;
     }
 }
 
