@@ -51,7 +51,8 @@ private:
     std::map<std::string, std::string> failures_;
 };
 
-// C++ source of the evaluator struct + kernels for one query on one space snapshot
+// C++ source of the evaluator struct + kernels for one query on one space snapshot (without the
+// common device headers, which JitCache::get prepends when it compiles; the cache key is this text)
 std::string jitSource(const Space& sp, const JitQuery& q);
 
 }  // namespace ngx
