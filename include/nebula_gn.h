@@ -234,8 +234,9 @@ typedef struct {
     const int64_t* dev_src;
     const int64_t* dev_dst;
     const int64_t* dev_rank;
-    const int32_t* dev_type;
+    const int32_t* dev_type;           /* NULL when the query has one OVER type: see dev_type_const */
     const ngx_dev_column* dev_cols;    /* ncols columns */
+    int32_t dev_type_const;            /* signed type of every row when dev_type is NULL */
 } ngx_go_result;
 
 int32_t ngx_go(ngx_ctx* ctx, const ngx_go_plan* plan, ngx_go_result** out);

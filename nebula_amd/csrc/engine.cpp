@@ -1012,6 +1012,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     bool wIsP = pushHere && gp.where && encodeExpr(*gp.pushed) == encodeExpr(*gp.where);
     std::vector<int32_t> hopTypes;
     HopSlots hs = makeHopSlots(sp, d, gp.edgeTypes, hopTypes);
+    // one OVER type: every row's type is hs.etype[0], so the final hop writes no per-row type column
+    const bool constType = hs.n == 1;
     const std::vector<int32_t> yAlias = keyAliases(progs, gp.colTypes, hs);
     // per-query straight-line kernels (jit.cpp); the interpreter kernels otherwise
     const JitKernels* jk = nullptr;
@@ -1180,7 +1182,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             a.oSrc = static_cast<int64_t*>(c->oSrc.p);
             a.oDst = static_cast<int64_t*>(c->oDst.p);
             a.oRank = static_cast<int64_t*>(c->oRank.p);
-            a.oType = static_cast<int32_t*>(c->oType.p);
+            a.oType = constType ? nullptr : static_cast<int32_t*>(c->oType.p);
             a.oEntry = nullptr;
             a.lbStatus = zeroedLookBack(c, chunks);
             c->timed("final", E * 8 * (2 + kf), [&] {
@@ -1252,7 +1254,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         R.r.dev_src = static_cast<const int64_t*>(c->oSrc.p);
         R.r.dev_dst = static_cast<const int64_t*>(c->oDst.p);
         R.r.dev_rank = static_cast<const int64_t*>(c->oRank.p);
-        R.r.dev_type = static_cast<const int32_t*>(c->oType.p);
+        R.r.dev_type = constType ? nullptr : static_cast<const int32_t*>(c->oType.p);
+        R.r.dev_type_const = constType ? hs.etype[0] : 0;
         R.devCols.clear();
         for (int32_t y = 0; y < nY; y++) {
             bool have = y < static_cast<int32_t>(c->oColView.size()) && totalRows;
@@ -1269,7 +1272,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         HIP_OK(hipMemcpyAsync(R.src.data(), c->oSrc.p, totalRows * 8, hipMemcpyDeviceToHost, c->stream));
         HIP_OK(hipMemcpyAsync(R.dst.data(), c->oDst.p, totalRows * 8, hipMemcpyDeviceToHost, c->stream));
         HIP_OK(hipMemcpyAsync(R.rank.data(), c->oRank.p, totalRows * 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_OK(hipMemcpyAsync(R.type.data(), c->oType.p, totalRows * 4, hipMemcpyDeviceToHost, c->stream));
+        if (constType) std::fill(R.type.begin(), R.type.end(), hs.etype[0]);
+        else HIP_OK(hipMemcpyAsync(R.type.data(), c->oType.p, totalRows * 4, hipMemcpyDeviceToHost, c->stream));
         raw = downloadCells(c, colSpec, gp.colTypes, totalRows, 0);
     }
     R.cells.resize(totalRows * nY);

@@ -98,7 +98,8 @@ class GoResultC(ctypes.Structure):
                 ("strings", ctypes.c_void_p), ("strings_len", c_u64), ("nhops", c_i32),
                 ("hop_frontier", P(c_u64)), ("hop_edges", P(c_u64)), ("hop_next", P(c_u64)),
                 ("device_ms", c_dbl), ("dev_src", ctypes.c_void_p), ("dev_dst", ctypes.c_void_p),
-                ("dev_rank", ctypes.c_void_p), ("dev_type", ctypes.c_void_p), ("dev_cols", ctypes.c_void_p)]
+                ("dev_rank", ctypes.c_void_p), ("dev_type", ctypes.c_void_p), ("dev_cols", ctypes.c_void_p),
+                ("dev_type_const", ctypes.c_int32)]
 
 
 class KernelStat(ctypes.Structure):
@@ -381,7 +382,8 @@ class Engine:
                     res.src = self._d2h(r.dev_src, n, np.int64)
                     res.dst = self._d2h(r.dev_dst, n, np.int64)
                     res.rank = self._d2h(r.dev_rank, n, np.int64)
-                    res.etype = self._d2h(r.dev_type, n, np.int32)
+                    res.etype = (self._d2h(r.dev_type, n, np.int32) if r.dev_type
+                                 else np.full(n, r.dev_type_const, np.int32))   # one OVER type: no column
                     cols = ctypes.cast(r.dev_cols, P(DevColumn)) if r.dev_cols else None
                     for c in range(r.ncols):
                         dc = cols[c]
