@@ -174,12 +174,34 @@ Space* findSpace(ngx_ctx* c, int32_t id) {
 }
 
 // ------------------------------------------------------------------------ upload
+// Integer columns can be stored at the narrowest signed width that holds every value (HBM bytes per
+// edge for a filter/YIELD column: 8 -> 1 for a 0..99 property); loads sign-extend (vm.h:loadI64).
+template <class T>
+const void* uploadAs(DeviceGraph& d, const std::vector<int64_t>& v, uint64_t n) {
+    std::vector<T> t(n);
+    for (uint64_t i = 0; i < n; i++) t[i] = static_cast<T>(v[i]);
+    return d.upload(t.data(), n);
+}
+const void* uploadNarrow(DeviceGraph& d, const std::vector<int64_t>& v, uint64_t n, int32_t& width) {
+    // Opt-in (NGX_NARROW=1): measured on MI355X at C2 the final hop reads 0.46 GB less per launch with
+    // p0 as int8 but runs 736 -> 775 us (same-box A/B, profiles/r01_s6n_*), so 8-byte storage stays the default.
+    const bool on = std::getenv("NGX_NARROW") != nullptr && std::getenv("NGX_NARROW")[0] == '1';
+    if (!on) { width = 8; return d.upload(v.data(), n); }
+    int64_t lo = 0, hi = 0;
+    for (uint64_t i = 0; i < n; i++) { lo = std::min(lo, v[i]); hi = std::max(hi, v[i]); }
+    if (lo >= INT8_MIN && hi <= INT8_MAX) { width = 1; return uploadAs<int8_t>(d, v, n); }
+    if (lo >= INT16_MIN && hi <= INT16_MAX) { width = 2; return uploadAs<int16_t>(d, v, n); }
+    if (lo >= INT32_MIN && hi <= INT32_MAX) { width = 4; return uploadAs<int32_t>(d, v, n); }
+    width = 8;
+    return d.upload(v.data(), n);
+}
+
 void uploadColumns(DeviceGraph& d, std::vector<HostColumn>& hc, uint64_t n) {
     for (auto& c : hc) {
         DCol dc{};
         dc.type = c.type;
         switch (c.type) {
-            case T_INT: case T_TIMESTAMP: case T_VID: dc.data = d.upload(c.i64.data(), n); break;
+            case T_INT: case T_TIMESTAMP: case T_VID: dc.data = uploadNarrow(d, c.i64, n, dc.width); break;
             case T_FLOAT: case T_DOUBLE: dc.data = d.upload(c.f64.data(), n); break;
             case T_BOOL: dc.data = d.upload(c.b.data(), n); break;
             case T_STRING: {
@@ -191,6 +213,7 @@ void uploadColumns(DeviceGraph& d, std::vector<HostColumn>& hc, uint64_t n) {
             default: break;
         }
         if (!c.allValid) dc.valid = d.upload(c.valid.data(), n);
+        if (dc.width) c.width = dc.width;
         d.cols.push_back(dc);
     }
 }
@@ -1043,7 +1066,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         if (!jk) c->jitNote = jerr.empty() ? "jit: unsupported program" : jerr;
     }
     // algorithmic-byte model inputs: k_f prop columns read by the filter, k_y yielded
-    uint64_t kf = 0, ky = 0;
+    uint64_t ky = 0, kfBytes = 0;
     {
         PropRefs wr, yr;
         if (gp.where) collectRefs(*gp.where, wr);
@@ -1053,8 +1076,21 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             for (auto& ap : r.alias) n += (ap.second != "_src" && ap.second != "_dst" && ap.second != "_rank" && ap.second != "_type");
             return n + r.srcTag.size() + r.dstTag.size();
         };
-        kf = count(wr);
         ky = count(yr);
+        // bytes per edge read for the filter's edge props: their stored width (narrowed INT columns)
+        for (auto& ap : wr.alias) {
+            if (ap.second == "_src" || ap.second == "_dst" || ap.second == "_rank" || ap.second == "_type") continue;
+            uint64_t w = 0;
+            for (int s = 0; s < hs.n; s++) {
+                const SchemaSet* es = sp.edge(std::abs(hs.etype[s]));
+                int32_t ci = es ? es->latest().index(ap.second) : -1;
+                if (ci < 0) continue;
+                const DCol& dc = d.cols[hs.colBase[s] + ci];
+                w = std::max<uint64_t>(w, dc.width > 0 ? static_cast<uint64_t>(dc.width) : 8);
+            }
+            kfBytes += w ? w : 8;
+        }
+        kfBytes += 8 * (wr.srcTag.size() + wr.dstTag.size());
     }
 
     if (p.result_on_device && p.distinct) return fail(c, NGX_E_UNSUPPORTED, "YIELD DISTINCT needs host results");
@@ -1185,7 +1221,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             a.oType = constType ? nullptr : static_cast<int32_t*>(c->oType.p);
             a.oEntry = nullptr;
             a.lbStatus = zeroedLookBack(c, chunks);
-            c->timed("final", E * 8 * (2 + kf), [&] {
+            c->timed("final", E * (16 + kfBytes), [&] {
                 if (kj) {
                     void* args[] = {&a};
                     HIP_OK(hipModuleLaunchKernel(kj->final, static_cast<unsigned>(chunks), 1, 1, 256, 1, 1, 0, c->stream, args, nullptr));

@@ -22,8 +22,8 @@ enum : uint8_t {
 // device column descriptor
 struct DCol {
     int32_t type;          // SType of the latest schema
-    int32_t pad;
-    const void* data;      // int64_t (INT/TIMESTAMP/VID), double (FLOAT/DOUBLE), uint8_t (BOOL)
+    int32_t width;         // INT/TIMESTAMP/VID storage bytes: 1, 2, 4 (narrowed at export, sign-extended) or 8
+    const void* data;      // int64_t (INT/TIMESTAMP/VID; see width), double (FLOAT/DOUBLE), uint8_t (BOOL)
     const uint64_t* soff;  // STRING: n + 1 offsets
     const char* sbytes;    // STRING bytes
     const uint8_t* valid;  // nullptr when every row had the field

@@ -66,6 +66,7 @@ struct HostColumn {
     std::string sbytes;                 // STRING bytes
     std::vector<uint8_t> valid;         // 0 where the row's schema version lacks the field
     bool allValid = true;
+    int32_t width = 8;                  // INT/TIMESTAMP/VID bytes per value on the device (set at upload)
 };
 
 struct HostSlot {                       // one signed edge type: CSR over the shard's vertex rows

@@ -123,9 +123,19 @@ __device__ __forceinline__ uint64_t hashBytes(const unsigned char* p, uint64_t n
     return h;
 }
 
+// integer column element: the column is stored at the narrowest signed width holding all its values
+// (export-time choice, uniform per column, so the branch is scalar)
+__device__ __forceinline__ int64_t loadI64(const DCol& c, uint64_t i) {
+    switch (c.width) {
+        case 1: return static_cast<const int8_t*>(c.data)[i];
+        case 2: return static_cast<const int16_t*>(c.data)[i];
+        case 4: return static_cast<const int32_t*>(c.data)[i];
+        default: return static_cast<const int64_t*>(c.data)[i];
+    }
+}
 __device__ __forceinline__ Val loadCol(const DCol& c, uint64_t i) {
     switch (c.type) {
-        case 2: case 21: case 3: return mkInt(static_cast<const int64_t*>(c.data)[i]);
+        case 2: case 21: case 3: return mkInt(loadI64(c, i));
         case 4: case 5: return mkDbl(static_cast<const double*>(c.data)[i]);
         case 1: return mkBool(static_cast<const uint8_t*>(c.data)[i] != 0);
         case 6: {
@@ -158,9 +168,17 @@ __device__ __forceinline__ bool mulOverflow(int64_t lv, int64_t rv) {    // Expr
 }
 
 // ------------------------------------------------------------------------------ loads
-template <int CT>                       // column type known at compile time (JIT)
+template <int W>                        // integer storage width known at compile time (JIT); 0: read c.width
+__device__ __forceinline__ int64_t loadI64T(const DCol& c, uint64_t i) {
+    if constexpr (W == 1) return static_cast<const int8_t*>(c.data)[i];
+    else if constexpr (W == 2) return static_cast<const int16_t*>(c.data)[i];
+    else if constexpr (W == 4) return static_cast<const int32_t*>(c.data)[i];
+    else if constexpr (W == 8) return static_cast<const int64_t*>(c.data)[i];
+    else return loadI64(c, i);
+}
+template <int CT, int W = 0>            // column type (and integer width) known at compile time (JIT)
 __device__ __forceinline__ Val loadColT(const DCol& c, uint64_t i) {
-    if constexpr (CT == 2 || CT == 21 || CT == 3) return mkInt(static_cast<const int64_t*>(c.data)[i]);
+    if constexpr (CT == 2 || CT == 21 || CT == 3) return mkInt(loadI64T<W>(c, i));
     else if constexpr (CT == 4 || CT == 5) return mkDbl(static_cast<const double*>(c.data)[i]);
     else if constexpr (CT == 1) return mkBool(static_cast<const uint8_t*>(c.data)[i] != 0);
     else if constexpr (CT == 6) {
@@ -177,13 +195,13 @@ __device__ __forceinline__ Val defaultOfTypeT() {
 }
 
 // OP_ECOL: edge column a of |type| b; mode bit0 mismatch -> dflt, bit1 missing field -> type default
-template <int CT>
+template <int CT, int W = 0>
 __device__ __forceinline__ Val opEcolT(const VmEnv& env, const EdgeCtx& ec, int32_t a, int32_t b, uint8_t mode, Val dflt) {
     int32_t at = ec.etype < 0 ? -ec.etype : ec.etype;
     if (at != b) return (mode & 1) ? dflt : mkErr();
     const DCol& c = ec.cols[a];
     if (c.valid != nullptr && c.valid[ec.pos] == 0) return (mode & 2) ? defaultOfTypeT<CT>() : mkErr();
-    return loadColT<CT>(c, ec.pos);
+    return loadColT<CT, W>(c, ec.pos);
 }
 __device__ __forceinline__ Val opEcol(const VmEnv& env, const EdgeCtx& ec, int32_t a, int32_t b, uint8_t mode, Val dflt) {
     int32_t at = ec.etype < 0 ? -ec.etype : ec.etype;
@@ -203,13 +221,13 @@ __device__ __forceinline__ Val opEdst(const EdgeCtx& ec, int32_t b) {
     return mkInt((b != 0 && at != b) ? 0 : ec.dst);
 }
 // OP_SRCTAG / OP_DSTTAG: column a of tag slot b for the src / dst row
-template <int CT>
+template <int CT, int W = 0>
 __device__ __forceinline__ Val opTagT(const VmEnv& env, uint32_t row, int32_t a, int32_t b, uint8_t mode, Val dflt) {
     const DTag& t = env.tags[b];
     if (row == kNoRow || t.present[row] == 0) return (mode & 1) ? dflt : mkErr();
     const DCol& c = env.cols[t.colBase + a];
     if (c.valid != nullptr && c.valid[row] == 0) return defaultOfTypeT<CT>();
-    return loadColT<CT>(c, row);
+    return loadColT<CT, W>(c, row);
 }
 __device__ __forceinline__ Val opTag(const VmEnv& env, uint32_t row, int32_t a, int32_t b, uint8_t mode, Val dflt) {
     const DTag& t = env.tags[b];

@@ -11,6 +11,8 @@ known answers.
 Results are compared sorted (verifyResult, src/graph/test/TestBase.h:188-233); integers and
 doubles bit-exact.
 """
+import os
+
 import pytest
 
 from nebula_amd import datagen, engine, ngql
@@ -25,23 +27,37 @@ def _engine(mode):
     """An engine on device 0 running the final hop through per-query hipRTC kernels ("jit") or the
     precompiled bytecode interpreter ("vm")."""
     e = engine.Engine(0)
-    e.set_flag("jit", 1 if mode == "jit" else 0)
+    e.set_flag("jit", 1 if mode.startswith("jit") else 0)
     return e
 
 
+def _load(ds, e, mode):
+    """Commit the dataset to the engine; "-narrow" modes store integer columns at their narrowest width
+    (NGX_NARROW=1, read at commit: int8/int16 columns sign-extended on load)."""
+    old = os.environ.get("NGX_NARROW")
+    os.environ["NGX_NARROW"] = "1" if mode.endswith("-narrow") else "0"
+    try:
+        ds.load_engine(e)
+    finally:
+        if old is None:
+            del os.environ["NGX_NARROW"]
+        else:
+            os.environ["NGX_NARROW"] = old
+
+
 def _check_jit(e, mode):
-    if mode == "jit":
+    if mode.startswith("jit"):
         assert e.get_flag("jit_failed") == 0, e.jit_note()
         assert e.jit_note() == ""
 
 
-@pytest.fixture(scope="module", params=["jit", "vm"])
+@pytest.fixture(scope="module", params=["jit", "vm", "jit-narrow", "vm-narrow"])
 def nba(request):
     ds = fixtures.nba()
     o = oracle.Oracle()
     ds.load_oracle(o)
     e = _engine(request.param)
-    ds.load_engine(e)
+    _load(ds, e, request.param)
     yield ds, o, e
     _check_jit(e, request.param)
     e.close()
@@ -190,14 +206,14 @@ RMAT_QUERIES = [
 ]
 
 
-@pytest.fixture(scope="module", params=["jit", "vm"])
+@pytest.fixture(scope="module", params=["jit", "vm", "jit-narrow", "vm-narrow"])
 def rmat(request):
     ds = fixtures.RmatDataset(12, with_in=True, with_tag=True)
     o = oracle.Oracle()
     o.set_flags(threads=8)
     ds.load_oracle(o)
     e = _engine(request.param)
-    ds.load_engine(e)
+    _load(ds, e, request.param)
     yield ds, o, e
     _check_jit(e, request.param)
     e.close()
@@ -284,7 +300,7 @@ def rmat16(request):
     o.set_flags(threads=8)
     ds.load_oracle(o)
     e = _engine(request.param)
-    ds.load_engine(e)
+    _load(ds, e, request.param)
     yield ds, o, e
     _check_jit(e, request.param)
     e.close()
@@ -322,7 +338,7 @@ def plaw(request):
     o.set_flags(threads=8)
     ds.load_oracle(o)
     e = _engine(request.param)
-    ds.load_engine(e)
+    _load(ds, e, request.param)
     yield ds, o, e
     _check_jit(e, request.param)
     e.close()
@@ -364,7 +380,7 @@ def snb(request):
     o.set_flags(threads=8)
     ds.load_oracle(o)
     e = _engine(request.param)
-    ds.load_engine(e)
+    _load(ds, e, request.param)
     yield ds, o, e
     _check_jit(e, request.param)
     e.close()
