@@ -49,3 +49,19 @@ def test_hash_string_is_libstdcxx_hash():
     for name in ["Tim Duncan", "Tony Parker", "LaMarcus Aldridge", ""]:
         b = name.encode()
         assert L.ngx_hash_string(b, len(b)) == ngql.nebula_hash(name)
+
+
+def test_go_result_layout_matches_header(tmp_path):
+    """The ctypes mirror of ngx_go_result (nebula_amd/engine.py) has the header's field offsets and size."""
+    from nebula_amd.engine import GoResultC
+    fields = [f[0] for f in GoResultC._fields_]
+    prog = tmp_path / "layout.c"
+    body = "".join(f'    printf("%s %zu\\n", "{f}", offsetof(ngx_go_result, {f}));\n' for f in fields)
+    prog.write_text("#include <stddef.h>\n#include <stdio.h>\n#include \"nebula_gn.h\"\nint main(void) {\n" + body +
+                    '    printf("sizeof %zu\\n", sizeof(ngx_go_result));\n    return 0;\n}\n')
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)])
+    got = dict(line.split() for line in subprocess.check_output([str(exe)], text=True).splitlines())
+    for f in fields:
+        assert int(got[f]) == getattr(GoResultC, f).offset, f
+    assert int(got["sizeof"]) == ctypes.sizeof(GoResultC)
