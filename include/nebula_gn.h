@@ -196,6 +196,7 @@ typedef struct {
     int32_t filter_pushdown;           /* FLAGS_filter_pushdown */
     int64_t now_sec;
     int32_t result_on_device;          /* 1: leave rows in HBM (dev_* below), no host cells / DISTINCT */
+    int32_t host_columnar;             /* 1 (host results): columnar host arrays (host_cols), no cells */
 } ngx_go_plan;
 
 /* One YIELD column of a device-resident result (result_on_device), columnar in HBM, nrows entries:
@@ -236,7 +237,13 @@ typedef struct {
     const int64_t* dev_rank;
     const int32_t* dev_type;           /* NULL when the query has one OVER type: see dev_type_const */
     const ngx_dev_column* dev_cols;    /* ncols columns */
-    int32_t dev_type_const;            /* signed type of every row when dev_type is NULL */
+    int32_t dev_type_const;            /* signed type of every row when dev_type / row_type is NULL */
+    /* host_columnar: one host column per YIELD column, nrows entries, laid out as ngx_dev_column
+     * but in host memory (page-locked staging of the context, valid until the next call on it):
+     * x holds int / double bits / bool, or for a string value a `const char*` to its bytes (len[r]
+     * bytes, not NUL-terminated); `cells` is NULL and row_type is NULL when every row has
+     * dev_type_const. row_src / row_dst / row_rank point into the same staging. */
+    const ngx_dev_column* host_cols;
 } ngx_go_result;
 
 int32_t ngx_go(ngx_ctx* ctx, const ngx_go_plan* plan, ngx_go_result** out);
@@ -260,7 +267,10 @@ int32_t ngx_kernel_stats(ngx_ctx* ctx, const ngx_kernel_stat** out, int32_t* n);
 /* Engine flags (the reference's gflags for this path):
  *   "jit"  1 (default; env NGX_JIT=0 turns it off): compile each query's WHERE / YIELD into
  *          final-hop kernels with hipRTC; 0: run the precompiled bytecode-interpreter kernels.
- * Read-only counters for ngx_get_flag: "jit_compiled", "jit_hits", "jit_failed", "jit_compile_us". */
+ *          Literals are launch arguments, so queries that differ only in literals share a kernel.
+ *   "jit_cache_capacity"  compiled query shapes kept loaded (LRU, default 64).
+ * Read-only counters for ngx_get_flag: "jit_compiled", "jit_hits", "jit_failed", "jit_compile_us",
+ * "jit_cached", "jit_evicted". */
 int32_t ngx_set_flag(ngx_ctx* ctx, const char* name, int64_t value);
 int32_t ngx_get_flag(ngx_ctx* ctx, const char* name, int64_t* value);
 /* why the last query ran on the interpreter kernels instead of a generated one ("" if it did not) */

@@ -14,6 +14,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <thread>
 #include <unordered_set>
 
 #include "exprc.h"
@@ -102,6 +103,21 @@ struct ngx_ctx {
     DBuf visited, F0, F1, estart, chunkFirst, tileSums, counters, lbStatus, seedPart, seedVid;
     DBuf oSrc, oDst, oRank, oType, oEntry, progBuf, sendBits, recvBits, vcells, misc, oColDesc;
     struct ColBuf { DBuf x, len, t; };
+    struct PinBuf {                                     // page-locked host staging for result D2H
+        void* p = nullptr;
+        size_t cap = 0;
+        char* get(size_t bytes) {
+            if (bytes > cap) {
+                if (p) (void)hipHostFree(p);
+                p = nullptr;
+                size_t c = std::max(bytes, cap * 3 / 2);
+                HIP_OK(hipHostMalloc(&p, c, hipHostMallocDefault));
+                cap = c;
+            }
+            return static_cast<char*>(p);
+        }
+        void release() { if (p) (void)hipHostFree(p); p = nullptr; cap = 0; }
+    } hostStage;
     std::vector<ColBuf> oCols;                          // result columns (columnar, HBM)
     std::vector<OutCol> oColView;                       // their device pointers, as uploaded to oColDesc
     uint64_t visitedSize = 0;
@@ -118,6 +134,21 @@ struct ngx_ctx {
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
     std::vector<hipEvent_t> eventPool;
     size_t eventNext = 0;
+
+    ~ngx_ctx() {                                       // also the cleanup of ngx_open's error paths
+        (void)hipSetDevice(device);
+        if (stream) (void)hipStreamSynchronize(stream);
+        spaces.clear();
+        for (DBuf* b : {&visited, &F0, &F1, &estart, &tileSums, &counters, &lbStatus, &seedPart, &seedVid, &oSrc,
+                        &oDst, &oRank, &oType, &oEntry, &chunkFirst, &oColDesc, &progBuf, &sendBits, &recvBits,
+                        &vcells, &misc}) b->release();
+        for (auto& cb : oCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
+        hostStage.release();
+        for (auto e : eventPool) (void)hipEventDestroy(e);
+        if (comm) (void)ncclCommDestroy(comm);
+        if (pin) (void)hipHostFree(pin);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
 
     hipEvent_t ev() {
         if (eventNext == eventPool.size()) {
@@ -334,17 +365,67 @@ std::string hostString(const DeviceGraph& d, const DevPrograms& dp, const std::s
     return std::string(it->host + (ptr - it->dev), len);
 }
 
-// ColumnValue per calculateExprType (GoExecutor::toThriftResponse, GoExecutor.cpp:775-829)
-bool toCell(const OutCell& v, int32_t colType, ngx_cell& out, std::string& strings,
-            const DeviceGraph& d, const DevPrograms& dp, const std::string& pool) {
+// device string pointer -> host bytes: the query's literal pool (copied to `pool`) or a snapshot
+// string column (DeviceGraph::strRanges)
+struct StrMap {
+    const DeviceGraph* d;
+    uint64_t poolDev;
+    const std::string* pool;
+    const char* host(uint64_t ptr, uint32_t len) const {
+        if (len == 0) return "";
+        if (ptr >= poolDev && ptr + len <= poolDev + pool->size()) return pool->data() + (ptr - poolDev);
+        auto it = std::upper_bound(d->strRanges.begin(), d->strRanges.end(), ptr,
+                                   [](uint64_t v, const DeviceGraph::Range& r) { return v < r.dev; });
+        if (it == d->strRanges.begin()) return "";
+        --it;
+        if (ptr + len > it->dev + it->len) return "";
+        return it->host + (ptr - it->dev);
+    }
+};
+
+// one result column staged on the host: value bits, string lengths, per-row types (UNKNOWN columns)
+struct ColView {
+    int32_t colType = T_UNKNOWN;
+    int64_t* x = nullptr;
+    uint32_t* len = nullptr;
+    uint8_t* t = nullptr;
+    uint8_t typeAt(uint64_t r) const {
+        if (t) return t[r];
+        switch (colType) {
+            case T_BOOL: return V_BOOL;
+            case T_INT: case T_VID: case T_TIMESTAMP: return V_INT;
+            case T_FLOAT: case T_DOUBLE: return V_DBL;
+            case T_STRING: return V_STR;
+            default: return V_ERR;
+        }
+    }
+};
+
+int hostThreads() {
+    unsigned n = std::thread::hardware_concurrency();
+    return static_cast<int>(std::max(1u, std::min(n, 16u)));
+}
+
+// f(lo, hi, t) over T contiguous row ranges on T threads (T = 0: hostThreads(), small n: one)
+template <typename F>
+void parallelRows(uint64_t n, F&& f, int T = 0) {
+    if (T <= 0) T = n < (1u << 16) ? 1 : hostThreads();
+    if (T == 1) { f(0, n, 0); return; }
+    std::vector<std::thread> ts;
+    for (int t = 0; t < T; t++) ts.emplace_back([&f, n, t, T] { f(n * t / T, n * (t + 1) / T, t); });
+    for (auto& th : ts) th.join();
+}
+
+// ColumnValue per calculateExprType (GoExecutor::toThriftResponse, GoExecutor.cpp:775-829); string
+// bytes are appended to `strings` (str_off relative to it)
+bool toCell(const OutCell& v, int32_t colType, ngx_cell& out, std::string& strings, const StrMap& sm) {
     out.str_len = 0;
     out.v.i = 0;
     auto str = [&]() {
-        std::string s = hostString(d, dp, pool, static_cast<uint64_t>(v.x), v.len);
         out.kind = NGX_CELL_STR;
-        out.str_len = static_cast<int32_t>(s.size());
+        out.str_len = static_cast<int32_t>(v.len);
         out.v.str_off = strings.size();
-        strings += s;
+        strings.append(sm.host(static_cast<uint64_t>(v.x), v.len), v.len);
     };
     switch (colType) {
         case T_BOOL: if (v.t != V_BOOL) return false; out.kind = NGX_CELL_BOOL; out.v.i = v.x; return true;
@@ -438,12 +519,16 @@ struct ColSpec { bool len, t; };
 struct GoResultHolder {
     ngx_go_result r{};
     std::vector<ngx_dev_column> devCols;
+    std::vector<ngx_dev_column> hostCols;
     std::vector<int32_t> colTypes;
     std::vector<ngx_cell> cells;
     std::vector<int64_t> src, dst, rank;
     std::vector<int32_t> type;
     std::string strings;
     std::vector<uint64_t> hopFrontier, hopEdges, hopNext;
+    // host_columnar: the row arrays live in the context's page-locked staging
+    const int64_t *rowSrcView = nullptr, *rowDstView = nullptr, *rowRankView = nullptr;
+    const int32_t* rowTypeView = nullptr;
 };
 struct GnResultHolder {
     ngx_gn_result r{};
@@ -515,6 +600,7 @@ int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
     c->device = cfg->device;
     c->rank = cfg->rank;
     c->world = cfg->world < 1 ? 1 : cfg->world;
+    if (c->rank < 0 || c->rank >= c->world || c->device < 0) return NGX_E_BAD_ARGUMENT;
     if (const char* j = std::getenv("NGX_JIT")) c->jitOn = std::string(j) != "0";
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return NGX_E_DEVICE;
@@ -541,21 +627,11 @@ int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
 void ngx_close(ngx_ctx* c) {
     if (!c) return;
     {
-        std::lock_guard<std::mutex> g(c->mu);
+        std::lock_guard<std::mutex> g(c->mu);          // waits for an in-flight call
         (void)hipSetDevice(c->device);
         (void)hipStreamSynchronize(c->stream);
-        c->spaces.clear();
-        for (DBuf* b : {&c->visited, &c->F0, &c->F1, &c->estart, &c->tileSums, &c->counters, &c->lbStatus,
-                        &c->seedPart, &c->seedVid, &c->oSrc, &c->oDst, &c->oRank, &c->oType, &c->oEntry,
-                        &c->chunkFirst, &c->oColDesc, &c->progBuf, &c->sendBits, &c->recvBits, &c->vcells,
-                        &c->misc}) b->release();
-        for (auto& cb : c->oCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
-        for (auto e : c->eventPool) (void)hipEventDestroy(e);
-        if (c->comm) ncclCommDestroy(c->comm);
-        if (c->pin) (void)hipHostFree(c->pin);
-        (void)hipStreamDestroy(c->stream);
     }
-    delete c;
+    delete c;                                          // ~ngx_ctx releases everything
 }
 
 const char* ngx_last_error(ngx_ctx* c) { return c ? c->lastError.c_str() : "no context"; }
@@ -718,6 +794,7 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
     std::lock_guard<std::mutex> g(c->mu);
     std::string n = name ? name : "";
     if (n == "jit") { c->jitOn = value != 0; return NGX_OK; }
+    if (n == "jit_cache_capacity") { c->jit.capacity = value < 1 ? 1 : static_cast<size_t>(value); return NGX_OK; }
     return fail(c, NGX_E_BAD_ARGUMENT, "unknown flag " + n);
 }
 
@@ -727,6 +804,8 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     if (n == "jit") *value = c->jitOn ? 1 : 0;
     else if (n == "jit_compiled") *value = static_cast<int64_t>(c->jit.compiled);
     else if (n == "jit_hits") *value = static_cast<int64_t>(c->jit.hits);
+    else if (n == "jit_cached") *value = static_cast<int64_t>(c->jit.size());
+    else if (n == "jit_evicted") *value = static_cast<int64_t>(c->jit.evicted);
     else if (n == "jit_failed") *value = static_cast<int64_t>(c->jit.failed);
     else if (n == "jit_compile_us") *value = static_cast<int64_t>(c->jit.compileSeconds * 1e6);
     else if (n == "jit_vgprs") *value = c->jit.lastRegs;          // registers / scratch of the last compiled
@@ -1004,13 +1083,21 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     Programs progs;
     std::string err;
     bool pushHere = p.filter_pushdown && p.direction == NGX_DIR_FORWARD && gp.pushed;
+    bool pushInvalid = false;
     if (pushHere) {
         Program pp;
         int32_t crc = compileStorage(*gp.pushed, sctx, pp, err);
-        if (crc == NGX_E_INVALID_FILTER) return fail(c, NGX_E_QUERY, "Get neighbors failed");   // every part fails
-        if (crc) return fail(c, crc, err);
-        // a $^ tag referenced only by the filter: every src tag prop of WHERE/YIELD is requested too
-        progs.P = progs.add(pp);
+        if (crc == NGX_E_INVALID_FILTER) {
+            // every part of the final-hop request fails (E_INVALID_FILTER), but only if that request is
+            // issued: a frontier that empties earlier ends the query with no rows (GoExecutor.cpp:580-606)
+            pushInvalid = true;
+            pushHere = false;
+        } else if (crc) {
+            return fail(c, crc, err);
+        } else {
+            // a $^ tag referenced only by the filter: every src tag prop of WHERE/YIELD is requested too
+            progs.P = progs.add(pp);
+        }
     }
     if (gp.where) {
         Program wp;
@@ -1041,6 +1128,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     // per-query straight-line kernels (jit.cpp); the interpreter kernels otherwise
     const JitKernels* jk = nullptr;
     const JitKernels* jkNoP = nullptr;                       // record hops before the last (no pushdown)
+    std::vector<int64_t> jitKc;                              // their literal table (FinalArgs::kc/kl)
+    std::vector<uint32_t> jitKl;
     c->jitNote.clear();
     if (c->jitOn) {
         JitQuery jq;
@@ -1052,6 +1141,18 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         for (int32_t off : progs.yOff) jq.Y.push_back(JitProgram{progs.code.data() + off, true});
         jq.yColType = gp.colTypes;
         jq.yKey = yAlias;
+        // literals -> launch-time constant slots (one kernel per query shape)
+        auto slotConsts = [&](const Insn* code) {
+            for (const Insn* in = code; in && in->op != OP_END; in++) {
+                if (in->op != OP_PUSH || static_cast<int>(jitKc.size()) >= kJitConsts) continue;
+                jq.constSlot[in] = static_cast<int32_t>(jitKc.size());
+                jitKc.push_back(in->imm);
+                jitKl.push_back(static_cast<uint32_t>(in->a));
+            }
+        };
+        if (jq.P.present) slotConsts(jq.P.code);
+        if (jq.W.present) slotConsts(jq.W.code);
+        for (auto& y : jq.Y) slotConsts(y.code);
         std::string jerr;
         std::string src = jitSource(sp, jq);
         if (!src.empty()) jk = c->jit.get(src, jerr);
@@ -1172,6 +1273,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             E = awaitPub(c, pub, estart + nEnt);
         }
         haveEstart = false;
+        if (isFinal && pushInvalid && nF) return fail(c, NGX_E_QUERY, "Get neighbors failed");
         R.hopFrontier.push_back(nF);
         R.hopEdges.push_back(E);
         uint64_t chunks = (E + kChunk - 1) / kChunk;
@@ -1206,6 +1308,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             a.ySlotType = nullptr;
             a.yColType = dp.yColType;
             a.wIsP = (isFinal && wIsP) ? 1u : 0u;
+            for (size_t k = 0; k < jitKc.size(); k++) { a.kc[k] = jitKc[k]; a.kl[k] = jitKl[k]; }
             const JitKernels* kj = isFinal ? jk : jkNoP;
             // outputs sized for every edge passing (rows are written in the same launch)
             uint64_t cap = totalRows + E;
@@ -1301,47 +1404,134 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         R.r.dev_cols = R.devCols.data();
         return NGX_OK;
     }
-    // ---- results to the host
-    R.src.resize(totalRows); R.dst.resize(totalRows); R.rank.resize(totalRows); R.type.resize(totalRows);
-    std::vector<OutCell> raw;
-    if (totalRows) {
-        HIP_OK(hipMemcpyAsync(R.src.data(), c->oSrc.p, totalRows * 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_OK(hipMemcpyAsync(R.dst.data(), c->oDst.p, totalRows * 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_OK(hipMemcpyAsync(R.rank.data(), c->oRank.p, totalRows * 8, hipMemcpyDeviceToHost, c->stream));
-        if (constType) std::fill(R.type.begin(), R.type.end(), hs.etype[0]);
-        else HIP_OK(hipMemcpyAsync(R.type.data(), c->oType.p, totalRows * 4, hipMemcpyDeviceToHost, c->stream));
-        raw = downloadCells(c, colSpec, gp.colTypes, totalRows, 0);
+    // ---- results to the host: every array in one batch of D2H copies into page-locked staging
+    const uint64_t n = totalRows;
+    struct HostArr { const void* dev; size_t bytes; char* host; };
+    std::vector<HostArr> arrs;
+    auto want = [&](const void* dev, size_t bytes) { arrs.push_back(HostArr{dev, bytes, nullptr}); return arrs.size() - 1; };
+    size_t iSrc = want(c->oSrc.p, n * 8), iDst = want(c->oDst.p, n * 8), iRank = want(c->oRank.p, n * 8);
+    size_t iType = constType ? SIZE_MAX : want(c->oType.p, n * 4);
+    std::vector<size_t> iX(nY, SIZE_MAX), iLen(nY, SIZE_MAX), iT(nY, SIZE_MAX);
+    for (int32_t y = 0; y < nY && n; y++) {
+        if (y < static_cast<int32_t>(yAlias.size()) && yAlias[y] >= 0) continue;       // = a key array
+        const OutCol& v = c->oColView[y];
+        iX[y] = want(v.x, n * 8);
+        if (v.len) iLen[y] = want(v.len, n * 4);
+        if (v.t) iT[y] = want(v.t, n);
     }
-    R.cells.resize(totalRows * nY);
-    for (uint64_t r = 0; r < totalRows; r++) {
-        for (int32_t y = 0; y < nY; y++) {
-            if (!toCell(raw[r * nY + y], gp.colTypes[y], R.cells[r * nY + y], R.strings, d, dp, progs.pool)) {
-                return fail(c, NGX_E_QUERY, "YIELD value does not match its column type (boost::get)");
-            }
+    size_t total = 0;
+    for (auto& a : arrs) total += (a.bytes + 63) & ~size_t(63);
+    char* stage = c->hostStage.get(std::max<size_t>(total, 64));
+    for (auto& a : arrs) {
+        a.host = stage;
+        stage += (a.bytes + 63) & ~size_t(63);
+        if (a.bytes) HIP_OK(hipMemcpyAsync(a.host, a.dev, a.bytes, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_OK(hipStreamSynchronize(c->stream));
+    int64_t* hSrc = reinterpret_cast<int64_t*>(arrs[iSrc].host);
+    int64_t* hDst = reinterpret_cast<int64_t*>(arrs[iDst].host);
+    int64_t* hRank = reinterpret_cast<int64_t*>(arrs[iRank].host);
+    int32_t* hType = iType == SIZE_MAX ? nullptr : reinterpret_cast<int32_t*>(arrs[iType].host);
+    std::vector<ColView> cols(nY);
+    for (int32_t y = 0; y < nY; y++) {
+        ColView& cv = cols[y];
+        cv.colType = gp.colTypes[y];
+        if (y < static_cast<int32_t>(yAlias.size()) && yAlias[y] >= 0) {
+            cv.x = yAlias[y] == 0 ? hSrc : yAlias[y] == 1 ? hDst : hRank;
+        } else if (n) {
+            cv.x = reinterpret_cast<int64_t*>(arrs[iX[y]].host);
+            cv.len = iLen[y] == SIZE_MAX ? nullptr : reinterpret_cast<uint32_t*>(arrs[iLen[y]].host);
+            cv.t = iT[y] == SIZE_MAX ? nullptr : reinterpret_cast<uint8_t*>(arrs[iT[y]].host);
         }
     }
-    if (p.distinct && totalRows) {                            // processFinalResult DISTINCT (:1298-1305)
-        std::vector<uint64_t> keep;
+    R.strings = progs.pool;                                    // string literals of YIELD, kept with the result
+    StrMap sm{&d, reinterpret_cast<uint64_t>(dp.pool), &R.strings};
+    uint64_t nOut = n;
+    if (p.distinct && n) {                                     // processFinalResult DISTINCT (:1298-1305)
+        // key = every column's value type and bits (string bytes), before the ColumnValue typing, as
+        // boost::hash_range over the VariantType record does
         std::unordered_set<std::string> seen;
-        for (uint64_t r = 0; r < totalRows; r++) {
-            std::string key;
+        seen.reserve(static_cast<size_t>(std::min<uint64_t>(n, 1u << 24)));
+        std::string key;
+        uint64_t w = 0;
+        for (uint64_t r = 0; r < n; r++) {
+            key.clear();
             for (int32_t y = 0; y < nY; y++) {
-                const ngx_cell& cl = R.cells[r * nY + y];
-                key.append(reinterpret_cast<const char*>(&cl.kind), 4);
-                if (cl.kind == NGX_CELL_STR) { key += R.strings.substr(cl.v.str_off, cl.str_len); key.push_back('\0'); }
-                else key.append(reinterpret_cast<const char*>(&cl.v.i), 8);
+                const ColView& cv = cols[y];
+                uint8_t t = cv.typeAt(r);
+                key.push_back(static_cast<char>(t));
+                if (t == V_STR) {
+                    uint32_t len = cv.len ? cv.len[r] : 0;
+                    key.append(reinterpret_cast<const char*>(&len), 4);
+                    key.append(sm.host(static_cast<uint64_t>(cv.x[r]), len), len);
+                } else {
+                    key.append(reinterpret_cast<const char*>(&cv.x[r]), 8);
+                }
             }
-            if (seen.insert(key).second) keep.push_back(r);
+            if (!seen.insert(key).second) continue;
+            if (w != r) {                                      // compact in place (w < r)
+                hSrc[w] = hSrc[r]; hDst[w] = hDst[r]; hRank[w] = hRank[r];
+                if (hType) hType[w] = hType[r];
+                for (int32_t y = 0; y < nY; y++) {
+                    ColView& cv = cols[y];
+                    if (y < static_cast<int32_t>(yAlias.size()) && yAlias[y] >= 0) continue;
+                    cv.x[w] = cv.x[r];
+                    if (cv.len) cv.len[w] = cv.len[r];
+                    if (cv.t) cv.t[w] = cv.t[r];
+                }
+            }
+            w++;
         }
-        auto compact = [&](auto& v, size_t w) {
-            std::remove_reference_t<decltype(v)> out;
-            for (auto r : keep) for (size_t k = 0; k < w; k++) out.push_back(v[r * w + k]);
-            v.swap(out);
-        };
-        compact(R.src, 1); compact(R.dst, 1); compact(R.rank, 1); compact(R.type, 1); compact(R.cells, nY);
-        totalRows = keep.size();
+        nOut = w;
     }
-    R.r.nrows = totalRows;
+    R.r.nrows = nOut;
+    R.r.dev_type_const = constType ? hs.etype[0] : 0;
+    if (p.host_columnar) {
+        // columnar host result, no per-cell conversion: string values become host pointers
+        parallelRows(nOut, [&](uint64_t lo, uint64_t hi, int) {
+            for (int32_t y = 0; y < nY; y++) {
+                ColView& cv = cols[y];
+                if (!cv.len) continue;
+                for (uint64_t r = lo; r < hi; r++) {
+                    if (cv.typeAt(r) == V_STR) cv.x[r] = reinterpret_cast<int64_t>(sm.host(static_cast<uint64_t>(cv.x[r]), cv.len[r]));
+                }
+            }
+        });
+        R.rowSrcView = hSrc; R.rowDstView = hDst; R.rowRankView = hRank; R.rowTypeView = hType;
+        for (int32_t y = 0; y < nY; y++) R.hostCols.push_back(ngx_dev_column{cols[y].x, cols[y].len, cols[y].t});
+        return NGX_OK;
+    }
+    R.src.assign(hSrc, hSrc + nOut);
+    R.dst.assign(hDst, hDst + nOut);
+    R.rank.assign(hRank, hRank + nOut);
+    if (hType) R.type.assign(hType, hType + nOut);
+    else R.type.assign(nOut, hs.etype[0]);
+    // typed cells (ColumnValue, toThriftResponse) in parallel; per-thread string arenas, then appended
+    R.cells.resize(nOut * nY);
+    const int T = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(hostThreads(), (nOut + 65535) / 65536)));
+    std::vector<std::string> arena(T);
+    std::vector<uint8_t> bad(T, 0);
+    parallelRows(nOut, [&](uint64_t lo, uint64_t hi, int t) {
+        std::string& out = arena[t];
+        for (uint64_t r = lo; r < hi && !bad[t]; r++) {
+            for (int32_t y = 0; y < nY; y++) {
+                OutCell v{cols[y].x[r], cols[y].len ? cols[y].len[r] : 0u, cols[y].typeAt(r), {0, 0, 0}};
+                if (!toCell(v, gp.colTypes[y], R.cells[r * nY + y], out, sm)) { bad[t] = 1; break; }
+            }
+        }
+    }, T);
+    for (int t = 0; t < T; t++) if (bad[t]) return fail(c, NGX_E_QUERY, "YIELD value does not match its column type (boost::get)");
+    {
+        // arena t's offsets are relative to it: rebase onto R.strings
+        std::vector<uint64_t> base(T);
+        uint64_t b = R.strings.size();
+        for (int t = 0; t < T; t++) { base[t] = b; b += arena[t].size(); }
+        parallelRows(nOut, [&](uint64_t lo, uint64_t hi, int t) {
+            for (uint64_t i = lo * nY; i < hi * nY; i++) if (R.cells[i].kind == NGX_CELL_STR) R.cells[i].v.str_off += base[t];
+        }, T);
+        R.strings.reserve(b);
+        for (int t = 0; t < T; t++) R.strings += arena[t];
+    }
     return NGX_OK;
 }
 
@@ -1363,10 +1553,11 @@ extern "C" int32_t ngx_go(ngx_ctx* c, const ngx_go_plan* p, ngx_go_result** out)
     R->r.ncols = static_cast<int32_t>(R->colTypes.size());
     R->r.col_types = R->colTypes.data();
     R->r.cells = R->cells.data();
-    R->r.row_src = R->src.data();
-    R->r.row_dst = R->dst.data();
-    R->r.row_rank = R->rank.data();
-    R->r.row_type = R->type.data();
+    R->r.row_src = R->rowSrcView ? R->rowSrcView : R->src.data();
+    R->r.row_dst = R->rowDstView ? R->rowDstView : R->dst.data();
+    R->r.row_rank = R->rowRankView ? R->rowRankView : R->rank.data();
+    R->r.row_type = R->rowSrcView ? R->rowTypeView : R->type.data();
+    R->r.host_cols = R->hostCols.empty() ? nullptr : R->hostCols.data();
     R->r.strings = R->strings.data();
     R->r.strings_len = R->strings.size();
     R->r.nhops = static_cast<int32_t>(R->hopEdges.size());

@@ -29,6 +29,9 @@ struct JitProgram {
 
 struct JitQuery {
     JitProgram P, W;
+    // PUSH literals passed at launch (FinalArgs::kc/kl) instead of being compiled in, so queries that
+    // differ only in literals share one kernel: instruction -> slot (< kJitConsts); others are inlined
+    std::map<const Insn*, int32_t> constSlot;
     std::vector<JitProgram> Y;
     std::vector<int32_t> yColType;  // calculateExprType per column
     std::vector<int32_t> yKey;      // >= 0: column is the edge's key prop (0 src, 1 dst, 2 rank), written
@@ -40,14 +43,19 @@ struct JitQuery {
 class JitCache {
 public:
     ~JitCache();
-    // nullptr when compilation failed (err set); compiled kernels are cached by source
+    // nullptr when compilation failed (err set); compiled kernels are cached by source, at most
+    // `capacity` modules (least recently used unloaded first; callers hold no kernel across queries)
     const JitKernels* get(const std::string& source, std::string& err);
-    uint64_t compiled = 0, hits = 0, failed = 0;
+    uint64_t compiled = 0, hits = 0, failed = 0, evicted = 0;
     double compileSeconds = 0;
     int64_t lastRegs = -1, lastScratch = -1;    // hipFuncGetAttribute of the last compiled kernel
+    size_t capacity = 64;
+    size_t size() const { return cache_.size(); }
 
 private:
-    std::map<std::string, JitKernels> cache_;
+    struct Entry { JitKernels k; uint64_t used = 0; };
+    uint64_t tick_ = 0;
+    std::map<std::string, Entry> cache_;
     std::map<std::string, std::string> failures_;
 };
 

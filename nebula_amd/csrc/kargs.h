@@ -33,6 +33,8 @@ struct OutCol {
     uint8_t* t;                         // V_* (0xFF none) per row; nullptr when every row has the column's static type
 };
 
+constexpr int kJitConsts = 24;          // PUSH literals a generated kernel reads from its arguments
+
 struct FinalArgs {
     const uint32_t* F;                  // frontier rows
     const uint64_t* estart;             // exclusive prefix of entry degrees, [nEnt] = E
@@ -66,6 +68,8 @@ struct FinalArgs {
     int32_t* oType;
     uint32_t* oEntry;                   // frontier index of each row (GetNeighbors), may be null
     const OutCol* oCols;                // nY columns (device array)
+    int64_t kc[kJitConsts];             // generated kernels: literal bits (string: pool offset)
+    uint32_t kl[kJitConsts];            // string literal lengths
 };
 
 struct VertexCellArgs {

@@ -89,7 +89,8 @@ class GoPlan(ctypes.Structure):
                 ("over_aliases", P(ctypes.c_char_p)), ("over_all", c_i32), ("direction", c_i32),
                 ("where", ctypes.c_char_p), ("where_len", c_u32), ("nyields", c_i32),
                 ("yields", P(ctypes.c_char_p)), ("yield_lens", P(c_u32)), ("distinct", c_i32),
-                ("filter_pushdown", c_i32), ("now_sec", c_i64), ("result_on_device", c_i32)]
+                ("filter_pushdown", c_i32), ("now_sec", c_i64), ("result_on_device", c_i32),
+                ("host_columnar", c_i32)]
 
 
 class GoResultC(ctypes.Structure):
@@ -99,7 +100,7 @@ class GoResultC(ctypes.Structure):
                 ("hop_frontier", P(c_u64)), ("hop_edges", P(c_u64)), ("hop_next", P(c_u64)),
                 ("device_ms", c_dbl), ("dev_src", ctypes.c_void_p), ("dev_dst", ctypes.c_void_p),
                 ("dev_rank", ctypes.c_void_p), ("dev_type", ctypes.c_void_p), ("dev_cols", ctypes.c_void_p),
-                ("dev_type_const", ctypes.c_int32)]
+                ("dev_type_const", ctypes.c_int32), ("host_cols", ctypes.c_void_p)]
 
 
 class KernelStat(ctypes.Structure):
@@ -347,10 +348,13 @@ class Engine:
 
     # ---- GO
     def go(self, space: int, s: Union[str, ngql.GoSentence], pushdown: bool = True, now_sec: int = 0,
-           raise_on_error: bool = False, rows: bool = True, on_device: bool = False, fetch: bool = False) -> GoResult:
+           raise_on_error: bool = False, rows: bool = True, on_device: bool = False, fetch: bool = False,
+           columnar: bool = False) -> GoResult:
         """Run one GO. rows=False skips decoding cells into Python tuples; on_device=True leaves the
         result rows in HBM (GoResult.nrows and the statistics only); with fetch=True the HBM arrays
-        (src/dst/rank/type and the columnar YIELD columns) are copied back into the result."""
+        (src/dst/rank/type and the columnar YIELD columns) are copied back into the result.
+        columnar=True asks for host_columnar results: no cells; with rows=True they are rebuilt here
+        from the columns (ColumnValue typing by col_types) so they compare with the cell path."""
         if isinstance(s, str):
             s = ngql.parse_go(s)
         starts = np.array(s.vids, dtype=np.int64)
@@ -363,7 +367,7 @@ class Engine:
         plan = GoPlan(space, s.record_from, s.record_to, len(starts), starts.ctypes.data_as(P(c_i64)), len(s.over),
                       names, aliases, 1 if s.over_all else 0, s.direction, where if where else None, len(where),
                       len(yb), yarr, ylen, 1 if s.distinct else 0, 1 if pushdown else 0, now_sec,
-                      1 if on_device else 0)
+                      1 if on_device else 0, 1 if columnar else 0)
         out = P(GoResultC)()
         rc = self.L.ngx_go(self.h, ctypes.byref(plan), ctypes.byref(out))
         try:
@@ -391,6 +395,8 @@ class Engine:
                                              self._d2h(dc.len, n, np.uint32) if dc.len else None,
                                              self._d2h(dc.type, n, np.uint8) if dc.type else None))
                 return res
+            if columnar:
+                return self._columnar(r, rc, err, rows)
             res = GoResult(
                 ok=rc == 0, error=err, code=rc, col_types=[r.col_types[i] for i in range(r.ncols)],
                 rows=_cells(r.cells, n, r.ncols, strings) if rows else [],
@@ -402,6 +408,49 @@ class Engine:
             return res
         finally:
             self.L.ngx_go_result_free(out)
+
+    def _columnar(self, r, rc, err, rows):
+        n = r.nrows
+        types = [r.col_types[i] for i in range(r.ncols)]
+        res = GoResult(ok=rc == 0, error=err, code=rc, col_types=types, rows=[], nrows=n,
+                       hop_frontier=[r.hop_frontier[i] for i in range(r.nhops)],
+                       hop_edges=[r.hop_edges[i] for i in range(r.nhops)],
+                       hop_next=[r.hop_next[i] for i in range(r.nhops)], device_ms=r.device_ms)
+        if rc != 0:
+            return res
+        res.src, res.dst, res.rank = _arr(r.row_src, n, np.int64), _arr(r.row_dst, n, np.int64), \
+            _arr(r.row_rank, n, np.int64)
+        res.etype = _arr(r.row_type, n, np.int32) if r.row_type else np.full(n, r.dev_type_const, np.int32)
+        cols = ctypes.cast(r.host_cols, P(DevColumn)) if r.host_cols else None
+        for c in range(r.ncols):
+            dc = cols[c]
+            x = _arr(ctypes.cast(dc.x, P(c_i64)), n, np.int64)
+            ln = _arr(ctypes.cast(dc.len, P(c_u32)), n, np.uint32) if dc.len else None
+            t = _arr(ctypes.cast(dc.type, P(ctypes.c_uint8)), n, np.uint8) if dc.type else None
+            res.dev_cols.append((x, ln, t))
+        if rows:
+            static = {1: 3, 2: 1, 3: 1, 21: 1, 4: 2, 5: 2, 6: 4}         # SupportedType -> V_* of its rows
+            kinds = {1: "bool", 2: "int", 3: "id", 21: "timestamp", 4: "float", 5: "double", 6: "str"}
+            out = []
+            for i in range(n):
+                row = []
+                for c, (x, ln, t) in enumerate(res.dev_cols):
+                    vt = int(t[i]) if t is not None else static.get(types[c], 0)
+                    v = int(x[i])
+                    if vt == 4:
+                        row.append(("str", ctypes.string_at(v, int(ln[i])).decode("utf-8", "surrogateescape")
+                                    if ln[i] else ""))
+                    elif vt == 2:
+                        row.append((kinds.get(types[c], "double"), float(np.int64(v).view(np.float64))))
+                    elif vt == 3:
+                        row.append(("bool", bool(v)) if types[c] == 1 else ("empty", None))
+                    elif vt == 1:
+                        row.append((kinds.get(types[c], "int"), v))
+                    else:
+                        row.append(("empty", None))
+                out.append(tuple(row))
+            res.rows = out
+        return res
 
     def _d2h(self, ptr, n, dtype):
         out = np.zeros(n, dtype=dtype)
