@@ -244,6 +244,7 @@ typedef struct {
      * bytes, not NUL-terminated); `cells` is NULL and row_type is NULL when every row has
      * dev_type_const. row_src / row_dst / row_rank point into the same staging. */
     const ngx_dev_column* host_cols;
+    const uint64_t* hop_exchange_bytes;/* world > 1: frontier bytes this shard sent per hop (0 otherwise) */
 } ngx_go_result;
 
 int32_t ngx_go(ngx_ctx* ctx, const ngx_go_plan* plan, ngx_go_result** out);
@@ -269,6 +270,9 @@ int32_t ngx_kernel_stats(ngx_ctx* ctx, const ngx_kernel_stat** out, int32_t* n);
  *          final-hop kernels with hipRTC; 0: run the precompiled bytecode-interpreter kernels.
  *          Literals are launch arguments, so queries that differ only in literals share a kernel.
  *   "jit_cache_capacity"  compiled query shapes kept loaded (LRU, default 64).
+ *   "rccl_timeout_ms"     deadline of every RCCL collective (default 120000; env NGX_RCCL_TIMEOUT_MS).
+ *          On a timeout or an asynchronous RCCL error the communicator is aborted, the call returns
+ *          NGX_E_DEVICE and every later call on the context fails (the caller exits).
  * Read-only counters for ngx_get_flag: "jit_compiled", "jit_hits", "jit_failed", "jit_compile_us",
  * "jit_cached", "jit_evicted". */
 int32_t ngx_set_flag(ngx_ctx* ctx, const char* name, int64_t value);

@@ -122,6 +122,10 @@ struct ngx_ctx {
     std::vector<OutCol> oColView;                       // their device pointers, as uploaded to oColDesc
     uint64_t visitedSize = 0;
     uint8_t epoch = 0;
+    // RCCL watchdog: collective work must finish within this; else the communicator is aborted
+    int64_t rcclTimeoutMs = 120000;
+    bool broken = false;                                // communicator aborted: every later call fails
+    uint64_t lastXchgBytes = 0;                         // bytes this shard sent in the last exchange
     // per-query kernels (hipRTC)
     bool jitOn = true;
     JitCache jit;
@@ -525,7 +529,7 @@ struct GoResultHolder {
     std::vector<int64_t> src, dst, rank;
     std::vector<int32_t> type;
     std::string strings;
-    std::vector<uint64_t> hopFrontier, hopEdges, hopNext;
+    std::vector<uint64_t> hopFrontier, hopEdges, hopNext, hopXchg;
     // host_columnar: the row arrays live in the context's page-locked staging
     const int64_t *rowSrcView = nullptr, *rowDstView = nullptr, *rowRankView = nullptr;
     const int32_t* rowTypeView = nullptr;
@@ -576,10 +580,41 @@ void hostExchange(ngx_ctx* c, int32_t op, const void* dsend, void* drecv, uint64
     HIP_OK(hipStreamSynchronize(c->stream));
 }
 
+// RCCL watchdog: wait for the stream (which holds collective work) with a deadline, polling the
+// communicator's asynchronous error. A peer that died or hangs must not hang this rank: on an error
+// or after rcclTimeoutMs the communicator is aborted (ncclCommAbort ends its kernels) and the call
+// fails; the context is then unusable (every later call returns NGX_E_DEVICE).
+void rcclWait(ngx_ctx* c, const char* what) {
+    if (!c->comm) return;
+    auto t0 = std::chrono::steady_clock::now();
+    auto abortWith = [&](const std::string& why) {
+        (void)ncclCommAbort(c->comm);
+        c->comm = nullptr;
+        c->broken = true;
+        throw Error{NGX_E_DEVICE, std::string("RCCL ") + what + ": " + why + "; communicator aborted"};
+    };
+    for (uint32_t i = 0;; i++) {
+        hipError_t q = hipStreamQuery(c->stream);
+        if (q == hipSuccess) return;
+        if (q != hipErrorNotReady) abortWith(std::string("stream error ") + hipGetErrorString(q));
+        ncclResult_t ae = ncclSuccess;
+        if (ncclCommGetAsyncError(c->comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+            abortWith(std::string("async error ") + ncclGetErrorString(ae));
+        if ((i & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(c->rcclTimeoutMs))
+            abortWith("timed out after " + std::to_string(c->rcclTimeoutMs) + " ms");
+        if (i > 4096) std::this_thread::sleep_for(std::chrono::microseconds(50));
+        else __builtin_ia32_pause();
+    }
+}
+
 // all-gather of `bytes` per rank (rank order) over RCCL or the host exchange
 void allGather(ngx_ctx* c, const void* dsend, void* drecv, uint64_t bytes) {
-    if (c->xchg) hostExchange(c, NGX_XCHG_ALLGATHER, dsend, drecv, bytes);
-    else NCCL_OK(ncclAllGather(dsend, drecv, bytes, ncclUint8, c->comm, c->stream));
+    if (c->xchg) {
+        hostExchange(c, NGX_XCHG_ALLGATHER, dsend, drecv, bytes);
+    } else {
+        NCCL_OK(ncclAllGather(dsend, drecv, bytes, ncclUint8, c->comm, c->stream));
+        rcclWait(c, "all-gather");
+    }
 }
 
 }  // namespace
@@ -602,6 +637,7 @@ int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
     c->world = cfg->world < 1 ? 1 : cfg->world;
     if (c->rank < 0 || c->rank >= c->world || c->device < 0) return NGX_E_BAD_ARGUMENT;
     if (const char* j = std::getenv("NGX_JIT")) c->jitOn = std::string(j) != "0";
+    if (const char* t = std::getenv("NGX_RCCL_TIMEOUT_MS")) c->rcclTimeoutMs = std::max<int64_t>(1, std::atoll(t));
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return NGX_E_DEVICE;
     if (hipSetDevice(c->device) != hipSuccess) return NGX_E_DEVICE;
@@ -794,6 +830,7 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
     std::lock_guard<std::mutex> g(c->mu);
     std::string n = name ? name : "";
     if (n == "jit") { c->jitOn = value != 0; return NGX_OK; }
+    if (n == "rccl_timeout_ms") { c->rcclTimeoutMs = value < 1 ? 1 : value; return NGX_OK; }
     if (n == "jit_cache_capacity") { c->jit.capacity = value < 1 ? 1 : static_cast<size_t>(value); return NGX_OK; }
     return fail(c, NGX_E_BAD_ARGUMENT, "unknown flag " + n);
 }
@@ -802,6 +839,7 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     std::lock_guard<std::mutex> g(c->mu);
     std::string n = name ? name : "";
     if (n == "jit") *value = c->jitOn ? 1 : 0;
+    else if (n == "rccl_timeout_ms") *value = c->rcclTimeoutMs;
     else if (n == "jit_compiled") *value = static_cast<int64_t>(c->jit.compiled);
     else if (n == "jit_hits") *value = static_cast<int64_t>(c->jit.hits);
     else if (n == "jit_cached") *value = static_cast<int64_t>(c->jit.size());
@@ -931,6 +969,8 @@ void exchangeFrontier(ngx_ctx* c, const DeviceGraph& d, uint8_t epoch) {
         uint64_t n = sb[q + 1] - sb[q];
         if (launchPack(c->visited.get<uint8_t>(d.vglobal), epoch, sb[q], n, send + q * maxWords, c->stream)) throw Error{NGX_E_DEVICE, "pack"};
     }
+    c->lastXchgBytes = 0;
+    for (int q = 0; q < W; q++) if (q != c->rank) c->lastXchgBytes += (sb[q + 1] - sb[q] + 63) / 64 * 8;
     if (c->xchg) {
         hostExchange(c, NGX_XCHG_ALLTOALL, send, recv, maxWords * 8);
     } else {
@@ -942,6 +982,7 @@ void exchangeFrontier(ngx_ctx* c, const DeviceGraph& d, uint8_t epoch) {
             if (myWords) NCCL_OK(ncclRecv(recv + q * maxWords, myWords * 8, ncclUint8, q, c->comm, c->stream));
         }
         NCCL_OK(ncclGroupEnd());
+        rcclWait(c, "frontier all-to-all");
     }
     for (int q = 0; q < W; q++) {
         if (q == c->rank) continue;
@@ -1345,7 +1386,11 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
                     throw Error{NGX_E_DEVICE, "expand"};
             });
         }
-        if (c->world > 1) c->timed("exchange", 0, [&] { exchangeFrontier(c, d, ep); });
+        if (c->world > 1) {
+            c->timed("exchange", 0, [&] { exchangeFrontier(c, d, ep); });
+            c->addBytes("exchange", c->lastXchgBytes);
+            R.hopXchg.push_back(c->lastXchgBytes);
+        }
         uint32_t* Fn = (F == c->F0.p) ? c->F1.get<uint32_t>(std::max<uint64_t>(d.V, 1)) : c->F0.get<uint32_t>(std::max<uint64_t>(d.V, 1));
         uint64_t* tiles2 = c->tileSums.get<uint64_t>((std::max<uint64_t>(d.V, 1) + kTile - 1) / kTile + 1);
         if (fuseDeg) {
@@ -1542,6 +1587,7 @@ extern "C" int32_t ngx_go(ngx_ctx* c, const ngx_go_plan* p, ngx_go_result** out)
     auto R = std::make_unique<GoResultHolder>();
     int32_t rc;
     try {
+        if (c->broken) throw Error{NGX_E_DEVICE, "context unusable: its RCCL communicator was aborted"};
         HIP_OK(hipSetDevice(c->device));
         Space* sp = findSpace(c, p->space);
         if (!sp || !sp->dev) rc = fail(c, NGX_E_NOT_LOADED, "space not committed");
@@ -1562,6 +1608,8 @@ extern "C" int32_t ngx_go(ngx_ctx* c, const ngx_go_plan* p, ngx_go_result** out)
     R->r.strings_len = R->strings.size();
     R->r.nhops = static_cast<int32_t>(R->hopEdges.size());
     R->hopNext.resize(R->hopEdges.size(), 0);
+    R->hopXchg.resize(R->hopEdges.size(), 0);
+    R->r.hop_exchange_bytes = R->hopXchg.data();
     R->r.hop_frontier = R->hopFrontier.data();
     R->r.hop_edges = R->hopEdges.data();
     R->r.hop_next = R->hopNext.data();

@@ -348,16 +348,13 @@ __global__ void k_vertex_cells(VertexCellArgs a) {
 }
 
 // ------------------------------------------------------------------------------ multi-GPU exchange
-// pack this shard's marks for peer q's rows into a bitmap; merge received bitmaps into visited
-__global__ void k_pack(const uint8_t* visited, uint8_t epoch, uint64_t lo, uint64_t n, uint64_t* bits) {
-    uint64_t w = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (w * 64 >= n) return;
-    uint64_t word = 0;
-    for (int b = 0; b < 64; b++) {
-        uint64_t i = w * 64 + b;
-        if (i < n && visited[lo + i] == epoch) word |= 1ULL << b;
-    }
-    bits[w] = word;
+// pack this shard's marks for peer q's rows into a bitmap: one row byte per lane (coalesced), the
+// wave's ballot is the 64-bit word of its 64 rows; merge received bitmaps into visited
+__global__ __launch_bounds__(256) void k_pack(const uint8_t* visited, uint8_t epoch, uint64_t lo, uint64_t n, uint64_t* bits) {
+    uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    bool mark = i < n && visited[lo + i] == epoch;
+    uint64_t word = __ballot(mark);
+    if ((threadIdx.x & 63) == 0 && i < n) bits[i >> 6] = word;
 }
 __global__ void k_merge(const uint64_t* bits, uint64_t nwords, uint8_t* visited, uint64_t lo, uint64_t n, uint8_t epoch) {
     uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -435,9 +432,8 @@ int launchVertexCells(const VertexCellArgs& a, hipStream_t s) {
 }
 
 int launchPack(const uint8_t* visited, uint8_t epoch, uint64_t lo, uint64_t n, uint64_t* bits, hipStream_t s) {
-    uint64_t words = (n + 63) / 64;
-    if (words == 0) return 0;
-    hipLaunchKernelGGL(k_pack, dim3(static_cast<unsigned>((words + 255) / 256)), dim3(256), 0, s, visited, epoch, lo, n, bits);
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_pack, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, visited, epoch, lo, n, bits);
     return static_cast<int>(hipGetLastError());
 }
 

@@ -100,7 +100,8 @@ class GoResultC(ctypes.Structure):
                 ("hop_frontier", P(c_u64)), ("hop_edges", P(c_u64)), ("hop_next", P(c_u64)),
                 ("device_ms", c_dbl), ("dev_src", ctypes.c_void_p), ("dev_dst", ctypes.c_void_p),
                 ("dev_rank", ctypes.c_void_p), ("dev_type", ctypes.c_void_p), ("dev_cols", ctypes.c_void_p),
-                ("dev_type_const", ctypes.c_int32), ("host_cols", ctypes.c_void_p)]
+                ("dev_type_const", ctypes.c_int32), ("host_cols", ctypes.c_void_p),
+                ("hop_exchange_bytes", P(c_u64))]
 
 
 class KernelStat(ctypes.Structure):
@@ -230,10 +231,12 @@ class GoResult:
     hop_frontier: List[int] = field(default_factory=list)
     hop_edges: List[int] = field(default_factory=list)
     hop_next: List[int] = field(default_factory=list)
+    hop_xchg: List[int] = field(default_factory=list)     # world > 1: frontier bytes sent per hop
     device_ms: float = 0.0
     nrows: int = 0
     # on_device + fetch: the HBM result copied back as arrays (x, len or None, type or None) per column
     dev_cols: List[tuple] = field(default_factory=list)
+    digests: object = None               # columnar + digest_fn: whatever digest_fn returned
 
 
 @dataclass
@@ -349,12 +352,14 @@ class Engine:
     # ---- GO
     def go(self, space: int, s: Union[str, ngql.GoSentence], pushdown: bool = True, now_sec: int = 0,
            raise_on_error: bool = False, rows: bool = True, on_device: bool = False, fetch: bool = False,
-           columnar: bool = False) -> GoResult:
+           columnar: bool = False, digest_fn=None) -> GoResult:
         """Run one GO. rows=False skips decoding cells into Python tuples; on_device=True leaves the
         result rows in HBM (GoResult.nrows and the statistics only); with fetch=True the HBM arrays
         (src/dst/rank/type and the columnar YIELD columns) are copied back into the result.
         columnar=True asks for host_columnar results: no cells; with rows=True they are rebuilt here
-        from the columns (ColumnValue typing by col_types) so they compare with the cell path."""
+        from the columns (ColumnValue typing by col_types) so they compare with the cell path.
+        digest_fn(col_types, nrows, x_ptrs, len_ptrs, type_ptrs) is called on the host columns
+        before the result is freed (tests: large-result comparison)."""
         if isinstance(s, str):
             s = ngql.parse_go(s)
         starts = np.array(s.vids, dtype=np.int64)
@@ -381,7 +386,9 @@ class Engine:
                 res = GoResult(ok=rc == 0, error=err, code=rc, col_types=[r.col_types[i] for i in range(r.ncols)],
                                rows=[], nrows=n, hop_frontier=[r.hop_frontier[i] for i in range(r.nhops)],
                                hop_edges=[r.hop_edges[i] for i in range(r.nhops)],
-                               hop_next=[r.hop_next[i] for i in range(r.nhops)], device_ms=r.device_ms)
+                               hop_next=[r.hop_next[i] for i in range(r.nhops)],
+                               hop_xchg=[r.hop_exchange_bytes[i] for i in range(r.nhops)] if r.hop_exchange_bytes else [],
+                               device_ms=r.device_ms)
                 if fetch and rc == 0:
                     res.src = self._d2h(r.dev_src, n, np.int64)
                     res.dst = self._d2h(r.dev_dst, n, np.int64)
@@ -396,7 +403,7 @@ class Engine:
                                              self._d2h(dc.type, n, np.uint8) if dc.type else None))
                 return res
             if columnar:
-                return self._columnar(r, rc, err, rows)
+                return self._columnar(r, rc, err, rows, digest_fn)
             res = GoResult(
                 ok=rc == 0, error=err, code=rc, col_types=[r.col_types[i] for i in range(r.ncols)],
                 rows=_cells(r.cells, n, r.ncols, strings) if rows else [],
@@ -404,24 +411,33 @@ class Engine:
                 rank=_arr(r.row_rank, n, np.int64), etype=_arr(r.row_type, n, np.int32),
                 hop_frontier=[r.hop_frontier[i] for i in range(r.nhops)],
                 hop_edges=[r.hop_edges[i] for i in range(r.nhops)],
-                hop_next=[r.hop_next[i] for i in range(r.nhops)], device_ms=r.device_ms, nrows=n)
+                hop_next=[r.hop_next[i] for i in range(r.nhops)],
+                               hop_xchg=[r.hop_exchange_bytes[i] for i in range(r.nhops)] if r.hop_exchange_bytes else [],
+                               device_ms=r.device_ms, nrows=n)
             return res
         finally:
             self.L.ngx_go_result_free(out)
 
-    def _columnar(self, r, rc, err, rows):
+    def _columnar(self, r, rc, err, rows, digest_fn=None):
         n = r.nrows
         types = [r.col_types[i] for i in range(r.ncols)]
         res = GoResult(ok=rc == 0, error=err, code=rc, col_types=types, rows=[], nrows=n,
                        hop_frontier=[r.hop_frontier[i] for i in range(r.nhops)],
                        hop_edges=[r.hop_edges[i] for i in range(r.nhops)],
-                       hop_next=[r.hop_next[i] for i in range(r.nhops)], device_ms=r.device_ms)
+                       hop_next=[r.hop_next[i] for i in range(r.nhops)],
+                               hop_xchg=[r.hop_exchange_bytes[i] for i in range(r.nhops)] if r.hop_exchange_bytes else [],
+                               device_ms=r.device_ms)
         if rc != 0:
             return res
         res.src, res.dst, res.rank = _arr(r.row_src, n, np.int64), _arr(r.row_dst, n, np.int64), \
             _arr(r.row_rank, n, np.int64)
         res.etype = _arr(r.row_type, n, np.int32) if r.row_type else np.full(n, r.dev_type_const, np.int32)
         cols = ctypes.cast(r.host_cols, P(DevColumn)) if r.host_cols else None
+        if digest_fn is not None:
+            res.digests = digest_fn(types, n, [cols[c].x for c in range(r.ncols)],
+                                    [cols[c].len for c in range(r.ncols)], [cols[c].type for c in range(r.ncols)])
+            if not rows:
+                return res
         for c in range(r.ncols):
             dc = cols[c]
             x = _arr(ctypes.cast(dc.x, P(c_i64)), n, np.int64)

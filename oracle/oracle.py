@@ -10,6 +10,7 @@ import ctypes
 import os
 import struct
 import subprocess
+import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -66,6 +67,8 @@ def lib():
         L.orc_row_read.restype = vp
         L.orc_row_schema_ver.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
         L.orc_row_schema_ver.restype = ctypes.c_int32
+        L.orc_digest_columns.argtypes = [ctypes.c_int32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.orc_gen_buckets.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]
         L.orc_gen_buckets.restype = ctypes.c_int32
         _lib = L
@@ -185,6 +188,26 @@ def gen_buckets(n: int, min_per_bucket: int, max_handlers: int) -> List[int]:
     return list(out[:k])
 
 
+def sort_digests(raw: np.ndarray) -> np.ndarray:
+    """16-byte row digests -> (n, 2) uint64 array in sorted row order (a multiset fingerprint)."""
+    d = np.ascontiguousarray(raw).view(np.uint64).reshape(-1, 2)
+    order = np.lexsort((d[:, 1], d[:, 0]))
+    return d[order]
+
+
+def digest_columns(col_types: Sequence[int], nrows: int, x_ptrs, len_ptrs, t_ptrs) -> np.ndarray:
+    """Sorted digests of rows given column-wise (pointers of a host_columnar device result)."""
+    n = len(col_types)
+    ct = (ctypes.c_int32 * max(1, n))(*col_types)
+    X = (ctypes.c_void_p * max(1, n))(*x_ptrs)
+    L_ = (ctypes.c_void_p * max(1, n))(*len_ptrs)
+    T = (ctypes.c_void_p * max(1, n))(*t_ptrs)
+    out = np.zeros(16 * max(nrows, 1), dtype=np.uint8)
+    if nrows:
+        lib().orc_digest_columns(n, ct, nrows, X, L_, T, out.ctypes.data)
+    return sort_digests(out[:16 * nrows])
+
+
 def _decode_row(r: _Rd):
     raw = r.str()
     n = r.get("i")
@@ -213,6 +236,7 @@ class GoResult:
     hop_scanned: List[int] = field(default_factory=list)
     seconds: float = 0.0                 # wall time of the restated GoExecutor run (no serialisation)
     nrows: int = 0
+    digests: Optional[np.ndarray] = None  # digest=True: sorted 16-byte row digests
 
 
 def _cell(r: _Rd):
@@ -290,7 +314,11 @@ class Oracle:
         for owner, i, name in return_columns:
             b += struct.pack("<ii", owner, i) + _s(name)
         b += struct.pack("<B", 1 if only_vertex_props else 0)
-        r = _Rd(_call(self.L.orc_get_neighbors, self.h, b, len(b)))
+        t0 = time.perf_counter()
+        n = ctypes.c_uint64(0)
+        p = self.L.orc_get_neighbors(self.h, b, len(b), ctypes.byref(n))
+        self.last_seconds = time.perf_counter() - t0     # processor + response encoding, no Python decode
+        r = _Rd(_take(p, n.value))
         failed = [r.get("ii") for _ in range(r.get("i"))]
 
         def schemas():
@@ -322,8 +350,9 @@ class Oracle:
             verts.append({"vid": vid, "tags": tags, "edges": edata})
         return NeighborsResponse(failed, vs, es, verts, r.get("i"))
 
-    def go(self, space: int, s, pushdown=True, rows=True) -> GoResult:
-        """Run a parsed nebula_amd.ngql.GoSentence through the restated GoExecutor."""
+    def go(self, space: int, s, pushdown=True, rows=True, digest=False) -> GoResult:
+        """Run a parsed nebula_amd.ngql.GoSentence through the restated GoExecutor. digest=True
+        returns the rows as sorted 128-bit digests of their serialized cells (digest_columns())."""
         b = struct.pack("<IIi", s.record_from, s.record_to, len(s.vids)) + struct.pack(f"<{len(s.vids)}q", *s.vids)
         b += struct.pack("<i", len(s.over))
         for n, a in s.over:
@@ -333,17 +362,21 @@ class Oracle:
         b += struct.pack("<Bi", 1 if s.distinct else 0, len(s.yields))
         for y in s.yields:
             b += _s(y.expr.encode()) + _s(y.alias)
-        b += struct.pack("<BB", 1 if pushdown else 0, 0 if rows else 1)
+        b += struct.pack("<BB", 1 if pushdown else 0, 2 if digest else (0 if rows else 1))
         r = _Rd(_call(self.L.orc_go, self.h, space, b, len(b)))
         ok = r.get("B") == 1
         err = r.str().decode()
         ncol = r.get("i")
         types = [r.get("i") for _ in range(ncol)]
         nrows = r.get("q")
-        out = [tuple(_cell(r) for _ in range(ncol)) for _ in range(nrows)] if rows else []
+        dig = None
+        if digest:
+            dig = sort_digests(np.frombuffer(r.b, dtype=np.uint8, count=16 * nrows, offset=r.p))
+            r.p += 16 * nrows
+        out = [tuple(_cell(r) for _ in range(ncol)) for _ in range(nrows)] if rows and not digest else []
         hops = r.get("i")
         fr, sc = [], []
         for _ in range(hops):
             fr.append(r.get("q"))
             sc.append(r.get("q"))
-        return GoResult(ok, err, types, out, fr, sc, r.get("d"), nrows)
+        return GoResult(ok, err, types, out, fr, sc, r.get("d"), nrows, dig)

@@ -1,3 +1,4 @@
+#include <thread>
 #include <chrono>
 // ORACLE — TEST INFRASTRUCTURE ONLY (see orc_core.h header).
 // extern "C" surface used by oracle/oracle.py (ctypes). Requests arrive as little-endian blobs
@@ -76,9 +77,82 @@ void cell(Writer& w, SupportedType t, const Variant& v) {
     }
 }
 
+template <typename F>
+void parallelChunks(uint64_t n, F&& f) {
+    unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (n < (1u << 15) || T == 1) { f(0, n); return; }
+    std::vector<std::thread> ts;
+    for (unsigned t = 0; t < T; t++) ts.emplace_back([&f, n, t, T] { f(n * t / T, n * (t + 1) / T); });
+    for (auto& th : ts) th.join();
+}
+
+// 128-bit digest of one serialized row (test comparison of large results: sorted digests of the
+// device's rows against the oracle's, instead of Python tuples)
+void rowDigest(const std::string& b, uint8_t* out16) {
+    uint64_t h1 = 1469598103934665603ULL, h2 = 0x9E3779B97F4A7C15ULL ^ b.size();
+    for (unsigned char ch : b) { h1 ^= ch; h1 *= 1099511628211ULL; }
+    size_t i = 0;
+    for (; i + 8 <= b.size(); i += 8) {
+        uint64_t k;
+        std::memcpy(&k, b.data() + i, 8);
+        k *= 0x87c37b91114253d5ULL; k = (k << 31) | (k >> 33); k *= 0x4cf5ad432745937fULL;
+        h2 ^= k; h2 = ((h2 << 27) | (h2 >> 37)) * 5 + 0x52dce729;
+    }
+    uint64_t k = 0;
+    for (size_t j = 0; i + j < b.size(); j++) k |= static_cast<uint64_t>(static_cast<unsigned char>(b[i + j])) << (8 * j);
+    h2 ^= k * 0x87c37b91114253d5ULL;
+    h2 ^= h2 >> 33; h2 *= 0xff51afd7ed558ccdULL; h2 ^= h2 >> 33;
+    std::memcpy(out16, &h1, 8);
+    std::memcpy(out16 + 8, &h2, 8);
+}
+
 }  // namespace
 
 extern "C" {
+
+// Digest rows given column-wise as the device path's host_columnar result (include/nebula_gn.h):
+// x = value bits (string: host pointer to bytes), len = string lengths or NULL, t = per-row V_* type
+// (1 int, 2 double, 3 bool, 4 string) or NULL for rows of the column's static type. Each row is
+// serialized exactly as orc_go serializes the oracle's cells (ColumnValue typing of
+// toThriftResponse), then digested.
+void orc_digest_columns(int32_t ncols, const int32_t* colTypes, uint64_t nrows, const int64_t* const* x,
+                        const uint32_t* const* len, const uint8_t* const* t, uint8_t* out16) {
+    parallelChunks(nrows, [&](uint64_t lo, uint64_t hi) {
+    Writer w;
+    for (uint64_t r = lo; r < hi; r++) {
+        w.b.clear();
+        for (int32_t c = 0; c < ncols; c++) {
+            int32_t ct = colTypes[c];
+            uint8_t vt;
+            if (t[c]) vt = t[c][r];
+            else vt = ct == BOOL ? 3 : (ct == FLOAT || ct == DOUBLE) ? 2 : ct == STRING ? 4 : 1;
+            int64_t v = x[c][r];
+            double d;
+            std::memcpy(&d, &v, 8);
+            auto str = [&] {
+                uint32_t n = len[c] ? len[c][r] : 0;
+                w.put<uint8_t>(6);
+                w.str(n ? std::string(reinterpret_cast<const char*>(v), n) : std::string());
+            };
+            switch (ct) {
+                case BOOL: w.put<uint8_t>(1); w.put<uint8_t>(v != 0); break;
+                case INT: w.put<uint8_t>(2); w.put<int64_t>(v); break;
+                case VID: w.put<uint8_t>(3); w.put<int64_t>(v); break;
+                case FLOAT: w.put<uint8_t>(4); w.put<double>(d); break;
+                case DOUBLE: w.put<uint8_t>(5); w.put<double>(d); break;
+                case STRING: str(); break;
+                case TIMESTAMP: w.put<uint8_t>(21); w.put<int64_t>(v); break;
+                default:
+                    if (vt == 1) { w.put<uint8_t>(2); w.put<int64_t>(v); }
+                    else if (vt == 2) { w.put<uint8_t>(5); w.put<double>(d); }
+                    else if (vt == 3) { w.put<uint8_t>(0); }
+                    else str();
+            }
+        }
+        rowDigest(w.b, out16 + 16 * r);
+    }
+    });
+}
 
 void* orc_engine_new() { return new StorageEngine(); }
 void orc_engine_free(void* e) { delete static_cast<StorageEngine*>(e); }
@@ -214,7 +288,8 @@ char* orc_go(void* e, int32_t space, const uint8_t* blob, uint64_t len, uint64_t
     for (int32_t i = 0; i < ny; i++) { auto x = r.str(); auto a = r.str(); s.yields.push_back({x, a}); }
     GoFlags f;
     f.filter_pushdown = r.get<uint8_t>() != 0;
-    bool countOnly = r.p < r.e && r.get<uint8_t>() != 0;
+    uint8_t mode = r.p < r.e ? r.get<uint8_t>() : 0;        // 0 cells, 1 count only, 2 row digests
+    bool countOnly = mode != 0;
     auto t0 = std::chrono::steady_clock::now();
     auto res = runGo(*eng, space, s, f);
     double seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -224,6 +299,18 @@ char* orc_go(void* e, int32_t space, const uint8_t* blob, uint64_t len, uint64_t
     w.put<int32_t>(static_cast<int32_t>(res.colTypes.size()));
     for (auto t : res.colTypes) w.put<int32_t>(t);
     w.put<int64_t>(static_cast<int64_t>(res.rows.size()));
+    if (mode == 2) {
+        std::string dig(16 * res.rows.size(), '\0');
+        parallelChunks(res.rows.size(), [&](uint64_t lo, uint64_t hi) {
+            Writer rw;
+            for (uint64_t i = lo; i < hi; i++) {
+                rw.b.clear();
+                for (size_t c = 0; c < res.rows[i].size(); c++) cell(rw, c < res.colTypes.size() ? res.colTypes[c] : UNKNOWN, res.rows[i][c]);
+                rowDigest(rw.b, reinterpret_cast<uint8_t*>(&dig[16 * i]));
+            }
+        });
+        w.b += dig;
+    }
     if (countOnly) res.rows.clear();
     for (auto& row : res.rows) {
         for (size_t c = 0; c < row.size(); c++) {

@@ -1,13 +1,17 @@
 """One shard of a world-N GO run (tests/test_multishard.py starts N of these as child processes).
 
-Every rank loads the same generated rows; ngx_load_kv keeps the parts with part % world == rank
-(Nebula's pickHosts placement, CreateSpaceProcessor.cpp:107-120), ngx_commit all-gathers the vertex
-tables, and each hop's frontier marks are exchanged through `engine.dist_exchange()` (gloo) — the
-host collective of ngx_config.exchange — so N shards can share one GPU. The rank writes its rows
-(normalized cells) and per-hop scanned-edge counts as JSON; the parent merges them as graphd would.
+The rank materialises only its own parts (datagen's sharded generator; ngx_load_kv would drop the
+others anyway: part % world == rank, Nebula's pickHosts placement, CreateSpaceProcessor.cpp:107-120),
+ngx_commit all-gathers the vertex tables, and each hop's frontier marks are exchanged through
+`engine.dist_exchange()` (gloo) — the host collective of ngx_config.exchange — so N shards can share
+one GPU. Per query the rank writes its status, per-hop scanned edges and exchange bytes as JSON and
+its rows as sorted 128-bit digests (oracle.digest_columns, the test checker) in a .npy file; the
+parent merges them as graphd merges storage responses.
 
-Usage: python tests/multishard_worker.py RANK WORLD PORT OUT.json SCALE QUERIES.json [jit|vm]
+Usage: python tests/multishard_worker.py RANK WORLD PORT OUT.json SCALE QUERIES.json [jit|vm] [full|plain]
+(full: in-edges + tag `vt`, the multi-shard parity graph; plain: the bench / C2 layout)
 """
+import datetime
 import json
 import os
 import sys
@@ -20,22 +24,32 @@ def main():
     rank, world, port = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
     out, scale, qfile = sys.argv[4], int(sys.argv[5]), sys.argv[6]
     mode = sys.argv[7] if len(sys.argv) > 7 else "jit"
+    full = (sys.argv[8] if len(sys.argv) > 8 else "full") == "full"
+    import numpy as np
     import torch.distributed as dist
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-    from nebula_amd import engine, ngql
-    from tests import fixtures
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=300))
+    from nebula_amd import datagen, engine, ngql
+    from oracle import oracle
 
     queries = json.load(open(qfile))
-    ds = fixtures.RmatDataset(scale, with_in=True, with_tag=True)
+    rows = datagen.rmat(scale, 16, 42, 100, full, full, rank=rank, world=world, threads=4)
     e = engine.Engine(0, rank, world, exchange=engine.dist_exchange())
     e.set_flag("jit", 1 if mode == "jit" else 0)
-    ds.load_engine(e)
+    e.add_space(datagen.RMAT_SPACE, 100)
+    for is_edge, sid, name, fields in datagen.rmat_schemas(full):
+        e.add_schema(datagen.RMAT_SPACE, is_edge, sid, name, fields)
+    e.load_kv(datagen.RMAT_SPACE, *rows.arrays())
+    rows.free()
+    e.commit(datagen.RMAT_SPACE)
     res = []
-    for q in queries:
-        r = e.go(ds.space, ngql.parse_go(q["text"]), pushdown=q.get("pushdown", True))
-        res.append({"ok": r.ok, "error": r.error, "col_types": list(r.col_types) if r.ok else [],
-                    "rows": [list(t) for t in fixtures.normalize_cells(r.rows)] if r.ok else [],
-                    "hop_edges": list(r.hop_edges), "jit_failed": e.get_flag("jit_failed")})
+    for i, q in enumerate(queries):
+        r = e.go(datagen.RMAT_SPACE, ngql.parse_go(q["text"]), pushdown=q.get("pushdown", True), columnar=True,
+                 rows=False, digest_fn=oracle.digest_columns)
+        np.save(f"{out}.{i}.npy", r.digests if r.ok else np.zeros((0, 2), np.uint64))
+        res.append({"ok": r.ok, "error": r.error, "col_types": list(r.col_types) if r.ok else [], "nrows": r.nrows,
+                    "hop_edges": list(r.hop_edges), "hop_xchg": list(r.hop_xchg),
+                    "jit_failed": e.get_flag("jit_failed")})
     e.close()
     with open(out, "w") as f:
         json.dump(res, f)

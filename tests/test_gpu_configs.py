@@ -1,0 +1,220 @@
+"""BASELINE.json configs at their stated sizes, HIP path (C ABI, device 0) against the oracle.
+
+* C1  NBA fixture (TraverseTestBase), GO 2 STEPS OVER like / serve WHERE ... YIELD ...
+* C2  RMAT scale 22, edge factor 16, 100 parts, e(p0 INT, p1 INT), the bench query
+      `GO 3 STEPS ... WHERE e.p0 < 50 YIELD e._dst, e._rank, e.p0, e.p1`: a seed subset row-for-row
+      against the oracle; the full 1000-seed batch through size-independent properties.
+* C4  power law with 4 supernodes of in-degree ~1e6 (one frontier entry spans ~470 chunks of 2048
+      edges), GO 1/2 STEPS REVERSELY.
+* C5  LDBC-SNB-like (knows / likes / hasCreator, string + int props), a 10k-vid batch, GO 4 STEPS,
+      compound WHERE, multi-column YIELD.
+(C3, 8 shards, is rehearsed in tests/test_multishard.py at world 8 over the host exchange.)
+
+Large results are compared as sorted 128-bit digests of each row's serialized cells (the oracle's
+ColumnValue bytes; oracle.digest_columns builds the same bytes from the device's host_columnar
+arrays), so a difference in any row, value, type or multiplicity fails.
+"""
+import numpy as np
+import pytest
+
+from nebula_amd import datagen, engine, ngql
+from oracle import oracle
+from tests import fixtures
+
+pytestmark = pytest.mark.gpu
+
+C2_QUERY = "GO 3 STEPS FROM {S} OVER e WHERE e.p0 < {K} YIELD e._dst, e._rank, e.p0, e.p1"
+
+
+def _digest_go(e, space, s, pushdown=True):
+    r = e.go(space, s, pushdown=pushdown, columnar=True, rows=False, digest_fn=oracle.digest_columns)
+    assert r.ok, r.error
+    return r
+
+
+def _same_digests(got, ref):
+    assert ref.ok, ref.error
+    assert got.nrows == ref.nrows
+    assert got.col_types == ref.col_types or ref.nrows == 0
+    assert np.array_equal(got.digests, ref.digests)
+
+
+def _seed_list(vids):
+    return ", ".join(str(int(v)) for v in vids)
+
+
+# ----------------------------------------------------------------------------------------- C1
+C1_QUERIES = [
+    "GO 2 STEPS FROM {P:Tim Duncan}, {P:Tony Parker}, {P:LeBron James} OVER like WHERE like.likeness > 80 "
+    "YIELD like._dst, like.likeness, $^.player.name, $$.player.age",
+    "GO 2 STEPS FROM {P:Tim Duncan}, {P:Kobe Bryant}, {P:Dwyane Wade} OVER like, serve "
+    "WHERE $^.player.age >= 30 YIELD like._dst, serve._dst, serve.start_year, like.likeness, $$.team.name",
+    "GO 2 STEPS FROM {P:Manu Ginobili} OVER serve, like REVERSELY WHERE $^.player.age > 30 "
+    "YIELD serve._dst, like._dst, $^.player.name",
+]
+
+
+@pytest.mark.parametrize("mode", ["jit", "vm"])
+@pytest.mark.parametrize("pushdown", [True, False])
+@pytest.mark.parametrize("qi", range(len(C1_QUERIES)))
+def test_c1_nba_go2(qi, pushdown, mode):
+    ds = fixtures.nba()
+    o = oracle.Oracle()
+    ds.load_oracle(o)
+    with engine.Engine(0) as e:
+        e.set_flag("jit", 1 if mode == "jit" else 0)
+        ds.load_engine(e)
+        s = ngql.parse_go(fixtures.nba_query(C1_QUERIES[qi]))
+        ref = o.go(ds.space, s, pushdown=pushdown)
+        got = e.go(ds.space, s, pushdown=pushdown)
+        assert got.ok == ref.ok, (got.error, ref.error)
+        assert ref.rows
+        assert fixtures.normalize_cells(got.rows) == fixtures.normalize_cells(ref.rows)
+        assert got.col_types == ref.col_types
+
+
+# ----------------------------------------------------------------------------------------- C2
+@pytest.fixture(scope="module")
+def c2(rmat22):
+    ds, o = rmat22
+    e = engine.Engine(0)
+    ds.load_engine(e)
+    info = e.info(ds.space)
+    assert info.vertices > 2_000_000 and info.edges > 60_000_000          # scale 22, ef 16, collapsed
+    yield ds, o, e
+    e.close()
+
+
+@pytest.mark.timeout(600)
+def test_c2_bench_query_seed_subset(c2):
+    """The bench query at full scale 22 from 2 seeds (hop 3 scans ~30 M edges, ~15 M rows): every
+    row equal to the oracle's, and every hop's scanned edges, with the generated and the interpreter
+    final-hop kernels."""
+    ds, o, e = c2
+    seeds = datagen.rmat_seeds(22, 2, 16, 42, 4242, threads=16)
+    s = ngql.parse_go(C2_QUERY.replace("{S}", _seed_list(seeds)).replace("{K}", "50"))
+    ref = o.go(ds.space, s, digest=True)
+    for mode in (1, 0):
+        e.set_flag("jit", mode)
+        got = _digest_go(e, ds.space, s)
+        assert got.hop_edges == ref.hop_scanned
+        assert sum(got.hop_edges) > 10_000_000
+        _same_digests(got, ref)
+    e.set_flag("jit", 1)
+
+
+@pytest.mark.timeout(600)
+def test_c2_full_batch_properties(c2):
+    """The bench step itself (1000 seeds, ~85 M scanned edges, ~32 M rows), checked through properties
+    that hold at any size:
+      * the precompiled interpreter kernels and the per-query generated kernels return the same rows;
+      * without WHERE every scanned edge of the last hop is a row;
+      * WHERE p0 < 50 and WHERE p0 >= 50 partition those rows (filter linearity), and the rows of
+        `p0 < 50` are exactly the p0 < 50 rows of the unfiltered result (p0 values counted)."""
+    ds, o, e = c2
+    seeds = _seed_list(datagen.rmat_seeds(22, 1000, 16, 42, 42, threads=16))
+    q50 = ngql.parse_go(C2_QUERY.replace("{S}", seeds).replace("{K}", "50"))
+    e.set_flag("jit", 1)
+    jit = _digest_go(e, ds.space, q50)
+    e.set_flag("jit", 0)
+    vm = _digest_go(e, ds.space, q50)
+    e.set_flag("jit", 1)
+    assert jit.nrows > 20_000_000 and jit.hop_edges == vm.hop_edges
+    assert np.array_equal(jit.digests, vm.digests)
+    everything = e.go(ds.space, ngql.parse_go(
+        f"GO 3 STEPS FROM {seeds} OVER e YIELD e._dst, e._rank, e.p0, e.p1"), columnar=True, rows=False)
+    ge = e.go(ds.space, ngql.parse_go(
+        f"GO 3 STEPS FROM {seeds} OVER e WHERE e.p0 >= 50 YIELD e._dst"), on_device=True)
+    assert everything.ok and ge.ok
+    assert everything.nrows == everything.hop_edges[-1] == jit.hop_edges[-1]
+    assert jit.nrows + ge.nrows == everything.nrows
+    p0 = everything.dev_cols[2][0]
+    assert int(np.count_nonzero(p0 < 50)) == jit.nrows
+
+
+# ----------------------------------------------------------------------------------------- C4
+@pytest.fixture(scope="module")
+def c4():
+    ds = fixtures.powerlaw_dataset(8_000_000, ef=2, nsuper=4, superdeg=1_000_000, threads=16)
+    o = oracle.Oracle()
+    o.set_flags(threads=16)
+    ds.load_oracle(o, threads=16)
+    e = engine.Engine(0)
+    ds.load_engine(e)
+    ds.rows.free()
+    yield ds, o, e
+    e.close()
+    o.close()
+
+
+SUPERNODES = [0, 7919, 15838, 23757]          # datagen.cpp ngd_powerlaw: (j / superdeg) * 7919 % n
+
+C4_QUERIES = [
+    "GO 1 STEPS FROM {S} OVER pl REVERSELY YIELD pl._dst, pl.w, pl.score",
+    "GO 2 STEPS FROM {S} OVER pl REVERSELY WHERE pl.w == 7 YIELD pl._dst, pl._src, pl.score",
+    "GO 2 STEPS FROM {S} OVER pl REVERSELY WHERE pl.w < 3 && pl.score > 0.5 YIELD pl._dst, pl.w * 2 + 1",
+]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("qi", range(len(C4_QUERIES)))
+def test_c4_supernodes_reversely(c4, qi):
+    """Supernode seeds: in-degree ~0.94e6 each, so a single frontier entry covers ~460 workgroup chunks
+    (edge-balanced expansion); REVERSELY has no pushdown, graphd evaluates WHERE (GoExecutor.cpp:528-533).
+    Generated and interpreter kernels."""
+    ds, o, e = c4
+    s = ngql.parse_go(C4_QUERIES[qi].replace("{S}", _seed_list(SUPERNODES)))
+    ref = o.go(ds.space, s, digest=True)
+    for mode in (1, 0):
+        e.set_flag("jit", mode)
+        got = _digest_go(e, ds.space, s)
+        assert got.hop_edges == ref.hop_scanned
+        assert got.hop_edges[0] > 3_600_000                  # ~4 x 0.94e6 in-edges in hop 1
+        _same_digests(got, ref)
+        assert got.nrows > 0
+    e.set_flag("jit", 1)
+
+
+# ----------------------------------------------------------------------------------------- C5
+@pytest.fixture(scope="module")
+def c5():
+    ds = fixtures.snb_dataset(50_000, knows_deg=20, likes_deg=10, threads=16)
+    o = oracle.Oracle()
+    o.set_flags(threads=16)
+    ds.load_oracle(o, threads=16)
+    e = engine.Engine(0)
+    ds.load_engine(e)
+    yield ds, o, e
+    e.close()
+    o.close()
+
+
+C5_QUERIES = [
+    "GO 4 STEPS FROM {S} OVER knows WHERE knows.creationDate > 1400000000 && $^.person.gender == \"female\" "
+    "YIELD knows._dst, knows.weight, $^.person.firstName, $$.person.age",
+    "GO 4 STEPS FROM {S} OVER knows, likes WHERE $^.person.age < 40 && $^.person.gender == \"male\" "
+    "YIELD knows._dst, likes._dst, likes.creationDate, knows.weight, $^.person.firstName",
+    "GO 4 STEPS FROM {S} OVER likes, hasCreator WHERE $$.post.lang == \"en\" || $$.person.age > 60 "
+    "YIELD likes._dst, hasCreator._dst, $$.post.content, $$.post.length, $$.person.firstName",
+]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("pushdown", [True, False])
+@pytest.mark.parametrize("qi", range(len(C5_QUERIES)))
+def test_c5_snb_10k_batch(c5, qi, pushdown):
+    """A 10 000-person seed batch, GO 4 STEPS, compound WHERE over edge / $^ / $$ props, string and int
+    YIELD columns (strings delivered as host pointers in the columnar result). Generated and
+    interpreter kernels."""
+    ds, o, e = c5
+    seeds = datagen.sample_vids(9000 + qi, ds.np, 10_000)
+    s = ngql.parse_go(C5_QUERIES[qi].replace("{S}", _seed_list(seeds)))
+    ref = o.go(ds.space, s, pushdown=pushdown, digest=True)
+    for mode in (1, 0):
+        e.set_flag("jit", mode)
+        got = _digest_go(e, ds.space, s, pushdown=pushdown)
+        assert got.hop_edges == ref.hop_scanned
+        assert got.hop_frontier[0] == 10_000
+        _same_digests(got, ref)
+        assert got.nrows > 0
+    e.set_flag("jit", 1)
