@@ -1,18 +1,26 @@
 """Benchmark: traversed edges/sec of `GO 3 STEPS FROM <1k vids> OVER e WHERE e.p0 < 50 YIELD e._dst,
-e._rank, e.p0, e.p1` on an RMAT graph (BASELINE.json configs[1]: scale 22, edge factor 16, 100 parts;
-weak scaling: scale 22 + log2(N) over N GPUs, parts hashed to GPUs as part % N).
+e._rank, e.p0, e.p1` on an RMAT graph (BASELINE.json metric).
 
-One step = one GO query through libnebula_gn (seeds on host -> result rows and cells on host),
+Workload by GPU count (one process per GPU, parts hashed to GPUs as part % N, Nebula's pickHosts):
+  N = 1  configs[1] (C2): RMAT scale 22, edge factor 16, 100 parts
+  N = 8  configs[2] (C3): RMAT scale 26, edge factor 16, 100 parts, per-hop frontier all-to-all (RCCL)
+  N = 2, 4: scale 22 + log2(N) (weak scaling between the two anchors); --scale overrides.
+
+One step = one GO query through libnebula_gn (seeds on host -> result rows and YIELD columns in HBM),
 with a fresh 1k-seed sample per step. Traversed edges = sum over hops of the edges scanned
-(SURVEY.md §8d). The JSON line also carries the HBM roofline of the dominant kernel (HIP events on
-the engine stream) and a CPU baseline (the oracle restatement on a bounded sample, rank 0, N=1).
+(SURVEY.md §8d), summed over ranks. The JSON line also carries the HBM roofline of the dominant
+kernel (HIP events on the engine stream), the per-hop frontier exchange (N > 1), the host-delivery
+cost of the rows, and a CPU baseline (rank 0, N = 1): the oracle restatement of the reference path
+on the same graph, all host cores for GO end to end plus one thread for storage-only GetNeighbors.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]; N > 1 under torch.distributed.run.
 """
 import argparse
+import datetime
 import json
 import math
 import os
+import platform
 import sys
 import time
 
@@ -22,6 +30,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
 METRIC = "traversed edges/sec for GO 3 STEPS WHERE on RMAT; % HBM roofline"
 QUERY = "GO 3 STEPS FROM {S} OVER e WHERE e.p0 < 50 YIELD e._dst, e._rank, e.p0, e.p1"
+NOT_HBM = ("exchange",)        # kernel classes whose bytes are not HBM traffic (xGMI, reported apart)
 
 
 def log(*a):
@@ -33,11 +42,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--scale", type=int, default=0, help="RMAT scale (default 22 + log2(N))")
+    p.add_argument("--scale", type=int, default=0, help="RMAT scale (default: 22 at N=1, 26 at N=8, else 22+log2 N)")
     p.add_argument("--ef", type=int, default=16)
     p.add_argument("--seeds", type=int, default=1000)
     p.add_argument("--parts", type=int, default=100)
-    p.add_argument("--cpu-budget", type=float, default=10.0, help="target seconds of oracle work (0: skip)")
+    p.add_argument("--cpu-budget", type=float, default=20.0, help="target seconds of oracle GO work (0: skip)")
     p.add_argument("--threads", type=int, default=16, help="host threads for datagen / oracle")
     p.add_argument("--host-exchange", action="store_true",
                    help="rehearsal of the N > 1 path on one GPU: every rank on device 0, frontier exchange "
@@ -47,6 +56,29 @@ def parse():
     return p.parse_args()
 
 
+def default_scale(world):
+    if world == 8:
+        return 26
+    return 22 + int(round(math.log2(world)))
+
+
+def cpu_info():
+    model = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, usable
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -54,7 +86,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
-    scale = args.scale or 22 + int(round(math.log2(world)))
+    scale = args.scale or default_scale(world)
 
     import numpy as np
     import torch
@@ -65,7 +97,8 @@ def main():
     torch.cuda.set_device(device)
     uid, xchg = None, None
     if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # bounded collectives: a dead rank ends the others instead of hanging the node
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=600))
         if args.host_exchange:
             xchg = engine.dist_exchange()
         else:
@@ -73,6 +106,10 @@ def main():
             dist.broadcast_object_list(obj, src=0)
             uid = obj[0]
 
+    build = engine.build_info()
+    if rank == 0:
+        log(f"[rank 0] libnebula_gn {build['raw']} (sources in tree: {build['tree_sha']}, "
+            f"match={build['matches_tree']})")
     t0 = time.time()
     rows = datagen.rmat(scale, args.ef, 42, args.parts, with_in=False, with_tag=False, rank=rank, world=world,
                         threads=args.threads)
@@ -97,8 +134,8 @@ def main():
 
     plans = [sentence(i, args.seeds) for i in range(args.warmup + args.steps)]
 
-    def step(s, on_device=True):
-        r = eng.go(datagen.RMAT_SPACE, s, rows=False, on_device=on_device)
+    def step(s, on_device=True, columnar=False, rows_=False):
+        r = eng.go(datagen.RMAT_SPACE, s, rows=rows_, on_device=on_device, columnar=columnar, arrays=False)
         if not r.ok:
             raise RuntimeError(r.error)
         return r
@@ -118,39 +155,51 @@ def main():
     result_rows = 0
     dev_ms = 0.0
     hop_edges = None
+    hop_xchg = None
     for i in range(args.steps):
         r = step(plans[args.warmup + i])
         edges += sum(r.hop_edges)
         result_rows += r.nrows
         dev_ms += r.device_ms
         hop_edges = r.hop_edges
+        hop_xchg = r.hop_xchg
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t_start
     stats = eng.kernel_stats()
     eng.set_profiling(False)
-    # the same steps with the result rows and typed cells delivered to host memory (reported only)
+
+    # the same steps with the rows delivered to host memory (reported, never `value`): columnar arrays
+    # in page-locked staging (host_columnar), and typed cells (ColumnValue) built on host threads
     host_steps = min(2, args.steps)
+    step(plans[0], on_device=False, columnar=True)          # sizes the page-locked staging once
     barrier()
     t_h = time.perf_counter()
     for i in range(host_steps):
-        step(plans[args.warmup + i], on_device=False)
+        step(plans[args.warmup + i], on_device=False, columnar=True)
     barrier()
-    host_ms = (time.perf_counter() - t_h) * 1e3 / max(host_steps, 1)
+    host_col_ms = (time.perf_counter() - t_h) * 1e3 / max(host_steps, 1)
+    t_h = time.perf_counter()
+    step(plans[args.warmup], on_device=False)
+    barrier()
+    host_cell_ms = (time.perf_counter() - t_h) * 1e3
     jit = {"compiled": eng.get_flag("jit_compiled"), "failed": eng.get_flag("jit_failed"),
            "compile_ms": eng.get_flag("jit_compile_us") / 1e3, "vgprs": eng.get_flag("jit_vgprs"),
            "scratch_bytes": eng.get_flag("jit_scratch"), "note": eng.jit_note()}
 
+    xchg_ms = stats.get("exchange", (0, 0.0, 0))[1]
+    xchg_bytes = stats.get("exchange", (0, 0.0, 0))[2]
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
+        t = torch.tensor([elapsed, xchg_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t[0])
-        e = torch.tensor([edges, result_rows], dtype=torch.int64)
+        elapsed, xchg_ms_max = float(t[0]), float(t[1])
+        e = torch.tensor([edges, result_rows, xchg_bytes], dtype=torch.int64)
         dist.all_reduce(e, op=dist.ReduceOp.SUM)
-        edges, result_rows = int(e[0]), int(e[1])
+        edges, result_rows, xchg_bytes_all = int(e[0]), int(e[1]), int(e[2])
 
     # dominant kernel roofline (algorithmic bytes / HIP-event time)
-    dom = max(stats.items(), key=lambda kv: kv[1][1]) if stats else None
+    hbm = {k: v for k, v in stats.items() if k not in NOT_HBM}
+    dom = max(hbm.items(), key=lambda kv: kv[1][1]) if hbm else None
     roof = None
     if dom:
         name, (launches, ms, algo) = dom
@@ -167,25 +216,28 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": name,
                 "launches": launches, "avg_launch_us": round(ms * 1e3 / max(launches, 1), 2),
                 "algo_bytes_per_launch": algo // max(launches, 1)}
-    all_ms = sum(v[1] for v in stats.values())
-    all_bytes = sum(v[2] for v in stats.values())
+    all_ms = sum(v[1] for v in hbm.values())
+    all_bytes = sum(v[2] for v in hbm.values())
 
     cpu = None
     if keep_rows:
-        cpu = cpu_baseline(rows, scale, args)
+        cpu = cpu_baseline(rows, scale, args, edges // max(args.steps, 1))
         rows.free()
 
     if rank == 0:
         tepss = edges / elapsed
+        workload = ("C3" if world == 8 and scale == 26 else "C2" if world == 1 and scale == 22 else "weak-scaling")
         out = {
             "metric": METRIC, "value": round(tepss, 1), "unit": "edges/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "int64",
             "data": "synthetic RMAT (Graph500 .57/.19/.19/.05, splitmix64 seed 42), reference KV format",
-            "config": {"workload": f"C2: RMAT scale-{scale} ef{args.ef}, 1 edge type e(p0 int, p1 int), "
-                                   f"{args.parts} parts, GO 3 STEPS from {args.seeds} vids WHERE e.p0 < 50",
+            "config": {"workload": f"{workload}: RMAT scale-{scale} ef{args.ef}, 1 edge type e(p0 int, p1 int), "
+                                   f"{args.parts} parts over {world} GPU(s), GO 3 STEPS from {args.seeds} vids "
+                                   "WHERE e.p0 < 50",
                        "scale": scale, "edge_factor": args.ef, "parts": args.parts, "seeds": args.seeds,
                        "query": QUERY.replace("{S}", f"<{args.seeds} vids>"),
+                       "scale_rule": "N=1: 22 (C2), N=8: 26 (C3), else 22+log2(N)",
                        "parallelism": f"{world} shard(s), part % {world}, "
                                       + ("host (gloo) exchange, all shards on GPU 0 (rehearsal)" if args.host_exchange
                                          else "RCCL bitmap all-to-all per hop")},
@@ -195,50 +247,84 @@ def main():
             "rows_per_step": result_rows // args.steps,
             "hop_edges_last_step": hop_edges,
             "device_ms_per_step": round(dev_ms / args.steps, 3),
-            "ms_per_step_host_rows": round(host_ms, 3),
-            "timed_region": "seeds on host -> result rows + YIELD cells in HBM (result_on_device); "
-                            "ms_per_step_host_rows adds D2H and host cell conversion",
+            "timed_region": "seeds on host -> result rows + YIELD columns in HBM (result_on_device)",
+            "host_delivery": {"ms_per_step_columnar": round(host_col_ms, 3), "ms_per_step_cells": round(host_cell_ms, 3),
+                              "note": "same query with the rows copied to host memory: columnar arrays in "
+                                      "page-locked staging (host_columnar), or typed ColumnValue cells"},
             "jit": jit,
             "path_roofline": {"algo_bytes": all_bytes, "kernel_ms": round(all_ms, 3),
                               "frac": round(all_bytes / (all_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if all_ms else None},
             "kernels": {k: {"launches": v[0], "ms": round(v[1], 3), "algo_bytes": v[2]} for k, v in stats.items()},
+            "build": {"library": build["raw"], "sources_sha": build["tree_sha"], "matches_tree": build["matches_tree"]},
         }
+        if world > 1:
+            out["exchange"] = {"bytes_per_step_all_ranks": xchg_bytes_all // args.steps,
+                               "rank0_bytes_per_hop_last_step": hop_xchg,
+                               "ms_per_step_max_rank": round(xchg_ms_max / args.steps, 3),
+                               "note": "per-hop bitmap all-to-all of next-frontier rows (RCCL send/recv over xGMI); "
+                                       "HIP-event time includes pack + merge kernels"}
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:
         dist.destroy_process_group()
 
 
-def cpu_baseline(rows, scale, args):
-    """The oracle (C++ restatement of storaged + GoExecutor) on the same graph and query shape, with a
-    seed count doubled from 4 until one run takes >= cpu_budget/2 seconds."""
+def cpu_baseline(rows, scale, args, gpu_edges_per_step):
+    """The oracle (C++ restatement of storaged + GoExecutor, the reference CPU path) on this host, same
+    graph: (1) GO end to end (the bench query) on all threads, seeds added until it traverses >= 10% of
+    one GPU step's edges and runs >= cpu_budget/2 s; (2) storage only, one thread: a GetNeighbors request
+    returning one edge prop, as the reference's GetNeighborsBenchmark (GetNeighborsBenchmark.cpp:390-402)."""
     from nebula_amd import datagen, ngql
     from oracle import oracle
+    model, nproc, usable = cpu_info()
+    threads = max(1, min(args.threads, usable))
     t0 = time.time()
     o = oracle.Oracle()
-    o.set_flags(threads=args.threads)
+    o.set_flags(threads=threads, max_handlers=threads)
     o.add_space(datagen.RMAT_SPACE, args.parts)
     for is_edge, sid, name, fields in datagen.rmat_schemas():
         o.add_schema(datagen.RMAT_SPACE, is_edge, sid, name, fields)
     o.put_kv(datagen.RMAT_SPACE, *rows.arrays())
-    o.finalize(args.threads)
+    o.finalize(threads)
     log(f"oracle loaded in {time.time() - t0:.1f}s")
-    k, best = 4, None
+    k, best = 1, None
     while True:
         seeds = datagen.rmat_seeds(scale, k, args.ef, 42, 42, threads=args.threads)
         s = ngql.parse_go(QUERY.replace("{S}", ", ".join(str(int(v)) for v in seeds)))
         r = o.go(datagen.RMAT_SPACE, s, rows=False)
         edges = sum(r.hop_scanned)
         best = (k, edges, r.seconds)
-        log(f"oracle: {k} seeds, {edges} edges, {r.seconds:.2f}s")
-        if r.seconds >= args.cpu_budget / 2 or k >= args.seeds:
+        log(f"oracle GO: {k} seeds, {edges} edges, {r.seconds:.2f}s")
+        if (edges >= 0.1 * gpu_edges_per_step and r.seconds >= args.cpu_budget / 2) or k >= args.seeds \
+                or r.seconds >= args.cpu_budget:
             break
         k *= 2
     k, edges, sec = best
+    # storage-only, one thread: GetNeighbors over a sample of vertices, `_dst` + one prop, no filter
+    o.set_flags(threads=1, max_handlers=1)
+    vids = datagen.rmat_seeds(scale, 50000, args.ef, 42, 4343, threads=args.threads)
+    parts = {}
+    for v in vids:
+        parts.setdefault(int(v) % args.parts + 1, []).append(int(v))
+    parts = sorted(parts.items())
+    gn = {}
+    for label, cols in (("one_prop", [(3, 1, "_dst"), (3, 1, "p0")]), ("dst_only", [(3, 1, "_dst")])):
+        resp = o.get_neighbors(datagen.RMAT_SPACE, parts, [1], cols)
+        gn[label] = round(resp.total_edges / o.last_seconds, 1)
+        gn["edges"] = resp.total_edges
     o.close()
-    return {"value": round(edges / sec, 1), "unit": "edges/s", "cores": args.threads, "kind": "port",
-            "sample": f"same graph and query, first {k} of the seed sample, {edges} edges traversed in "
-                      f"{sec:.2f}s (oracle C++ restatement, {args.threads} threads)"}
+    return {"value": round(edges / sec, 1), "unit": "edges/s", "cores": threads, "kind": "port",
+            "sample": f"same graph and query, first {k} seed(s) of the seed sample: {edges} edges traversed "
+                      f"({100.0 * edges / max(gpu_edges_per_step, 1):.0f}% of one GPU step) in {sec:.2f}s, "
+                      f"oracle C++ restatement on {threads} threads",
+            "cpu_model": model, "nproc": nproc, "usable_cpus": usable,
+            "storage_get_neighbors_1thread": {
+                "edges_per_s_one_prop": gn["one_prop"], "edges_per_s_dst_only": gn["dst_only"],
+                "edges": gn["edges"],
+                "reference_published": "1.51e6 edges/s one prop, 5.28e6 _dst only, 1 thread, Xeon E5-2690 v2 "
+                                       "(GetNeighborsBenchmark.cpp:390-403)"},
+            "note": "GO end to end is bounded by graphd's single-threaded processFinalResult (re-decode + "
+                    "WHERE + YIELD per returned edge, GoExecutor.cpp:1082-1335), not by the storage scan"}
 
 
 if __name__ == "__main__":

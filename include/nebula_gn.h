@@ -40,6 +40,7 @@ extern "C" {
 #define NGX_E_EDGE_NOT_FOUND (-24)
 #define NGX_E_TAG_NOT_FOUND (-25)
 #define NGX_E_SPACE_NOT_FOUND (-13)
+#define NGX_E_PART_NOT_FOUND (-14)      /* a part this shard does not hold (per-part failed code) */
 #define NGX_E_BAD_ARGUMENT (-1001)
 #define NGX_E_UNSUPPORTED (-1002)       /* a construct the device path does not implement */
 #define NGX_E_QUERY (-1003)             /* graphd-side evaluation error (GoExecutor doError) */
@@ -79,6 +80,9 @@ typedef struct {
 int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out);
 void ngx_close(ngx_ctx* ctx);
 const char* ngx_last_error(ngx_ctx* ctx);
+/* "src_sha=<16 hex> arch=gfx950 built=<date time>": src_sha digests every library source (Makefile
+ * SRCS), so a run can check that the library it loaded was built from the sources beside it */
+const char* ngx_build_info(void);
 /* rank 0 calls this and broadcasts the 128 bytes to the other ranks before ngx_open */
 int32_t ngx_get_unique_id(void* out128);
 
@@ -148,8 +152,8 @@ typedef struct {
     uint32_t filter_len;
     int32_t ncols;
     const ngx_prop_def* cols;     /* return_columns */
-    int32_t max_edges_per_vertex; /* FLAGS_max_edge_returned_per_vertex, <= 0: unlimited */
-    int64_t now_sec;              /* clock for TTL (WallClock::fastNowInSec) */
+    int32_t max_edges_per_vertex; /* FLAGS_max_edge_returned_per_vertex, <= 0 or INT32_MAX: unlimited */
+    int64_t now_sec;              /* clock for TTL (WallClock::fastNowInSec); <= 0: the current time */
 } ngx_gn_request;
 
 typedef struct {
@@ -194,7 +198,7 @@ typedef struct {
     const uint32_t* yield_lens;
     int32_t distinct;                  /* YIELD DISTINCT */
     int32_t filter_pushdown;           /* FLAGS_filter_pushdown */
-    int64_t now_sec;
+    int64_t now_sec;                   /* clock for TTL; <= 0: the current time */
     int32_t result_on_device;          /* 1: leave rows in HBM (dev_* below), no host cells / DISTINCT */
     int32_t host_columnar;             /* 1 (host results): columnar host arrays (host_cols), no cells */
 } ngx_go_plan;
@@ -270,6 +274,9 @@ int32_t ngx_kernel_stats(ngx_ctx* ctx, const ngx_kernel_stat** out, int32_t* n);
  *          final-hop kernels with hipRTC; 0: run the precompiled bytecode-interpreter kernels.
  *          Literals are launch arguments, so queries that differ only in literals share a kernel.
  *   "jit_cache_capacity"  compiled query shapes kept loaded (LRU, default 64).
+ *   "max_edge_returned_per_vertex"  storaged's flag for the storage requests of every GO hop: at most
+ *          this many edges emitted per (vertex, edge type) in key order, counted after the storage
+ *          checks and the pushed filter (QueryBaseProcessor.inl:501-505); <= 0: unlimited (default).
  *   "rccl_timeout_ms"     deadline of every RCCL collective (default 120000; env NGX_RCCL_TIMEOUT_MS).
  *          On a timeout or an asynchronous RCCL error the communicator is aborted, the call returns
  *          NGX_E_DEVICE and every later call on the context fails (the caller exits).

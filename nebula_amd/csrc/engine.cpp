@@ -14,6 +14,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <ctime>
 #include <thread>
 #include <unordered_set>
 
@@ -101,7 +102,8 @@ struct ngx_ctx {
     std::mutex mu;
     // scratch
     DBuf visited, F0, F1, estart, chunkFirst, tileSums, counters, lbStatus, seedPart, seedVid;
-    DBuf oSrc, oDst, oRank, oType, oEntry, progBuf, sendBits, recvBits, vcells, misc, oColDesc;
+    DBuf oSrc, oDst, oRank, oType, oEntry, progBuf, sendBits, recvBits, vcells, misc, oColDesc, edgeMask;
+    int64_t maxEdgesPerVertex = INT32_MAX;             // storaged FLAGS_max_edge_returned_per_vertex (GO hops)
     struct ColBuf { DBuf x, len, t; };
     struct PinBuf {                                     // page-locked host staging for result D2H
         void* p = nullptr;
@@ -145,7 +147,7 @@ struct ngx_ctx {
         spaces.clear();
         for (DBuf* b : {&visited, &F0, &F1, &estart, &tileSums, &counters, &lbStatus, &seedPart, &seedVid, &oSrc,
                         &oDst, &oRank, &oType, &oEntry, &chunkFirst, &oColDesc, &progBuf, &sendBits, &recvBits,
-                        &vcells, &misc}) b->release();
+                        &vcells, &misc, &edgeMask}) b->release();
         for (auto& cb : oCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         hostStage.release();
         for (auto e : eventPool) (void)hipEventDestroy(e);
@@ -253,7 +255,22 @@ void uploadColumns(DeviceGraph& d, std::vector<HostColumn>& hc, uint64_t n) {
     }
 }
 
-std::unique_ptr<DeviceGraph> upload(HostGraph& g) {
+// TTL info of a schema (buildTTLInfoAndRespSchema, QueryBaseProcessor.inl:670-797): present when
+// ttl_col is set and ttl_duration > 0 (rows are then read, bad rows skipped); the column is checked
+// only when the latest schema types it INT / TIMESTAMP / VID (checkDataExpiredForTTL), else -1
+bool ttlInfo(const SchemaSet* ss, int32_t& col, int64_t& dur) {
+    col = -1;
+    dur = 0;
+    if (!ss) return false;
+    const SchemaDef& l = ss->latest();
+    if (l.ttlCol.empty() || l.ttlDur <= 0) return false;
+    int32_t t = l.typeOf(l.ttlCol);
+    if (t == T_INT || t == T_TIMESTAMP || t == T_VID) col = l.index(l.ttlCol);
+    dur = l.ttlDur;
+    return true;
+}
+
+std::unique_ptr<DeviceGraph> upload(HostGraph& g, const Space& sp) {
     auto d = std::make_unique<DeviceGraph>();
     d->V = g.vid.size();
     d->gbase = g.gbase;
@@ -292,6 +309,7 @@ std::unique_ptr<DeviceGraph> upload(HostGraph& g) {
         dt.colBase = static_cast<int32_t>(d->cols.size());
         dt.ncols = static_cast<int32_t>(t.cols.size());
         dt.present = d->upload(t.present.data(), t.present.size());
+        if (!ttlInfo(sp.tag(t.tag), dt.ttlCol, dt.ttlDur)) dt.ttlCol = -1;
         uploadColumns(*d, t.cols, d->V);
         d->tags.push_back(dt);
     }
@@ -672,6 +690,13 @@ void ngx_close(ngx_ctx* c) {
 
 const char* ngx_last_error(ngx_ctx* c) { return c ? c->lastError.c_str() : "no context"; }
 
+#ifndef NGX_SRC_SHA
+#define NGX_SRC_SHA "unknown"
+#endif
+const char* ngx_build_info(void) {
+    return "src_sha=" NGX_SRC_SHA " arch=gfx950 built=" __DATE__ " " __TIME__;
+}
+
 int32_t ngx_add_space(ngx_ctx* c, int32_t space, int32_t numParts) {
     std::lock_guard<std::mutex> g(c->mu);
     auto& sp = c->spaces[space];
@@ -774,7 +799,7 @@ int32_t ngx_commit(ngx_ctx* c, int32_t space) {
         resolveDstRows(*sp, *hg, tables, c->world);
         if (hg->shardBase.empty()) { hg->shardBase = {0, hg->vid.size()}; hg->vglobal = hg->vid.size(); }
         hg->gbase = hg->shardBase[c->rank];
-        sp->dev = upload(*hg);
+        sp->dev = upload(*hg, *sp);
         sp->host = std::move(hg);
         sp->staged = StagedRows();
         return NGX_OK;
@@ -831,6 +856,7 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
     std::string n = name ? name : "";
     if (n == "jit") { c->jitOn = value != 0; return NGX_OK; }
     if (n == "rccl_timeout_ms") { c->rcclTimeoutMs = value < 1 ? 1 : value; return NGX_OK; }
+    if (n == "max_edge_returned_per_vertex") { c->maxEdgesPerVertex = value <= 0 ? INT32_MAX : value; return NGX_OK; }
     if (n == "jit_cache_capacity") { c->jit.capacity = value < 1 ? 1 : static_cast<size_t>(value); return NGX_OK; }
     return fail(c, NGX_E_BAD_ARGUMENT, "unknown flag " + n);
 }
@@ -840,6 +866,7 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     std::string n = name ? name : "";
     if (n == "jit") *value = c->jitOn ? 1 : 0;
     else if (n == "rccl_timeout_ms") *value = c->rcclTimeoutMs;
+    else if (n == "max_edge_returned_per_vertex") *value = c->maxEdgesPerVertex;
     else if (n == "jit_compiled") *value = static_cast<int64_t>(c->jit.compiled);
     else if (n == "jit_hits") *value = static_cast<int64_t>(c->jit.hits);
     else if (n == "jit_cached") *value = static_cast<int64_t>(c->jit.size());
@@ -1089,6 +1116,7 @@ std::vector<OutCell> downloadCells(ngx_ctx* c, const std::vector<ColSpec>& spec,
 
 int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     DeviceGraph& d = *sp.dev;
+    const int64_t now = p.now_sec > 0 ? p.now_sec : static_cast<int64_t>(std::time(nullptr));   // WallClock
     GoPlan gp;
     int32_t rc = prepareGo(c, sp, p, gp);
     if (rc) return rc;
@@ -1153,10 +1181,6 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         progs.yOff.push_back(progs.add(yp));
     }
     if (progs.usesDst && c->world > 1) return fail(c, NGX_E_UNSUPPORTED, "$$ props across shards are not fetched yet");
-    for (auto& t : sp.tags) {
-        if (!t.second.latest().ttlCol.empty() && t.second.latest().ttlDur > 0)
-            return fail(c, NGX_E_UNSUPPORTED, "tag TTL is not evaluated on the device");
-    }
     std::vector<int32_t> ySlotType(progs.yOff.size(), 0);
     DevPrograms dp = uploadPrograms(c, progs, ySlotType, gp.colTypes);
     // WHERE fully pushed: for edges whose storage filter ran, graphd's re-evaluation is implied
@@ -1297,6 +1321,16 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         pos32 = pos32 && es < (1ULL << 32);
     }
     const bool fuseDeg = d.V < (1ULL << (64 - kFdShift)) && slotEdges <= kFdMask && hs.n > 0;
+    // storage-side request of each hop (getStepOutProps): props only on record hops, TTL info always
+    uint32_t recordPropsMask = 0, ttlMask = 0;
+    int32_t ttlCol[kMaxSlots];
+    int64_t ttlDur[kMaxSlots];
+    for (int s = 0; s < hs.n; s++) {
+        if (gctx.respSchema.count(hs.etype[s]) && !gctx.respSchema[hs.etype[s]].empty()) recordPropsMask |= 1u << s;
+        if (ttlInfo(sp.edge(std::abs(hs.etype[s])), ttlCol[s], ttlDur[s])) ttlMask |= 1u << s;
+    }
+    const int64_t edgeCap = c->maxEdgesPerVertex;              // FLAGS_max_edge_returned_per_vertex
+    const bool capped = edgeCap < INT32_MAX;
     for (uint32_t h = 1; h <= steps; h++) {
         bool isRecord = h >= recordFrom;
         bool isFinal = h == steps;
@@ -1324,25 +1358,36 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
                 if (launchChunkFirst(estart, nEnt, chunkFirst, c->stream)) throw Error{NGX_E_DEVICE, "chunk first"};
             });
         }
+        // the hop's storage request: which edges the processor emits (collectEdgeProps, .inl:501-608)
+        FinalArgs a{};
+        a.F = F; a.estart = estart; a.chunkFirst = chunkFirst; a.nEnt = nEnt; a.E = E; a.hs = hs;
+        a.vid = d.vid; a.V = d.V; a.gbase = d.gbase;
+        a.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1, now};
+        a.P = (isFinal && progs.P >= 0) ? dp.code + progs.P : nullptr;
+        a.propsMask = isRecord ? recordPropsMask : 0;
+        a.ttlMask = ttlMask;
+        for (int s = 0; s < hs.n; s++) { a.ttlCol[s] = ttlCol[s]; a.ttlDur[s] = ttlDur[s]; }
+        a.now = now;
+        a.err = errFlag;
+        // Edges the expansion must skip (rows read with TTL / bad rows, intermediate hops) or a per-vertex
+        // cap: the storage outcome is materialised per hop edge (k_storage_pass + k_cap) and both the
+        // final kernel and the expansion read it; otherwise the final kernel checks storage in place.
+        bool checks = false;
+        for (int s = 0; s < hs.n; s++) {
+            if (((a.propsMask | a.ttlMask) >> s & 1u) && (hs.eflags[s] != nullptr || ttlCol[s] >= 0)) checks = true;
+        }
+        const uint8_t* mask = nullptr;
+        if (E && (capped || (!isFinal && checks))) {
+            uint8_t* m = c->edgeMask.get<uint8_t>(E);
+            c->timed("storage_mask", E, [&] {
+                if (launchStoragePass(a, m, c->stream)) throw Error{NGX_E_DEVICE, "storage pass"};
+                if (capped && launchCap(estart, nEnt, m, edgeCap, c->stream)) throw Error{NGX_E_DEVICE, "cap"};
+            });
+            mask = m;
+        }
+        a.mask = mask;
         if (isRecord && E) {
-            FinalArgs a{};
-            a.F = F; a.estart = estart; a.chunkFirst = chunkFirst; a.nEnt = nEnt; a.E = E; a.hs = hs;
-            a.vid = d.vid; a.V = d.V; a.gbase = d.gbase;
-            a.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1};
-            a.P = (isFinal && progs.P >= 0) ? dp.code + progs.P : nullptr;
             a.W = progs.W >= 0 ? dp.code + progs.W : nullptr;
-            a.propsMask = 0;
-            for (int s = 0; s < hs.n; s++) {
-                if (gctx.respSchema.count(hs.etype[s]) && !gctx.respSchema[hs.etype[s]].empty()) a.propsMask |= 1u << s;
-                a.ttlCol[s] = -1;
-                const SchemaSet* es = sp.edge(std::abs(hs.etype[s]));
-                if (es && !es->latest().ttlCol.empty() && es->latest().ttlDur > 0) {
-                    a.ttlCol[s] = es->latest().index(es->latest().ttlCol);
-                    a.ttlDur[s] = es->latest().ttlDur;
-                }
-            }
-            a.now = p.now_sec;
-            a.err = errFlag;
             a.nY = static_cast<int32_t>(progs.yOff.size());
             a.yCode = dp.code;
             a.yOff = dp.yOff;
@@ -1350,7 +1395,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             a.yColType = dp.yColType;
             a.wIsP = (isFinal && wIsP) ? 1u : 0u;
             for (size_t k = 0; k < jitKc.size(); k++) { a.kc[k] = jitKc[k]; a.kl[k] = jitKl[k]; }
-            const JitKernels* kj = isFinal ? jk : jkNoP;
+            // a masked hop (max-edges cap) runs on the interpreter kernel: the generated ones skip the mask
+            const JitKernels* kj = mask ? nullptr : (isFinal ? jk : jkNoP);
             // outputs sized for every edge passing (rows are written in the same launch)
             uint64_t cap = totalRows + E;
             growKeep(c, c->oSrc, cap * 8, totalRows * 8);
@@ -1382,7 +1428,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         uint8_t ep = nextEpoch(c);
         if (E) {
             c->timed("expand", E * 8, [&] {
-                if (launchExpandMark(F, estart, chunkFirst, nEnt, E, hs, c->visited.get<uint8_t>(d.vglobal), ep, pos32, c->stream))
+                if (launchExpandMark(F, estart, chunkFirst, nEnt, E, hs, c->visited.get<uint8_t>(d.vglobal), ep, pos32, c->stream,
+                                     mask))
                     throw Error{NGX_E_DEVICE, "expand"};
             });
         }
@@ -1672,12 +1719,9 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
             }
         }
     }
-    if (q.max_edges_per_vertex > 0 && q.max_edges_per_vertex < INT32_MAX)
-        return fail(c, NGX_E_UNSUPPORTED, "max_edge_returned_per_vertex is not applied on the device yet");
-    for (auto& t : sp.tags) {
-        if (tagCols.count(t.first) && !t.second.latest().ttlCol.empty() && t.second.latest().ttlDur > 0)
-            return fail(c, NGX_E_UNSUPPORTED, "tag TTL is not evaluated on the device");
-    }
+    const int64_t edgeCap = (q.max_edges_per_vertex > 0 && q.max_edges_per_vertex < INT32_MAX) ? q.max_edges_per_vertex
+                                                                                               : INT32_MAX;
+    const int64_t now = q.now_sec > 0 ? q.now_sec : static_cast<int64_t>(std::time(nullptr));    // WallClock
     // processed types: edge contexts with props (QueryBoundProcessor.cpp:65-81)
     std::vector<int32_t> types;
     for (auto& kv : edgeCols) if (!kv.second.empty()) types.push_back(kv.first);
@@ -1708,12 +1752,21 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
         progs.yOff.push_back(progs.add(yp));
     }
     DevPrograms dp = uploadPrograms(c, progs, ySlotType);
-    // seeds in request order
+    // seeds in request order; a part this shard does not hold fails with E_PART_NOT_FOUND (NebulaStore::
+    // prefix -> ERR_PART_NOT_FOUND, BaseProcessor::to; QueryBaseProcessor.inl:835-851) and its vids match
+    // no vertex row
     std::vector<int32_t> sparts;
     std::vector<int64_t> svids;
     uint64_t k = 0;
     for (int32_t i = 0; i < q.nparts; i++) {
-        for (uint32_t j = 0; j < q.part_nvids[i]; j++) { sparts.push_back(q.parts[i]); svids.push_back(q.vids[k++]); }
+        int32_t part = q.parts[i];
+        bool held = sp.numParts <= 0 ||                                   // test-only layouts: every part
+                    (part >= 1 && part <= sp.numParts && part % c->world == c->rank);
+        if (!held && q.part_nvids[i]) { R.failed.push_back(NGX_E_PART_NOT_FOUND); R.failed.push_back(part); }
+        for (uint32_t j = 0; j < q.part_nvids[i]; j++) {
+            sparts.push_back(held ? part : INT32_MIN);
+            svids.push_back(q.vids[k++]);
+        }
     }
     uint64_t nF = svids.size();
     uint32_t* F = c->F0.get<uint32_t>(std::max<uint64_t>(nF, 1));
@@ -1722,7 +1775,7 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
         int64_t* dv = c->seedVid.get<int64_t>(nF);
         HIP_OK(hipMemcpyAsync(dpart, sparts.data(), nF * 4, hipMemcpyHostToDevice, c->stream));
         HIP_OK(hipMemcpyAsync(dv, svids.data(), nF * 8, hipMemcpyHostToDevice, c->stream));
-        if (launchLookup(dpart, dv, nF, d.vpart, d.vid, d.V, F, c->stream)) throw Error{NGX_E_DEVICE, "lookup"};
+        if (launchIndexLookup(dpart, dv, nF, d.vindex, F, c->stream)) throw Error{NGX_E_DEVICE, "lookup"};
     }
     std::vector<int32_t> hopTypes;
     HopSlots hs = makeHopSlots(sp, d, types, hopTypes);
@@ -1747,22 +1800,23 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
         FinalArgs a{};
         a.F = F; a.estart = estart; a.chunkFirst = chunkFirst; a.nEnt = nEnt; a.E = E; a.hs = hs;
         a.vid = d.vid; a.V = d.V; a.gbase = d.gbase;
-        a.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1};
+        a.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1, now};
         a.P = progs.P >= 0 ? dp.code + progs.P : nullptr;
         a.W = nullptr;
         for (int s = 0; s < hs.n; s++) {
             bool onlyStructure = true;
             for (int32_t ci : edgeCols[hs.etype[s]]) if (std::string(q.cols[ci].name) != "_dst") onlyStructure = false;
             if (!onlyStructure) a.propsMask |= 1u << s;
-            a.ttlCol[s] = -1;
-            const SchemaSet* es = sp.edge(std::abs(hs.etype[s]));
-            if (es && !es->latest().ttlCol.empty() && es->latest().ttlDur > 0) {
-                a.ttlCol[s] = es->latest().index(es->latest().ttlCol);
-                a.ttlDur[s] = es->latest().ttlDur;
-            }
+            if (ttlInfo(sp.edge(std::abs(hs.etype[s])), a.ttlCol[s], a.ttlDur[s])) a.ttlMask |= 1u << s;
         }
-        a.now = q.now_sec;
+        a.now = now;
         a.err = errFlag;
+        if (edgeCap < INT32_MAX) {                                // max_edge_returned_per_vertex (.inl:501-505)
+            uint8_t* m = c->edgeMask.get<uint8_t>(E);
+            if (launchStoragePass(a, m, c->stream)) throw Error{NGX_E_DEVICE, "storage pass"};
+            if (launchCap(estart, nEnt, m, edgeCap, c->stream)) throw Error{NGX_E_DEVICE, "cap"};
+            a.mask = m;
+        }
         a.nY = nY;
         a.yCode = dp.code;
         a.yOff = dp.yOff;
@@ -1786,6 +1840,13 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
             HIP_OK(hipMemcpyAsync(R.edgeType.data(), a.oType, nrows * 4, hipMemcpyDeviceToHost, c->stream));
             HIP_OK(hipMemcpyAsync(R.edgeDst.data(), a.oDst, nrows * 8, hipMemcpyDeviceToHost, c->stream));
             raw = downloadCells(c, spec, std::vector<int32_t>(nY, T_UNKNOWN), nrows, 0);
+            HIP_OK(hipStreamSynchronize(c->stream));
+            // IdAndProp.dst is set only by a `_dst` return column of the edge type (PropsCollector::
+            // collectDstId, Collector.h:77-82); without one the reference leaves it 0
+            std::set<int32_t> withDst;
+            for (auto& kv : edgeCols)
+                for (int32_t ci : kv.second) if (std::string(q.cols[ci].name) == "_dst") withDst.insert(kv.first);
+            for (uint64_t i = 0; i < nrows; i++) if (!withDst.count(R.edgeType[i])) R.edgeDst[i] = 0;
         }
     }
     // per-vertex tag columns
@@ -1804,7 +1865,7 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
         HIP_OK(hipMemcpyAsync(dts, both.data(), both.size() * 4, hipMemcpyHostToDevice, c->stream));
         VertexCellArgs va{};
         va.rows = F; va.n = nF; va.ncols = nY; va.tagSlot = dts; va.col = dts + nY;
-        va.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1};
+        va.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1, now};
         va.out = c->vcells.get<OutCell>(nF * nY);
         if (launchVertexCells(va, c->stream)) throw Error{NGX_E_DEVICE, "vertex cells"};
         HIP_OK(hipMemcpyAsync(vraw.data(), va.out, nF * nY * sizeof(OutCell), hipMemcpyDeviceToHost, c->stream));

@@ -49,7 +49,8 @@ struct FinalArgs {
     const Insn* P;                      // pushed storage filter, nullptr if none
     const Insn* W;                      // graphd WHERE, nullptr if none
     uint32_t propsMask;                 // hop slot s reads rows (not onlyStructure)
-    int32_t ttlCol[kMaxSlots];          // TTL column of hop slot s, -1 if none
+    uint32_t ttlMask;                   // hop slot s has TTL info: rows are read even without props
+    int32_t ttlCol[kMaxSlots];          // TTL column of hop slot s (INT / TIMESTAMP / VID), -1 if none
     int64_t ttlDur[kMaxSlots];
     int64_t now;
     uint64_t* lbStatus;                 // [0] chunk ticket, [1 + c] look-back status of chunk c (zeroed per launch)
@@ -68,6 +69,8 @@ struct FinalArgs {
     int32_t* oType;
     uint32_t* oEntry;                   // frontier index of each row (GetNeighbors), may be null
     const OutCol* oCols;                // nY columns (device array)
+    const uint8_t* mask;                // per hop edge: storage emitted it (max_edge_returned_per_vertex
+                                        // path); when set, replaces the storage checks. nullptr: none
     int64_t kc[kJitConsts];             // generated kernels: literal bits (string: pool offset)
     uint32_t kl[kJitConsts];            // string literal lengths
 };

@@ -37,6 +37,7 @@ constexpr uint64_t kSeedFuseMax = 4096;
 int launchSeedFrontier(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, const HopSlots& hs,
                        uint32_t* F, uint64_t* estart, Publish pub, hipStream_t s);
 
+int launchIndexLookup(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, uint32_t* out, hipStream_t s);
 int launchLookup(const int32_t* qpart, const int64_t* qvid, uint64_t n, const int32_t* vpart, const int64_t* vid,
                  uint64_t V, uint32_t* out, hipStream_t s);
 // estart must hold nEnt + 1 entries; estart[nEnt] receives E
@@ -44,8 +45,15 @@ int launchDegreeScan(const uint32_t* F, uint64_t nEnt, const HopSlots& hs, uint6
                      hipStream_t s, Publish pub = Publish{nullptr, 0});
 // chunkFirst must hold ceil(E / kChunk) entries (estart[nEnt] = E)
 int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst, hipStream_t s);
+// mask (nullptr: every edge): only hop edges e with mask[e] != 0 are expanded
 int launchExpandMark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst, uint64_t nEnt, uint64_t E,
-                     const HopSlots& hs, uint8_t* visited, uint8_t epoch, bool pos32, hipStream_t s);
+                     const HopSlots& hs, uint8_t* visited, uint8_t epoch, bool pos32, hipStream_t s,
+                     const uint8_t* mask = nullptr);
+// storage outcome per hop edge (a.E entries of out: 1 = emitted) for the max-edges / TTL mask path;
+// a's F / estart / chunkFirst / hs / env / P / propsMask / ttl fields are read
+int launchStoragePass(const FinalArgs& a, uint8_t* out, hipStream_t s);
+// keep the first `cap` set flags of every frontier entry's hop edges, clear the others
+int launchCap(const uint64_t* estart, uint64_t nEnt, uint8_t* mask, int64_t cap, hipStream_t s);
 int launchCompact(const uint8_t* visited, uint64_t gbase, uint64_t V, uint8_t epoch, uint32_t* outF,
                   uint64_t* tileSums, uint64_t* count, hipStream_t s);
 // fused compaction + next-hop degree scan (kernels.hip FlagDegIn): outF gets the next frontier,

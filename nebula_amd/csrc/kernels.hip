@@ -190,6 +190,13 @@ __device__ __forceinline__ uint32_t vindexFind(const VIndex& idx, int32_t part, 
     return kNoRow;
 }
 
+// seed (part, vid) -> vertex row through the commit-time hash index (GetNeighbors requests)
+__global__ void k_index_lookup(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, uint32_t* out) {
+    uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = vindexFind(idx, qpart[i], qvid[i]);
+}
+
 // 1024 threads; thread t owns seeds [t*per, t*per + per) and their entries (contiguous)
 __global__ __launch_bounds__(1024) void k_seed_frontier(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx,
                                                         HopSlots hs, uint32_t* F, uint64_t* estart, Publish pub) {
@@ -260,10 +267,11 @@ __global__ void k_chunk_first(const uint64_t* estart, uint64_t nEnt, uint64_t* c
 // hop's epoch into visited[] (the frontier dedup of GoExecutor::getDstIdsFromResp, a set of dsts).
 // The store is unconditional: a byte store needs no read and duplicates write the same value.
 // P32: CSR positions fit 32 bits (20 KiB chunk map instead of 28, see ChunkMap)
-template <bool ONE, bool P32>
+// MASK: only edges with mask[e] != 0 (the storage outcome of a hop with TTL or a max-edges cap)
+template <bool ONE, bool P32, bool MASK>
 __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst,
                                                     uint64_t nEnt, uint64_t E, HopSlots hs, uint8_t* visited,
-                                                    uint8_t epoch) {
+                                                    uint8_t epoch, const uint8_t* mask) {
     __shared__ ChunkMap<ONE, false, P32> m;
     // direct-mapped LDS filter of the rows this workgroup already marked: a repeated destination
     // (hubs of a power-law graph) costs an LDS probe instead of another L2 byte-store transaction
@@ -278,7 +286,7 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
     for (int k = 0; k < CITEMS; k++) {
         uint32_t p = threadIdx.x + k * WG;
         g[k] = kNoRow;
-        if (p < cnt) {
+        if (p < cnt && (!MASK || mask[base + p])) {
             uint32_t q = m.at[p];
             int s = ONE ? 0 : m.slot[q];
             uint64_t pos = P32 ? static_cast<uint64_t>(static_cast<uint32_t>(base + p) + static_cast<uint32_t>(m.pb[q]))
@@ -300,6 +308,7 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
 struct VmEv {
     static constexpr int kEager = -1;                 // YIELD evaluated in the write pass
     static constexpr bool kPos32 = false;             // 64-bit CSR positions in the chunk map
+    static constexpr bool kMask = true;               // reads FinalArgs::mask when set
     static __device__ __forceinline__ void YV(const FinalArgs&, const EdgeCtx&, Val*) {}
     static __device__ __forceinline__ void YS(const FinalArgs&, const Val*, uint64_t, uint32_t&) {}
     static __device__ __forceinline__ bool hasP(const FinalArgs& a) { return a.P != nullptr; }
@@ -327,6 +336,42 @@ struct VmEv {
 template <bool ONE, bool FIDX>
 __global__ __launch_bounds__(WG) void k_final(FinalArgs a) { finalBody<VmEv, ONE, FIDX, FIDX>(a); }
 
+// ------------------------------------------------------------------------------ max_edge_returned_per_vertex
+// Storage outcome of every hop edge (bad row / TTL / pushed filter; the interpreter evaluates the
+// filter) -> out[e] = 1 if the processor would emit it, before the per-vertex cap.
+template <bool ONE>
+__global__ __launch_bounds__(WG) void k_storage_pass(FinalArgs a, uint8_t* out) {
+    __shared__ ChunkMap<ONE, false, false> m;
+    const uint64_t base = static_cast<uint64_t>(blockIdx.x) * CE;
+    const uint32_t cnt = static_cast<uint32_t>(a.E - base < CE ? a.E - base : CE);
+    buildMap<ONE, false, false>(a.estart, a.chunkFirst, a.nEnt, blockIdx.x, gridDim.x, base, cnt, a.F, a.hs, m);
+    for (int k = 0; k < CITEMS; k++) {
+        uint32_t p = threadIdx.x + k * WG;
+        if (p >= cnt) continue;
+        EdgeCtx ec;
+        int s;
+        edgeCtxAt<ONE, false, false>(a, m, base, p, ec, s);
+        bool pe = false;
+        out[base + p] = storagePass<VmEv>(a, ec, s, pe) ? 1 : 0;
+    }
+}
+
+// collectEdgeProps stops once `cap` edges of the (vertex, type) prefix were emitted, in key order
+// (QueryBaseProcessor.inl:501-505, ++cnt at :606): keep the first `cap` set flags of every frontier
+// entry (its hop edges estart[i] .. estart[i + 1] - 1, in key order), clear the rest.
+__global__ void k_cap(const uint64_t* estart, uint64_t nEnt, uint8_t* mask, int64_t cap) {
+    uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= nEnt) return;
+    uint64_t lo = estart[i], hi = estart[i + 1];
+    if (hi - lo <= static_cast<uint64_t>(cap)) return;
+    int64_t kept = 0;
+    for (uint64_t e = lo; e < hi; e++) {
+        if (!mask[e]) continue;
+        if (kept < cap) kept++;
+        else mask[e] = 0;
+    }
+}
+
 // ------------------------------------------------------------------------------ vertex cells
 __global__ void k_vertex_cells(VertexCellArgs a) {
     uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -337,7 +382,7 @@ __global__ void k_vertex_cells(VertexCellArgs a) {
         int tslot = a.tagSlot[c];
         if (tslot >= 0 && r != kNoRow) {
             const DTag& t = a.env.tags[tslot];
-            if (t.present[r]) {
+            if (!tagAbsent(a.env, t, r)) {
                 const DCol& col = a.env.cols[t.colBase + a.col[c]];
                 Val v = (col.valid != nullptr && col.valid[r] == 0) ? defaultOfType(col.type) : loadCol(col, r);
                 out.t = v.t; out.len = v.len; out.x = v.x;
@@ -371,6 +416,12 @@ int launchLookup(const int32_t* qpart, const int64_t* qvid, uint64_t n, const in
     return static_cast<int>(hipGetLastError());
 }
 
+int launchIndexLookup(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, uint32_t* out, hipStream_t s) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_index_lookup, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, qpart, qvid, n, idx, out);
+    return static_cast<int>(hipGetLastError());
+}
+
 int launchDegreeScan(const uint32_t* F, uint64_t nEnt, const HopSlots& hs, uint64_t* estart, uint64_t* tileSums,
                      hipStream_t s, Publish pub) {
     return scan3(DegreeIn{F, hs}, nEnt, WriteEstart{estart}, tileSums, estart + nEnt, s, nullptr, 0, pub);
@@ -390,13 +441,33 @@ int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst
 }
 
 int launchExpandMark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst, uint64_t nEnt, uint64_t E,
-                     const HopSlots& hs, uint8_t* visited, uint8_t epoch, bool pos32, hipStream_t s) {
+                     const HopSlots& hs, uint8_t* visited, uint8_t epoch, bool pos32, hipStream_t s, const uint8_t* mask) {
     if (E == 0) return 0;
     dim3 grid(static_cast<unsigned>((E + CE - 1) / CE));
-    if (hs.n == 1 && pos32) hipLaunchKernelGGL((k_expand_mark<true, true>), grid, dim3(WG), 0, s, F, estart, chunkFirst, nEnt, E, hs, visited, epoch);
-    else if (hs.n == 1) hipLaunchKernelGGL((k_expand_mark<true, false>), grid, dim3(WG), 0, s, F, estart, chunkFirst, nEnt, E, hs, visited, epoch);
-    else if (pos32) hipLaunchKernelGGL((k_expand_mark<false, true>), grid, dim3(WG), 0, s, F, estart, chunkFirst, nEnt, E, hs, visited, epoch);
-    else hipLaunchKernelGGL((k_expand_mark<false, false>), grid, dim3(WG), 0, s, F, estart, chunkFirst, nEnt, E, hs, visited, epoch);
+#define NGX_EXPAND(ONE, P32, MASK) hipLaunchKernelGGL((k_expand_mark<ONE, P32, MASK>), grid, dim3(WG), 0, s, F, estart, \
+                                                    chunkFirst, nEnt, E, hs, visited, epoch, mask)
+    if (mask) {
+        if (hs.n == 1) NGX_EXPAND(true, false, true);
+        else NGX_EXPAND(false, false, true);
+    } else if (hs.n == 1 && pos32) NGX_EXPAND(true, true, false);
+    else if (hs.n == 1) NGX_EXPAND(true, false, false);
+    else if (pos32) NGX_EXPAND(false, true, false);
+    else NGX_EXPAND(false, false, false);
+#undef NGX_EXPAND
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchStoragePass(const FinalArgs& a, uint8_t* out, hipStream_t s) {
+    if (a.E == 0) return 0;
+    dim3 grid(static_cast<unsigned>((a.E + CE - 1) / CE));
+    if (a.hs.n == 1) hipLaunchKernelGGL((k_storage_pass<true>), grid, dim3(WG), 0, s, a, out);
+    else hipLaunchKernelGGL((k_storage_pass<false>), grid, dim3(WG), 0, s, a, out);
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchCap(const uint64_t* estart, uint64_t nEnt, uint8_t* mask, int64_t cap, hipStream_t s) {
+    if (nEnt == 0) return 0;
+    hipLaunchKernelGGL(k_cap, dim3(static_cast<unsigned>((nEnt + 255) / 256)), dim3(256), 0, s, estart, nEnt, mask, cap);
     return static_cast<int>(hipGetLastError());
 }
 

@@ -45,8 +45,9 @@ struct DTag {
     int32_t tag;
     int32_t ncols;
     int32_t colBase;
-    int32_t pad;
+    int32_t ttlCol;        // TTL column (INT / TIMESTAMP / VID of the latest schema), -1: no TTL check
     const uint8_t* present;
+    int64_t ttlDur;        // ttl_duration (> 0 when ttlCol >= 0)
 };
 
 // ------------------------------------------------------------------ bytecode

@@ -40,6 +40,7 @@ struct VmEnv {
     const DCol* cols;
     const char* pool;
     uint32_t* unsupported;     // set when a value needs a host-only construct
+    int64_t now;               // WallClock::fastNowInSec of the request (TTL)
 };
 
 __device__ __forceinline__ Val mkInt(int64_t v) { return Val{v, 0, V_INT}; }
@@ -220,18 +221,29 @@ __device__ __forceinline__ Val opEdst(const EdgeCtx& ec, int32_t b) {
     int32_t at = ec.etype < 0 ? -ec.etype : ec.etype;
     return mkInt((b != 0 && at != b) ? 0 : ec.dst);
 }
+// no tag row for the vertex, or its TTL expired: collectVertexProps collects nothing for the tag
+// (QueryBaseProcessor.inl:440-476; checkDataExpiredForTTL, CommonUtils.cpp:13-49: an unreadable TTL
+// field never expires)
+__device__ __forceinline__ bool tagAbsent(const VmEnv& env, const DTag& t, uint32_t row) {
+    if (row == kNoRow || t.present[row] == 0) return true;
+    if (t.ttlCol < 0) return false;
+    const DCol& c = env.cols[t.colBase + t.ttlCol];
+    if (c.valid != nullptr && c.valid[row] == 0) return false;
+    return env.now > loadI64(c, row) + t.ttlDur;
+}
+
 // OP_SRCTAG / OP_DSTTAG: column a of tag slot b for the src / dst row
 template <int CT, int W = 0>
 __device__ __forceinline__ Val opTagT(const VmEnv& env, uint32_t row, int32_t a, int32_t b, uint8_t mode, Val dflt) {
     const DTag& t = env.tags[b];
-    if (row == kNoRow || t.present[row] == 0) return (mode & 1) ? dflt : mkErr();
+    if (tagAbsent(env, t, row)) return (mode & 1) ? dflt : mkErr();
     const DCol& c = env.cols[t.colBase + a];
     if (c.valid != nullptr && c.valid[row] == 0) return defaultOfTypeT<CT>();
     return loadColT<CT, W>(c, row);
 }
 __device__ __forceinline__ Val opTag(const VmEnv& env, uint32_t row, int32_t a, int32_t b, uint8_t mode, Val dflt) {
     const DTag& t = env.tags[b];
-    if (row == kNoRow || t.present[row] == 0) return (mode & 1) ? dflt : mkErr();
+    if (tagAbsent(env, t, row)) return (mode & 1) ? dflt : mkErr();
     const DCol& c = env.cols[t.colBase + a];
     if (c.valid != nullptr && c.valid[row] == 0) return defaultOfType(c.type);
     return loadCol(c, row);

@@ -113,6 +113,7 @@ SIGNATURES = {
     "ngx_open": (c_i32, [P(Config), P(ctypes.c_void_p)]),
     "ngx_close": (None, [ctypes.c_void_p]),
     "ngx_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
+    "ngx_build_info": (ctypes.c_char_p, []),
     "ngx_get_unique_id": (c_i32, [ctypes.c_void_p]),
     "ngx_add_space": (c_i32, [ctypes.c_void_p, c_i32, c_i32]),
     "ngx_add_schema": (c_i32, [ctypes.c_void_p, c_i32, c_i32, c_i32, ctypes.c_char_p, c_i64, c_i32,
@@ -352,7 +353,7 @@ class Engine:
     # ---- GO
     def go(self, space: int, s: Union[str, ngql.GoSentence], pushdown: bool = True, now_sec: int = 0,
            raise_on_error: bool = False, rows: bool = True, on_device: bool = False, fetch: bool = False,
-           columnar: bool = False, digest_fn=None) -> GoResult:
+           columnar: bool = False, digest_fn=None, arrays: bool = True) -> GoResult:
         """Run one GO. rows=False skips decoding cells into Python tuples; on_device=True leaves the
         result rows in HBM (GoResult.nrows and the statistics only); with fetch=True the HBM arrays
         (src/dst/rank/type and the columnar YIELD columns) are copied back into the result.
@@ -403,6 +404,10 @@ class Engine:
                                              self._d2h(dc.type, n, np.uint8) if dc.type else None))
                 return res
             if columnar:
+                if not arrays:                             # delivery only (bench): no Python copies
+                    return GoResult(ok=rc == 0, error=err, code=rc, col_types=[r.col_types[i] for i in range(r.ncols)],
+                                    rows=[], nrows=r.nrows, hop_edges=[r.hop_edges[i] for i in range(r.nhops)],
+                                    device_ms=r.device_ms)
                 return self._columnar(r, rc, err, rows, digest_fn)
             res = GoResult(
                 ok=rc == 0, error=err, code=rc, col_types=[r.col_types[i] for i in range(r.ncols)],
@@ -495,6 +500,27 @@ class Engine:
         n = c_i32()
         self._check(self.L.ngx_kernel_stats(self.h, ctypes.byref(p), ctypes.byref(n)), "kernel_stats")
         return {p[i].name.decode(): (p[i].launches, p[i].total_ms, p[i].algo_bytes) for i in range(n.value)}
+
+
+def build_info() -> dict:
+    """ngx_build_info() parsed, plus whether its source digest matches the sources in this tree."""
+    import hashlib
+    import glob
+    raw = lib().ngx_build_info().decode()
+    info = dict(kv.split("=", 1) for kv in raw.replace(" built=", " built=").split(" ") if "=" in kv)
+    csrc = os.path.join(HERE, "csrc")
+    srcs = sorted(glob.glob(os.path.join(csrc, "*.cpp")) + glob.glob(os.path.join(csrc, "*.h")) +
+                  glob.glob(os.path.join(csrc, "*.hip")) +
+                  [os.path.join(csrc, "../../include/nebula_gn.h"), os.path.join(csrc, "exports.map"),
+                   os.path.join(csrc, "Makefile")], key=lambda p: os.path.relpath(p, csrc))
+    h = hashlib.sha256()
+    for p in srcs:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    info["tree_sha"] = h.hexdigest()[:16]
+    info["matches_tree"] = info.get("src_sha") == info["tree_sha"]
+    info["raw"] = raw
+    return info
 
 
 def hash_string(s: str) -> int:

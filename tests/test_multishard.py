@@ -201,3 +201,35 @@ def test_c3_rehearsal_world8_scale22(tmp_path, rmat22):
     _check_merged(o, ds.space, queries, shards, digests)
     for s in shards:
         assert s[0]["hop_xchg"][:2] and all(b > 0 for b in s[0]["hop_xchg"][:2])
+
+
+@pytest.mark.gpu
+def test_exchange_failure_fails_the_query():
+    """A failing collective (ngx_config.exchange returning non-zero, as a dead or timed-out peer makes
+    RCCL fail) ends ngx_go with NGX_E_DEVICE instead of hanging or returning partial rows."""
+    from nebula_amd import datagen, engine, ngql
+
+    def fn(user, op, send, recv, nbytes):
+        if op == engine.XCHG_ALLGATHER:              # commit: the peer (rank 1) holds no vertices
+            ctypes.memmove(recv, send, nbytes)
+            ctypes.memset(recv + nbytes, 0, nbytes)
+            return 0
+        return 1                                     # the per-hop frontier all-to-all fails
+
+    cb = engine.ExchangeFn(fn)
+    e = engine.Engine(0, 0, 2, exchange=cb)
+    try:
+        rows = datagen.rmat(10, 8, 42, 100, False, False)
+        e.add_space(datagen.RMAT_SPACE, 100)
+        for is_edge, sid, name, fields in datagen.rmat_schemas():
+            e.add_schema(datagen.RMAT_SPACE, is_edge, sid, name, fields)
+        e.load_kv(datagen.RMAT_SPACE, *rows.arrays())
+        e.commit(datagen.RMAT_SPACE)
+        seeds = ", ".join(str(int(v)) for v in datagen.sample_vids(3, 1 << 10, 20))
+        one = e.go(datagen.RMAT_SPACE, ngql.parse_go(f"GO FROM {seeds} OVER e"))   # no exchange in 1 hop
+        assert one.ok
+        with pytest.raises(engine.EngineError) as ei:
+            e.go(datagen.RMAT_SPACE, ngql.parse_go(f"GO 2 STEPS FROM {seeds} OVER e"))
+        assert ei.value.code == engine.E_DEVICE and "exchange" in str(ei.value)
+    finally:
+        e.close()
