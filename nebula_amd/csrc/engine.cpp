@@ -220,9 +220,11 @@ const void* uploadAs(DeviceGraph& d, const std::vector<int64_t>& v, uint64_t n) 
     return d.upload(t.data(), n);
 }
 const void* uploadNarrow(DeviceGraph& d, const std::vector<int64_t>& v, uint64_t n, int32_t& width) {
-    // Opt-in (NGX_NARROW=1): measured on MI355X at C2 the final hop reads 0.46 GB less per launch with
-    // p0 as int8 but runs 736 -> 775 us (same-box A/B, profiles/r01_s6n_*), so 8-byte storage stays the default.
-    const bool on = std::getenv("NGX_NARROW") != nullptr && std::getenv("NGX_NARROW")[0] == '1';
+    // Default on (NGX_NARROW=0 keeps 8 bytes): fewer HBM bytes per scanned edge. A strided-load
+    // microbenchmark of the final hop's access pattern (tools/mb_final.hip) runs 607 -> 468 us with dst
+    // int32, rank / filter column int8 (profiles/r02_mb_final.txt).
+    const char* env = std::getenv("NGX_NARROW");
+    const bool on = env == nullptr || env[0] != '0';
     if (!on) { width = 8; return d.upload(v.data(), n); }
     int64_t lo = 0, hi = 0;
     for (uint64_t i = 0; i < n; i++) { lo = std::min(lo, v[i]); hi = std::max(hi, v[i]); }
@@ -295,9 +297,9 @@ std::unique_ptr<DeviceGraph> upload(HostGraph& g, const Space& sp) {
         ds.colBase = static_cast<int32_t>(d->cols.size());
         ds.ncols = static_cast<int32_t>(s.cols.size());
         ds.off = d->upload(s.off.data(), s.off.size());
-        ds.dst = d->upload(s.dst.data(), s.dst.size());
+        ds.dst = uploadNarrow(*d, s.dst, s.dst.size(), ds.dstW);
         ds.dgid = d->upload(s.dgid.data(), s.dgid.size());
-        ds.rank = d->upload(s.rank.data(), s.rank.size());
+        ds.rank = uploadNarrow(*d, s.rank, s.rank.size(), ds.rankW);
         ds.hasFlags = s.anyFlags ? 1 : 0;
         ds.eflags = s.anyFlags ? d->upload(s.eflags.data(), s.eflags.size()) : nullptr;
         uploadColumns(*d, s.cols, s.dst.size());
@@ -579,6 +581,8 @@ HopSlots makeHopSlots(const Space& sp, const DeviceGraph& d, const std::vector<i
         hs.dgid[hs.n] = ds.dgid;
         hs.dst[hs.n] = ds.dst;
         hs.rank[hs.n] = ds.rank;
+        hs.dstW[hs.n] = static_cast<int8_t>(ds.dstW);
+        hs.rankW[hs.n] = static_cast<int8_t>(ds.rankW);
         hs.eflags[hs.n] = ds.hasFlags ? ds.eflags : nullptr;
         hs.colBase[hs.n] = ds.colBase;
         hs.n++;
@@ -1206,6 +1210,19 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         for (int32_t off : progs.yOff) jq.Y.push_back(JitProgram{progs.code.data() + off, true});
         jq.yColType = gp.colTypes;
         jq.yKey = yAlias;
+        for (int s = 0; s < hs.n; s++) {
+            jq.slots.push_back(hs.slotIdx[s]);
+            int32_t tc;
+            int64_t td;
+            jq.ttl = jq.ttl || ttlInfo(sp.edge(std::abs(hs.etype[s])), tc, td);
+        }
+        jq.etype0 = hs.n == 1 ? hs.etype[0] : 0;
+        jq.dstW = hs.n ? hs.dstW[0] : 0;
+        jq.rankW = hs.n ? hs.rankW[0] : 0;
+        for (int s = 1; s < hs.n; s++) {
+            if (hs.dstW[s] != jq.dstW) jq.dstW = 0;
+            if (hs.rankW[s] != jq.rankW) jq.rankW = 0;
+        }
         // literals -> launch-time constant slots (one kernel per query shape)
         auto slotConsts = [&](const Insn* code) {
             for (const Insn* in = code; in && in->op != OP_END; in++) {
@@ -1243,18 +1260,10 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             return n + r.srcTag.size() + r.dstTag.size();
         };
         ky = count(yr);
-        // bytes per edge read for the filter's edge props: their stored width (narrowed INT columns)
+        // 8 logical bytes per edge for each filter edge prop (§8d), whatever width it is stored at
         for (auto& ap : wr.alias) {
             if (ap.second == "_src" || ap.second == "_dst" || ap.second == "_rank" || ap.second == "_type") continue;
-            uint64_t w = 0;
-            for (int s = 0; s < hs.n; s++) {
-                const SchemaSet* es = sp.edge(std::abs(hs.etype[s]));
-                int32_t ci = es ? es->latest().index(ap.second) : -1;
-                if (ci < 0) continue;
-                const DCol& dc = d.cols[hs.colBase[s] + ci];
-                w = std::max<uint64_t>(w, dc.width > 0 ? static_cast<uint64_t>(dc.width) : 8);
-            }
-            kfBytes += w ? w : 8;
+            kfBytes += 8;
         }
         kfBytes += 8 * (wr.srcTag.size() + wr.dstTag.size());
     }

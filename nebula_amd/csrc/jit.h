@@ -38,6 +38,10 @@ struct JitQuery {
                                     // once as oSrc/oDst/oRank and aliased, not stored again (engine.cpp keyAliases)
     bool oneSlot = false;           // the hop expands a single edge-type slot (ONE kernels)
     bool pos32 = false;             // every CSR position of the hop's slots fits 32 bits (ChunkMap P32)
+    int dstW = 0, rankW = 0;        // key column widths shared by every slot of the hop (0: per slot)
+    std::vector<int32_t> slots;     // the hop's slots (HostGraph::slots indices)
+    bool ttl = false;               // some slot's edge type has TTL info
+    int32_t etype0 = 0;             // the only slot's signed type (0: several slots)
 };
 
 class JitCache {

@@ -13,8 +13,10 @@ struct HopSlots {
     int32_t etype[kMaxSlots];
     const uint64_t* off[kMaxSlots];
     const uint32_t* dgid[kMaxSlots];
-    const int64_t* dst[kMaxSlots];
-    const int64_t* rank[kMaxSlots];
+    const void* dst[kMaxSlots];         // at dstW / rankW bytes per element (DSlot)
+    const void* rank[kMaxSlots];
+    int8_t dstW[kMaxSlots];
+    int8_t rankW[kMaxSlots];
     const uint8_t* eflags[kMaxSlots];   // per-edge EF_* flags, nullptr when the slot has none
     int32_t colBase[kMaxSlots];         // first DCol of the slot in the column table
 };

@@ -309,6 +309,11 @@ struct VmEv {
     static constexpr int kEager = -1;                 // YIELD evaluated in the write pass
     static constexpr bool kPos32 = false;             // 64-bit CSR positions in the chunk map
     static constexpr bool kMask = true;               // reads FinalArgs::mask when set
+    static constexpr int kDstW = 0, kRankW = 0;       // key column widths read per slot
+    static constexpr bool kDrow = true;               // programs may read $$ props
+    static constexpr bool kFlat = false;              // branchy passes(): programs evaluated only when needed
+    static constexpr bool kEflags = true, kTtl = true; // per-edge flags / TTL read when the slot has them
+    static constexpr int kEtype = 0;                  // edge type read per slot
     static __device__ __forceinline__ void YV(const FinalArgs&, const EdgeCtx&, Val*) {}
     static __device__ __forceinline__ void YS(const FinalArgs&, const Val*, uint64_t, uint32_t&) {}
     static __device__ __forceinline__ bool hasP(const FinalArgs& a) { return a.P != nullptr; }
@@ -326,9 +331,9 @@ struct VmEv {
                 if (v.t == V_ERR) errs |= 1u;
                 else if (a.yColType != nullptr && !cellTypeOk(a.yColType[y], v.t)) errs |= 4u;
             }
-            oc.x[o] = v.x;
-            if (oc.len) oc.len[o] = v.len;
-            if (oc.t) oc.t[o] = v.t;
+            gst<int64_t>(oc.x, o, v.x);
+            if (oc.len) gst<uint32_t>(oc.len, o, v.len);
+            if (oc.t) gst<uint8_t>(oc.t, o, v.t);
         }
     }
 };
@@ -350,7 +355,7 @@ __global__ __launch_bounds__(WG) void k_storage_pass(FinalArgs a, uint8_t* out) 
         if (p >= cnt) continue;
         EdgeCtx ec;
         int s;
-        edgeCtxAt<ONE, false, false>(a, m, base, p, ec, s);
+        edgeCtxAt<VmEv, ONE, false, false>(a, m, base, p, ec, s);
         bool pe = false;
         out[base + p] = storagePass<VmEv>(a, ec, s, pe) ? 1 : 0;
     }

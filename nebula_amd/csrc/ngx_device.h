@@ -35,11 +35,14 @@ struct DSlot {
     int32_t colBase;       // first DCol of this slot in the column table
     int32_t hasFlags;
     const uint64_t* off;   // V + 1
-    const int64_t* dst;
+    const void* dst;       // dst vids at dstW bytes (1 / 2 / 4 / 8, sign-extended on load)
     const uint32_t* dgid;
-    const int64_t* rank;
+    const void* rank;      // ranks at rankW bytes
     const uint8_t* eflags;
+    int32_t dstW, rankW;
 };
+
+
 
 struct DTag {
     int32_t tag;

@@ -43,6 +43,37 @@ struct VmEnv {
     int64_t now;               // WallClock::fastNowInSec of the request (TTL)
 };
 
+// Loads through the global address space. Column pointers come from device-side tables (DCol, DTag),
+// which the compiler cannot prove global, so plain dereferences become flat loads (ordered with LDS
+// traffic: every wait on them also waits on lgkmcnt).
+template <typename T>
+__device__ __forceinline__ T gld(const void* p, uint64_t i) {
+    return ((const __attribute__((address_space(1))) T*)p)[i];
+}
+
+template <typename T>
+__device__ __forceinline__ void gst(void* p, uint64_t i, T v) {
+    ((__attribute__((address_space(1))) T*)p)[i] = v;
+}
+
+// element i of an integer array stored at its narrowest signed width w (1, 2, 4 or 8 bytes)
+__device__ __forceinline__ int64_t loadW(const void* p, int32_t w, uint64_t i) {
+    switch (w) {
+        case 1: return gld<int8_t>(p, i);
+        case 2: return gld<int16_t>(p, i);
+        case 4: return gld<int32_t>(p, i);
+        default: return gld<int64_t>(p, i);
+    }
+}
+template <int W>                        // width known at compile time (generated kernels); 0: runtime w
+__device__ __forceinline__ int64_t loadWT(const void* p, int32_t w, uint64_t i) {
+    if constexpr (W == 1) return gld<int8_t>(p, i);
+    else if constexpr (W == 2) return gld<int16_t>(p, i);
+    else if constexpr (W == 4) return gld<int32_t>(p, i);
+    else if constexpr (W == 8) return gld<int64_t>(p, i);
+    else return loadW(p, w, i);
+}
+
 __device__ __forceinline__ Val mkInt(int64_t v) { return Val{v, 0, V_INT}; }
 __device__ __forceinline__ Val mkBool(bool v) { return Val{v ? 1 : 0, 0, V_BOOL}; }
 __device__ __forceinline__ Val mkDbl(double d) { return Val{__double_as_longlong(d), 0, V_DBL}; }
@@ -128,20 +159,20 @@ __device__ __forceinline__ uint64_t hashBytes(const unsigned char* p, uint64_t n
 // (export-time choice, uniform per column, so the branch is scalar)
 __device__ __forceinline__ int64_t loadI64(const DCol& c, uint64_t i) {
     switch (c.width) {
-        case 1: return static_cast<const int8_t*>(c.data)[i];
-        case 2: return static_cast<const int16_t*>(c.data)[i];
-        case 4: return static_cast<const int32_t*>(c.data)[i];
-        default: return static_cast<const int64_t*>(c.data)[i];
+        case 1: return gld<int8_t>(c.data, i);
+        case 2: return gld<int16_t>(c.data, i);
+        case 4: return gld<int32_t>(c.data, i);
+        default: return gld<int64_t>(c.data, i);
     }
 }
 __device__ __forceinline__ Val loadCol(const DCol& c, uint64_t i) {
     switch (c.type) {
         case 2: case 21: case 3: return mkInt(loadI64(c, i));
-        case 4: case 5: return mkDbl(static_cast<const double*>(c.data)[i]);
-        case 1: return mkBool(static_cast<const uint8_t*>(c.data)[i] != 0);
+        case 4: case 5: return mkDbl(gld<double>(c.data, i));
+        case 1: return mkBool(gld<uint8_t>(c.data, i) != 0);
         case 6: {
-            uint64_t o = c.soff[i];
-            return Val{reinterpret_cast<int64_t>(c.sbytes + o), static_cast<uint32_t>(c.soff[i + 1] - o), V_STR};
+            uint64_t o = gld<uint64_t>(c.soff, i);
+            return Val{reinterpret_cast<int64_t>(c.sbytes + o), static_cast<uint32_t>(gld<uint64_t>(c.soff, i + 1) - o), V_STR};
         }
         default: return mkErr();
     }
@@ -171,20 +202,20 @@ __device__ __forceinline__ bool mulOverflow(int64_t lv, int64_t rv) {    // Expr
 // ------------------------------------------------------------------------------ loads
 template <int W>                        // integer storage width known at compile time (JIT); 0: read c.width
 __device__ __forceinline__ int64_t loadI64T(const DCol& c, uint64_t i) {
-    if constexpr (W == 1) return static_cast<const int8_t*>(c.data)[i];
-    else if constexpr (W == 2) return static_cast<const int16_t*>(c.data)[i];
-    else if constexpr (W == 4) return static_cast<const int32_t*>(c.data)[i];
-    else if constexpr (W == 8) return static_cast<const int64_t*>(c.data)[i];
+    if constexpr (W == 1) return gld<int8_t>(c.data, i);
+    else if constexpr (W == 2) return gld<int16_t>(c.data, i);
+    else if constexpr (W == 4) return gld<int32_t>(c.data, i);
+    else if constexpr (W == 8) return gld<int64_t>(c.data, i);
     else return loadI64(c, i);
 }
 template <int CT, int W = 0>            // column type (and integer width) known at compile time (JIT)
 __device__ __forceinline__ Val loadColT(const DCol& c, uint64_t i) {
     if constexpr (CT == 2 || CT == 21 || CT == 3) return mkInt(loadI64T<W>(c, i));
-    else if constexpr (CT == 4 || CT == 5) return mkDbl(static_cast<const double*>(c.data)[i]);
-    else if constexpr (CT == 1) return mkBool(static_cast<const uint8_t*>(c.data)[i] != 0);
+    else if constexpr (CT == 4 || CT == 5) return mkDbl(gld<double>(c.data, i));
+    else if constexpr (CT == 1) return mkBool(gld<uint8_t>(c.data, i) != 0);
     else if constexpr (CT == 6) {
-        uint64_t o = c.soff[i];
-        return Val{reinterpret_cast<int64_t>(c.sbytes + o), static_cast<uint32_t>(c.soff[i + 1] - o), V_STR};
+        uint64_t o = gld<uint64_t>(c.soff, i);
+        return Val{reinterpret_cast<int64_t>(c.sbytes + o), static_cast<uint32_t>(gld<uint64_t>(c.soff, i + 1) - o), V_STR};
     } else return mkErr();
 }
 template <int CT>
@@ -196,19 +227,23 @@ __device__ __forceinline__ Val defaultOfTypeT() {
 }
 
 // OP_ECOL: edge column a of |type| b; mode bit0 mismatch -> dflt, bit1 missing field -> type default
-template <int CT, int W = 0>
+// VALID: the column may lack rows (a valid[] bitmap exists); false when the host knows every row of
+// every slot has the field, which keeps the value's type a compile-time constant
+template <int CT, int W = 0, bool VALID = true>
 __device__ __forceinline__ Val opEcolT(const VmEnv& env, const EdgeCtx& ec, int32_t a, int32_t b, uint8_t mode, Val dflt) {
     int32_t at = ec.etype < 0 ? -ec.etype : ec.etype;
     if (at != b) return (mode & 1) ? dflt : mkErr();
     const DCol& c = ec.cols[a];
-    if (c.valid != nullptr && c.valid[ec.pos] == 0) return (mode & 2) ? defaultOfTypeT<CT>() : mkErr();
+    if constexpr (VALID) {
+        if (c.valid != nullptr && gld<uint8_t>(c.valid, ec.pos) == 0) return (mode & 2) ? defaultOfTypeT<CT>() : mkErr();
+    }
     return loadColT<CT, W>(c, ec.pos);
 }
 __device__ __forceinline__ Val opEcol(const VmEnv& env, const EdgeCtx& ec, int32_t a, int32_t b, uint8_t mode, Val dflt) {
     int32_t at = ec.etype < 0 ? -ec.etype : ec.etype;
     if (at != b) return (mode & 1) ? dflt : mkErr();
     const DCol& c = ec.cols[a];
-    if (c.valid != nullptr && c.valid[ec.pos] == 0) return (mode & 2) ? defaultOfType(c.type) : mkErr();
+    if (c.valid != nullptr && gld<uint8_t>(c.valid, ec.pos) == 0) return (mode & 2) ? defaultOfType(c.type) : mkErr();
     return loadCol(c, ec.pos);
 }
 // OP_EKEY: key prop a (0 src, 1 dst, 2 rank, 3 type) of alias type b (0: any)
@@ -225,27 +260,29 @@ __device__ __forceinline__ Val opEdst(const EdgeCtx& ec, int32_t b) {
 // (QueryBaseProcessor.inl:440-476; checkDataExpiredForTTL, CommonUtils.cpp:13-49: an unreadable TTL
 // field never expires)
 __device__ __forceinline__ bool tagAbsent(const VmEnv& env, const DTag& t, uint32_t row) {
-    if (row == kNoRow || t.present[row] == 0) return true;
+    if (row == kNoRow || gld<uint8_t>(t.present, row) == 0) return true;
     if (t.ttlCol < 0) return false;
     const DCol& c = env.cols[t.colBase + t.ttlCol];
-    if (c.valid != nullptr && c.valid[row] == 0) return false;
+    if (c.valid != nullptr && gld<uint8_t>(c.valid, row) == 0) return false;
     return env.now > loadI64(c, row) + t.ttlDur;
 }
 
 // OP_SRCTAG / OP_DSTTAG: column a of tag slot b for the src / dst row
-template <int CT, int W = 0>
+template <int CT, int W = 0, bool VALID = true>
 __device__ __forceinline__ Val opTagT(const VmEnv& env, uint32_t row, int32_t a, int32_t b, uint8_t mode, Val dflt) {
     const DTag& t = env.tags[b];
     if (tagAbsent(env, t, row)) return (mode & 1) ? dflt : mkErr();
     const DCol& c = env.cols[t.colBase + a];
-    if (c.valid != nullptr && c.valid[row] == 0) return defaultOfTypeT<CT>();
+    if constexpr (VALID) {
+        if (c.valid != nullptr && gld<uint8_t>(c.valid, row) == 0) return defaultOfTypeT<CT>();
+    }
     return loadColT<CT, W>(c, row);
 }
 __device__ __forceinline__ Val opTag(const VmEnv& env, uint32_t row, int32_t a, int32_t b, uint8_t mode, Val dflt) {
     const DTag& t = env.tags[b];
     if (tagAbsent(env, t, row)) return (mode & 1) ? dflt : mkErr();
     const DCol& c = env.cols[t.colBase + a];
-    if (c.valid != nullptr && c.valid[row] == 0) return defaultOfType(c.type);
+    if (c.valid != nullptr && gld<uint8_t>(c.valid, row) == 0) return defaultOfType(c.type);
     return loadCol(c, row);
 }
 
