@@ -147,7 +147,6 @@ def main():
     for i in range(args.warmup):
         step(plans[i])
     log(f"[rank {rank}] warmup done")
-    eng.set_profiling(True)
     barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
@@ -156,16 +155,23 @@ def main():
     dev_ms = 0.0
     hop_edges = None
     hop_xchg = None
+    prep_ms = tail_ms = 0.0
     for i in range(args.steps):
         r = step(plans[args.warmup + i])
         edges += sum(r.hop_edges)
         result_rows += r.nrows
         dev_ms += r.device_ms
+        prep_ms += r.host_prep_ms
+        tail_ms += r.host_tail_ms
         hop_edges = r.hop_edges
         hop_xchg = r.hop_xchg
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t_start
+    # the same steps again with per-kernel HIP events (their records would perturb the timed loop)
+    eng.set_profiling(True)
+    for i in range(args.steps):
+        step(plans[args.warmup + i])
     stats = eng.kernel_stats()
     eng.set_profiling(False)
 
@@ -247,6 +253,9 @@ def main():
             "rows_per_step": result_rows // args.steps,
             "hop_edges_last_step": hop_edges,
             "device_ms_per_step": round(dev_ms / args.steps, 3),
+            "host_ms_per_step": {"library_prep": round(prep_ms / args.steps, 3), "library_tail": round(tail_ms / args.steps, 3),
+                                 "note": "inside ngx_go: before the first launch (plan, programs, seeds) / after the "
+                                         "device finished; the rest of ms_per_step - device_ms is the Python caller"},
             "timed_region": "seeds on host -> result rows + YIELD columns in HBM (result_on_device)",
             "host_delivery": {"ms_per_step_columnar": round(host_col_ms, 3), "ms_per_step_cells": round(host_cell_ms, 3),
                               "note": "same query with the rows copied to host memory: columnar arrays in "

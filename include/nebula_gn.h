@@ -249,6 +249,8 @@ typedef struct {
      * dev_type_const. row_src / row_dst / row_rank point into the same staging. */
     const ngx_dev_column* host_cols;
     const uint64_t* hop_exchange_bytes;/* world > 1: frontier bytes this shard sent per hop (0 otherwise) */
+    double host_prep_ms;               /* host time from the call to the first launch (plan, programs) */
+    double host_tail_ms;               /* host time after the device finished (results, checks) */
 } ngx_go_result;
 
 int32_t ngx_go(ngx_ctx* ctx, const ngx_go_plan* plan, ngx_go_result** out);

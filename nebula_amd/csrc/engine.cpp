@@ -11,6 +11,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -118,8 +119,17 @@ struct ngx_ctx {
             }
             return static_cast<char*>(p);
         }
+        // grow keeping the first `keep` bytes (the caller has synchronised with copies out of the old block)
+        char* getKeep(size_t bytes, size_t keep) {
+            if (bytes <= cap) return static_cast<char*>(p);
+            std::vector<char> save(static_cast<char*>(p), static_cast<char*>(p) + std::min(keep, cap));
+            char* n = get(bytes);
+            std::memcpy(n, save.data(), save.size());
+            return n;
+        }
         void release() { if (p) (void)hipHostFree(p); p = nullptr; cap = 0; }
-    } hostStage;
+    } hostStage, inStage;
+    size_t progStageBytes = 0;                          // bytes of inStage holding this call's programs                               // results D2H / query inputs H2D (programs, seeds)
     std::vector<ColBuf> oCols;                          // result columns (columnar, HBM)
     std::vector<OutCol> oColView;                       // their device pointers, as uploaded to oColDesc
     uint64_t visitedSize = 0;
@@ -150,6 +160,7 @@ struct ngx_ctx {
                         &vcells, &misc, &edgeMask}) b->release();
         for (auto& cb : oCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         hostStage.release();
+        inStage.release();
         for (auto e : eventPool) (void)hipEventDestroy(e);
         if (comm) (void)ncclCommDestroy(comm);
         if (pin) (void)hipHostFree(pin);
@@ -359,14 +370,17 @@ DevPrograms uploadPrograms(ngx_ctx* c, const Programs& pr, const std::vector<int
     size_t poolOff = (codeBytes + yBytes + tBytes + cBytes + 63) & ~size_t(63);
     size_t total = poolOff + pr.pool.size() + 64;
     char* base = c->progBuf.get<char>(total);
-    std::vector<char> host(total, 0);
-    std::memcpy(host.data(), pr.code.data(), codeBytes);
-    std::memcpy(host.data() + codeBytes, pr.yOff.data(), yBytes);
-    std::memcpy(host.data() + codeBytes + yBytes, ySlotType.data(), tBytes);
-    std::memcpy(host.data() + codeBytes + yBytes + tBytes, yColType.data(), cBytes);
-    std::memcpy(host.data() + poolOff, pr.pool.data(), pr.pool.size());
-    HIP_OK(hipMemcpyAsync(base, host.data(), total, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipStreamSynchronize(c->stream));
+    // staged in page-locked memory: the copy is asynchronous (the stage is reused only by the next call,
+    // after this one has synchronised with its kernels)
+    char* host = c->inStage.get(total);
+    c->progStageBytes = total;
+    std::memset(host, 0, total);
+    std::memcpy(host, pr.code.data(), codeBytes);
+    std::memcpy(host + codeBytes, pr.yOff.data(), yBytes);
+    std::memcpy(host + codeBytes + yBytes, ySlotType.data(), tBytes);
+    std::memcpy(host + codeBytes + yBytes + tBytes, yColType.data(), cBytes);
+    std::memcpy(host + poolOff, pr.pool.data(), pr.pool.size());
+    HIP_OK(hipMemcpyAsync(base, host, total, hipMemcpyHostToDevice, c->stream));
     DevPrograms d;
     d.code = reinterpret_cast<const Insn*>(base);
     d.yOff = reinterpret_cast<const int32_t*>(base + codeBytes);
@@ -374,6 +388,21 @@ DevPrograms uploadPrograms(ngx_ctx* c, const Programs& pr, const std::vector<int
     d.yColType = cBytes ? reinterpret_cast<const int32_t*>(base + codeBytes + yBytes + tBytes) : nullptr;
     d.pool = base + poolOff;
     return d;
+}
+
+// seeds (part, vid) to the device through the page-locked input stage, after the programs in it
+void stageSeeds(ngx_ctx* c, const std::vector<int32_t>& parts, const std::vector<int64_t>& vids, int32_t* dpart,
+                int64_t* dvid) {
+    const size_t n = vids.size();
+    const size_t progBytes = (c->progStageBytes + 63) & ~size_t(63);
+    // the stage may move when it grows: the programs' copy was issued from the old one, so wait for it
+    if (c->inStage.cap < progBytes + n * 12 + 64) HIP_OK(hipStreamSynchronize(c->stream));
+    char* host = c->inStage.getKeep(progBytes + n * 12 + 64, progBytes);
+    char* hp = host + progBytes;
+    std::memcpy(hp, vids.data(), n * 8);
+    std::memcpy(hp + n * 8, parts.data(), n * 4);
+    HIP_OK(hipMemcpyAsync(dvid, hp, n * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(dpart, hp + n * 8, n * 4, hipMemcpyHostToDevice, c->stream));
 }
 
 // VM string pointer -> host bytes
@@ -550,6 +579,8 @@ struct GoResultHolder {
     std::vector<int32_t> type;
     std::string strings;
     std::vector<uint64_t> hopFrontier, hopEdges, hopNext, hopXchg;
+    // host-side timing of the call (steady clock): entry, first launch, device done
+    std::chrono::steady_clock::time_point tIn, tLaunch, tDone;
     // host_columnar: the row arrays live in the context's page-locked staging
     const int64_t *rowSrcView = nullptr, *rowDstView = nullptr, *rowRankView = nullptr;
     const int32_t* rowTypeView = nullptr;
@@ -804,6 +835,8 @@ int32_t ngx_commit(ngx_ctx* c, int32_t space) {
         if (hg->shardBase.empty()) { hg->shardBase = {0, hg->vid.size()}; hg->vglobal = hg->vid.size(); }
         hg->gbase = hg->shardBase[c->rank];
         sp->dev = upload(*hg, *sp);
+        static std::atomic<uint64_t> generations{0};
+        sp->gen = ++generations;
         sp->host = std::move(hg);
         sp->staged = StagedRows();
         return NGX_OK;
@@ -1035,13 +1068,10 @@ void growKeep(ngx_ctx* c, DBuf& b, size_t bytes, size_t keep) {
     b = nb;
 }
 
-// the final kernel's look-back words (ticket + one status per chunk), zeroed on the stream
-uint64_t* zeroedLookBack(ngx_ctx* c, uint64_t chunks) {
-    size_t bytes = ((chunks + 1) * 8 + 15) & ~size_t(15);
-    uint64_t* p = c->lbStatus.get<uint64_t>(bytes / 8);
-    HIP_OK(hipMemsetAsync(p, 0, bytes, c->stream));
-    return p;
-}
+// the final kernel's look-back words: ticket / row counter, one status per chunk, the done counter
+// (chunks + 2 words); zeroed by the hop's k_chunk_first launch
+uint64_t lookBackWords(uint64_t chunks) { return chunks + 2; }
+uint64_t* lookBack(ngx_ctx* c, uint64_t chunks) { return c->lbStatus.get<uint64_t>(lookBackWords(chunks)); }
 
 // YIELD columns that are exactly an edge key prop of every edge the hop expands (`e._dst`,
 // `e._src`, `e._rank` of the only OVER type, typed INT/VID): their cells equal the oSrc/oDst/oRank
@@ -1063,8 +1093,8 @@ std::vector<int32_t> keyAliases(const Programs& progs, const std::vector<int32_t
 
 // size the result columns for `cap` rows (keeping `keep`) and upload their descriptors; aliased
 // key columns (keyAliases) point at oSrc/oDst/oRank, which must already be sized
-const OutCol* prepareCols(ngx_ctx* c, const std::vector<ColSpec>& spec, uint64_t cap, uint64_t keep,
-                          const std::vector<int32_t>& alias = {}) {
+void prepareCols(ngx_ctx* c, FinalArgs& a, const std::vector<ColSpec>& spec, uint64_t cap, uint64_t keep,
+                 const std::vector<int32_t>& alias = {}) {
     if (c->oCols.size() < spec.size()) c->oCols.resize(spec.size());
     c->oColView.assign(spec.size(), OutCol{nullptr, nullptr, nullptr});
     for (size_t y = 0; y < spec.size(); y++) {
@@ -1079,11 +1109,14 @@ const OutCol* prepareCols(ngx_ctx* c, const std::vector<ColSpec>& spec, uint64_t
         if (spec[y].len) { growKeep(c, cb.len, cap * 4, keep * 4); c->oColView[y].len = static_cast<uint32_t*>(cb.len.p); }
         if (spec[y].t) { growKeep(c, cb.t, cap, keep); c->oColView[y].t = static_cast<uint8_t*>(cb.t.p); }
     }
-    OutCol* dev = c->oColDesc.get<OutCol>(std::max<size_t>(spec.size(), 1));
-    if (!spec.empty()) {
+    // the first kInlineCols descriptors travel in the kernel arguments; only wider results upload a table
+    for (size_t y = 0; y < spec.size() && y < static_cast<size_t>(kInlineCols); y++) a.oColsIn[y] = c->oColView[y];
+    a.oCols = nullptr;
+    if (spec.size() > static_cast<size_t>(kInlineCols)) {
+        OutCol* dev = c->oColDesc.get<OutCol>(spec.size());
         HIP_OK(hipMemcpyAsync(dev, c->oColView.data(), spec.size() * sizeof(OutCol), hipMemcpyHostToDevice, c->stream));
+        a.oCols = dev;
     }
-    return dev;
 }
 
 // result columns rows [first, first + n) -> host OutCells (row-major); a typed column's rows carry its static type
@@ -1236,12 +1269,11 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         if (jq.W.present) slotConsts(jq.W.code);
         for (auto& y : jq.Y) slotConsts(y.code);
         std::string jerr;
-        std::string src = jitSource(sp, jq);
-        if (!src.empty()) jk = c->jit.get(src, jerr);
+        // kernels cached by query shape: the source is generated only on a miss
+        jk = c->jit.get(jitShapeKey(sp, jq), [&] { return jitSource(sp, jq); }, jerr);
         if (jk && jq.P.present && recordFrom < steps) {
             jq.P = JitProgram{};
-            std::string src2 = jitSource(sp, jq);
-            if (!src2.empty()) jkNoP = c->jit.get(src2, jerr);
+            jkNoP = c->jit.get(jitShapeKey(sp, jq), [&] { return jitSource(sp, jq); }, jerr);
             if (!jkNoP) jk = nullptr;
         } else {
             jkNoP = jk;
@@ -1285,7 +1317,11 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     }
     ensureVisited(c, d.vglobal);
     hipEvent_t t0 = c->ev(), t1 = c->ev();
+    R.tLaunch = std::chrono::steady_clock::now();
     HIP_OK(hipEventRecord(t0, c->stream));
+    uint64_t* counters = c->counters.get<uint64_t>(8);
+    uint32_t* errFlag = reinterpret_cast<uint32_t*>(counters + 4);
+    HIP_OK(hipMemsetAsync(counters, 0, 64, c->stream));           // before the seed hop: no bubble
     uint64_t nF = svids.size();
     uint32_t* F = c->F0.get<uint32_t>(std::max<uint64_t>(nF, 1));
     bool haveEstart = false;                                   // estart[] / E of the next hop already built
@@ -1293,8 +1329,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     if (nF) {
         int32_t* dp_ = c->seedPart.get<int32_t>(nF);
         int64_t* dv = c->seedVid.get<int64_t>(nF);
-        HIP_OK(hipMemcpyAsync(dp_, sparts.data(), nF * 4, hipMemcpyHostToDevice, c->stream));
-        HIP_OK(hipMemcpyAsync(dv, svids.data(), nF * 8, hipMemcpyHostToDevice, c->stream));
+        stageSeeds(c, sparts, svids, dp_, dv);
         const uint64_t nEnt0 = nF * static_cast<uint64_t>(hs.n);
         if (hs.n > 0 && nF <= kSeedFuseMax && nEnt0 <= kSeedFuseMax && d.vindex.slots) {
             // lookup + degrees + scan of the seed hop in one workgroup; E published (no stream round trip)
@@ -1311,9 +1346,6 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             });
         }
     }
-    uint64_t* counters = c->counters.get<uint64_t>(8);
-    uint32_t* errFlag = reinterpret_cast<uint32_t*>(counters + 4);
-    HIP_OK(hipMemsetAsync(counters, 0, 64, c->stream));
     uint64_t totalRows = 0;
     // result columns: value bits always; lengths when strings can appear; per-row types when the
     // column's static type is unknown
@@ -1362,9 +1394,11 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         R.hopEdges.push_back(E);
         uint64_t chunks = (E + kChunk - 1) / kChunk;
         uint64_t* chunkFirst = c->chunkFirst.get<uint64_t>(std::max<uint64_t>(chunks, 1));
+        uint64_t* lb = (isRecord && E) ? lookBack(c, chunks) : nullptr;
         if (E) {
             c->timed("chunk_first", nEnt * 16, [&] {
-                if (launchChunkFirst(estart, nEnt, chunkFirst, c->stream)) throw Error{NGX_E_DEVICE, "chunk first"};
+                if (launchChunkFirst(estart, nEnt, chunkFirst, c->stream, lb, lb ? lookBackWords(chunks) : 0))
+                    throw Error{NGX_E_DEVICE, "chunk first"};
             });
         }
         // the hop's storage request: which edges the processor emits (collectEdgeProps, .inl:501-608)
@@ -1412,14 +1446,18 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             growKeep(c, c->oDst, cap * 8, totalRows * 8);
             growKeep(c, c->oRank, cap * 8, totalRows * 8);
             growKeep(c, c->oType, cap * 4, totalRows * 4);
-            a.oCols = prepareCols(c, colSpec, cap, totalRows, yAlias);
+            prepareCols(c, a, colSpec, cap, totalRows, yAlias);
             a.oBase = totalRows;
             a.oSrc = static_cast<int64_t*>(c->oSrc.p);
             a.oDst = static_cast<int64_t*>(c->oDst.p);
             a.oRank = static_cast<int64_t*>(c->oRank.p);
             a.oType = constType ? nullptr : static_cast<int32_t*>(c->oType.p);
             a.oEntry = nullptr;
-            a.lbStatus = zeroedLookBack(c, chunks);
+            a.lbStatus = lb;
+            a.done = reinterpret_cast<uint32_t*>(lb + chunks + 1);
+            Publish rowsPub = nextPub(c);                       // the last chunk publishes the row count
+            a.rowsPub = rowsPub.slot;
+            a.rowsSeq = rowsPub.seq;
             c->timed("final", E * (16 + kfBytes), [&] {
                 if (kj) {
                     void* args[] = {&a};
@@ -1428,7 +1466,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
                     throw Error{NGX_E_DEVICE, "final"};
                 }
             });
-            uint64_t nrows = readScalar(c, a.lbStatus);      // GO: rows reserved by atomicAdd
+            uint64_t nrows = awaitPub(c, rowsPub, a.lbStatus);   // GO: rows reserved by atomicAdd
             c->addBytes("final", nrows * (24 + 8 * ky));
             totalRows += nrows;
         }
@@ -1481,6 +1519,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     HIP_OK(hipEventElapsedTime(&ms, t0, t1));
     c->collectTimings();
     R.r.device_ms = ms;
+    R.tDone = std::chrono::steady_clock::now();
     uint32_t flags[4];
     HIP_OK(hipMemcpy(flags, errFlag, 16, hipMemcpyDeviceToHost));
     if (flags[3]) return fail(c, NGX_E_DEVICE, "final-hop look-back did not complete (device fault)");
@@ -1641,6 +1680,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
 extern "C" int32_t ngx_go(ngx_ctx* c, const ngx_go_plan* p, ngx_go_result** out) {
     std::lock_guard<std::mutex> g(c->mu);
     auto R = std::make_unique<GoResultHolder>();
+    R->tIn = std::chrono::steady_clock::now();
+    R->tLaunch = R->tDone = R->tIn;
     int32_t rc;
     try {
         if (c->broken) throw Error{NGX_E_DEVICE, "context unusable: its RCCL communicator was aborted"};
@@ -1660,6 +1701,11 @@ extern "C" int32_t ngx_go(ngx_ctx* c, const ngx_go_plan* p, ngx_go_result** out)
     R->r.row_rank = R->rowRankView ? R->rowRankView : R->rank.data();
     R->r.row_type = R->rowSrcView ? R->rowTypeView : R->type.data();
     R->r.host_cols = R->hostCols.empty() ? nullptr : R->hostCols.data();
+    auto msBetween = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    R->r.host_prep_ms = msBetween(R->tIn, R->tLaunch);
+    R->r.host_tail_ms = msBetween(R->tDone, std::chrono::steady_clock::now());
     R->r.strings = R->strings.data();
     R->r.strings_len = R->strings.size();
     R->r.nhops = static_cast<int32_t>(R->hopEdges.size());
@@ -1782,8 +1828,7 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
     if (nF) {
         int32_t* dpart = c->seedPart.get<int32_t>(nF);
         int64_t* dv = c->seedVid.get<int64_t>(nF);
-        HIP_OK(hipMemcpyAsync(dpart, sparts.data(), nF * 4, hipMemcpyHostToDevice, c->stream));
-        HIP_OK(hipMemcpyAsync(dv, svids.data(), nF * 8, hipMemcpyHostToDevice, c->stream));
+        stageSeeds(c, sparts, svids, dpart, dv);
         if (launchIndexLookup(dpart, dv, nF, d.vindex, F, c->stream)) throw Error{NGX_E_DEVICE, "lookup"};
     }
     std::vector<int32_t> hopTypes;
@@ -1805,7 +1850,8 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
     if (E) {
         uint64_t chunks = (E + kChunk - 1) / kChunk;
         uint64_t* chunkFirst = c->chunkFirst.get<uint64_t>(chunks);
-        if (launchChunkFirst(estart, nEnt, chunkFirst, c->stream)) throw Error{NGX_E_DEVICE, "chunk first"};
+        uint64_t* lb = lookBack(c, chunks);
+        if (launchChunkFirst(estart, nEnt, chunkFirst, c->stream, lb, lookBackWords(chunks))) throw Error{NGX_E_DEVICE, "chunk first"};
         FinalArgs a{};
         a.F = F; a.estart = estart; a.chunkFirst = chunkFirst; a.nEnt = nEnt; a.E = E; a.hs = hs;
         a.vid = d.vid; a.V = d.V; a.gbase = d.gbase;
@@ -1837,8 +1883,8 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
         a.oType = c->oType.get<int32_t>(E);
         a.oEntry = c->oEntry.get<uint32_t>(E);
         std::vector<ColSpec> spec(nY, ColSpec{true, true});   // raw value cells: every column typed per row
-        a.oCols = prepareCols(c, spec, E, 0);
-        a.lbStatus = zeroedLookBack(c, chunks);
+        prepareCols(c, a, spec, E, 0);
+        a.lbStatus = lb;
         if (launchFinal(a, c->stream)) throw Error{NGX_E_DEVICE, "final"};
         nrows = readScalar(c, a.lbStatus + chunks) & ((1ULL << 62) - 1);
         R.edgeVertex.resize(nrows);

@@ -8,6 +8,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <map>
 #include <string>
 #include <vector>
@@ -47,9 +48,10 @@ struct JitQuery {
 class JitCache {
 public:
     ~JitCache();
-    // nullptr when compilation failed (err set); compiled kernels are cached by source, at most
-    // `capacity` modules (least recently used unloaded first; callers hold no kernel across queries)
-    const JitKernels* get(const std::string& source, std::string& err);
+    // nullptr when compilation failed (err set). Kernels are cached by query shape (jitShapeKey), at most
+    // `capacity` modules (least recently used unloaded first; callers hold no kernel across queries);
+    // `source` generates the hipRTC source on a miss.
+    const JitKernels* get(const std::string& shape, const std::function<std::string()>& source, std::string& err);
     uint64_t compiled = 0, hits = 0, failed = 0, evicted = 0;
     double compileSeconds = 0;
     int64_t lastRegs = -1, lastScratch = -1;    // hipFuncGetAttribute of the last compiled kernel
@@ -64,7 +66,10 @@ private:
 };
 
 // C++ source of the evaluator struct + kernels for one query on one space snapshot (without the
-// common device headers, which JitCache::get prepends when it compiles; the cache key is this text)
+// common device headers, which JitCache::get prepends when it compiles)
 std::string jitSource(const Space& sp, const JitQuery& q);
+// everything jitSource depends on, compactly: snapshot generation, programs (slotted literals as slot
+// numbers), column types, key aliases, hop flags
+std::string jitShapeKey(const Space& sp, const JitQuery& q);
 
 }  // namespace ngx

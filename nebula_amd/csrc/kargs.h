@@ -36,6 +36,7 @@ struct OutCol {
 };
 
 constexpr int kJitConsts = 24;          // PUSH literals a generated kernel reads from its arguments
+constexpr int kInlineCols = 12;         // result column descriptors passed in the arguments themselves
 
 struct FinalArgs {
     const uint32_t* F;                  // frontier rows
@@ -70,7 +71,11 @@ struct FinalArgs {
     int64_t* oRank;
     int32_t* oType;
     uint32_t* oEntry;                   // frontier index of each row (GetNeighbors), may be null
-    const OutCol* oCols;                // nY columns (device array)
+    const OutCol* oCols;                // nY columns (device array; columns >= kInlineCols read it)
+    OutCol oColsIn[kInlineCols];        // the first columns' descriptors, by value (no upload)
+    uint64_t* rowsPub;                  // host-mapped [rows, seq] published by the last chunk (GO), or null
+    uint64_t rowsSeq;
+    uint32_t* done;                     // chunks finished (zeroed with lbStatus), for rowsPub
     const uint8_t* mask;                // per hop edge: storage emitted it (max_edge_returned_per_vertex
                                         // path); when set, replaces the storage checks. nullptr: none
     int64_t kc[kJitConsts];             // generated kernels: literal bits (string: pool offset)

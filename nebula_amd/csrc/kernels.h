@@ -44,7 +44,8 @@ int launchLookup(const int32_t* qpart, const int64_t* qvid, uint64_t n, const in
 int launchDegreeScan(const uint32_t* F, uint64_t nEnt, const HopSlots& hs, uint64_t* estart, uint64_t* tileSums,
                      hipStream_t s, Publish pub = Publish{nullptr, 0});
 // chunkFirst must hold ceil(E / kChunk) entries (estart[nEnt] = E)
-int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst, hipStream_t s);
+int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst, hipStream_t s, uint64_t* zero = nullptr,
+                     uint64_t nzero = 0);
 // mask (nullptr: every edge): only hop edges e with mask[e] != 0 are expanded
 int launchExpandMark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst, uint64_t nEnt, uint64_t E,
                      const HopSlots& hs, uint8_t* visited, uint8_t epoch, bool pos32, hipStream_t s,

@@ -255,8 +255,11 @@ __global__ __launch_bounds__(1024) void k_seed_frontier(const int32_t* qpart, co
 
 // ------------------------------------------------------------------------------ chunk -> first entry
 // chunkFirst[c] = the entry holding edge c * CE (the only entry with estart[i] <= c*CE < estart[i+1])
-__global__ void k_chunk_first(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst) {
+// zero[0 .. nzero) is cleared on the way (the next final launch's look-back words: no memset launch)
+__global__ void k_chunk_first(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst, uint64_t* zero,
+                              uint64_t nzero) {
     uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    for (uint64_t z = i; z < nzero; z += static_cast<uint64_t>(gridDim.x) * blockDim.x) zero[z] = 0;
     if (i >= nEnt) return;
     uint64_t s = estart[i], t = estart[i + 1];
     for (uint64_t c = (s + CE - 1) / CE; c * CE < t; c++) chunkFirst[c] = i;
@@ -322,7 +325,7 @@ struct VmEv {
     static __device__ __forceinline__ Val W(const FinalArgs& a, const EdgeCtx& ec) { return vmEval(a.W, a.env, ec); }
     static __device__ __forceinline__ void Y(const FinalArgs& a, const EdgeCtx& ec, uint64_t o, uint32_t& errs) {
         for (int y = 0; y < a.nY; y++) {
-            const OutCol& oc = a.oCols[y];
+            const OutCol& oc = outCol(a, y);
             Val v;
             if (a.ySlotType != nullptr && a.ySlotType[y] != 0 && a.ySlotType[y] != ec.etype) {
                 v.t = 0xFF; v.len = 0; v.x = 0;              // column of another edge type (GetNeighbors)
@@ -439,9 +442,12 @@ int launchSeedFrontier(const int32_t* qpart, const int64_t* qvid, uint64_t n, VI
     return static_cast<int>(hipGetLastError());
 }
 
-int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst, hipStream_t s) {
-    if (nEnt == 0) return 0;
-    hipLaunchKernelGGL(k_chunk_first, dim3(static_cast<unsigned>((nEnt + 255) / 256)), dim3(256), 0, s, estart, nEnt, chunkFirst);
+int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst, hipStream_t s, uint64_t* zero,
+                     uint64_t nzero) {
+    if (nEnt == 0 && nzero == 0) return 0;
+    uint64_t n = nEnt > nzero ? nEnt : nzero;
+    hipLaunchKernelGGL(k_chunk_first, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, estart, nEnt, chunkFirst,
+                       zero, nzero);
     return static_cast<int>(hipGetLastError());
 }
 

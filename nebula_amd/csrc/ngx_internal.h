@@ -110,6 +110,7 @@ struct DeviceGraph;                     // engine.cpp
 struct Space {
     int32_t id = 0;
     int32_t numParts = 0;
+    uint64_t gen = 0;                   // snapshot generation (bumped by every commit; keys cached kernels)
     std::map<int32_t, SchemaSet> tags, edges;
     std::map<std::string, int32_t> tagByName, edgeByName;
     std::vector<std::string> edgeOrder;

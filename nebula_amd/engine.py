@@ -101,7 +101,7 @@ class GoResultC(ctypes.Structure):
                 ("device_ms", c_dbl), ("dev_src", ctypes.c_void_p), ("dev_dst", ctypes.c_void_p),
                 ("dev_rank", ctypes.c_void_p), ("dev_type", ctypes.c_void_p), ("dev_cols", ctypes.c_void_p),
                 ("dev_type_const", ctypes.c_int32), ("host_cols", ctypes.c_void_p),
-                ("hop_exchange_bytes", P(c_u64))]
+                ("hop_exchange_bytes", P(c_u64)), ("host_prep_ms", c_dbl), ("host_tail_ms", c_dbl)]
 
 
 class KernelStat(ctypes.Structure):
@@ -238,6 +238,8 @@ class GoResult:
     # on_device + fetch: the HBM result copied back as arrays (x, len or None, type or None) per column
     dev_cols: List[tuple] = field(default_factory=list)
     digests: object = None               # columnar + digest_fn: whatever digest_fn returned
+    host_prep_ms: float = 0.0            # library host time before the first launch / after the device
+    host_tail_ms: float = 0.0
 
 
 @dataclass
@@ -363,13 +365,23 @@ class Engine:
         before the result is freed (tests: large-result comparison)."""
         if isinstance(s, str):
             s = ngql.parse_go(s)
-        starts = np.array(s.vids, dtype=np.int64)
-        names = (ctypes.c_char_p * max(1, len(s.over)))(*[n.encode() for n, _ in s.over])
-        aliases = (ctypes.c_char_p * max(1, len(s.over)))(*[(a or "").encode() for _, a in s.over])
-        where = s.where.encode() if s.where is not None else b""
-        yb = [y.expr.encode() for y in s.yields]
-        yarr = (ctypes.c_char_p * max(1, len(yb)))(*yb)
-        ylen = (c_u32 * max(1, len(yb)))(*[len(y) for y in yb])
+        # the sentence's encoded form (expressions in Expression::encode bytes, vids as int64) is built once
+        # per sentence object and kept on it
+        enc = getattr(s, "_ngx_enc", None)
+        if enc is None:
+            starts = np.array(s.vids, dtype=np.int64)
+            names = (ctypes.c_char_p * max(1, len(s.over)))(*[n.encode() for n, _ in s.over])
+            aliases = (ctypes.c_char_p * max(1, len(s.over)))(*[(a or "").encode() for _, a in s.over])
+            where = s.where.encode() if s.where is not None else b""
+            yb = [y.expr.encode() for y in s.yields]
+            yarr = (ctypes.c_char_p * max(1, len(yb)))(*yb)
+            ylen = (c_u32 * max(1, len(yb)))(*[len(y) for y in yb])
+            enc = (starts, names, aliases, where, yb, yarr, ylen)
+            try:
+                s._ngx_enc = enc
+            except AttributeError:
+                pass
+        starts, names, aliases, where, yb, yarr, ylen = enc
         plan = GoPlan(space, s.record_from, s.record_to, len(starts), starts.ctypes.data_as(P(c_i64)), len(s.over),
                       names, aliases, 1 if s.over_all else 0, s.direction, where if where else None, len(where),
                       len(yb), yarr, ylen, 1 if s.distinct else 0, 1 if pushdown else 0, now_sec,
@@ -385,7 +397,8 @@ class Engine:
             n = r.nrows
             if on_device:
                 res = GoResult(ok=rc == 0, error=err, code=rc, col_types=[r.col_types[i] for i in range(r.ncols)],
-                               rows=[], nrows=n, hop_frontier=[r.hop_frontier[i] for i in range(r.nhops)],
+                               rows=[], nrows=n, host_prep_ms=r.host_prep_ms, host_tail_ms=r.host_tail_ms,
+                               hop_frontier=[r.hop_frontier[i] for i in range(r.nhops)],
                                hop_edges=[r.hop_edges[i] for i in range(r.nhops)],
                                hop_next=[r.hop_next[i] for i in range(r.nhops)],
                                hop_xchg=[r.hop_exchange_bytes[i] for i in range(r.nhops)] if r.hop_exchange_bytes else [],
@@ -407,7 +420,7 @@ class Engine:
                 if not arrays:                             # delivery only (bench): no Python copies
                     return GoResult(ok=rc == 0, error=err, code=rc, col_types=[r.col_types[i] for i in range(r.ncols)],
                                     rows=[], nrows=r.nrows, hop_edges=[r.hop_edges[i] for i in range(r.nhops)],
-                                    device_ms=r.device_ms)
+                                    device_ms=r.device_ms, host_prep_ms=r.host_prep_ms, host_tail_ms=r.host_tail_ms)
                 return self._columnar(r, rc, err, rows, digest_fn)
             res = GoResult(
                 ok=rc == 0, error=err, code=rc, col_types=[r.col_types[i] for i in range(r.ncols)],
