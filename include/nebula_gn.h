@@ -154,7 +154,17 @@ typedef struct {
     const ngx_prop_def* cols;     /* return_columns */
     int32_t max_edges_per_vertex; /* FLAGS_max_edge_returned_per_vertex, <= 0 or INT32_MAX: unlimited */
     int64_t now_sec;              /* clock for TTL (WallClock::fastNowInSec); <= 0: the current time */
+    int32_t encode_rows;          /* 1: also return the QueryResponse payload (RowWriter rows, schemas) */
 } ngx_gn_request;
+
+/* One response schema of a QueryResponse (common.thrift Schema): columns in order. */
+typedef struct {
+    int32_t is_edge;              /* 1: edge_schema[id] (signed edge type), 0: vertex_schema[id] (tag) */
+    int32_t id;
+    int32_t ncols;
+    const char* const* names;
+    const int32_t* types;         /* NGX_T_* */
+} ngx_schema_def;
 
 typedef struct {
     int32_t code;                 /* NGX_OK, or the code pushed for every part (checkAndBuildContexts) */
@@ -171,6 +181,22 @@ typedef struct {
     const uint8_t* vertex_has_tag;/* [v * ncols + c] 1 if the vertex has that tag row */
     const char* strings;
     uint64_t strings_len;
+    /* encode_rows: the wire payload of QueryResponse (storage.thrift:112-151), byte-exact with the
+     * reference processor. Edge e's IdAndProp.props is edge_props[edge_props_off[e] ..
+     * edge_props_off[e + 1]): a RowWriter row (src/dataman/RowWriter.cpp:48-87) of the response
+     * schema of its type, encoded on the device; an empty range for a type returning only _dst
+     * (onlyStructure: props unset). TagData rows (QueryBoundProcessor.cpp:175-204): tag_row_vertex[k]
+     * (request vid index), tag_row_tag[k], data = tag_props[tag_props_off[k] .. tag_props_off[k + 1]),
+     * in request-vid order, tags in response order per vertex. */
+    const uint8_t* edge_props;
+    const uint64_t* edge_props_off;   /* nedges + 1 */
+    int32_t nschemas;                 /* edge_schema entries, then vertex_schema entries */
+    const ngx_schema_def* schemas;
+    uint32_t ntag_rows;
+    const uint32_t* tag_row_vertex;
+    const int32_t* tag_row_tag;
+    const uint8_t* tag_props;
+    const uint64_t* tag_props_off;    /* ntag_rows + 1 */
 } ngx_gn_result;
 
 int32_t ngx_get_neighbors(ngx_ctx* ctx, const ngx_gn_request* req, ngx_gn_result** out);

@@ -22,6 +22,7 @@
 #include "exprc.h"
 #include "jit.h"
 #include "kernels.h"
+#include "rowcodec.h"
 
 using namespace ngx;
 
@@ -103,7 +104,11 @@ struct ngx_ctx {
     std::mutex mu;
     // scratch
     DBuf visited, F0, F1, estart, chunkFirst, tileSums, counters, lbStatus, seedPart, seedVid;
+    DBuf cmpStatus[2];                                  // k_compact_lb look-back words (double buffer, kept zeroed)
+    uint64_t cmpWords = 0;                              // capacity of each cmpStatus buffer, in words
+    int cmpPar = 0;
     DBuf oSrc, oDst, oRank, oType, oEntry, progBuf, sendBits, recvBits, vcells, misc, oColDesc, edgeMask;
+    DBuf oFlags, rowCols, rowLen, rowOff, rowBytes;     // GetNeighbors response rows (encode_rows)
     int64_t maxEdgesPerVertex = INT32_MAX;             // storaged FLAGS_max_edge_returned_per_vertex (GO hops)
     struct ColBuf { DBuf x, len, t; };
     struct PinBuf {                                     // page-locked host staging for result D2H
@@ -157,7 +162,8 @@ struct ngx_ctx {
         spaces.clear();
         for (DBuf* b : {&visited, &F0, &F1, &estart, &tileSums, &counters, &lbStatus, &seedPart, &seedVid, &oSrc,
                         &oDst, &oRank, &oType, &oEntry, &chunkFirst, &oColDesc, &progBuf, &sendBits, &recvBits,
-                        &vcells, &misc, &edgeMask}) b->release();
+                        &vcells, &misc, &edgeMask, &cmpStatus[0], &cmpStatus[1], &oFlags, &rowCols, &rowLen,
+                        &rowOff, &rowBytes}) b->release();
         for (auto& cb : oCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         hostStage.release();
         inStage.release();
@@ -594,6 +600,14 @@ struct GnResultHolder {
     std::vector<ngx_cell> edgeCells, vertexCells;
     std::vector<uint8_t> vertexHasTag;
     std::string strings;
+    // encode_rows: QueryResponse payload
+    std::vector<uint8_t> edgeProps, tagProps;
+    std::vector<uint64_t> edgePropsOff, tagPropsOff;
+    std::vector<uint32_t> tagRowVertex;
+    std::vector<int32_t> tagRowTag;
+    struct Schema { int32_t isEdge, id; std::vector<std::string> names; std::vector<const char*> cnames; std::vector<int32_t> types; };
+    std::vector<Schema> schemas;
+    std::vector<ngx_schema_def> schemaView;
 };
 
 HopSlots makeHopSlots(const Space& sp, const DeviceGraph& d, const std::vector<int32_t>& types,
@@ -1213,6 +1227,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     }
     for (auto& y : gp.yields) {
         Program yp;
+        if (builtStringAtRoot(*y)) return fail(c, NGX_E_UNSUPPORTED, "YIELD of a (string) cast: result strings are not built on the device");
         int32_t crc = compileGraphd(*y, gctx, yp, err);
         if (crc) return fail(c, crc, err);
         progs.yOff.push_back(progs.add(yp));
@@ -1316,6 +1331,33 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         svids.push_back(v);
     }
     ensureVisited(c, d.vglobal);
+    // the compaction after an intermediate hop also writes the next hop's estart[] and E (fused
+    // scan) when the packed (|F|, E) total fits; the slot totals bound E
+    uint64_t slotEdges = 0;
+    bool pos32 = true;                                         // every CSR position fits 32 bits
+    for (int s = 0; s < hs.n; s++) {
+        uint64_t es = sp.host->slots[hs.slotIdx[s]].dst.size();
+        slotEdges += es;
+        pos32 = pos32 && es < (1ULL << 32);
+    }
+    const bool fuseDeg = d.V < (1ULL << (64 - kFdShift)) && slotEdges <= kFdMask && hs.n > 0;
+    // single-pass compaction (k_compact_lb): the next hop's chunk heads come with its estart; every
+    // hop after the seed hop has unique frontier rows, so E <= slotEdges bounds chunkFirst
+    const bool lbCompact = fuseDeg && d.V < kCompactLbMaxV;
+    const uint64_t cfCap = slotEdges / kChunk + 2;
+    c->chunkFirst.get<uint64_t>(cfCap);
+    uint64_t* lbw = lookBack(c, std::max<uint64_t>(cfCap, kDoneOff));   // GO final words: [0] rows, [kDoneOff] done
+    if (lbCompact) {
+        const uint64_t words = (d.V + kTile - 1) / kTile + 2;
+        if (c->cmpWords < words) {
+            for (DBuf& b : c->cmpStatus) {
+                b.get<uint64_t>(words);
+                HIP_OK(hipMemsetAsync(b.p, 0, b.cap, c->stream));
+            }
+            c->cmpWords = std::min(c->cmpStatus[0].cap, c->cmpStatus[1].cap) / 8;
+        }
+    }
+    bool haveHeads = false;                                    // chunkFirst of the next hop already built
     hipEvent_t t0 = c->ev(), t1 = c->ev();
     R.tLaunch = std::chrono::steady_clock::now();
     HIP_OK(hipEventRecord(t0, c->stream));
@@ -1332,14 +1374,26 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         stageSeeds(c, sparts, svids, dp_, dv);
         const uint64_t nEnt0 = nF * static_cast<uint64_t>(hs.n);
         if (hs.n > 0 && nF <= kSeedFuseMax && nEnt0 <= kSeedFuseMax && d.vindex.slots) {
-            // lookup + degrees + scan of the seed hop in one workgroup; E published (no stream round trip)
+            // lookup + degrees + scan + chunk heads of the seed hop in one workgroup; E published (no
+            // stream round trip); the first hop's final-kernel words cleared on the way
             uint64_t* est0 = c->estart.get<uint64_t>(nEnt0 + 1);
             Publish pub = nextPub(c);
+            // seeds may repeat (no DISTINCT): E <= slot edges x the largest multiplicity
+            uint64_t mult = 1;
+            {
+                std::unordered_map<int64_t, uint64_t> m;
+                for (int64_t v : svids) mult = std::max<uint64_t>(mult, ++m[v]);
+            }
+            const uint64_t cf0 = (slotEdges * mult + kChunk - 1) / kChunk + 1;
+            uint64_t* cf = c->chunkFirst.get<uint64_t>(std::max(cf0, cfCap));
             c->timed("seed", nF * 12 + nEnt0 * 24, [&] {
-                if (launchSeedFrontier(dp_, dv, nF, d.vindex, hs, F, est0, pub, c->stream)) throw Error{NGX_E_DEVICE, "seed"};
+                if (launchSeedFrontierCf(dp_, dv, nF, d.vindex, hs, F, est0, pub, cf, std::max(cf0, cfCap), lbw, 2, errFlag,
+                                         c->stream))
+                    throw Error{NGX_E_DEVICE, "seed"};
             });
             fusedE = awaitPub(c, pub, est0 + nEnt0);
             haveEstart = true;
+            haveHeads = true;
         } else {
             c->timed("lookup", nF * 12, [&] {
                 if (launchLookup(dp_, dv, nF, d.vpart, d.vid, d.V, F, c->stream)) throw Error{NGX_E_DEVICE, "lookup"};
@@ -1352,16 +1406,6 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     std::vector<ColSpec> colSpec;
     for (int32_t ct : gp.colTypes) colSpec.push_back(ColSpec{ct == T_UNKNOWN || ct == T_STRING, ct == T_UNKNOWN});
 
-    // the compaction after an intermediate hop also writes the next hop's estart[] and E (fused
-    // scan) when the packed (|F|, E) total fits; the slot totals bound E
-    uint64_t slotEdges = 0;
-    bool pos32 = true;                                         // every CSR position fits 32 bits
-    for (int s = 0; s < hs.n; s++) {
-        uint64_t es = sp.host->slots[hs.slotIdx[s]].dst.size();
-        slotEdges += es;
-        pos32 = pos32 && es < (1ULL << 32);
-    }
-    const bool fuseDeg = d.V < (1ULL << (64 - kFdShift)) && slotEdges <= kFdMask && hs.n > 0;
     // storage-side request of each hop (getStepOutProps): props only on record hops, TTL info always
     uint32_t recordPropsMask = 0, ttlMask = 0;
     int32_t ttlCol[kMaxSlots];
@@ -1394,13 +1438,14 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         R.hopEdges.push_back(E);
         uint64_t chunks = (E + kChunk - 1) / kChunk;
         uint64_t* chunkFirst = c->chunkFirst.get<uint64_t>(std::max<uint64_t>(chunks, 1));
-        uint64_t* lb = (isRecord && E) ? lookBack(c, chunks) : nullptr;
-        if (E) {
+        uint64_t* lb = (isRecord && E) ? lbw : nullptr;        // GO final: [0] rows reserved, [kDoneOff] chunks done
+        if (E && !haveHeads) {
             c->timed("chunk_first", nEnt * 16, [&] {
-                if (launchChunkFirst(estart, nEnt, chunkFirst, c->stream, lb, lb ? lookBackWords(chunks) : 0))
+                if (launchChunkFirst(estart, nEnt, chunkFirst, c->stream, lb, lb ? kDoneOff + 1 : 0))
                     throw Error{NGX_E_DEVICE, "chunk first"};
             });
         }
+        haveHeads = false;
         // the hop's storage request: which edges the processor emits (collectEdgeProps, .inl:501-608)
         FinalArgs a{};
         a.F = F; a.estart = estart; a.chunkFirst = chunkFirst; a.nEnt = nEnt; a.E = E; a.hs = hs;
@@ -1454,7 +1499,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             a.oType = constType ? nullptr : static_cast<int32_t*>(c->oType.p);
             a.oEntry = nullptr;
             a.lbStatus = lb;
-            a.done = reinterpret_cast<uint32_t*>(lb + chunks + 1);
+            a.done = reinterpret_cast<uint32_t*>(lb + kDoneOff);
             Publish rowsPub = nextPub(c);                       // the last chunk publishes the row count
             a.rowsPub = rowsPub.slot;
             a.rowsSeq = rowsPub.seq;
@@ -1487,7 +1532,37 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         }
         uint32_t* Fn = (F == c->F0.p) ? c->F1.get<uint32_t>(std::max<uint64_t>(d.V, 1)) : c->F0.get<uint32_t>(std::max<uint64_t>(d.V, 1));
         uint64_t* tiles2 = c->tileSums.get<uint64_t>((std::max<uint64_t>(d.V, 1) + kTile - 1) / kTile + 1);
-        if (fuseDeg) {
+        if (lbCompact) {
+            // one launch: next frontier + estart + chunk heads; the look-back words of the next
+            // compaction cleared on the way
+            CompactArgs ca{};
+            ca.visited = c->visited.get<uint8_t>(d.vglobal) + d.gbase;
+            ca.V = d.V;
+            ca.hs = hs;
+            ca.outF = Fn;
+            ca.estart = c->estart.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
+            ca.chunkFirst = c->chunkFirst.get<uint64_t>(cfCap);
+            ca.cfCap = cfCap;
+            ca.status = static_cast<uint64_t*>(c->cmpStatus[c->cmpPar].p);
+            ca.nextStatus = static_cast<uint64_t*>(c->cmpStatus[c->cmpPar ^ 1].p);
+            ca.nNext = c->cmpWords;
+            c->cmpPar ^= 1;
+            ca.total = counters + 2;
+            ca.pub = nextPub(c);
+            ca.zero = lbw;
+            ca.nzero = 2;
+            ca.err = errFlag;
+            ca.epoch = ep;
+            c->timed("compact_degrees", 0, [&] {
+                if (launchCompactLb(ca, c->stream)) throw Error{NGX_E_DEVICE, "compact"};
+            });
+            uint64_t packed = awaitPub(c, ca.pub, counters + 2);
+            nF = packed >> kFdShift;
+            fusedE = packed & kFdMask;
+            haveEstart = true;
+            haveHeads = true;
+            c->addBytes("compact_degrees", nF * 8 + nF * static_cast<uint64_t>(hs.n) * 24);
+        } else if (fuseDeg) {
             // estart sized for any next frontier (every row of the shard) so the next hop's get() keeps it
             uint64_t* est = c->estart.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
             Publish pub = nextPub(c);
@@ -1725,6 +1800,106 @@ namespace {
 
 const std::map<std::string, int> kKeyProps = {{"_src", 0}, {"_dst", 1}, {"_rank", 2}, {"_type", 3}};
 
+struct HostSchemaView {
+    int32_t isEdge, id;
+    std::vector<std::string> names;
+    std::vector<int32_t> types;
+};
+void addSchema(GnResultHolder& R, const HostSchemaView& hv) {
+    GnResultHolder::Schema s{hv.isEdge, hv.id, hv.names, {}, hv.types};
+    R.schemas.push_back(std::move(s));
+}
+
+// IdAndProp.props of every returned edge, encoded on the device (kernels.hip k_encode_rows): row
+// lengths, their scan, then the bytes; copied to the result on the context's stream
+void encodeEdgeRows(ngx_ctx* c, const FinalArgs& a, uint64_t nrows,
+                    const std::map<int32_t, std::vector<std::pair<int32_t, int32_t>>>& respCols, GnResultHolder& R) {
+    RowEncArgs e{};
+    e.n = nrows;
+    e.oType = a.oType;
+    e.oSrc = a.oSrc;
+    e.oRank = a.oRank;
+    e.oFlags = a.oFlags;
+    // every column descriptor in one device table (the final kernel took the first kInlineCols by value)
+    OutCol* dcols = c->oColDesc.get<OutCol>(std::max<size_t>(c->oColView.size(), 1));
+    HIP_OK(hipMemcpyAsync(dcols, c->oColView.data(), c->oColView.size() * sizeof(OutCol), hipMemcpyHostToDevice, c->stream));
+    e.cols = dcols;
+    std::vector<int32_t> srcs, types;                     // rcSrc then rcType, slot after slot
+    e.nslots = 0;
+    e.cbeg[0] = 0;
+    for (auto& kv : respCols) {
+        if (e.nslots >= kMaxSlots) throw Error{NGX_E_UNSUPPORTED, "too many edge types in one request"};
+        e.etype[e.nslots] = kv.first;
+        for (auto& p : kv.second) { srcs.push_back(p.first); types.push_back(p.second); }
+        e.cbeg[e.nslots + 1] = static_cast<int32_t>(srcs.size());
+        e.nslots++;
+    }
+    srcs.insert(srcs.end(), types.begin(), types.end());
+    int32_t* drc = c->rowCols.get<int32_t>(std::max<size_t>(srcs.size(), 1));
+    HIP_OK(hipMemcpyAsync(drc, srcs.data(), srcs.size() * 4, hipMemcpyHostToDevice, c->stream));
+    e.rcSrc = drc;
+    e.rcType = drc + types.size();
+    uint64_t* len = c->rowLen.get<uint64_t>(nrows + 1);
+    uint64_t* off = c->rowOff.get<uint64_t>(nrows + 1);
+    uint64_t* tiles = c->tileSums.get<uint64_t>((nrows + kTile - 1) / kTile + 1);
+    e.rowLen = len;
+    if (launchEncodeRows(e, false, c->stream)) throw Error{NGX_E_DEVICE, "row sizes"};
+    if (launchScanU64(len, nrows, off, tiles, c->stream)) throw Error{NGX_E_DEVICE, "row offsets"};
+    uint64_t total = readScalar(c, off + nrows);
+    e.rowOff = off;
+    e.out = c->rowBytes.get<uint8_t>(std::max<uint64_t>(total, 1));
+    if (launchEncodeRows(e, true, c->stream)) throw Error{NGX_E_DEVICE, "rows"};
+    R.edgePropsOff.resize(nrows + 1);
+    R.edgeProps.resize(total);
+    HIP_OK(hipMemcpyAsync(R.edgePropsOff.data(), off, (nrows + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+    if (total) HIP_OK(hipMemcpyAsync(R.edgeProps.data(), e.out, total, hipMemcpyDeviceToHost, c->stream));
+}
+
+// TagData rows (QueryBoundProcessor.cpp:175-204): per request vid, per tag of the response in order, the
+// RowWriter row of its return columns when the vertex has a live row of the tag (collectVertexProps
+// collected something: writer.size() > 1)
+void encodeTagRows(const ngx_gn_request& q, const std::vector<int32_t>& tagOrder, uint64_t nF, GnResultHolder& R) {
+    const int32_t nY = q.ncols;
+    R.tagPropsOff.assign(1, 0);
+    for (uint64_t v = 0; v < nF; v++) {
+        for (int32_t t : tagOrder) {
+            std::vector<int32_t> cols;
+            for (int32_t i = 0; i < nY; i++) {
+                if ((q.cols[i].owner == 1 || q.cols[i].owner == 2) && q.cols[i].id == t) cols.push_back(i);
+            }
+            if (cols.empty() || !R.vertexHasTag[v * nY + cols[0]]) continue;
+            const GnResultHolder::Schema* sch = nullptr;
+            for (auto& s : R.schemas) if (!s.isEdge && s.id == t) sch = &s;
+            // the cord, recording a block offset after every 16 fields (RW_CLEAN_UP_WRITE)
+            std::vector<uint64_t> offs;
+            auto cord = [&](RowSink& s) {
+                offs.clear();
+                for (size_t k = 0; k < cols.size(); k++) {
+                    const ngx_cell& cell = R.vertexCells[v * nY + cols[k]];
+                    uint8_t vt = cell.kind == NGX_CELL_BOOL ? V_BOOL : cell.kind == NGX_CELL_DOUBLE ? V_DBL
+                               : cell.kind == NGX_CELL_STR ? V_STR : V_INT;
+                    int64_t x = vt == V_STR ? reinterpret_cast<int64_t>(R.strings.data() + cell.v.str_off) : cell.v.i;
+                    rowField(s, vt, x, static_cast<uint32_t>(cell.str_len), sch->types[k]);
+                    if (((k + 1) & 15) == 0) offs.push_back(s.n);
+                }
+            };
+            RowSink cs{nullptr, 0};
+            cord(cs);
+            const int ob = rowOffsetBytes(cs.n);
+            const size_t at = R.tagProps.size();
+            R.tagProps.resize(at + 1 + offs.size() * ob + cs.n);
+            RowSink hs{R.tagProps.data() + at, 0};
+            hs.put(static_cast<uint8_t>(ob - 1));
+            for (uint64_t o : offs) hs.le(o, ob);
+            RowSink ws{R.tagProps.data() + at + hs.n, 0};
+            cord(ws);
+            R.tagPropsOff.push_back(R.tagProps.size());
+            R.tagRowVertex.push_back(static_cast<uint32_t>(v));
+            R.tagRowTag.push_back(t);
+        }
+    }
+}
+
 int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResultHolder& R) {
     DeviceGraph& d = *sp.dev;
     auto failAll = [&](int32_t code) {
@@ -1776,6 +1951,43 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
     }
     const int64_t edgeCap = (q.max_edges_per_vertex > 0 && q.max_edges_per_vertex < INT32_MAX) ? q.max_edges_per_vertex
                                                                                                : INT32_MAX;
+    // response schemas (buildTTLInfoAndRespSchema, QueryBaseProcessor.inl:670-797): per edge type its
+    // return columns but _dst, in request order; per tag its return columns, tags in first-appearance order
+    std::map<int32_t, std::vector<std::pair<int32_t, int32_t>>> respCols;    // type -> (source, field type)
+    std::vector<int32_t> tagOrder;
+    if (q.encode_rows) {
+        for (auto& kv : edgeCols) {
+            std::vector<std::pair<int32_t, int32_t>> rc;
+            HostSchemaView hv{1, kv.first};
+            for (int32_t ci : kv.second) {
+                std::string name = q.cols[ci].name;
+                if (name == "_dst") continue;
+                int32_t src = name == "_src" ? kRcSrc : name == "_rank" ? kRcRank : name == "_type" ? kRcType : ci;
+                int32_t ft = name == "_src" ? T_VID : (name == "_rank" || name == "_type") ? T_INT
+                                                     : sp.edge(std::abs(kv.first))->latest().typeOf(name);
+                rc.push_back({src, ft});
+                hv.names.push_back(name);
+                hv.types.push_back(ft);
+            }
+            if (rc.empty()) continue;
+            if (rc.size() > static_cast<size_t>(kMaxRespCols)) return fail(c, NGX_E_UNSUPPORTED, "too many return columns of one edge type");
+            respCols[kv.first] = rc;
+            addSchema(R, hv);
+        }
+        for (int32_t i = 0; i < q.ncols; i++) {
+            if (q.cols[i].owner != 1 && q.cols[i].owner != 2) continue;
+            if (std::find(tagOrder.begin(), tagOrder.end(), q.cols[i].id) == tagOrder.end()) tagOrder.push_back(q.cols[i].id);
+        }
+        for (int32_t t : tagOrder) {
+            HostSchemaView hv{0, t};
+            for (int32_t i = 0; i < q.ncols; i++) {
+                if ((q.cols[i].owner != 1 && q.cols[i].owner != 2) || q.cols[i].id != t) continue;
+                hv.names.push_back(q.cols[i].name);
+                hv.types.push_back(sp.tag(t)->latest().typeOf(q.cols[i].name));
+            }
+            addSchema(R, hv);
+        }
+    }
     const int64_t now = q.now_sec > 0 ? q.now_sec : static_cast<int64_t>(std::time(nullptr));    // WallClock
     // processed types: edge contexts with props (QueryBoundProcessor.cpp:65-81)
     std::vector<int32_t> types;
@@ -1882,6 +2094,7 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
         a.oRank = c->oRank.get<int64_t>(E);
         a.oType = c->oType.get<int32_t>(E);
         a.oEntry = c->oEntry.get<uint32_t>(E);
+        a.oFlags = q.encode_rows ? c->oFlags.get<uint8_t>(E) : nullptr;
         std::vector<ColSpec> spec(nY, ColSpec{true, true});   // raw value cells: every column typed per row
         prepareCols(c, a, spec, E, 0);
         a.lbStatus = lb;
@@ -1895,6 +2108,7 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
             HIP_OK(hipMemcpyAsync(R.edgeType.data(), a.oType, nrows * 4, hipMemcpyDeviceToHost, c->stream));
             HIP_OK(hipMemcpyAsync(R.edgeDst.data(), a.oDst, nrows * 8, hipMemcpyDeviceToHost, c->stream));
             raw = downloadCells(c, spec, std::vector<int32_t>(nY, T_UNKNOWN), nrows, 0);
+            if (q.encode_rows) encodeEdgeRows(c, a, nrows, respCols, R);
             HIP_OK(hipStreamSynchronize(c->stream));
             // IdAndProp.dst is set only by a `_dst` return column of the edge type (PropsCollector::
             // collectDstId, Collector.h:77-82); without one the reference leaves it 0
@@ -1940,6 +2154,10 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
     }
     R.r.nvertices = static_cast<uint32_t>(nF);
     R.r.nedges = nrows;
+    if (q.encode_rows) {
+        if (R.edgePropsOff.empty()) R.edgePropsOff.assign(nrows + 1, 0);
+        encodeTagRows(q, tagOrder, nF, R);
+    }
     return NGX_OK;
 }
 
@@ -1969,6 +2187,23 @@ extern "C" int32_t ngx_get_neighbors(ngx_ctx* c, const ngx_gn_request* q, ngx_gn
     R->r.vertex_has_tag = R->vertexHasTag.data();
     R->r.strings = R->strings.data();
     R->r.strings_len = R->strings.size();
+    if (q->encode_rows) {
+        R->r.edge_props = R->edgeProps.data();
+        R->r.edge_props_off = R->edgePropsOff.data();
+        for (auto& sc : R->schemas) {
+            sc.cnames.clear();
+            for (auto& n : sc.names) sc.cnames.push_back(n.c_str());
+            R->schemaView.push_back(ngx_schema_def{sc.isEdge, sc.id, static_cast<int32_t>(sc.names.size()),
+                                                   sc.cnames.data(), sc.types.data()});
+        }
+        R->r.nschemas = static_cast<int32_t>(R->schemaView.size());
+        R->r.schemas = R->schemaView.data();
+        R->r.ntag_rows = static_cast<uint32_t>(R->tagRowVertex.size());
+        R->r.tag_row_vertex = R->tagRowVertex.data();
+        R->r.tag_row_tag = R->tagRowTag.data();
+        R->r.tag_props = R->tagProps.data();
+        R->r.tag_props_off = R->tagPropsOff.data();
+    }
     *out = &R.release()->r;
     return rc;
 }

@@ -214,6 +214,7 @@ namespace {
 
 struct Emitter {
     Program& P;
+    int strCasts = 0;                   // (string) casts emitted (each takes one evaluation buffer)
     void emit(uint8_t op, int32_t a = 0, int32_t b = 0, uint8_t t1 = 0, uint8_t t2 = 0, uint8_t mode = 0, int64_t imm = 0) {
         Insn in{};
         in.op = op; in.a = a; in.b = b; in.t1 = t1; in.t2 = t2; in.mode = mode; in.imm = imm;
@@ -256,7 +257,10 @@ int32_t compileCommon(const ExprNode& n, Emitter& em, std::string& err,
             return NGX_OK;
         }
         case K_CAST: {
-            if (n.op == 1) { err = "(string) cast builds a new string: not evaluated on the device"; return NGX_E_UNSUPPORTED; }
+            if (n.op == 1 && ++em.strCasts > kMaxStrCasts) {
+                err = "more (string) casts in one expression than the device evaluator buffers";
+                return NGX_E_UNSUPPORTED;
+            }
             int32_t rc = rec(*n.kids[0]);
             if (rc) return rc;
             em.emit(OP_CAST, 0, 0, n.op);
@@ -466,6 +470,14 @@ int32_t exprType(const ExprNode& n, const Space& sp) {
         }
         default: return T_UNKNOWN;
     }
+}
+
+// a (string) cast at the root of an expression (through unary +): its value is a string built in
+// the evaluation's own buffer, which a YIELD would have to store
+bool builtStringAtRoot(const ExprNode& n) {
+    if (n.kind == K_CAST) return n.op == 1;
+    if (n.kind == K_UNARY && n.op == 0 && !n.kids.empty()) return builtStringAtRoot(*n.kids[0]);
+    return false;
 }
 
 }  // namespace ngx

@@ -82,6 +82,9 @@ struct GraphdCtx {
 int32_t compileStorage(const ExprNode& n, StorageCtx& ctx, Program& out, std::string& err);
 int32_t compileGraphd(const ExprNode& n, GraphdCtx& ctx, Program& out, std::string& err);
 
+// the expression's value may be a string a (string) cast built (not storable as a YIELD column)
+bool builtStringAtRoot(const ExprNode& n);
+
 // TraverseExecutor::calculateExprType (src/graph/TraverseExecutor.cpp:88-165)
 int32_t exprType(const ExprNode& n, const Space& sp);
 

@@ -71,6 +71,7 @@ struct FinalArgs {
     int64_t* oRank;
     int32_t* oType;
     uint32_t* oEntry;                   // frontier index of each row (GetNeighbors), may be null
+    uint8_t* oFlags;                    // EF_* flags of each row's edge (GetNeighbors row encoding), may be null
     const OutCol* oCols;                // nY columns (device array; columns >= kInlineCols read it)
     OutCol oColsIn[kInlineCols];        // the first columns' descriptors, by value (no upload)
     uint64_t* rowsPub;                  // host-mapped [rows, seq] published by the last chunk (GO), or null

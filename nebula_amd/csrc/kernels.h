@@ -65,6 +65,67 @@ constexpr uint64_t kFdMask = (1ULL << kFdShift) - 1;
 int launchCompactDegrees(const uint8_t* visited, uint64_t gbase, uint64_t V, uint8_t epoch, const HopSlots& hs,
                          uint32_t* outF, uint64_t* estart, uint64_t* tileSums, uint64_t* packedTotal, hipStream_t s,
                          Publish pub = Publish{nullptr, 0});
+// Single-pass compaction of an intermediate hop (kernels.hip k_compact_lb): visited[row] == epoch ->
+// next frontier outF, its entries' estart (|F| * hs.n + 1 entries, the last = E) and the next hop's
+// chunk heads chunkFirst (what k_chunk_first computes), in ONE launch: tiles of kTile rows taken by
+// ticket, prefix by decoupled look-back over packed (count << kFdShift | degree) aggregates.
+// status: [0] ticket + one word per tile, zero at launch; the launch clears nextStatus[0 .. nNext)
+// for the launch after it (double buffer, no memset between hops). zero[0 .. nzero): words the next
+// hop's final kernel needs cleared. Requires V < 2^(62 - kFdShift) (look-back words carry 62 bits).
+struct CompactArgs {
+    const uint8_t* visited;             // this shard's rows (visited + gbase)
+    uint64_t V;
+    HopSlots hs;
+    uint32_t* outF;
+    uint64_t* estart;
+    uint64_t* chunkFirst;
+    uint64_t cfCap;                     // entries of chunkFirst (overflow sets err[3])
+    uint64_t* status;
+    uint64_t* nextStatus;
+    uint64_t nNext;
+    uint64_t* total;                    // device copy of the packed total
+    Publish pub;
+    uint64_t* zero;
+    uint32_t nzero;
+    uint32_t* err;
+    uint8_t epoch;
+};
+constexpr uint64_t kCompactLbMaxV = 1ULL << (62 - kFdShift);
+// GO final kernel words: [0] rows reserved (one atomicAdd per chunk), [kDoneOff] chunks finished. Kept
+// 8 KiB apart: two per-chunk atomics on one cache line serialize at the memory side (+300 us/launch).
+// The seed / compaction kernels clear zero[k * kDoneOff] for k < nzero.
+constexpr uint64_t kDoneOff = 1024;
+int launchCompactLb(const CompactArgs& a, hipStream_t s);
+// seed hop variant that also writes chunkFirst (cfCap entries) and clears zero[0 .. nzero)
+int launchSeedFrontierCf(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, const HopSlots& hs,
+                         uint32_t* F, uint64_t* estart, Publish pub, uint64_t* chunkFirst, uint64_t cfCap,
+                         uint64_t* zero, uint32_t nzero, uint32_t* err, hipStream_t s);
+// QueryResponse rows of GetNeighbors (storage.thrift IdAndProp.props): per returned edge, the RowWriter
+// row of its type's response edge schema (QueryBoundProcessor.cpp:38-43 with collectProps,
+// QueryBaseProcessor.inl:325-399). Two launches: write == false stores each row's length in rowLen,
+// write == true writes the bytes at rowOff (the exclusive scan of rowLen).
+constexpr int32_t kRcSrc = -1, kRcRank = -2, kRcType = -3;    // key props of a response column
+constexpr int kMaxRespCols = 128;                             // response columns per edge type
+struct RowEncArgs {
+    uint64_t n;
+    const int32_t* oType;               // signed type per row
+    const int64_t* oSrc;
+    const int64_t* oRank;
+    const uint8_t* oFlags;              // EF_* per row (EF_EMPTY_VALUE: no RowReader), nullptr: none
+    const OutCol* cols;                 // the request's return columns (device array)
+    int32_t nslots;
+    int32_t etype[kMaxSlots];
+    int32_t cbeg[kMaxSlots + 1];        // response columns of slot s: [cbeg[s], cbeg[s + 1])
+    const int32_t* rcSrc;               // request column index, or kRcSrc / kRcRank / kRcType
+    const int32_t* rcType;              // response field type (NGX_T_*)
+    uint64_t* rowLen;
+    const uint64_t* rowOff;
+    uint8_t* out;
+};
+int launchEncodeRows(const RowEncArgs& a, bool write, hipStream_t s);
+// out[0 .. n) = exclusive prefix of in, out[n] = total (3-phase scan, tileSums as launchDegreeScan)
+int launchScanU64(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tileSums, hipStream_t s);
+
 // final hop, one pass (interpreter kernel): a.lbStatus zeroed, ceil(E / kChunk) + 1 words; outputs
 // sized for a.oBase + a.E rows. a.oEntry set (GetNeighbors): rows in edge order, rows written = the
 // inclusive status of the last chunk; else (GO) chunks in completion order, rows written = lbStatus[0]

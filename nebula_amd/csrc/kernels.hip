@@ -20,9 +20,12 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
+#include <algorithm>
 
 #include "kernels.h"
 #include "final_kernels.h"
+#include "rowcodec.h"
 
 namespace ngx {
 
@@ -197,9 +200,22 @@ __global__ void k_index_lookup(const int32_t* qpart, const int64_t* qvid, uint64
     out[i] = vindexFind(idx, qpart[i], qvid[i]);
 }
 
+// chunk heads of entry i (hop edges [e, e + d)): every chunk whose first edge c * CE lies in the range
+__device__ __forceinline__ void writeChunkHeads(uint64_t* cf, uint64_t cap, uint64_t i, uint64_t e, uint64_t d, uint32_t* err) {
+    for (uint64_t c = (e + CE - 1) / CE; c * CE < e + d; c++) {
+        if (c >= cap) { atomicOr(err + 3, 1u); return; }
+        cf[c] = i;
+    }
+}
+
 // 1024 threads; thread t owns seeds [t*per, t*per + per) and their entries (contiguous)
+// CF: also the hop's chunk heads (chunkFirst, k_chunk_first's job) and the words zero[0 .. nzero)
+template <bool CF>
 __global__ __launch_bounds__(1024) void k_seed_frontier(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx,
-                                                        HopSlots hs, uint32_t* F, uint64_t* estart, Publish pub) {
+                                                        HopSlots hs, uint32_t* F, uint64_t* estart, Publish pub,
+                                                        uint64_t* chunkFirst, uint64_t cfCap, uint64_t* zero,
+                                                        uint32_t nzero, uint32_t* err) {
+    if (CF && threadIdx.x < nzero) zero[threadIdx.x * kDoneOff] = 0;
     __shared__ uint64_t sm[1024 / 64 + 1];
     constexpr int kPer = static_cast<int>(kSeedFuseMax / 1024);
     const uint64_t per = (n + 1023) / 1024;
@@ -241,7 +257,10 @@ __global__ __launch_bounds__(1024) void k_seed_frontier(const int32_t* qpart, co
         if (k >= static_cast<int>(per) || i >= n) continue;
         for (int s = 0; s < hs.n; s++) {
             estart[i * hs.n + s] = pre;
-            if (rows[k] != kNoRow) pre += hs.off[s][rows[k] + 1] - hs.off[s][rows[k]];
+            if (rows[k] == kNoRow) continue;
+            uint64_t d = hs.off[s][rows[k] + 1] - hs.off[s][rows[k]];
+            if (CF) writeChunkHeads(chunkFirst, cfCap, i * hs.n + s, pre, d, err);
+            pre += d;
         }
     }
     if (threadIdx.x == 0) {
@@ -274,7 +293,7 @@ __global__ void k_chunk_first(const uint64_t* estart, uint64_t nEnt, uint64_t* c
 template <bool ONE, bool P32, bool MASK>
 __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst,
                                                     uint64_t nEnt, uint64_t E, HopSlots hs, uint8_t* visited,
-                                                    uint8_t epoch, const uint8_t* mask) {
+                                                    uint8_t epoch, const uint8_t* mask, int mode) {
     __shared__ ChunkMap<ONE, false, P32> m;
     // direct-mapped LDS filter of the rows this workgroup already marked: a repeated destination
     // (hubs of a power-law graph) costs an LDS probe instead of another L2 byte-store transaction
@@ -294,8 +313,15 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
             int s = ONE ? 0 : m.slot[q];
             uint64_t pos = P32 ? static_cast<uint64_t>(static_cast<uint32_t>(base + p) + static_cast<uint32_t>(m.pb[q]))
                                : static_cast<uint64_t>(static_cast<int64_t>(base + p) + static_cast<int64_t>(m.pb[q]));
-            g[k] = hs.dgid[s][pos];
+            g[k] = (mode & 1) ? __builtin_nontemporal_load(hs.dgid[s] + pos) : hs.dgid[s][pos];
         }
+    }
+    if (mode & 2) {                                      // already marked: no store
+        uint8_t cur[CITEMS];
+#pragma unroll
+        for (int k = 0; k < CITEMS; k++) cur[k] = g[k] == kNoRow ? epoch : visited[g[k]];
+#pragma unroll
+        for (int k = 0; k < CITEMS; k++) if (cur[k] == epoch) g[k] = kNoRow;
     }
 #pragma unroll
     for (int k = 0; k < CITEMS; k++) {
@@ -304,6 +330,90 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
         if (seen[h] == g[k]) continue;                  // marked by this workgroup already (its store is issued)
         seen[h] = g[k];
         visited[g[k]] = epoch;
+    }
+}
+
+// ------------------------------------------------------------------------------ single-pass compaction
+// visited[row] == epoch -> next frontier + its entries' estart + the next hop's chunk heads, one launch.
+// A tile is kTile rows (16 consecutive rows per thread; one 16-byte load of their marks when the
+// shard's segment of visited[] is 16-byte aligned). The tile's packed (rows << kFdShift | degrees) sum
+// goes through the decoupled look-back of final_kernels.h (tiles by ticket, dispatch order), so the
+// marks and offsets are read once (the 3-phase scan read them twice and took three launches).
+template <bool ONE, bool AL>
+__global__ __launch_bounds__(WG) void k_compact_lb(CompactArgs a) {
+    __shared__ uint64_t sm[NW + 1];
+    __shared__ uint32_t sTile;
+    __shared__ uint64_t sPrefix;
+    if (threadIdx.x == 0) sTile = atomicAdd(reinterpret_cast<uint32_t*>(a.status), 1u);
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * WG;
+    for (uint64_t z = static_cast<uint64_t>(blockIdx.x) * WG + threadIdx.x; z < a.nNext; z += stride) a.nextStatus[z] = 0;
+    __syncthreads();
+    const uint32_t tile = sTile;
+    const uint64_t base = static_cast<uint64_t>(tile) * TILE + static_cast<uint64_t>(threadIdx.x) * ITEMS;
+    uint32_t flags = 0;
+    if (AL && base + ITEMS <= a.V) {
+        const uint4 w = *reinterpret_cast<const uint4*>(a.visited + base);
+        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int k = 0; k < ITEMS; k++) flags |= (((ws[k >> 2] >> (8 * (k & 3))) & 0xFFu) == a.epoch ? 1u : 0u) << k;
+    } else {
+#pragma unroll
+        for (int k = 0; k < ITEMS; k++) flags |= (base + k < a.V && a.visited[base + k] == a.epoch ? 1u : 0u) << k;
+    }
+    const int ns = a.hs.n;
+    uint64_t deg[ONE ? ITEMS : 1];
+    uint64_t dsum = 0;
+#pragma unroll
+    for (int k = 0; k < ITEMS; k++) {
+        if (ONE) deg[k] = 0;
+        if (!(flags >> k & 1u)) continue;
+        const uint64_t r = base + k;
+        if (ONE) {
+            deg[k] = a.hs.off[0][r + 1] - a.hs.off[0][r];
+            dsum += deg[k];
+        } else {
+            for (int s = 0; s < ns; s++) dsum += a.hs.off[s][r + 1] - a.hs.off[s][r];
+        }
+    }
+    const uint64_t v = (static_cast<uint64_t>(__popc(flags)) << kFdShift) | dsum;
+    uint64_t tot;
+    const uint64_t pre = blockExScan(v, tot, sm);
+    if (threadIdx.x < 64) {
+        const uint64_t excl = lookBack(a.status + 1, tile, tot, a.err);
+        if (threadIdx.x == 0) sPrefix = excl;
+    }
+    __syncthreads();
+    const uint64_t excl = sPrefix;
+    const uint64_t at = excl + pre;
+    uint64_t f = at >> kFdShift, e = at & kFdMask;
+#pragma unroll
+    for (int k = 0; k < ITEMS; k++) {
+        if (!(flags >> k & 1u)) continue;
+        const uint64_t r = base + k;
+        a.outF[f] = static_cast<uint32_t>(r);
+        if (ONE) {
+            a.estart[f] = e;
+            writeChunkHeads(a.chunkFirst, a.cfCap, f, e, deg[k], a.err);
+            e += deg[k];
+        } else {
+            for (int s = 0; s < ns; s++) {
+                const uint64_t d = a.hs.off[s][r + 1] - a.hs.off[s][r];
+                a.estart[f * ns + s] = e;
+                writeChunkHeads(a.chunkFirst, a.cfCap, f * ns + s, e, d, a.err);
+                e += d;
+            }
+        }
+        f++;
+    }
+    if (tile == 0 && threadIdx.x < a.nzero) a.zero[threadIdx.x * kDoneOff] = 0;
+    if (tile == gridDim.x - 1 && threadIdx.x == 0) {
+        const uint64_t incl = excl + tot;
+        a.estart[(incl >> kFdShift) * static_cast<uint64_t>(ns)] = incl & kFdMask;
+        *a.total = incl;
+        if (a.pub.slot) {
+            __hip_atomic_store(a.pub.slot, incl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.pub.slot + 1, a.pub.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -400,6 +510,69 @@ __global__ void k_vertex_cells(VertexCellArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------ response rows
+// RowWriter rows of response schemas (rowcodec.h), one thread per returned edge
+// the data part of row i of slot sl; offs gets the block offsets (their count returned in nb)
+__device__ __forceinline__ void rowCord(const RowEncArgs& a, uint64_t i, int sl, RowSink& s, uint64_t* offs, int& nb) {
+    const int b = a.cbeg[sl], nf = a.cbeg[sl + 1] - b;
+    const bool reader = !(a.oFlags != nullptr && (a.oFlags[i] & EF_EMPTY_VALUE));
+    int col = 0;
+    nb = 0;
+    for (int j = 0; j < nf; j++) {
+        const int32_t src = a.rcSrc[b + j];
+        const int32_t ft = a.rcType[b + col];            // the field the next write lands in
+        if (src == kRcSrc) rowField(s, V_INT, a.oSrc[i], 0, ft);
+        else if (src == kRcRank) rowField(s, V_INT, a.oRank[i], 0, ft);
+        else if (src == kRcType) rowField(s, V_INT, a.oType[i], 0, ft);
+        else if (!reader) continue;                      // collectProps without a RowReader: not collected
+        else {
+            const OutCol& oc = a.cols[src];
+            rowField(s, oc.t != nullptr ? oc.t[i] : V_INT, oc.x[i], oc.len != nullptr ? oc.len[i] : 0u, ft);
+        }
+        col++;
+        if ((col & 15) == 0) offs[nb++] = s.n;         // RW_CLEAN_UP_WRITE: every 16 fields written
+    }
+    for (int k = col; k < nf; k++) {                    // encode(): Skip the fields never written
+        rowDefault(s, a.rcType[b + k]);
+        if (k != 0 && (k & 15) == 0) offs[nb++] = s.n;  // Skip's own block check (on the field index)
+    }
+}
+
+__global__ void k_encode_rows(RowEncArgs a, int write) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    int sl = -1;
+    for (int s = 0; s < a.nslots; s++) if (a.etype[s] == a.oType[i]) sl = s;
+    if (sl < 0 || a.cbeg[sl + 1] == a.cbeg[sl]) {        // onlyStructure type: no props
+        if (!write) a.rowLen[i] = 0;
+        return;
+    }
+    uint64_t offs[kMaxRespCols / 16 + 2];
+    int nb = 0;
+    RowSink cs{nullptr, 0};
+    rowCord(a, i, sl, cs, offs, nb);
+    const int ob = rowOffsetBytes(cs.n);
+    if (!write) {
+        a.rowLen[i] = 1 + static_cast<uint64_t>(nb) * ob + cs.n;
+        return;
+    }
+    uint8_t* dst = a.out + a.rowOff[i];
+    RowSink hs{dst, 0};
+    hs.put(static_cast<uint8_t>(ob - 1));
+    for (int k = 0; k < nb; k++) hs.le(offs[k], ob);
+    RowSink ws{dst + hs.n, 0};
+    rowCord(a, i, sl, ws, offs, nb);
+}
+
+struct ArrIn {
+    const uint64_t* v;
+    __device__ __forceinline__ uint64_t operator()(uint64_t i) const { return v[i]; }
+};
+struct WriteArr {
+    uint64_t* out;
+    __device__ __forceinline__ void operator()(uint64_t i, uint64_t v, uint64_t pre) const { (void)v; out[i] = pre; }
+};
+
 // ------------------------------------------------------------------------------ multi-GPU exchange
 // pack this shard's marks for peer q's rows into a bitmap: one row byte per lane (coalesced), the
 // wave's ballot is the 64-bit word of its 64 rows; merge received bitmaps into visited
@@ -438,7 +611,17 @@ int launchDegreeScan(const uint32_t* F, uint64_t nEnt, const HopSlots& hs, uint6
 int launchSeedFrontier(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, const HopSlots& hs,
                        uint32_t* F, uint64_t* estart, Publish pub, hipStream_t s) {
     if (n * static_cast<uint64_t>(hs.n) > kSeedFuseMax || n > kSeedFuseMax || idx.slots == nullptr) return 1;
-    hipLaunchKernelGGL(k_seed_frontier, dim3(1), dim3(1024), 0, s, qpart, qvid, n, idx, hs, F, estart, pub);
+    hipLaunchKernelGGL(k_seed_frontier<false>, dim3(1), dim3(1024), 0, s, qpart, qvid, n, idx, hs, F, estart, pub,
+                       nullptr, 0, nullptr, 0u, nullptr);
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchSeedFrontierCf(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, const HopSlots& hs,
+                         uint32_t* F, uint64_t* estart, Publish pub, uint64_t* chunkFirst, uint64_t cfCap,
+                         uint64_t* zero, uint32_t nzero, uint32_t* err, hipStream_t s) {
+    if (n * static_cast<uint64_t>(hs.n) > kSeedFuseMax || n > kSeedFuseMax || idx.slots == nullptr || nzero > 1024) return 1;
+    hipLaunchKernelGGL(k_seed_frontier<true>, dim3(1), dim3(1024), 0, s, qpart, qvid, n, idx, hs, F, estart, pub,
+                       chunkFirst, cfCap, zero, nzero, err);
     return static_cast<int>(hipGetLastError());
 }
 
@@ -455,8 +638,9 @@ int launchExpandMark(const uint32_t* F, const uint64_t* estart, const uint64_t* 
                      const HopSlots& hs, uint8_t* visited, uint8_t epoch, bool pos32, hipStream_t s, const uint8_t* mask) {
     if (E == 0) return 0;
     dim3 grid(static_cast<unsigned>((E + CE - 1) / CE));
+    static const int mode = getenv("NGX_EXPAND_MODE") ? atoi(getenv("NGX_EXPAND_MODE")) : 0;
 #define NGX_EXPAND(ONE, P32, MASK) hipLaunchKernelGGL((k_expand_mark<ONE, P32, MASK>), grid, dim3(WG), 0, s, F, estart, \
-                                                    chunkFirst, nEnt, E, hs, visited, epoch, mask)
+                                                    chunkFirst, nEnt, E, hs, visited, epoch, mask, mode)
     if (mask) {
         if (hs.n == 1) NGX_EXPAND(true, false, true);
         else NGX_EXPAND(false, false, true);
@@ -492,6 +676,31 @@ int launchCompactDegrees(const uint8_t* visited, uint64_t gbase, uint64_t V, uin
                          Publish pub) {
     return scan3(FlagDegIn{visited, gbase, epoch, hs}, V, WriteCompactEstart{outF, estart, hs}, tileSums, packedTotal,
                  s, estart, hs.n, pub);
+}
+
+int launchCompactLb(const CompactArgs& a, hipStream_t s) {
+    if (a.V >= kCompactLbMaxV || a.nzero > WG) return 1;
+    const uint64_t nt = std::max<uint64_t>((a.V + TILE - 1) / TILE, 1);
+    const bool al = (reinterpret_cast<uintptr_t>(a.visited) & 15) == 0;
+    dim3 grid(static_cast<unsigned>(nt));
+    if (a.hs.n == 1) {
+        if (al) hipLaunchKernelGGL((k_compact_lb<true, true>), grid, dim3(WG), 0, s, a);
+        else hipLaunchKernelGGL((k_compact_lb<true, false>), grid, dim3(WG), 0, s, a);
+    } else {
+        if (al) hipLaunchKernelGGL((k_compact_lb<false, true>), grid, dim3(WG), 0, s, a);
+        else hipLaunchKernelGGL((k_compact_lb<false, false>), grid, dim3(WG), 0, s, a);
+    }
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchEncodeRows(const RowEncArgs& a, bool write, hipStream_t s) {
+    if (a.n == 0) return 0;
+    hipLaunchKernelGGL(k_encode_rows, dim3(static_cast<unsigned>((a.n + 255) / 256)), dim3(256), 0, s, a, write ? 1 : 0);
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchScanU64(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tileSums, hipStream_t s) {
+    return scan3(ArrIn{in}, n, WriteArr{out}, tileSums, out + n, s);
 }
 
 int launchFinal(const FinalArgs& a, hipStream_t s) {

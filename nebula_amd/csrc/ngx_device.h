@@ -12,6 +12,8 @@ namespace ngx {
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 constexpr int kMaxSlots = 16;
 constexpr int kMaxStack = 12;
+constexpr int kStrCastBytes = 24;           // buffer of one (string) cast (vm.h castToString)
+constexpr int kMaxStrCasts = 4;             // (string) casts per program (exprc.cpp refuses more)
 
 // per-edge flags (HostSlot::eflags)
 enum : uint8_t {

@@ -305,6 +305,34 @@ __device__ __forceinline__ Val opCast(Val v, uint8_t t1, const VmEnv& env) {
     return mkBool(asBool(v));
 }
 
+// (string) cast, Expression::toString (Expressions.h:334-348), into a 24-byte buffer of the
+// evaluation (the caller's private memory: a WHERE / pushed filter consumes the string before the
+// program returns; a YIELD whose value is such a string is refused at compile time). int64 prints as
+// folly::to<std::string> (decimal, '-' sign), bool as "true" / "false"; a double needs folly's
+// shortest round-trip form: host only.
+__device__ __forceinline__ Val castToString(Val v, char* buf, const VmEnv& env) {
+    if (v.t == V_ERR || v.t == V_STR) return v;
+    uint32_t n = 0;
+    if (v.t == V_BOOL) {
+        const char* w = v.x ? "true" : "false";
+        for (; w[n]; n++) buf[n] = w[n];
+    } else if (v.t == V_INT) {
+        uint64_t u = v.x < 0 ? 0ULL - static_cast<uint64_t>(v.x) : static_cast<uint64_t>(v.x);
+        uint32_t digits = 1;
+        for (uint64_t t = u; t >= 10; t /= 10) digits++;
+        if (v.x < 0) buf[n++] = '-';
+        for (uint32_t k = digits; k > 0; k--) {
+            buf[n + k - 1] = static_cast<char>('0' + u % 10);
+            u /= 10;
+        }
+        n += digits;
+    } else {
+        atomicOr(env.unsupported, 1u);
+        return mkErr();
+    }
+    return Val{reinterpret_cast<int64_t>(buf), n, V_STR};
+}
+
 // ------------------------------------------------------------------------------ arithmetic
 __device__ __forceinline__ Val opArith(uint8_t op, Val l, Val r, const VmEnv& env) {
     if (l.t == V_ERR) return l;
@@ -457,7 +485,8 @@ __device__ __forceinline__ Val opFunc(int32_t fid, const Val* args, int argc, co
 // ------------------------------------------------------------------------------ interpreter
 static __device__ __noinline__ Val vmEval(const Insn* code, const VmEnv& env, const EdgeCtx& ec) {
     Val st[kMaxStack];
-    int sp = 0;
+    char sbuf[kMaxStrCasts][kStrCastBytes];
+    int sp = 0, nsb = 0;
     for (int pc = 0;; pc++) {
         const Insn in = code[pc];
         switch (in.op) {
@@ -474,7 +503,10 @@ static __device__ __noinline__ Val vmEval(const Insn* code, const VmEnv& env, co
             case OP_PLUS: break;
             case OP_NEG: st[sp - 1] = opNeg(st[sp - 1]); break;
             case OP_NOT: st[sp - 1] = opNot(st[sp - 1]); break;
-            case OP_CAST: st[sp - 1] = opCast(st[sp - 1], in.t1, env); break;
+            case OP_CAST:
+                if (in.t1 == 1) st[sp - 1] = nsb < kMaxStrCasts ? castToString(st[sp - 1], sbuf[nsb++], env) : mkErr();
+                else st[sp - 1] = opCast(st[sp - 1], in.t1, env);
+                break;
             case OP_ADD: case OP_SUB: case OP_MUL: case OP_DIV: case OP_MOD: case OP_AXOR:
                 sp--; st[sp - 1] = opArith(in.op, st[sp - 1], st[sp], env); break;
             case OP_LT: case OP_LE: case OP_GT: case OP_GE: case OP_EQ: case OP_NE: case OP_CONTAINS:

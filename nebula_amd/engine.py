@@ -73,14 +73,22 @@ class GnRequest(ctypes.Structure):
     _fields_ = [("space", c_i32), ("nparts", c_i32), ("parts", P(c_i32)), ("part_nvids", P(c_u32)),
                 ("vids", P(c_i64)), ("nedge_types", c_i32), ("edge_types", P(c_i32)), ("filter", ctypes.c_char_p),
                 ("filter_len", c_u32), ("ncols", c_i32), ("cols", P(PropDef)), ("max_edges_per_vertex", c_i32),
-                ("now_sec", c_i64)]
+                ("now_sec", c_i64), ("encode_rows", c_i32)]
+
+
+class SchemaDefC(ctypes.Structure):
+    _fields_ = [("is_edge", c_i32), ("id", c_i32), ("ncols", c_i32), ("names", P(ctypes.c_char_p)),
+                ("types", P(c_i32))]
 
 
 class GnResult(ctypes.Structure):
     _fields_ = [("code", c_i32), ("nfailed", c_i32), ("failed_codes", P(c_i32)), ("nedges", c_u64),
                 ("edge_vertex", P(c_u32)), ("edge_type", P(c_i32)), ("edge_dst", P(c_i64)), ("ncols", c_i32),
                 ("edge_cells", P(Cell)), ("nvertices", c_u32), ("vertex_cells", P(Cell)),
-                ("vertex_has_tag", P(ctypes.c_uint8)), ("strings", ctypes.c_void_p), ("strings_len", c_u64)]
+                ("vertex_has_tag", P(ctypes.c_uint8)), ("strings", ctypes.c_void_p), ("strings_len", c_u64),
+                ("edge_props", ctypes.c_void_p), ("edge_props_off", P(c_u64)), ("nschemas", c_i32),
+                ("schemas", P(SchemaDefC)), ("ntag_rows", c_u32), ("tag_row_vertex", P(c_u32)),
+                ("tag_row_tag", P(c_i32)), ("tag_props", ctypes.c_void_p), ("tag_props_off", P(c_u64))]
 
 
 class GoPlan(ctypes.Structure):
@@ -253,6 +261,11 @@ class NeighborsResult:
     edge_cells: List[tuple]
     vertex_cells: List[tuple]
     vertex_has_tag: np.ndarray
+    # encode_rows: the QueryResponse payload (RowWriter rows, schemas)
+    edge_props: Optional[List[bytes]] = None           # IdAndProp.props per returned edge
+    edge_schema: Optional[dict] = None                 # signed type -> [(name, type)]
+    vertex_schema: Optional[dict] = None               # tag id -> [(name, type)]
+    tag_rows: Optional[List[Tuple[int, int, bytes]]] = None   # (request vid index, tag id, TagData.data)
 
 
 def _arr(ptr, n, dtype):
@@ -324,7 +337,8 @@ class Engine:
     # ---- GetNeighbors
     def get_neighbors(self, space, parts: Sequence[Tuple[int, Sequence[int]]], edge_types: Optional[Sequence[int]],
                       return_columns: Sequence[Tuple[int, int, str]], filter_bytes: bytes = b"",
-                      max_edges_per_vertex: int = 2**31 - 1, now_sec: int = 0) -> NeighborsResult:
+                      max_edges_per_vertex: int = 2**31 - 1, now_sec: int = 0,
+                      encode_rows: bool = False) -> NeighborsResult:
         pid = np.array([p for p, _ in parts], dtype=np.int32)
         nv = np.array([len(v) for _, v in parts], dtype=np.uint32)
         vids = np.array([x for _, v in parts for x in v], dtype=np.int64)
@@ -332,7 +346,8 @@ class Engine:
         cols = (PropDef * max(1, len(return_columns)))(*[PropDef(o, i, n.encode()) for o, i, n in return_columns])
         req = GnRequest(space, len(parts), pid.ctypes.data_as(P(c_i32)), nv.ctypes.data_as(P(c_u32)),
                         vids.ctypes.data_as(P(c_i64)), len(et), et.ctypes.data_as(P(c_i32)), filter_bytes,
-                        len(filter_bytes), len(return_columns), cols, max_edges_per_vertex, now_sec)
+                        len(filter_bytes), len(return_columns), cols, max_edges_per_vertex, now_sec,
+                        1 if encode_rows else 0)
         out = P(GnResult)()
         rc = self.L.ngx_get_neighbors(self.h, ctypes.byref(req), ctypes.byref(out))
         try:
@@ -342,13 +357,28 @@ class Engine:
             failed = [(r.failed_codes[2 * i], r.failed_codes[2 * i + 1]) for i in range(r.nfailed)]
             strings = ctypes.string_at(r.strings, r.strings_len) if r.strings_len else b""
             nc = r.ncols
+            enc = {}
+            if encode_rows:
+                off = _arr(r.edge_props_off, r.nedges + 1, np.uint64)
+                blob = ctypes.string_at(r.edge_props, int(off[-1])) if r.nedges and off[-1] else b""
+                enc["edge_props"] = [blob[int(off[i]):int(off[i + 1])] for i in range(r.nedges)]
+                es, vs = {}, {}
+                for k in range(r.nschemas):
+                    sd = r.schemas[k]
+                    cols_ = [(sd.names[j].decode(), sd.types[j]) for j in range(sd.ncols)]
+                    (es if sd.is_edge else vs)[sd.id] = cols_
+                enc["edge_schema"], enc["vertex_schema"] = es, vs
+                toff = _arr(r.tag_props_off, r.ntag_rows + 1, np.uint64)
+                tblob = ctypes.string_at(r.tag_props, int(toff[-1])) if r.ntag_rows and toff[-1] else b""
+                enc["tag_rows"] = [(int(r.tag_row_vertex[k]), int(r.tag_row_tag[k]), tblob[int(toff[k]):int(toff[k + 1])])
+                                   for k in range(r.ntag_rows)]
             return NeighborsResult(
                 code=r.code, failed_codes=failed, total_edges=r.nedges,
                 edge_vertex=_arr(r.edge_vertex, r.nedges, np.uint32), edge_type=_arr(r.edge_type, r.nedges, np.int32),
                 edge_dst=_arr(r.edge_dst, r.nedges, np.int64),
                 edge_cells=_cells(r.edge_cells, r.nedges, nc, strings),
                 vertex_cells=_cells(r.vertex_cells, r.nvertices, nc, strings),
-                vertex_has_tag=_arr(r.vertex_has_tag, r.nvertices * nc, np.uint8))
+                vertex_has_tag=_arr(r.vertex_has_tag, r.nvertices * nc, np.uint8), **enc)
         finally:
             self.L.ngx_gn_result_free(out)
 

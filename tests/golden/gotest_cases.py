@@ -7,6 +7,29 @@ expected row stand for that vid. Rows are compared sorted, as verifyResult does
 (src/graph/test/TestBase.h:188-233). "empty": the response had no rows.
 """
 
+RK = ("T:Mavericks",), ("T:Kings",), ("T:Bulls",)
+MTON_PROPS = [("P:Manu Ginobili", 95, "Manu Ginobili"), ("P:LaMarcus Aldridge", 90, "LaMarcus Aldridge"),
+              ("P:Tim Duncan", 95, "Tim Duncan"), ("P:Tony Parker", 95, "Tony Parker"),
+              ("P:Tony Parker", 75, "Tony Parker"), ("P:Tim Duncan", 75, "Tim Duncan"),
+              ("P:Tim Duncan", 90, "Tim Duncan")]
+MTON_REV = [("P:Tim Duncan",), ("P:LaMarcus Aldridge",), ("P:Marco Belinelli",), ("P:Boris Diaw",),
+            ("P:Dejounte Murray",), ("P:Tony Parker",), ("P:Manu Ginobili",), ("P:Danny Green",),
+            ("P:Aron Baynes",), ("P:Tiago Splitter",), ("P:Shaquile O'Neal",), ("P:Rudy Gay",),
+            ("P:Damian Lillard",)]
+MTON_SPURS = [("P:" + n,) for n in (
+    "Tim Duncan", "Tony Parker", "Manu Ginobili", "LaMarcus Aldridge", "Rudy Gay", "Marco Belinelli",
+    "Danny Green", "Kyle Anderson", "Aron Baynes", "Boris Diaw", "Tiago Splitter", "Cory Joseph", "David West",
+    "Jonathon Simmons", "Dejounte Murray", "Tracy McGrady", "Paul Gasol", "Marco Belinelli")]
+MTON_BI = MTON_REV + [("P:" + n,) for n in (
+    "LeBron James", "Russell Westbrook", "Chris Paul", "Kyle Anderson", "Kevin Durant", "James Harden")]
+MTON_STAR = [("T:Thunders", 0), (0, "P:Paul George"), (0, "P:James Harden"), ("T:Pacers", 0), ("T:Thunders", 0),
+             (0, "P:Russell Westbrook"), ("T:Thunders", 0), ("T:Rockets", 0), (0, "P:Russell Westbrook")]
+MTON_STAR_PROPS = [("T:Thunders", 0, 2008, 0, ""), (0, "P:Paul George", 0, 90, "Paul George"),
+                   (0, "P:James Harden", 0, 90, "James Harden"), ("T:Pacers", 0, 2010, 0, ""),
+                   ("T:Thunders", 0, 2017, 0, ""), (0, "P:Russell Westbrook", 0, 95, "Russell Westbrook"),
+                   ("T:Thunders", 0, 2009, 0, ""), ("T:Rockets", 0, 2012, 0, ""),
+                   (0, "P:Russell Westbrook", 0, 80, "Russell Westbrook")]
+
 CASES = [
     # OneStepOutBound (GoTest.cpp:35-168)
     dict(line=37, query="GO FROM {P:Tim Duncan} OVER serve", rows=[("T:Spurs",)]),
@@ -126,4 +149,175 @@ CASES = [
                           '$$.team.name == "Kings")&& serve.start_year > 2013',
          pushdown="(true&&(serve.start_year>2013))",
          rows=[("T:Mavericks",), ("T:Kings",), ("T:Bulls",)]),
+    # FilterPushdown, rest of the section (:1751-2275; the $-.id pipe case at :2061 is out of scope)
+    dict(line=1754, query='GO FROM {P:Rajon Rondo} OVER serve WHERE $$.team.name == "Celtics" || $$.team.name == "Kings"',
+         pushdown=None, rows=[("T:Celtics",), ("T:Kings",)]),
+    dict(line=1779, query='GO FROM {P:Rajon Rondo} OVER serve WHERE serve.start_year > 2013 && serve.end_year < 2018 '
+                          '&& $$.team.name == "Kings"',
+         pushdown="(((serve.start_year>2013)&&(serve.end_year<2018))&&true)", rows=[("T:Kings",)]),
+    dict(line=1804, query='GO FROM {P:Rajon Rondo} OVER serve WHERE serve.start_year > 2013 && $$.team.name == "Kings" '
+                          '&& serve.end_year < 2018',
+         pushdown="(((serve.start_year>2013)&&true)&&(serve.end_year<2018))", rows=[("T:Kings",)]),
+    dict(line=1830, query='GO FROM {P:Rajon Rondo} OVER serve WHERE $$.team.name == "Kings" && serve.start_year > 2013 '
+                          '&& serve.end_year < 2018',
+         pushdown="((true&&(serve.start_year>2013))&&(serve.end_year<2018))", rows=[("T:Kings",)]),
+    dict(line=1857, query="GO FROM {P:Rajon Rondo} OVER serve WHERE serve.start_year == 2013 "
+                          "OR serve.start_year > 2013 && serve.end_year < 2018",
+         pushdown="((serve.start_year==2013)||((serve.start_year>2013)&&(serve.end_year<2018)))", rows=list(RK)),
+    dict(line=1886, query="GO FROM {P:Rajon Rondo} OVER serve WHERE serve.start_year > 2013 && serve.end_year <= 2015 "
+                          "OR serve.start_year >= 2015 && serve.end_year < 2018",
+         pushdown="(((serve.start_year>2013)&&(serve.end_year<=2015))||((serve.start_year>=2015)&&(serve.end_year<2018)))",
+         rows=list(RK)),
+    dict(line=1916, query='GO FROM {P:Rajon Rondo} OVER serve WHERE serve.start_year > 2013 && serve.end_year <= 2015 '
+                          '&& $$.team.name == "Mavericks" OR serve.start_year >= 2015 && serve.end_year < 2018',
+         pushdown="((((serve.start_year>2013)&&(serve.end_year<=2015))&&true)"
+                  "||((serve.start_year>=2015)&&(serve.end_year<2018)))", rows=list(RK)),
+    dict(line=1946, query='GO FROM {P:Rajon Rondo} OVER serve WHERE $$.team.name == "Pelicans" '
+                          'OR serve.start_year > 2013 && serve.end_year < 2018',
+         pushdown=None, rows=list(RK) + [("T:Pelicans",)]),
+    dict(line=1975, query='GO FROM {P:Rajon Rondo} OVER serve WHERE $$.team.name == "Pelicans" '
+                          'OR serve.start_year > 2013 && serve.end_year <= 2015 '
+                          'OR serve.start_year >= 2015 && serve.end_year < 2018',
+         pushdown=None, rows=list(RK) + [("T:Pelicans",)]),
+    dict(line=2006, query="GO FROM {P:Rajon Rondo} OVER serve WHERE serve.start_year > 2013 && serve.end_year <= 2015 "
+                          "XOR serve.start_year >= 2015 && serve.end_year < 2018",
+         pushdown="(((serve.start_year>2013)&&(serve.end_year<=2015))XOR((serve.start_year>=2015)&&(serve.end_year<2018)))",
+         rows=list(RK)),
+    dict(line=2035, query='GO FROM {P:Rajon Rondo} OVER serve WHERE serve.start_year > 2013 && serve.end_year <= 2015 '
+                          '&& $$.team.name == "Mavericks" XOR serve.start_year >= 2015 && serve.end_year < 2018',
+         pushdown=None, rows=list(RK)),
+    dict(line=2090, query="GO FROM {P:Tim Duncan} OVER serve WHERE serve._src == {P:Tim Duncan} && serve._rank == 0 "
+                          "&& serve._dst == {T:Spurs} YIELD serve._dst AS id",
+         pushdown="(((serve._src==5662213458193308137)&&(serve._rank==0))&&(serve._dst==7193291116733635180))",
+         rows=[("T:Spurs",)]),
+    dict(line=2116, query="GO FROM {P:Rajon Rondo} OVER serve WHERE udf_is_in(serve._dst, 1, 2, 3)",
+         pushdown="udf_is_in(serve._dst,1,2,3)", empty=True),
+    dict(line=2137, query="GO FROM {P:Rajon Rondo} OVER serve WHERE udf_is_in(serve._dst, {T:Celtics}, 2, 3)",
+         pushdown="udf_is_in(serve._dst,{T:Celtics},2,3)", rows=[("T:Celtics",)]),
+    dict(line=2161, query='GO FROM {P:Rajon Rondo} OVER serve WHERE udf_is_in("test", $$.team.name)',
+         pushdown=None, empty=True),
+    dict(line=2182, query='GO FROM {P:Tim Duncan} OVER serve WHERE udf_is_in($^.player.name, "Tim Duncan")',
+         pushdown="udf_is_in($^.player.name,Tim Duncan)", rows=[("T:Spurs",)]),
+    dict(line=2205, query='GO FROM {P:Tim Duncan} OVER serve WHERE !udf_is_in($^.player.name, "Tim Duncan")',
+         pushdown="!(udf_is_in($^.player.name,Tim Duncan))", empty=True),
+    dict(line=2228, query="GO FROM {P:Boris Diaw} OVER serve WHERE $$.team.name CONTAINS Haw "
+                          "YIELD $^.player.name, serve.start_year, serve.end_year, $$.team.name",
+         pushdown=None, rows=[("Boris Diaw", 2003, 2005, "Hawks")]),
+    dict(line=2253, query='GO FROM {P:Boris Diaw} OVER serve WHERE (string)serve.start_year CONTAINS "05" '
+                          '&& $^.player.name CONTAINS "Boris" '
+                          'YIELD $^.player.name, serve.start_year, serve.end_year, $$.team.name',
+         pushdown="(((string)serve.start_year CONTAINS 05)&&($^.player.name CONTAINS Boris))",
+         rows=[("Boris Diaw", 2005, 2008, "Suns")]),
+    # DuplicateColumnName (:2279-2297)
+    dict(line=2282, query="GO FROM {P:Tim Duncan} OVER serve YIELD serve._dst, serve._dst", rows=[("T:Spurs", "T:Spurs")]),
+    # Contains (:2308-2401)
+    dict(line=2312, query="GO FROM {P:Boris Diaw} OVER serve WHERE $$.team.name CONTAINS Haw "
+                          "YIELD $^.player.name, serve.start_year, serve.end_year, $$.team.name",
+         rows=[("Boris Diaw", 2003, 2005, "Hawks")]),
+    dict(line=2332, query='GO FROM {P:Boris Diaw} OVER serve WHERE (string)serve.start_year CONTAINS "05" '
+                          'YIELD $^.player.name, serve.start_year, serve.end_year, $$.team.name',
+         rows=[("Boris Diaw", 2005, 2008, "Suns")]),
+    dict(line=2352, query='GO FROM {P:Boris Diaw} OVER serve WHERE $^.player.name CONTAINS "Boris" '
+                          'YIELD $^.player.name, serve.start_year, serve.end_year, $$.team.name',
+         rows=[("Boris Diaw", 2003, 2005, "Hawks"), ("Boris Diaw", 2005, 2008, "Suns"),
+               ("Boris Diaw", 2008, 2012, "Hornets"), ("Boris Diaw", 2012, 2016, "Spurs"),
+               ("Boris Diaw", 2016, 2017, "Jazz")]),
+    dict(line=2376, query='GO FROM {P:Boris Diaw} OVER serve WHERE !($^.player.name CONTAINS "Boris") '
+                          'YIELD $^.player.name, serve.start_year, serve.end_year, $$.team.name', empty=True),
+    dict(line=2390, query='GO FROM {P:Boris Diaw} OVER serve WHERE "Leo" CONTAINS "Boris" '
+                          'YIELD $^.player.name, serve.start_year, serve.end_year, $$.team.name', empty=True),
+    # WithIntermediateData: GO M TO N STEPS (:2403-2841; the two REVERSELY over * blocks at :2808-2841
+    # assert nothing and are left out)
+    dict(line=2408, query="GO 0 TO 0 STEPS FROM {P:Tony Parker} OVER like YIELD DISTINCT like._dst", empty=True),
+    dict(line=2421, query="GO 1 TO 2 STEPS FROM {P:Tony Parker} OVER like YIELD DISTINCT like._dst",
+         rows=[("P:Tony Parker",), ("P:Manu Ginobili",), ("P:LaMarcus Aldridge",), ("P:Tim Duncan",)]),
+    dict(line=2437, query="GO 0 TO 2 STEPS FROM {P:Tony Parker} OVER like YIELD DISTINCT like._dst",
+         rows=[("P:Tony Parker",), ("P:Manu Ginobili",), ("P:LaMarcus Aldridge",), ("P:Tim Duncan",)]),
+    dict(line=2454, query="GO 1 TO 2 STEPS FROM {P:Tony Parker} OVER like "
+                          "YIELD DISTINCT like._dst, like.likeness, $$.player.name",
+         rows=MTON_PROPS),
+    dict(line=2474, query="GO 0 TO 2 STEPS FROM {P:Tony Parker} OVER like "
+                          "YIELD DISTINCT like._dst, like.likeness, $$.player.name",
+         rows=MTON_PROPS),
+    dict(line=2494, query="GO 1 TO 3 STEPS FROM {P:Tim Duncan} OVER serve", rows=[("T:Spurs",)]),
+    dict(line=2506, query="GO 0 TO 3 STEPS FROM {P:Tim Duncan} OVER serve", rows=[("T:Spurs",)]),
+    dict(line=2518, query="GO 2 TO 3 STEPS FROM {P:Tim Duncan} OVER serve", empty=True),
+    dict(line=2532, query="GO 1 TO 2 STEPS FROM {P:Tony Parker} OVER like REVERSELY YIELD DISTINCT like._dst",
+         rows=MTON_REV),
+    dict(line=2556, query="GO 0 TO 2 STEPS FROM {P:Tony Parker} OVER like REVERSELY YIELD DISTINCT like._dst",
+         rows=MTON_REV),
+    dict(line=2580, query="GO 2 TO 2 STEPS FROM {P:Tony Parker} OVER like REVERSELY YIELD DISTINCT like._dst",
+         rows=MTON_REV[1:]),
+    dict(line=2603, query="GO 1 TO 3 STEPS FROM {T:Spurs} OVER serve REVERSELY", rows=MTON_SPURS),
+    dict(line=2632, query="GO 0 TO 3 STEPS FROM {T:Spurs} OVER serve REVERSELY", rows=MTON_SPURS),
+    dict(line=2664, query="GO 1 TO 2 STEPS FROM {P:Tony Parker} OVER like BIDIRECT YIELD DISTINCT like._dst",
+         rows=MTON_BI),
+    dict(line=2695, query="GO 0 TO 2 STEPS FROM {P:Tony Parker} OVER like BIDIRECT YIELD DISTINCT like._dst",
+         rows=MTON_BI),
+    dict(line=2727, query="GO 1 TO 2 STEPS FROM {P:Russell Westbrook} OVER * YIELD serve._dst, like._dst",
+         rows=MTON_STAR),
+    dict(line=2747, query="GO 0 TO 2 STEPS FROM {P:Russell Westbrook} OVER * YIELD serve._dst, like._dst",
+         rows=MTON_STAR),
+    dict(line=2768, query="GO 1 TO 2 STEPS FROM {P:Russell Westbrook} OVER * "
+                          "YIELD serve._dst, like._dst, serve.start_year, like.likeness, $$.player.name",
+         rows=MTON_STAR_PROPS),
+    dict(line=2789, query="GO 0 TO 2 STEPS FROM {P:Russell Westbrook} OVER * "
+                          "YIELD serve._dst, like._dst, serve.start_year, like.likeness, $$.player.name",
+         rows=MTON_STAR_PROPS),
+    # ErrorMsg (:2844-2854): a team vertex has no player tag -> default ""
+    dict(line=2847, query="GO FROM {P:Tim Duncan} OVER serve YIELD $$.player.name as name", rows=[("",)]),
+    # ZeroStep (:2856-2883)
+    dict(line=2862, query="GO 0 STEPS FROM {P:Tim Duncan} OVER serve BIDIRECT", empty=True),
+    dict(line=2874, query="GO 0 STEPS FROM {P:Tim Duncan} OVER serve", empty=True),
+    # VertexNotExist (:343-381): no rows at all
+    dict(line=357, query="GO FROM hash('NON EXIST VERTEX ID') OVER serve", empty=True),
+    dict(line=365, query="GO FROM hash('NON EXIST VERTEX ID') OVER serve YIELD "
+                         "$^.player.name, serve.start_year, serve.end_year, $$.team.name", empty=True),
+    dict(line=374, query="GO FROM hash('NON EXIST VERTEX ID') OVER serve YIELD DISTINCT "
+                         "$^.player.name, serve.start_year, serve.end_year, $$.team.name", empty=True),
+    # NonexistentProp (:878-900): E_EXECUTION_ERROR
+    dict(line=881, query="GO FROM {P:Tim Duncan} OVER serve YIELD $^.player.test", error=True),
+    dict(line=888, query="GO FROM {P:Tim Duncan} OVER serve yield $^.player.test", error=True),
+    dict(line=895, query="GO FROM {P:Tim Duncan} OVER serve YIELD serve.test", error=True),
+    # is_inCall (:902-923; the two $-.id pipe cases are out of scope)
+    dict(line=906, query='GO FROM {P:Boris Diaw} OVER serve WHERE udf_is_in($$.team.name, "Hawks", "Suns") '
+                         'YIELD $^.player.name, serve.start_year, serve.end_year, $$.team.name',
+         rows=[("Boris Diaw", 2003, 2005, "Hawks"), ("Boris Diaw", 2005, 2008, "Suns")]),
+    # OneStepOutBound (:97-115)
+    dict(line=97, query="GO FROM {P:Rajon Rondo} OVER serve WHERE serve.start_year >= 2013 && serve.end_year <= 2018 "
+                        "YIELD $^.player.name, serve.start_year, serve.end_year, $$.team.name",
+         rows=[("Rajon Rondo", 2014, 2015, "Mavericks"), ("Rajon Rondo", 2015, 2016, "Kings"),
+               ("Rajon Rondo", 2016, 2017, "Bulls"), ("Rajon Rondo", 2017, 2018, "Pelicans")]),
+    # MULTI_EDGES, rest (:466-660; the pipe cases at :662-702 are out of scope)
+    dict(line=468, query="GO FROM {P:Russell Westbrook} OVER serve, like REVERSELY YIELD serve._src, like._src",
+         rows=[(0, "P:Russell Westbrook")] * 3),
+    dict(line=482, query="GO FROM {P:Russell Westbrook} OVER serve, like REVERSELY",
+         rows=[(0, "P:James Harden"), (0, "P:Dejounte Murray"), (0, "P:Paul George")]),
+    dict(line=496, query="GO FROM {P:Russell Westbrook} OVER * REVERSELY YIELD serve._dst, like._dst",
+         rows=[(0, "P:James Harden"), (0, "P:Dejounte Murray"), (0, "P:Paul George")]),
+    dict(line=510, query="GO FROM {P:Russell Westbrook} OVER * REVERSELY YIELD serve._src, like._src",
+         rows=[(0, "P:Russell Westbrook")] * 3),
+    dict(line=524, query="GO FROM {P:Russell Westbrook} OVER * REVERSELY",
+         rows=[(0, "P:James Harden", 0), (0, "P:Dejounte Murray", 0), (0, "P:Paul George", 0)]),
+    dict(line=539, query="GO FROM {P:Manu Ginobili} OVER like, teammate REVERSELY YIELD like.likeness, "
+                         "teammate.start_year, $$.player.name",
+         rows=[(95, 0, "Tim Duncan"), (95, 0, "Tony Parker"), (90, 0, "Tiago Splitter"), (99, 0, "Dejounte Murray"),
+               (0, 2002, "Tim Duncan"), (0, 2002, "Tony Parker")]),
+    dict(line=557, query="GO FROM {P:Manu Ginobili} OVER * REVERSELY YIELD like.likeness, teammate.start_year, "
+                         "serve.start_year, $$.player.name",
+         rows=[(95, 0, 0, "Tim Duncan"), (95, 0, 0, "Tony Parker"), (90, 0, 0, "Tiago Splitter"),
+               (99, 0, 0, "Dejounte Murray"), (0, 2002, 0, "Tim Duncan"), (0, 2002, 0, "Tony Parker")]),
+    dict(line=575, query="GO FROM {P:Russell Westbrook} OVER serve, like "
+                         "YIELD serve.start_year, like.likeness, serve._type, like._type",
+         rows=[(2008, 0, 4, 0), (0, 90, 0, 5), (0, 90, 0, 5)]),
+    dict(line=591, query="GO FROM {P:Shaquile O'Neal} OVER serve, like",
+         rows=[("T:Magic", 0), ("T:Lakers", 0), ("T:Heat", 0), ("T:Suns", 0), ("T:Cavaliers", 0), ("T:Celtics", 0),
+               (0, "P:JaVale McGee"), (0, "P:Tim Duncan")]),
+    dict(line=611, query="GO FROM {P:Dirk Nowitzki} OVER * YIELD serve._dst, like._dst",
+         rows=[("T:Mavericks", 0), (0, "P:Steve Nash"), (0, "P:Jason Kidd"), (0, "P:Dwyane Wade")]),
+    dict(line=627, query="GO FROM {P:Paul Gasol} OVER *",
+         rows=[("T:Grizzlies", 0, 0), ("T:Lakers", 0, 0), ("T:Bulls", 0, 0), ("T:Spurs", 0, 0), ("T:Bucks", 0, 0),
+               (0, "P:Kobe Bryant", 0), (0, "P:Marc Gasol", 0)]),
+    dict(line=648, query="GO FROM {P:LaMarcus Aldridge} OVER * YIELD $$.team.name, $$.player.name",
+         rows=[("Trail Blazers", ""), ("", "Tim Duncan"), ("", "Tony Parker"), ("Spurs", "")]),
 ]
