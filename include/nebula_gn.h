@@ -16,6 +16,11 @@
  *   ngx_load_kv / ngx_commit    the part -> CSR snapshot export: KVStore::prefix over a part
  *                               (src/kvstore/KVStore.h:108-111, NebulaStore.cpp:451-464) as dumped by
  *                               DumpEdgesTool (src/tools/dump-edges/DumpEdgesTool.cpp:17-50)
+ *   ngx_load_snapshot_rows      a part's raft snapshot stream: SnapshotManagerImpl::accessAllRowsInSnapshot
+ *                               rows (src/kvstore/SnapshotManagerImpl.cpp:15-53) as Part::commitSnapshot
+ *                               applies them (src/kvstore/Part.cpp:319-344), encodeKV records
+ *   ngx_save/open_snapshot      RocksEngine::createCheckpoint (src/kvstore/RocksEngine.cpp:433-480) for the
+ *                               device copy: a named, versioned file of the committed shard
  *   ngx_get_neighbors           QueryBoundProcessor::process (src/storage/query/QueryBaseProcessor.inl:800-855,
  *                               src/storage/query/QueryBoundProcessor.cpp:18-261), invoked from
  *                               StorageServiceHandler::future_getBound (src/storage/StorageServiceHandler.cpp:45-53)
@@ -46,6 +51,7 @@ extern "C" {
 #define NGX_E_QUERY (-1003)             /* graphd-side evaluation error (GoExecutor doError) */
 #define NGX_E_DEVICE (-1004)            /* HIP / RCCL failure */
 #define NGX_E_NOT_LOADED (-1005)
+#define NGX_E_SNAPSHOT (-1006)          /* snapshot file unreadable, corrupt, or of another space / shard / schema */
 
 /* SupportedType (src/interface/common.thrift:30-56) */
 #define NGX_T_BOOL 1
@@ -106,6 +112,21 @@ int32_t ngx_load_kv(ngx_ctx* ctx, int32_t space, const ngx_kv_batch* batch);
 /* Build the per-part CSR + columnar props from the staged rows and upload them to HBM.
  * Collective when world > 1 (vertex tables are exchanged to resolve destination rows). */
 int32_t ngx_commit(ngx_ctx* ctx, int32_t space);
+
+/* Stage one part's snapshot stream: `rows` holds back-to-back records in the reference's encodeKV
+ * layout (src/kvstore/LogEncoder.cpp:16-27): u32 key size, u32 value size, key bytes, value bytes,
+ * as SnapshotManagerImpl streams a part (prefix iteration over snapshotPrefix(part)). Keys that are not
+ * vertex / edge data (system, uuid keys) are skipped at commit; rows of parts this shard does not own
+ * are dropped. NGX_E_BAD_ARGUMENT (nothing staged) if the last record is truncated. */
+int32_t ngx_load_snapshot_rows(ngx_ctx* ctx, int32_t space, const uint8_t* rows, uint64_t len);
+
+/* Device snapshot file of the committed shard (CSR, destination rows, prop and tag columns), so a
+ * restart skips the KV decode. `tag` (<= 63 bytes) names the checkpoint. ngx_open_snapshot needs the
+ * space added with the same num_parts and identical schemas (digest), the same rank / world, and
+ * replaces any committed data of the space; tag_out (64 bytes, may be NULL) receives the tag. A file
+ * that fails any check returns NGX_E_SNAPSHOT and leaves the space as it was. */
+int32_t ngx_save_snapshot(ngx_ctx* ctx, int32_t space, const char* path, const char* tag);
+int32_t ngx_open_snapshot(ngx_ctx* ctx, int32_t space, const char* path, char* tag_out);
 
 typedef struct {
     uint64_t vertices;            /* rows in this shard's vertex table */

@@ -38,6 +38,13 @@ struct DeviceGraph {
     int64_t* vid = nullptr;
     VIndex vindex{nullptr, 0};                          // (part, vid) -> row hash index (seed lookup)
     std::vector<DSlot> slots;
+    std::vector<int32_t> mirror;                        // per slot: the slot holding its exact transpose, or -1
+    // $$ props across shards: every tag table over ALL global rows (replicas of the other shards'
+    // rows), gathered on the first query that reads a $$ prop, kept until the next commit
+    bool replicas = false;
+    std::vector<HostColumn> repHost;                    // host copies (string bytes back result cells)
+    DTag* rtags = nullptr;
+    DCol* rcols = nullptr;
     std::vector<DTag> tags;
     std::vector<DCol> cols;
     DSlot* dslots = nullptr;
@@ -139,6 +146,11 @@ struct ngx_ctx {
     std::vector<OutCol> oColView;                       // their device pointers, as uploaded to oColDesc
     uint64_t visitedSize = 0;
     uint8_t epoch = 0;
+    // pull expansion (kernels.h launchPull): segment queue + its counters, kept zero between launches
+    DBuf pullSeg, pullCtl;
+    uint64_t pullSegWords = 0;
+    int64_t pullFactor = 200;                           // pull when 100 x hop edges >= pullFactor x shard rows (0: never)
+    uint64_t pullHops = 0;
     // RCCL watchdog: collective work must finish within this; else the communicator is aborted
     int64_t rcclTimeoutMs = 120000;
     bool broken = false;                                // communicator aborted: every later call fails
@@ -163,7 +175,7 @@ struct ngx_ctx {
         for (DBuf* b : {&visited, &F0, &F1, &estart, &tileSums, &counters, &lbStatus, &seedPart, &seedVid, &oSrc,
                         &oDst, &oRank, &oType, &oEntry, &chunkFirst, &oColDesc, &progBuf, &sendBits, &recvBits,
                         &vcells, &misc, &edgeMask, &cmpStatus[0], &cmpStatus[1], &oFlags, &rowCols, &rowLen,
-                        &rowOff, &rowBytes}) b->release();
+                        &rowOff, &rowBytes, &pullSeg, &pullCtl}) b->release();
         for (auto& cb : oCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         hostStage.release();
         inStage.release();
@@ -475,6 +487,63 @@ void parallelRows(uint64_t n, F&& f, int T = 0) {
     for (auto& th : ts) th.join();
 }
 
+// Mirror slots for the pull expansion (kernels.h launchPull): slot j is the mirror of slot i when
+// etype[j] == -etype[i] and the multiset of (src row, dst row) pairs of i equals that of (dst row,
+// src row) of j -- every out-edge was also written as its in-edge with the same rank, as
+// InsertEdgeExecutor does, and nothing else. One shard holding every row (world == 1). Compared by
+// edge count and two independent 64-bit sums of mixed pairs (a commutative digest of the multiset).
+uint64_t mixPair(uint64_t a, uint64_t b, uint64_t seed) {
+    uint64_t z = (a << 32 | b) + seed;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+struct PairDigest {
+    uint64_t n = 0, h1 = 0, h2 = 0;
+    bool ok = true;
+    bool operator==(const PairDigest& o) const { return ok && o.ok && n == o.n && h1 == o.h1 && h2 == o.h2; }
+};
+
+PairDigest slotDigest(const HostSlot& s, bool transpose) {
+    const uint64_t V = s.off.empty() ? 0 : s.off.size() - 1;
+    const int T = V < (1u << 16) ? 1 : hostThreads();
+    std::vector<PairDigest> part(T);
+    parallelRows(V, [&](uint64_t lo, uint64_t hi, int t) {
+        PairDigest d;
+        for (uint64_t r = lo; r < hi; r++) {
+            for (uint64_t e = s.off[r]; e < s.off[r + 1]; e++) {
+                const uint64_t g = s.dgid[e];
+                if (g == kNoRow) { d.ok = false; continue; }
+                const uint64_t a = transpose ? g : r, b = transpose ? r : g;
+                d.h1 += mixPair(a, b, 0x9E3779B97F4A7C15ULL);
+                d.h2 += mixPair(b, a, 0xD1B54A32D192ED03ULL);
+                d.n++;
+            }
+        }
+        part[t] = d;
+    }, T);
+    PairDigest out;
+    for (auto& d : part) { out.n += d.n; out.h1 += d.h1; out.h2 += d.h2; out.ok = out.ok && d.ok; }
+    return out;
+}
+
+std::vector<int32_t> findMirrors(const HostGraph& g) {
+    std::vector<int32_t> m(g.slots.size(), -1);
+    if (g.vid.size() >= (1ULL << 32)) return m;
+    for (size_t i = 0; i < g.slots.size(); i++) {
+        if (m[i] >= 0 || g.slots[i].etype <= 0) continue;
+        for (size_t j = 0; j < g.slots.size(); j++) {
+            if (g.slots[j].etype != -g.slots[i].etype) continue;
+            if (g.slots[i].dst.size() == g.slots[j].dst.size() && slotDigest(g.slots[i], false) == slotDigest(g.slots[j], true)) {
+                m[i] = static_cast<int32_t>(j);
+                m[j] = static_cast<int32_t>(i);
+            }
+        }
+    }
+    return m;
+}
+
 // ColumnValue per calculateExprType (GoExecutor::toThriftResponse, GoExecutor.cpp:775-829); string
 // bytes are appended to `strings` (str_off relative to it)
 bool toCell(const OutCell& v, int32_t colType, ngx_cell& out, std::string& strings, const StrMap& sm) {
@@ -684,6 +753,128 @@ void allGather(ngx_ctx* c, const void* dsend, void* drecv, uint64_t bytes) {
     }
 }
 
+// all-gather of host data: `bytes` per rank -> world blocks in rank order (host memory)
+std::vector<uint8_t> gatherHost(ngx_ctx* c, const void* host, uint64_t bytes) {
+    std::vector<uint8_t> out(bytes * c->world);
+    if (bytes == 0) return out;
+    uint8_t* ds = c->sendBits.get<uint8_t>(bytes);
+    uint8_t* dr = c->recvBits.get<uint8_t>(bytes * c->world);
+    HIP_OK(hipMemcpyAsync(ds, host, bytes, hipMemcpyHostToDevice, c->stream));
+    allGather(c, ds, dr, bytes);
+    HIP_OK(hipMemcpyAsync(out.data(), dr, out.size(), hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return out;
+}
+
+// rows of every shard in global row order: each shard contributes its rows' `elem`-byte values
+template <typename T>
+std::vector<T> gatherRows(ngx_ctx* c, const HostGraph& g, const std::vector<T>& local) {
+    uint64_t maxV = 0;
+    for (int r = 0; r < c->world; r++) maxV = std::max(maxV, g.shardBase[r + 1] - g.shardBase[r]);
+    std::vector<T> send(std::max<uint64_t>(maxV, 1));
+    std::copy(local.begin(), local.end(), send.begin());
+    std::vector<uint8_t> all = gatherHost(c, send.data(), maxV * sizeof(T));
+    std::vector<T> out(g.vglobal);
+    for (int r = 0; r < c->world; r++) {
+        const uint64_t n = g.shardBase[r + 1] - g.shardBase[r];
+        if (n) std::memcpy(out.data() + g.shardBase[r], all.data() + r * maxV * sizeof(T), n * sizeof(T));
+    }
+    return out;
+}
+
+// $$ props across shards (GoExecutor::fetchVertexProps -> QueryVertexPropsProcessor,
+// src/graph/GoExecutor.cpp:937-973, src/storage/query/QueryVertexPropsProcessor.cpp:16-58): instead of
+// a per-query fetch of the destinations' tag rows, every shard keeps replicas of all tag tables over
+// the global rows (288 GB of HBM per GPU holds them), gathered once per snapshot on the first query
+// that reads a $$ prop. Collective: every rank runs the same queries (GO is SPMD over the shards).
+void ensureDstReplicas(ngx_ctx* c, Space& sp) {
+    DeviceGraph& d = *sp.dev;
+    const HostGraph& g = *sp.host;
+    if (d.replicas) return;
+    const uint64_t VG = g.vglobal;
+    std::vector<DTag> rt;
+    std::vector<DCol> rc;
+    d.repHost.clear();
+    std::vector<std::vector<HostColumn>> repCols(g.tags.size());
+    for (size_t k = 0; k < g.tags.size(); k++) {
+        const HostTag& t = g.tags[k];
+        DTag dt = d.tags[k];
+        dt.present = d.upload(gatherRows(c, g, t.present).data(), VG);
+        dt.colBase = static_cast<int32_t>(rc.size());
+        for (const HostColumn& lc : t.cols) {
+            HostColumn h;
+            h.type = lc.type;
+            h.width = 8;
+            switch (lc.type) {
+                case T_INT: case T_TIMESTAMP: case T_VID: h.i64 = gatherRows(c, g, lc.i64); break;
+                case T_FLOAT: case T_DOUBLE: h.f64 = gatherRows(c, g, lc.f64); break;
+                case T_BOOL: h.b = gatherRows(c, g, lc.b); break;
+                case T_STRING: {
+                    std::vector<uint32_t> len(lc.soff.empty() ? 0 : lc.soff.size() - 1);
+                    for (size_t i = 0; i < len.size(); i++) len[i] = static_cast<uint32_t>(lc.soff[i + 1] - lc.soff[i]);
+                    std::vector<uint32_t> glen = gatherRows(c, g, len);
+                    uint64_t mine = lc.sbytes.size();
+                    std::vector<uint8_t> tot = gatherHost(c, &mine, 8);
+                    uint64_t maxB = 0;
+                    std::vector<uint64_t> per(c->world);
+                    for (int r = 0; r < c->world; r++) { std::memcpy(&per[r], tot.data() + 8 * r, 8); maxB = std::max(maxB, per[r]); }
+                    std::string sendB(lc.sbytes);
+                    sendB.resize(std::max<uint64_t>(maxB, 1));
+                    std::vector<uint8_t> allB = gatherHost(c, sendB.data(), maxB);
+                    for (int r = 0; r < c->world; r++) h.sbytes.append(reinterpret_cast<const char*>(allB.data()) + r * maxB, per[r]);
+                    h.soff.assign(VG + 1, 0);
+                    for (uint64_t i = 0; i < VG; i++) h.soff[i + 1] = h.soff[i] + glen[i];
+                    if (h.soff[VG] != h.sbytes.size()) throw Error{NGX_E_DEVICE, "tag replica string bytes disagree"};
+                    break;
+                }
+                default: break;
+            }
+            // validity: replicated when any shard's column lacks values for some rows
+            uint8_t allValid = lc.allValid ? 1 : 0;
+            std::vector<uint8_t> flags = gatherHost(c, &allValid, 1);
+            h.allValid = std::all_of(flags.begin(), flags.end(), [](uint8_t f) { return f != 0; });
+            if (!h.allValid) {
+                std::vector<uint8_t> lv = lc.allValid ? std::vector<uint8_t>(g.vid.size(), 1) : lc.valid;
+                h.valid = gatherRows(c, g, lv);
+            }
+            repCols[k].push_back(std::move(h));
+        }
+        rt.push_back(dt);
+    }
+    // upload at 8 bytes per integer (the generated kernels read replicas at that width); repHost is
+    // sized once: strRanges point into its strings
+    size_t ncols = 0;
+    for (auto& v : repCols) ncols += v.size();
+    d.repHost.reserve(ncols);
+    for (size_t k = 0; k < repCols.size(); k++) {
+        for (HostColumn& h : repCols[k]) {
+            DCol dc{};
+            dc.type = h.type;
+            switch (h.type) {
+                case T_INT: case T_TIMESTAMP: case T_VID: dc.width = 8; dc.data = d.upload(h.i64.data(), VG); break;
+                case T_FLOAT: case T_DOUBLE: dc.data = d.upload(h.f64.data(), VG); break;
+                case T_BOOL: dc.data = d.upload(h.b.data(), VG); break;
+                case T_STRING:
+                    dc.soff = d.upload(h.soff.data(), VG + 1);
+                    dc.sbytes = h.sbytes.empty() ? nullptr : d.upload(h.sbytes.data(), h.sbytes.size());
+                    break;
+                default: break;
+            }
+            if (!h.allValid) dc.valid = d.upload(h.valid.data(), VG);
+            d.repHost.push_back(std::move(h));
+            if (dc.sbytes) {
+                const HostColumn& kept = d.repHost.back();
+                d.strRanges.push_back({reinterpret_cast<uint64_t>(dc.sbytes), kept.sbytes.data(), kept.sbytes.size()});
+            }
+            rc.push_back(dc);
+        }
+    }
+    std::sort(d.strRanges.begin(), d.strRanges.end(), [](const DeviceGraph::Range& a, const DeviceGraph::Range& b) { return a.dev < b.dev; });
+    d.rtags = d.upload(rt.data(), rt.size());
+    d.rcols = d.upload(rc.data(), rc.size());
+    d.replicas = true;
+}
+
 }  // namespace
 
 // ============================================================================ C ABI
@@ -779,6 +970,32 @@ int32_t ngx_add_schema(ngx_ctx* c, int32_t space, int32_t isEdge, int32_t id, co
     return NGX_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// one KV row into the space's staging (rows of parts another shard owns are dropped)
+void stageRow(ngx_ctx* c, StagedRows& st, const uint8_t* k, uint64_t kl, const uint8_t* v, uint64_t vl) {
+    if (kl < 4) return;
+    int32_t item;
+    std::memcpy(&item, k, 4);
+    int32_t part = item >> 8;
+    if (c->world > 1 && ((part % c->world) + c->world) % c->world != c->rank) return;   // not ours
+    st.koff.push_back(st.keys.size());
+    st.klen.push_back(static_cast<uint32_t>(kl));
+    st.keys.insert(st.keys.end(), k, k + kl);
+    st.vals.insert(st.vals.end(), v, v + vl);
+    st.voff.push_back(st.vals.size());
+}
+
+// snapshot generation: bumped by every commit / snapshot open (keys the JIT cache)
+uint64_t nextGeneration() {
+    static std::atomic<uint64_t> generations{0};
+    return ++generations;
+}
+}  // namespace
+
+extern "C" {
+
 int32_t ngx_load_kv(ngx_ctx* c, int32_t space, const ngx_kv_batch* b) {
     std::lock_guard<std::mutex> g(c->mu);
     Space* sp = findSpace(c, space);
@@ -786,21 +1003,75 @@ int32_t ngx_load_kv(ngx_ctx* c, int32_t space, const ngx_kv_batch* b) {
     auto& st = sp->staged;
     if (st.voff.empty()) st.voff.push_back(0);
     for (uint64_t i = 0; i < b->n; i++) {
-        uint64_t kl = b->key_off[i + 1] - b->key_off[i];
-        const uint8_t* k = b->keys + b->key_off[i];
-        if (kl < 4) continue;
-        int32_t item;
-        std::memcpy(&item, k, 4);
-        int32_t part = item >> 8;
-        if (c->world > 1 && ((part % c->world) + c->world) % c->world != c->rank) continue;   // not ours
-        st.koff.push_back(st.keys.size());
-        st.klen.push_back(static_cast<uint32_t>(kl));
-        st.keys.insert(st.keys.end(), k, k + kl);
-        uint64_t vl = b->val_off[i + 1] - b->val_off[i];
-        st.vals.insert(st.vals.end(), b->vals + b->val_off[i], b->vals + b->val_off[i] + vl);
-        st.voff.push_back(st.vals.size());
+        stageRow(c, st, b->keys + b->key_off[i], b->key_off[i + 1] - b->key_off[i], b->vals + b->val_off[i],
+                 b->val_off[i + 1] - b->val_off[i]);
     }
     return NGX_OK;
+}
+
+// encodeKV records (LogEncoder.cpp:16-27) of a part's snapshot stream; decodeKV as Part::commitSnapshot
+int32_t ngx_load_snapshot_rows(ngx_ctx* c, int32_t space, const uint8_t* rows, uint64_t len) {
+    if (!c || (len && !rows)) return NGX_E_BAD_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    Space* sp = findSpace(c, space);
+    if (!sp) return fail(c, NGX_E_SPACE_NOT_FOUND, "space not found");
+    // validate the whole stream first: a truncated record stages nothing
+    for (uint64_t p = 0; p < len;) {
+        if (len - p < 8) return fail(c, NGX_E_BAD_ARGUMENT, "truncated snapshot record header");
+        uint32_t ks, vs;
+        std::memcpy(&ks, rows + p, 4);
+        std::memcpy(&vs, rows + p + 4, 4);
+        if (len - p - 8 < static_cast<uint64_t>(ks) + vs) return fail(c, NGX_E_BAD_ARGUMENT, "truncated snapshot record");
+        p += 8 + static_cast<uint64_t>(ks) + vs;
+    }
+    auto& st = sp->staged;
+    if (st.voff.empty()) st.voff.push_back(0);
+    for (uint64_t p = 0; p < len;) {
+        uint32_t ks, vs;
+        std::memcpy(&ks, rows + p, 4);
+        std::memcpy(&vs, rows + p + 4, 4);
+        stageRow(c, st, rows + p + 8, ks, rows + p + 8 + ks, vs);
+        p += 8 + static_cast<uint64_t>(ks) + vs;
+    }
+    return NGX_OK;
+}
+
+int32_t ngx_save_snapshot(ngx_ctx* c, int32_t space, const char* path, const char* tag) {
+    if (!c || !path) return NGX_E_BAD_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    Space* sp = findSpace(c, space);
+    if (!sp) return fail(c, NGX_E_SPACE_NOT_FOUND, "space not found");
+    if (!sp->host) return fail(c, NGX_E_NOT_LOADED, "space not committed");
+    Error e = writeSnapshotFile(*sp, *sp->host, c->rank, c->world, path, tag ? tag : "");
+    return e.code ? fail(c, e.code, e.msg) : NGX_OK;
+}
+
+int32_t ngx_open_snapshot(ngx_ctx* c, int32_t space, const char* path, char* tagOut) {
+    if (!c || !path) return NGX_E_BAD_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    Space* sp = findSpace(c, space);
+    if (!sp) return fail(c, NGX_E_SPACE_NOT_FOUND, "space not found");
+    try {
+        HIP_OK(hipSetDevice(c->device));
+        auto hg = std::make_unique<HostGraph>();
+        std::string tag;
+        Error e = readSnapshotFile(*sp, path, c->rank, c->world, *hg, tag);
+        if (e.code) return fail(c, e.code, e.msg);
+        auto dev = upload(*hg, *sp);
+        dev->mirror = c->world == 1 ? findMirrors(*hg) : std::vector<int32_t>(hg->slots.size(), -1);
+        HIP_OK(hipDeviceSynchronize());
+        sp->dev = std::move(dev);
+        sp->gen = nextGeneration();
+        sp->host = std::move(hg);
+        sp->staged = StagedRows();
+        if (tagOut) {
+            std::memset(tagOut, 0, 64);
+            std::memcpy(tagOut, tag.data(), std::min<size_t>(tag.size(), 63));
+        }
+        return NGX_OK;
+    } catch (const Error& e) {
+        return fail(c, e.code, e.msg);
+    }
 }
 
 int32_t ngx_commit(ngx_ctx* c, int32_t space) {
@@ -849,8 +1120,8 @@ int32_t ngx_commit(ngx_ctx* c, int32_t space) {
         if (hg->shardBase.empty()) { hg->shardBase = {0, hg->vid.size()}; hg->vglobal = hg->vid.size(); }
         hg->gbase = hg->shardBase[c->rank];
         sp->dev = upload(*hg, *sp);
-        static std::atomic<uint64_t> generations{0};
-        sp->gen = ++generations;
+        sp->dev->mirror = c->world == 1 ? findMirrors(*hg) : std::vector<int32_t>(hg->slots.size(), -1);
+        sp->gen = nextGeneration();
         sp->host = std::move(hg);
         sp->staged = StagedRows();
         return NGX_OK;
@@ -909,6 +1180,7 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
     if (n == "rccl_timeout_ms") { c->rcclTimeoutMs = value < 1 ? 1 : value; return NGX_OK; }
     if (n == "max_edge_returned_per_vertex") { c->maxEdgesPerVertex = value <= 0 ? INT32_MAX : value; return NGX_OK; }
     if (n == "jit_cache_capacity") { c->jit.capacity = value < 1 ? 1 : static_cast<size_t>(value); return NGX_OK; }
+    if (n == "pull_factor") { c->pullFactor = value < 0 ? 0 : value; return NGX_OK; }
     return fail(c, NGX_E_BAD_ARGUMENT, "unknown flag " + n);
 }
 
@@ -918,6 +1190,8 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     if (n == "jit") *value = c->jitOn ? 1 : 0;
     else if (n == "rccl_timeout_ms") *value = c->rcclTimeoutMs;
     else if (n == "max_edge_returned_per_vertex") *value = c->maxEdgesPerVertex;
+    else if (n == "pull_factor") *value = c->pullFactor;
+    else if (n == "pull_hops") *value = static_cast<int64_t>(c->pullHops);
     else if (n == "jit_compiled") *value = static_cast<int64_t>(c->jit.compiled);
     else if (n == "jit_hits") *value = static_cast<int64_t>(c->jit.hits);
     else if (n == "jit_cached") *value = static_cast<int64_t>(c->jit.size());
@@ -1232,7 +1506,11 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         if (crc) return fail(c, crc, err);
         progs.yOff.push_back(progs.add(yp));
     }
-    if (progs.usesDst && c->world > 1) return fail(c, NGX_E_UNSUPPORTED, "$$ props across shards are not fetched yet");
+    // $$ props: tag tables over every global row (world > 1: replicas of the other shards' rows)
+    const bool dstReplica = progs.usesDst && c->world > 1;
+    if (dstReplica) ensureDstReplicas(c, sp);
+    const DTag* dstTags = dstReplica ? d.rtags : d.dtags;
+    const DCol* dstCols = dstReplica ? d.rcols : d.dcols;
     std::vector<int32_t> ySlotType(progs.yOff.size(), 0);
     DevPrograms dp = uploadPrograms(c, progs, ySlotType, gp.colTypes);
     // WHERE fully pushed: for edges whose storage filter ran, graphd's re-evaluation is implied
@@ -1265,6 +1543,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             jq.ttl = jq.ttl || ttlInfo(sp.edge(std::abs(hs.etype[s])), tc, td);
         }
         jq.etype0 = hs.n == 1 ? hs.etype[0] : 0;
+        jq.dstReplica = dstReplica;
         jq.dstW = hs.n ? hs.dstW[0] : 0;
         jq.rankW = hs.n ? hs.rankW[0] : 0;
         for (int s = 1; s < hs.n; s++) {
@@ -1330,7 +1609,43 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         sparts.push_back(part);
         svids.push_back(v);
     }
-    ensureVisited(c, d.vglobal);
+    // marks over global rows: [0, vAl) the push expansion's (and the exchange's), [vAl, 2 vAl) a pull
+    // hop's output, so a pull never overwrites the frontier marks it reads; one epoch counter for both
+    const uint64_t vAl = (d.vglobal + 15) & ~15ULL;
+    ensureVisited(c, 2 * vAl);
+    uint8_t* const marksA = c->visited.get<uint8_t>(2 * vAl);
+    uint8_t* const marksB = marksA + vAl;
+    const uint8_t* curMarks = nullptr;                          // current frontier F: curMarks[g] == curEp
+    uint8_t curEp = 0;
+    PullArgs pa{};                                              // pull expansion (kernels.h launchPull)
+    bool pullable = c->pullFactor > 0 && c->world == 1 && hs.n >= 1 && hs.n <= kPullMaxSlots && d.V < (1ULL << 32) &&
+                    d.mirror.size() == d.slots.size();
+    if (pullable) {
+        uint64_t inEdges = 0;
+        pa.n = hs.n;
+        for (int s = 0; s < hs.n && pullable; s++) {
+            const int32_t m = d.mirror[hs.slotIdx[s]];
+            if (m < 0) { pullable = false; break; }
+            pa.ioff[s] = d.slots[m].off;
+            pa.isrc[s] = d.slots[m].dgid;
+            inEdges += sp.host->slots[m].dst.size();
+        }
+        if (pullable) {
+            pa.segCap = d.V * static_cast<uint64_t>(hs.n) + inEdges / kPullSeg + 1;
+            if (c->pullSegWords < pa.segCap) {
+                c->pullSeg.get<uint64_t>(pa.segCap);
+                HIP_OK(hipMemsetAsync(c->pullSeg.p, 0, c->pullSeg.cap, c->stream));
+                c->pullSegWords = c->pullSeg.cap / 8;
+            }
+            if (!c->pullCtl.p) {
+                c->pullCtl.get<uint32_t>(16);
+                HIP_OK(hipMemsetAsync(c->pullCtl.p, 0, c->pullCtl.cap, c->stream));
+            }
+            pa.seg = static_cast<uint64_t*>(c->pullSeg.p);
+            pa.ctl = static_cast<uint32_t*>(c->pullCtl.p);
+            pa.V = d.V;
+        }
+    }
     // the compaction after an intermediate hop also writes the next hop's estart[] and E (fused
     // scan) when the packed (|F|, E) total fits; the slot totals bound E
     uint64_t slotEdges = 0;
@@ -1450,7 +1765,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         FinalArgs a{};
         a.F = F; a.estart = estart; a.chunkFirst = chunkFirst; a.nEnt = nEnt; a.E = E; a.hs = hs;
         a.vid = d.vid; a.V = d.V; a.gbase = d.gbase;
-        a.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1, now};
+        a.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1, now, dstTags, dstCols};
         a.P = (isFinal && progs.P >= 0) ? dp.code + progs.P : nullptr;
         a.propsMask = isRecord ? recordPropsMask : 0;
         a.ttlMask = ttlMask;
@@ -1517,14 +1832,42 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         }
         if (isFinal) break;
         // ---- expand to the next frontier (set of distinct dsts)
+        // pull when the hop's edges outnumber the shard's rows pullFactor/100 times (every row's in-list is
+        // probed instead of every frontier edge storing a mark); push otherwise, or when a storage mask
+        // (TTL / max-edges) decides which edges count
+        const bool pull = pullable && !mask && E && E * 100 >= static_cast<uint64_t>(c->pullFactor) * d.V;
+        uint8_t* marks = marksA;
+        if (pull && (curMarks == nullptr || c->epoch >= 254)) {
+            // the seed frontier has no marks yet, or the epoch counter would wrap (clearing every mark)
+            // between the frontier's epoch and the pull's: re-mark F after the clear
+            if (c->epoch >= 254) {
+                HIP_OK(hipMemsetAsync(c->visited.p, 0, c->visitedSize, c->stream));
+                c->epoch = 0;
+            }
+            curEp = nextEpoch(c);
+            curMarks = marksA;
+            if (launchMarkRows(F, nF, marksA, curEp, c->stream)) throw Error{NGX_E_DEVICE, "mark rows"};
+        }
         uint8_t ep = nextEpoch(c);
-        if (E) {
+        if (pull) {
+            marks = curMarks == marksA ? marksB : marksA;
+            pa.cur = curMarks;
+            pa.curEp = curEp;
+            pa.out = marks + d.gbase;
+            pa.ep = ep;
+            pa.err = errFlag;
+            c->timed("pull", d.V * (16 * static_cast<uint64_t>(hs.n) + 1), [&] {
+                if (launchPull(pa, c->stream)) throw Error{NGX_E_DEVICE, "pull"};
+            });
+            c->pullHops++;
+        } else if (E) {
             c->timed("expand", E * 8, [&] {
-                if (launchExpandMark(F, estart, chunkFirst, nEnt, E, hs, c->visited.get<uint8_t>(d.vglobal), ep, pos32, c->stream,
-                                     mask))
+                if (launchExpandMark(F, estart, chunkFirst, nEnt, E, hs, marksA, ep, pos32, c->stream, mask))
                     throw Error{NGX_E_DEVICE, "expand"};
             });
         }
+        curMarks = marks;
+        curEp = ep;
         if (c->world > 1) {
             c->timed("exchange", 0, [&] { exchangeFrontier(c, d, ep); });
             c->addBytes("exchange", c->lastXchgBytes);
@@ -1536,7 +1879,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             // one launch: next frontier + estart + chunk heads; the look-back words of the next
             // compaction cleared on the way
             CompactArgs ca{};
-            ca.visited = c->visited.get<uint8_t>(d.vglobal) + d.gbase;
+            ca.visited = marks + d.gbase;
             ca.V = d.V;
             ca.hs = hs;
             ca.outF = Fn;
@@ -1567,7 +1910,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             uint64_t* est = c->estart.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
             Publish pub = nextPub(c);
             c->timed("compact_degrees", 0, [&] {
-                if (launchCompactDegrees(c->visited.get<uint8_t>(d.vglobal), d.gbase, d.V, ep, hs, Fn, est, tiles2,
+                if (launchCompactDegrees(marks, d.gbase, d.V, ep, hs, Fn, est, tiles2,
                                          counters + 2, c->stream, pub))
                     throw Error{NGX_E_DEVICE, "compact"};
             });
@@ -1578,7 +1921,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             c->addBytes("compact_degrees", nF * 8 + nF * static_cast<uint64_t>(hs.n) * 24);
         } else {
             c->timed("compact", 0, [&] {
-                if (launchCompact(c->visited.get<uint8_t>(d.vglobal), d.gbase, d.V, ep, Fn, tiles2, counters + 2, c->stream))
+                if (launchCompact(marks, d.gbase, d.V, ep, Fn, tiles2, counters + 2, c->stream))
                     throw Error{NGX_E_DEVICE, "compact"};
             });
             nF = readScalar(c, counters + 2);
@@ -1637,11 +1980,33 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     size_t total = 0;
     for (auto& a : arrs) total += (a.bytes + 63) & ~size_t(63);
     char* stage = c->hostStage.get(std::max<size_t>(total, 64));
+    // the copy: a kernel streaming into the mapped staging (all CUs, PCIe write rate; default) or the
+    // DMA engine (NGX_D2H=dma)
+    static const bool dmaCopy = [] { const char* e = std::getenv("NGX_D2H"); return e && std::string(e) == "dma"; }();
+    char* stageDev = nullptr;
+    if (!dmaCopy && hipHostGetDevicePointer(reinterpret_cast<void**>(&stageDev), c->hostStage.p, 0) != hipSuccess)
+        stageDev = nullptr;
+    CopyBatch cb{};
     for (auto& a : arrs) {
+        const size_t at = stage - static_cast<char*>(c->hostStage.p);
         a.host = stage;
         stage += (a.bytes + 63) & ~size_t(63);
-        if (a.bytes) HIP_OK(hipMemcpyAsync(a.host, a.dev, a.bytes, hipMemcpyDeviceToHost, c->stream));
+        if (!a.bytes) continue;
+        if (stageDev == nullptr) {
+            HIP_OK(hipMemcpyAsync(a.host, a.dev, a.bytes, hipMemcpyDeviceToHost, c->stream));
+            continue;
+        }
+        if (cb.n == kMaxCopies) {
+            if (launchCopyBatch(cb, c->stream)) throw Error{NGX_E_DEVICE, "copy to host"};
+            cb = CopyBatch{};
+        }
+        cb.src[cb.n] = static_cast<const uint8_t*>(a.dev);
+        cb.dst[cb.n] = reinterpret_cast<uint8_t*>(stageDev + at);
+        cb.bytes[cb.n] = a.bytes;
+        cb.start[cb.n + 1] = cb.start[cb.n] + (a.bytes + 15) / 16;
+        cb.n++;
     }
+    if (cb.n && launchCopyBatch(cb, c->stream)) throw Error{NGX_E_DEVICE, "copy to host"};
     HIP_OK(hipStreamSynchronize(c->stream));
     int64_t* hSrc = reinterpret_cast<int64_t*>(arrs[iSrc].host);
     int64_t* hDst = reinterpret_cast<int64_t*>(arrs[iDst].host);
@@ -2067,7 +2432,7 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
         FinalArgs a{};
         a.F = F; a.estart = estart; a.chunkFirst = chunkFirst; a.nEnt = nEnt; a.E = E; a.hs = hs;
         a.vid = d.vid; a.V = d.V; a.gbase = d.gbase;
-        a.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1, now};
+        a.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1, now, d.dtags, d.dcols};
         a.P = progs.P >= 0 ? dp.code + progs.P : nullptr;
         a.W = nullptr;
         for (int s = 0; s < hs.n; s++) {
@@ -2134,7 +2499,7 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
         HIP_OK(hipMemcpyAsync(dts, both.data(), both.size() * 4, hipMemcpyHostToDevice, c->stream));
         VertexCellArgs va{};
         va.rows = F; va.n = nF; va.ncols = nY; va.tagSlot = dts; va.col = dts + nY;
-        va.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1, now};
+        va.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1, now, d.dtags, d.dcols};
         va.out = c->vcells.get<OutCell>(nF * nY);
         if (launchVertexCells(va, c->stream)) throw Error{NGX_E_DEVICE, "vertex cells"};
         HIP_OK(hipMemcpyAsync(vraw.data(), va.out, nF * nY * sizeof(OutCell), hipMemcpyDeviceToHost, c->stream));

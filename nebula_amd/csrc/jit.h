@@ -43,6 +43,7 @@ struct JitQuery {
     std::vector<int32_t> slots;     // the hop's slots (HostGraph::slots indices)
     bool ttl = false;               // some slot's edge type has TTL info
     int32_t etype0 = 0;             // the only slot's signed type (0: several slots)
+    bool dstReplica = false;        // $$ props read the cross-shard replicas (8-byte, may lack values)
 };
 
 class JitCache {

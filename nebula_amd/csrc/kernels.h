@@ -130,6 +130,48 @@ int launchScanU64(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tileS
 // sized for a.oBase + a.E rows. a.oEntry set (GetNeighbors): rows in edge order, rows written = the
 // inclusive status of the last chunk; else (GO) chunks in completion order, rows written = lbStatus[0]
 int launchFinal(const FinalArgs& a, hipStream_t s);
+
+// Direction-optimizing ("pull", Beamer et al. SC'12) intermediate hop, one shard holding every row:
+// row r joins the next frontier iff one of its in-neighbours over a hop slot's MIRROR slot (-t for t,
+// verified at commit to be the exact transpose of t) is in the current frontier (cur[g] == curEp).
+// Same set as the push expansion (getDstIdsFromResp, GoExecutor.cpp:675-718), fewer random accesses
+// when the frontier's edges outnumber the shard's rows. A thread probes up to kPullProbe in-neighbours
+// per slot of its row; longer in-lists left unresolved go to a segment queue (kPullSeg in-edges per
+// segment) that the workgroups drain after their rows, so a supernode spreads over many workgroups.
+// Reached rows get out[r] = ep. seg: segCap words and ctl[0..3) zero between launches (the kernel's
+// last workgroup leaves them zero).
+constexpr int kPullMaxSlots = 4;
+constexpr int kPullProbe = 8;
+constexpr uint64_t kPullSeg = 1024;
+struct PullArgs {
+    int32_t n;
+    const uint64_t* ioff[kPullMaxSlots];   // mirror slot CSR offsets (V + 1)
+    const uint32_t* isrc[kPullMaxSlots];   // mirror slot dgid: global row of each in-neighbour
+    const uint8_t* cur;                    // frontier marks over global rows
+    uint8_t* out;                          // this shard's marks (marks + gbase)
+    uint64_t V;
+    uint64_t* seg;
+    uint64_t segCap;
+    uint32_t* ctl;                         // [0] segments reserved, [1] taken, [2] workgroups done
+    uint32_t* err;                         // [3] queue overflow / spin limit (device fault)
+    uint8_t curEp, ep;
+};
+// worst-case queue words for in-degrees over the mirror slots: V * n + in-edges / kPullSeg + 1
+int launchPull(const PullArgs& a, hipStream_t s);
+// marks[F[i]] = ep for the rows of a frontier list (kNoRow entries skipped)
+int launchMarkRows(const uint32_t* F, uint64_t n, uint8_t* marks, uint8_t ep, hipStream_t s);
+// Batched device -> host copy by a kernel: every array is streamed with 16-byte loads and stores into
+// page-locked host memory mapped into the device address space (dst = hipHostGetDevicePointer), so
+// the copy runs at the PCIe write rate on all CUs instead of on one DMA engine.
+constexpr int kMaxCopies = 32;
+struct CopyBatch {
+    int32_t n;
+    const uint8_t* src[kMaxCopies];
+    uint8_t* dst[kMaxCopies];
+    uint64_t bytes[kMaxCopies];
+    uint64_t start[kMaxCopies + 1];     // exclusive prefix of 16-byte units per array
+};
+int launchCopyBatch(const CopyBatch& b, hipStream_t s);
 int launchVertexCells(const VertexCellArgs& a, hipStream_t s);
 int launchPack(const uint8_t* visited, uint8_t epoch, uint64_t lo, uint64_t n, uint64_t* bits, hipStream_t s);
 int launchMerge(const uint64_t* bits, uint64_t n, uint8_t* visited, uint64_t lo, uint8_t epoch, hipStream_t s);

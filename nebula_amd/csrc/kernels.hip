@@ -417,6 +417,158 @@ __global__ __launch_bounds__(WG) void k_compact_lb(CompactArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------ pull (direction-optimizing) hop
+// Segment word: ready bit | k (27 bits: segment index in the row's remaining in-list) | slot (4) | row (32).
+// One 8-byte agent-scope store publishes it whole: the consumer reads nothing else the producer wrote
+// (offsets, in-lists and frontier marks are read-only during the launch).
+__device__ __forceinline__ uint64_t pullSegWord(uint32_t row, int s, uint64_t k) {
+    return (1ULL << 63) | (k << 36) | (static_cast<uint64_t>(s) << 32) | row;
+}
+
+template <bool ONE>
+__global__ __launch_bounds__(WG) void k_pull(PullArgs a) {
+    __shared__ uint64_t sm[NW + 1];
+    __shared__ uint32_t sBase;
+    __shared__ uint64_t sSeg;
+    const int ns = ONE ? 1 : a.n;
+    const uint64_t r = static_cast<uint64_t>(blockIdx.x) * WG + threadIdx.x;
+    uint64_t rb[kPullMaxSlots], re[kPullMaxSlots];
+    uint32_t nseg = 0;
+    if (r < a.V) {
+        bool found = false;
+#pragma unroll
+        for (int s = 0; s < kPullMaxSlots; s++) {
+            if (s >= ns) break;
+            rb[s] = a.ioff[s][r];
+            re[s] = a.ioff[s][r + 1];
+        }
+#pragma unroll
+        for (int s = 0; s < kPullMaxSlots; s++) {
+            if (s >= ns || found) break;
+            const uint64_t b = rb[s], e = re[s];
+            const uint32_t* in = a.isrc[s];
+            uint32_t u[kPullProbe];
+#pragma unroll
+            for (int k = 0; k < kPullProbe; k++) u[k] = b + k < e ? in[b + k] : kNoRow;
+            // two frontier probes per round, next round only for rows still unresolved
+#pragma unroll
+            for (int k = 0; k < kPullProbe; k += 2) {
+                if (found) break;
+                const bool h0 = u[k] != kNoRow && a.cur[u[k]] == a.curEp;
+                const bool h1 = u[k + 1] != kNoRow && a.cur[u[k + 1]] == a.curEp;
+                found = h0 || h1;
+            }
+        }
+        if (found) {
+            a.out[r] = a.ep;
+        } else {
+#pragma unroll
+            for (int s = 0; s < kPullMaxSlots; s++) {
+                if (s >= ns) break;
+                if (re[s] > rb[s] + kPullProbe) nseg += static_cast<uint32_t>((re[s] - rb[s] - kPullProbe + kPullSeg - 1) / kPullSeg);
+            }
+        }
+    }
+    // rows with longer in-lists: reserve queue words for their remaining segments
+    if (__syncthreads_or(nseg != 0)) {
+        uint64_t tot;
+        const uint64_t pre = blockExScan(nseg, tot, sm);
+        if (threadIdx.x == 0) sBase = atomicAdd(&a.ctl[0], static_cast<uint32_t>(tot));
+        __syncthreads();
+        uint64_t at = sBase + pre;
+        if (nseg) {
+            for (int s = 0; s < ns; s++) {
+                if (re[s] <= rb[s] + kPullProbe) continue;
+                const uint64_t cnt = (re[s] - rb[s] - kPullProbe + kPullSeg - 1) / kPullSeg;
+                for (uint64_t k = 0; k < cnt; k++, at++) {
+                    if (at < a.segCap) __hip_atomic_store(a.seg + at, pullSegWord(static_cast<uint32_t>(r), s, k),
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    else atomicOr(a.err + 3, 1u);
+                }
+            }
+        }
+    }
+    // drain the queue: take segments while any are reserved and not yet taken
+    for (;;) {
+        if (threadIdx.x == 0) {
+            uint64_t w = 0;
+            uint32_t nx = __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (;;) {
+                const uint32_t rs = __hip_atomic_load(&a.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (nx >= rs || nx >= a.segCap) break;
+                if (__hip_atomic_compare_exchange_strong(&a.ctl[1], &nx, nx + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)) {
+                    // its producer has reserved it and is writing it
+                    uint64_t* p = a.seg + nx;
+                    uint32_t spins = 0;
+                    while ((w = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
+                        if (++spins > (1u << 24)) { atomicOr(a.err + 3, 1u); break; }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    __hip_atomic_store(p, 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // zero for the next launch
+                    break;
+                }
+            }
+            sSeg = w;
+        }
+        __syncthreads();
+        const uint64_t w = sSeg;
+        if (w == 0) break;
+        const uint32_t row = static_cast<uint32_t>(w);
+        const int s = static_cast<int>((w >> 32) & 0xF);
+        const uint64_t k = (w >> 36) & ((1ULL << 27) - 1);
+        const uint64_t e = a.ioff[s][row + 1];
+        const uint64_t b = a.ioff[s][row] + kPullProbe + k * kPullSeg;
+        const uint64_t be = b + kPullSeg < e ? b + kPullSeg : e;
+        const uint32_t* in = a.isrc[s];
+        bool hit = false;
+        uint32_t u[kPullSeg / WG];
+#pragma unroll
+        for (int j = 0; j < static_cast<int>(kPullSeg / WG); j++) {
+            const uint64_t p = b + threadIdx.x + static_cast<uint64_t>(j) * WG;
+            u[j] = p < be ? in[p] : kNoRow;
+        }
+#pragma unroll
+        for (int j = 0; j < static_cast<int>(kPullSeg / WG); j++) hit |= u[j] != kNoRow && a.cur[u[j]] == a.curEp;
+        if (hit) a.out[row] = a.ep;
+        __syncthreads();                                  // sSeg is rewritten by the next take
+    }
+    // the last workgroup out leaves the queue counters zero for the next launch (every segment is
+    // taken and finished by then: each workgroup drains after its own reservations)
+    if (threadIdx.x == 0) {
+        const uint32_t d = atomicAdd(&a.ctl[2], 1u);
+        if (d == gridDim.x - 1) {
+            __hip_atomic_store(&a.ctl[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&a.ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&a.ctl[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// 16-byte units of a batch of arrays, grid-stride; unit u of array k covers bytes [16 (u - start[k]) ..)
+__global__ __launch_bounds__(256) void k_copy_batch(CopyBatch b) {
+    const uint64_t total = b.start[b.n];
+    for (uint64_t u = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; u < total;
+         u += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+        int k = 0;
+        while (k + 1 < b.n && b.start[k + 1] <= u) k++;
+        const uint64_t off = (u - b.start[k]) * 16;
+        const uint64_t left = b.bytes[k] - off;
+        if (left >= 16 && ((reinterpret_cast<uintptr_t>(b.src[k]) | reinterpret_cast<uintptr_t>(b.dst[k])) & 15) == 0) {
+            const uint4 v = __builtin_nontemporal_load(reinterpret_cast<const uint4*>(b.src[k] + off));
+            *reinterpret_cast<uint4*>(b.dst[k] + off) = v;
+        } else {
+            const uint64_t m = left < 16 ? left : 16;
+            for (uint64_t i = 0; i < m; i++) b.dst[k][off + i] = b.src[k][off + i];
+        }
+    }
+}
+
+__global__ void k_mark_rows(const uint32_t* F, uint64_t n, uint8_t* marks, uint8_t ep) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n && F[i] != kNoRow) marks[F[i]] = ep;
+}
+
 // ------------------------------------------------------------------------------ final hop (interpreter)
 struct VmEv {
     static constexpr int kEager = -1;                 // YIELD evaluated in the write pass
@@ -713,6 +865,29 @@ int launchFinal(const FinalArgs& a, hipStream_t s) {
         if (a.hs.n == 1) hipLaunchKernelGGL((k_final<true, false>), grid, dim3(WG), 0, s, a);
         else hipLaunchKernelGGL((k_final<false, false>), grid, dim3(WG), 0, s, a);
     }
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchPull(const PullArgs& a, hipStream_t s) {
+    if (a.V == 0) return 0;
+    if (a.n < 1 || a.n > kPullMaxSlots || a.V >= (1ULL << 32)) return 1;
+    dim3 grid(static_cast<unsigned>((a.V + WG - 1) / WG));
+    if (a.n == 1) hipLaunchKernelGGL((k_pull<true>), grid, dim3(WG), 0, s, a);
+    else hipLaunchKernelGGL((k_pull<false>), grid, dim3(WG), 0, s, a);
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchCopyBatch(const CopyBatch& b, hipStream_t s) {
+    if (b.n <= 0 || b.start[b.n] == 0) return 0;
+    const uint64_t units = b.start[b.n];
+    const unsigned grid = static_cast<unsigned>(std::min<uint64_t>((units + 255) / 256, 4096));
+    hipLaunchKernelGGL(k_copy_batch, dim3(grid), dim3(256), 0, s, b);
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchMarkRows(const uint32_t* F, uint64_t n, uint8_t* marks, uint8_t ep, hipStream_t s) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_mark_rows, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, F, n, marks, ep);
     return static_cast<int>(hipGetLastError());
 }
 

@@ -135,6 +135,12 @@ inline int32_t idHash(int64_t vid, int32_t numParts) {        // ID_HASH (src/co
 
 // exporter.cpp: build the shard snapshot from staged rows
 Error exportSnapshot(Space& sp, int32_t rank, int32_t world, HostGraph& out);
+// snapshot.cpp: device snapshot files of a committed shard
+uint64_t schemaDigest(const Space& sp);
+Error writeSnapshotFile(const Space& sp, const HostGraph& g, int32_t rank, int32_t world, const std::string& path,
+                        const std::string& tag);
+Error readSnapshotFile(const Space& sp, const std::string& path, int32_t rank, int32_t world, HostGraph& out,
+                       std::string& tag);
 // resolve dst -> global row with the vertex tables of every shard (world == 1: local only)
 void resolveDstRows(const Space& sp, HostGraph& g,
                     const std::vector<std::vector<std::pair<int32_t, int64_t>>>& shardTables, int32_t world);

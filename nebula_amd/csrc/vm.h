@@ -30,7 +30,7 @@ struct EdgeCtx {
     const DCol* cols;   // first column of the slot's edge schema
     uint64_t pos;       // edge index inside the slot arrays
     uint32_t srow;      // local row of the source vertex
-    uint32_t drow;      // local row of the destination (kNoRow when not on this shard)
+    uint32_t drow;      // global row of the destination (kNoRow: no vertex row on any shard)
     int64_t src, dst, rank;
 };
 
@@ -41,6 +41,8 @@ struct VmEnv {
     const char* pool;
     uint32_t* unsupported;     // set when a value needs a host-only construct
     int64_t now;               // WallClock::fastNowInSec of the request (TTL)
+    const DTag* dtags;         // $$ props: tag tables over GLOBAL rows (world 1: the shard's own tables;
+    const DCol* dcols;         // world > 1: replicas of every shard's rows, built on first use)
 };
 
 // Loads through the global address space. Column pointers come from device-side tables (DCol, DTag),
@@ -259,29 +261,37 @@ __device__ __forceinline__ Val opEdst(const EdgeCtx& ec, int32_t b) {
 // no tag row for the vertex, or its TTL expired: collectVertexProps collects nothing for the tag
 // (QueryBaseProcessor.inl:440-476; checkDataExpiredForTTL, CommonUtils.cpp:13-49: an unreadable TTL
 // field never expires)
-__device__ __forceinline__ bool tagAbsent(const VmEnv& env, const DTag& t, uint32_t row) {
+__device__ __forceinline__ bool tagAbsentIn(const VmEnv& env, const DCol* cols, const DTag& t, uint32_t row) {
     if (row == kNoRow || gld<uint8_t>(t.present, row) == 0) return true;
     if (t.ttlCol < 0) return false;
-    const DCol& c = env.cols[t.colBase + t.ttlCol];
+    const DCol& c = cols[t.colBase + t.ttlCol];
     if (c.valid != nullptr && gld<uint8_t>(c.valid, row) == 0) return false;
     return env.now > loadI64(c, row) + t.ttlDur;
 }
 
-// OP_SRCTAG / OP_DSTTAG: column a of tag slot b for the src / dst row
-template <int CT, int W = 0, bool VALID = true>
+__device__ __forceinline__ bool tagAbsent(const VmEnv& env, const DTag& t, uint32_t row) {
+    return tagAbsentIn(env, env.cols, t, row);
+}
+
+// OP_SRCTAG / OP_DSTTAG: column a of tag slot b for the src row (the shard's tables, local row) or
+// the dst row (DST: env.dtags / dcols, global row)
+template <int CT, int W = 0, bool VALID = true, bool DST = false>
 __device__ __forceinline__ Val opTagT(const VmEnv& env, uint32_t row, int32_t a, int32_t b, uint8_t mode, Val dflt) {
-    const DTag& t = env.tags[b];
-    if (tagAbsent(env, t, row)) return (mode & 1) ? dflt : mkErr();
-    const DCol& c = env.cols[t.colBase + a];
+    const DCol* cols = DST ? env.dcols : env.cols;
+    const DTag& t = (DST ? env.dtags : env.tags)[b];
+    if (tagAbsentIn(env, cols, t, row)) return (mode & 1) ? dflt : mkErr();
+    const DCol& c = cols[t.colBase + a];
     if constexpr (VALID) {
         if (c.valid != nullptr && gld<uint8_t>(c.valid, row) == 0) return defaultOfTypeT<CT>();
     }
     return loadColT<CT, W>(c, row);
 }
-__device__ __forceinline__ Val opTag(const VmEnv& env, uint32_t row, int32_t a, int32_t b, uint8_t mode, Val dflt) {
-    const DTag& t = env.tags[b];
-    if (tagAbsent(env, t, row)) return (mode & 1) ? dflt : mkErr();
-    const DCol& c = env.cols[t.colBase + a];
+__device__ __forceinline__ Val opTag(const VmEnv& env, uint32_t row, int32_t a, int32_t b, uint8_t mode, Val dflt,
+                                     bool dst = false) {
+    const DCol* cols = dst ? env.dcols : env.cols;
+    const DTag& t = (dst ? env.dtags : env.tags)[b];
+    if (tagAbsentIn(env, cols, t, row)) return (mode & 1) ? dflt : mkErr();
+    const DCol& c = cols[t.colBase + a];
     if (c.valid != nullptr && gld<uint8_t>(c.valid, row) == 0) return defaultOfType(c.type);
     return loadCol(c, row);
 }
@@ -498,7 +508,7 @@ static __device__ __noinline__ Val vmEval(const Insn* code, const VmEnv& env, co
             case OP_EDST: st[sp++] = opEdst(ec, in.b); break;
             case OP_SRCTAG: case OP_DSTTAG:
                 st[sp++] = opTag(env, in.op == OP_SRCTAG ? ec.srow : ec.drow, in.a, in.b, in.mode,
-                                 constVal(in.t2, in.imm, 0, env.pool));
+                                 constVal(in.t2, in.imm, 0, env.pool), in.op == OP_DSTTAG);
                 break;
             case OP_PLUS: break;
             case OP_NEG: st[sp - 1] = opNeg(st[sp - 1]); break;

@@ -25,9 +25,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libnebula_gn.so")
 
 NGX_OK = 0
+E_BAD_ARGUMENT = -1001
 E_UNSUPPORTED = -1002
 E_QUERY = -1003
 E_DEVICE = -1004
+E_NOT_LOADED = -1005
+E_SNAPSHOT = -1006
 
 SOURCE, DEST, EDGE = 1, 2, 3
 
@@ -140,6 +143,9 @@ SIGNATURES = {
     "ngx_jit_note": (ctypes.c_char_p, [ctypes.c_void_p]),
     "ngx_hash_string": (c_i64, [ctypes.c_char_p, c_u64]),
     "ngx_device_to_host": (c_i32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_u64]),
+    "ngx_load_snapshot_rows": (c_i32, [ctypes.c_void_p, c_i32, ctypes.c_void_p, c_u64]),
+    "ngx_save_snapshot": (c_i32, [ctypes.c_void_p, c_i32, ctypes.c_char_p, ctypes.c_char_p]),
+    "ngx_open_snapshot": (c_i32, [ctypes.c_void_p, c_i32, ctypes.c_char_p, ctypes.c_char_p]),
 }
 
 
@@ -325,6 +331,21 @@ class Engine:
 
     def load_batch(self, space: int, batch):
         self.load_kv(space, *batch.arrays())
+
+    def load_snapshot_rows(self, space: int, rows: bytes):
+        """Stage a part's snapshot stream: encodeKV records (kvfmt.encode_kv), as SnapshotManagerImpl
+        streams them (src/kvstore/SnapshotManagerImpl.cpp:15-53)."""
+        buf = ctypes.create_string_buffer(bytes(rows), len(rows)) if rows else None
+        self._check(self.L.ngx_load_snapshot_rows(self.h, space, buf, len(rows)), "load_snapshot_rows")
+
+    def save_snapshot(self, space: int, path: str, tag: str = ""):
+        self._check(self.L.ngx_save_snapshot(self.h, space, path.encode(), tag.encode()), "save_snapshot")
+
+    def open_snapshot(self, space: int, path: str) -> str:
+        """Load a device snapshot file saved by save_snapshot; returns its checkpoint tag."""
+        tag = ctypes.create_string_buffer(64)
+        self._check(self.L.ngx_open_snapshot(self.h, space, path.encode(), tag), "open_snapshot")
+        return tag.value.decode()
 
     def commit(self, space: int):
         self._check(self.L.ngx_commit(self.h, space), "commit")

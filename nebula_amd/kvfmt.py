@@ -30,6 +30,18 @@ def vertex_key(part: int, vid: int, tag: int, ver: int = 0) -> bytes:
     return struct.pack("<iqiq", item, vid, tag & ~0x40000000, ver)
 
 
+def encode_kv(key: bytes, val: bytes) -> bytes:
+    """One record of a raft snapshot stream / WAL batch: u32 key size, u32 value size, key, value
+    (kvstore::encodeKV, src/kvstore/LogEncoder.cpp:16-27)."""
+    return struct.pack("<II", len(key), len(val)) + key + val
+
+
+def decode_kv(rec: bytes) -> Tuple[bytes, bytes]:
+    """kvstore::decodeKV (src/kvstore/LogEncoder.cpp:29-36)."""
+    ks, vs = struct.unpack_from("<II", rec, 0)
+    return rec[8:8 + ks], rec[8 + ks:8 + ks + vs]
+
+
 def varint(v: int) -> bytes:
     v &= (1 << 64) - 1
     out = bytearray()

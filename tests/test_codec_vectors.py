@@ -149,3 +149,11 @@ def test_varint_extremes():
     for v in (0, 1, 127, 128, 2 ** 31, 2 ** 63 - 1, -2 ** 63, -1):
         row = oracle.row_write([INT], [(0, v)])
         assert oracle.row_read([INT], row) == [v]
+
+
+def test_encode_kv_layout():
+    """LogEncoderTest.KVTest (src/kvstore/test/LogEncoderTest.cpp:117-122): the raft snapshot record
+    ngx_load_snapshot_rows ingests."""
+    rec = kvfmt.encode_kv(b"KV_key", b"KV_val")
+    assert rec == struct.pack("<II", 6, 6) + b"KV_keyKV_val"
+    assert kvfmt.decode_kv(rec) == (b"KV_key", b"KV_val")

@@ -109,6 +109,9 @@ MS_QUERIES = [
     ("GO 2 STEPS FROM {S} OVER e WHERE $^.vt.v0 > 100 && e.p0 % 3 == 0 YIELD $^.vt.name, e.p0 + e.p1", True),
     ("GO 3 STEPS FROM {S} OVER e YIELD DISTINCT e._dst", True),
     ("GO 4 STEPS FROM {S} OVER e WHERE e.p0 < 10 YIELD e._dst, e.p0", False),
+    # $$ props of destinations on other shards (tag replicas, GoExecutor.cpp:937-973)
+    ("GO 2 STEPS FROM {S} OVER e WHERE $$.vt.v0 > 100 YIELD $$.vt.name, $$.vt.v0, e._dst", True),
+    ("GO FROM {S} OVER e REVERSELY WHERE $$.vt.name CONTAINS \"3\" YIELD $$.vt.v0 + e.p0, $^.vt.name", True),
 ]
 
 
