@@ -555,7 +555,7 @@ __global__ __launch_bounds__(256) void k_copy_batch(CopyBatch b) {
         const uint64_t off = (u - b.start[k]) * 16;
         const uint64_t left = b.bytes[k] - off;
         if (left >= 16 && ((reinterpret_cast<uintptr_t>(b.src[k]) | reinterpret_cast<uintptr_t>(b.dst[k])) & 15) == 0) {
-            const uint4 v = __builtin_nontemporal_load(reinterpret_cast<const uint4*>(b.src[k] + off));
+            const uint4 v = *reinterpret_cast<const uint4*>(b.src[k] + off);
             *reinterpret_cast<uint4*>(b.dst[k] + off) = v;
         } else {
             const uint64_t m = left < 16 ? left : 16;
