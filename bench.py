@@ -48,6 +48,7 @@ def parse():
     p.add_argument("--parts", type=int, default=100)
     p.add_argument("--cpu-budget", type=float, default=20.0, help="target seconds of oracle GO work (0: skip)")
     p.add_argument("--threads", type=int, default=16, help="host threads for datagen / oracle")
+    p.add_argument("--out-only", action="store_true", help="store out-edges only (no -e in-edge slot)")
     p.add_argument("--host-exchange", action="store_true",
                    help="rehearsal of the N > 1 path on one GPU: every rank on device 0, frontier exchange "
                         "through the host collective (gloo) instead of RCCL")
@@ -111,7 +112,11 @@ def main():
         log(f"[rank 0] libnebula_gn {build['raw']} (sources in tree: {build['tree_sha']}, "
             f"match={build['matches_tree']})")
     t0 = time.time()
-    rows = datagen.rmat(scale, args.ef, 42, args.parts, with_in=False, with_tag=False, rank=rank, world=world,
+    # every out-edge also stored as its in-edge (-e), as InsertEdgeExecutor writes them;
+    # one shard only: the in-edge slot is what the pull hops read (world > 1 pushes, so the 8-GPU run
+    # keeps the out-edge layout and its host memory)
+    with_in = world == 1 and not args.out_only
+    rows = datagen.rmat(scale, args.ef, 42, args.parts, with_in=with_in, with_tag=False, rank=rank, world=world,
                         threads=args.threads)
     log(f"[rank {rank}] generated {rows.n} rows of RMAT scale {scale} in {time.time() - t0:.1f}s")
     eng = engine.Engine(device, rank, world, uid, exchange=xchg)
@@ -244,6 +249,7 @@ def main():
                        "scale": scale, "edge_factor": args.ef, "parts": args.parts, "seeds": args.seeds,
                        "query": QUERY.replace("{S}", f"<{args.seeds} vids>"),
                        "scale_rule": "N=1: 22 (C2), N=8: 26 (C3), else 22+log2(N)",
+                       "edge_layout": "out-edges + in-edges (-e)" if with_in else "out-edges",
                        "parallelism": f"{world} shard(s), part % {world}, "
                                       + ("host (gloo) exchange, all shards on GPU 0 (rehearsal)" if args.host_exchange
                                          else "RCCL bitmap all-to-all per hop")},

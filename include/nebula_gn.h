@@ -323,6 +323,13 @@ int32_t ngx_kernel_stats(ngx_ctx* ctx, const ngx_kernel_stat** out, int32_t* n);
  *          final-hop kernels with hipRTC; 0: run the precompiled bytecode-interpreter kernels.
  *          Literals are launch arguments, so queries that differ only in literals share a kernel.
  *   "jit_cache_capacity"  compiled query shapes kept loaded (LRU, default 64).
+ *   "jit_async"  0 (default) / 1: compile a new query shape on a background thread; until its module is
+ *          ready the queries of that shape run on the interpreter kernels (no hipRTC time on the query's
+ *          critical path). "jit_wait" (any value) blocks until the queued compiles have finished.
+ *   "pull_factor"  direction-optimizing hops: an intermediate hop with E scanned edges over a shard of
+ *          V rows pulls (probes every row's in-edges) when 100 * E >= pull_factor * V and the hop's
+ *          in-edge slots mirror its out-edge slots exactly; default 200, 0 = never. Same results.
+ * Read-only "pull_hops": intermediate hops that pulled so far.
  *   "max_edge_returned_per_vertex"  storaged's flag for the storage requests of every GO hop: at most
  *          this many edges emitted per (vertex, edge type) in key order, counted after the storage
  *          checks and the pushed filter (QueryBaseProcessor.inl:501-505); <= 0: unlimited (default).

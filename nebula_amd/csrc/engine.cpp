@@ -1181,6 +1181,8 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
     if (n == "max_edge_returned_per_vertex") { c->maxEdgesPerVertex = value <= 0 ? INT32_MAX : value; return NGX_OK; }
     if (n == "jit_cache_capacity") { c->jit.capacity = value < 1 ? 1 : static_cast<size_t>(value); return NGX_OK; }
     if (n == "pull_factor") { c->pullFactor = value < 0 ? 0 : value; return NGX_OK; }
+    if (n == "jit_async") { c->jit.async = value != 0; c->jit.device = c->device; return NGX_OK; }
+    if (n == "jit_wait") { c->jit.drain(); return NGX_OK; }
     return fail(c, NGX_E_BAD_ARGUMENT, "unknown flag " + n);
 }
 
@@ -1191,6 +1193,7 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "rccl_timeout_ms") *value = c->rcclTimeoutMs;
     else if (n == "max_edge_returned_per_vertex") *value = c->maxEdgesPerVertex;
     else if (n == "pull_factor") *value = c->pullFactor;
+    else if (n == "jit_async") *value = c->jit.async ? 1 : 0;
     else if (n == "pull_hops") *value = static_cast<int64_t>(c->pullHops);
     else if (n == "jit_compiled") *value = static_cast<int64_t>(c->jit.compiled);
     else if (n == "jit_hits") *value = static_cast<int64_t>(c->jit.hits);

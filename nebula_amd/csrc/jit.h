@@ -8,9 +8,12 @@
 
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
 #include <functional>
 #include <map>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ngx_internal.h"
@@ -51,19 +54,39 @@ public:
     ~JitCache();
     // nullptr when compilation failed (err set). Kernels are cached by query shape (jitShapeKey), at most
     // `capacity` modules (least recently used unloaded first; callers hold no kernel across queries);
-    // `source` generates the hipRTC source on a miss.
+    // `source` generates the hipRTC source on a miss. With `async` set, a miss queues the compile on a
+    // background thread and returns nullptr at once (err "jit: compiling"): the query runs on the
+    // interpreter kernels and a later query of the same shape finds the module (hipRTC's ~170 ms stays
+    // off the query's critical path). Finished modules enter the cache only inside get(), on the
+    // caller's thread, so a module in use by the calling query is never evicted under it.
     const JitKernels* get(const std::string& shape, const std::function<std::string()>& source, std::string& err);
+    // block until every queued compile has finished (tests, warm-up)
+    void drain();
     uint64_t compiled = 0, hits = 0, failed = 0, evicted = 0;
     double compileSeconds = 0;
     int64_t lastRegs = -1, lastScratch = -1;    // hipFuncGetAttribute of the last compiled kernel
     size_t capacity = 64;
+    bool async = false;
+    int device = 0;                             // HIP device the background thread loads modules on
     size_t size() const { return cache_.size(); }
 
 private:
     struct Entry { JitKernels k; uint64_t used = 0; };
+    struct Done { std::string shape; JitKernels k; std::string err; double seconds; int64_t regs, scratch; };
+    void admit();                               // finished background compiles -> cache_ / failures_
+    void insert(const std::string& shape, const JitKernels& k);
     uint64_t tick_ = 0;
     std::map<std::string, Entry> cache_;
     std::map<std::string, std::string> failures_;
+    // background compiler
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::thread worker_;
+    bool stop_ = false;
+    size_t busy_ = 0;                           // jobs queued or compiling
+    std::vector<std::pair<std::string, std::string>> jobs_;   // (shape, full source)
+    std::vector<Done> done_;
+    std::map<std::string, bool> pending_;
 };
 
 // C++ source of the evaluator struct + kernels for one query on one space snapshot (without the

@@ -38,6 +38,8 @@ def _run(e, o, space, q, factor, pushdown=True):
         assert fixtures.normalize_cells(got.rows) == fixtures.normalize_cells(ref.rows)
     if factor == 0:
         assert pulled == 0
+    if factor == 1 and ref.ok and any(got.hop_edges[:-1]):
+        assert pulled > 0                # every intermediate hop with edges pulls when forced
     return pulled
 
 
@@ -68,9 +70,7 @@ def test_pull_rmat12(rmat12, qi, factor):
     ds, o, e = rmat12
     seeds = datagen.sample_vids(900 + qi, 1 << ds.scale, 30)
     q = RMAT_Q[qi].replace("{S}", ", ".join(str(int(v)) for v in seeds))
-    pulled = _run(e, o, ds.space, q, factor)
-    if factor == 1 and "1 TO" not in q and "STEPS" in q:
-        assert pulled > 0
+    _run(e, o, ds.space, q, factor)
 
 
 def test_pull_rmat16_bench_query():
@@ -116,9 +116,7 @@ def test_pull_powerlaw_supernodes(plaw, qi, factor):
     ds, o, e = plaw
     for seeds in ([11, 12, 13], [0, 7919] + [int(v) for v in datagen.sample_vids(40 + qi, ds.n, 10)]):
         q = PL_Q[qi].replace("{S}", ", ".join(str(v) for v in seeds))
-        pulled = _run(e, o, ds.space, q, factor)
-        if factor == 1:
-            assert pulled > 0
+        _run(e, o, ds.space, q, factor)
 
 
 @pytest.fixture(scope="module")
