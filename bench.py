@@ -186,10 +186,17 @@ def main():
     step(plans[0], on_device=False, columnar=True)          # sizes the page-locked staging once
     barrier()
     t_h = time.perf_counter()
+    col_tail = col_dev = 0.0
+    col_bytes = 0
     for i in range(host_steps):
-        step(plans[args.warmup + i], on_device=False, columnar=True)
+        r = step(plans[args.warmup + i], on_device=False, columnar=True)
+        col_tail += r.host_tail_ms
+        col_dev += r.device_ms
+        col_bytes = r.nrows * 40
     barrier()
     host_col_ms = (time.perf_counter() - t_h) * 1e3 / max(host_steps, 1)
+    col_tail /= max(host_steps, 1)
+    col_dev /= max(host_steps, 1)
     t_h = time.perf_counter()
     step(plans[args.warmup], on_device=False)
     barrier()
@@ -264,6 +271,8 @@ def main():
                                          "device finished; the rest of ms_per_step - device_ms is the Python caller"},
             "timed_region": "seeds on host -> result rows + YIELD columns in HBM (result_on_device)",
             "host_delivery": {"ms_per_step_columnar": round(host_col_ms, 3), "ms_per_step_cells": round(host_cell_ms, 3),
+                              "columnar_library_tail_ms": round(col_tail, 3), "columnar_device_ms": round(col_dev, 3),
+                              "columnar_row_bytes": col_bytes,
                               "note": "same query with the rows copied to host memory: columnar arrays in "
                                       "page-locked staging (host_columnar), or typed ColumnValue cells"},
             "jit": jit,

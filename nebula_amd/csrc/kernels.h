@@ -135,13 +135,13 @@ int launchFinal(const FinalArgs& a, hipStream_t s);
 // row r joins the next frontier iff one of its in-neighbours over a hop slot's MIRROR slot (-t for t,
 // verified at commit to be the exact transpose of t) is in the current frontier (cur[g] == curEp).
 // Same set as the push expansion (getDstIdsFromResp, GoExecutor.cpp:675-718), fewer random accesses
-// when the frontier's edges outnumber the shard's rows. A thread probes up to kPullProbe in-neighbours
-// per slot of its row; longer in-lists left unresolved go to a segment queue (kPullSeg in-edges per
-// segment) that the workgroups drain after their rows, so a supernode spreads over many workgroups.
-// Reached rows get out[r] = ep. seg: segCap words and ctl[0..3) zero between launches (the kernel's
-// last workgroup leaves them zero).
+// when the frontier's edges outnumber the shard's rows. Two launches: a row pass (a thread per row,
+// up to kPullProbe in-neighbours per slot with early exit) and a segment pass over the longer in-lists
+// still unresolved (kPullSeg in-edges per segment, a workgroup each), so a supernode spreads over many
+// workgroups. Reached rows get out[r] = ep. ctl[0..3) is zero between launches (the segment pass's
+// last workgroup leaves it so).
 constexpr int kPullMaxSlots = 4;
-constexpr int kPullProbe = 8;
+constexpr int kPullProbe = 32;
 constexpr uint64_t kPullSeg = 1024;
 struct PullArgs {
     int32_t n;
@@ -152,7 +152,7 @@ struct PullArgs {
     uint64_t V;
     uint64_t* seg;
     uint64_t segCap;
-    uint32_t* ctl;                         // [0] segments reserved, [1] taken, [2] workgroups done
+    uint32_t* ctl;                         // [0] segments reserved, [2] segment-pass workgroups done
     uint32_t* err;                         // [3] queue overflow / spin limit (device fault)
     uint8_t curEp, ep;
 };

@@ -418,18 +418,18 @@ __global__ __launch_bounds__(WG) void k_compact_lb(CompactArgs a) {
 }
 
 // ------------------------------------------------------------------------------ pull (direction-optimizing) hop
-// Segment word: ready bit | k (27 bits: segment index in the row's remaining in-list) | slot (4) | row (32).
-// One 8-byte agent-scope store publishes it whole: the consumer reads nothing else the producer wrote
-// (offsets, in-lists and frontier marks are read-only during the launch).
+// Segment word: k (28 bits: segment index in the row's remaining in-list) | slot (4) | row (32).
 __device__ __forceinline__ uint64_t pullSegWord(uint32_t row, int s, uint64_t k) {
-    return (1ULL << 63) | (k << 36) | (static_cast<uint64_t>(s) << 32) | row;
+    return (k << 36) | (static_cast<uint64_t>(s) << 32) | row;
 }
 
+// Row pass: one thread per row; up to kPullProbe in-neighbours per slot, loaded 8 at a time and
+// probed two per round, the next round only while the row is unresolved. Rows whose in-list is longer
+// and still unresolved reserve segment words (one atomicAdd per workgroup) for k_pull_segments.
 template <bool ONE>
 __global__ __launch_bounds__(WG) void k_pull(PullArgs a) {
     __shared__ uint64_t sm[NW + 1];
     __shared__ uint32_t sBase;
-    __shared__ uint64_t sSeg;
     const int ns = ONE ? 1 : a.n;
     const uint64_t r = static_cast<uint64_t>(blockIdx.x) * WG + threadIdx.x;
     uint64_t rb[kPullMaxSlots], re[kPullMaxSlots];
@@ -445,18 +445,19 @@ __global__ __launch_bounds__(WG) void k_pull(PullArgs a) {
 #pragma unroll
         for (int s = 0; s < kPullMaxSlots; s++) {
             if (s >= ns || found) break;
-            const uint64_t b = rb[s], e = re[s];
+            const uint64_t e = re[s];
             const uint32_t* in = a.isrc[s];
-            uint32_t u[kPullProbe];
+            for (uint64_t b = rb[s]; b < e && b < rb[s] + kPullProbe && !found; b += 8) {
+                uint32_t u[8];
 #pragma unroll
-            for (int k = 0; k < kPullProbe; k++) u[k] = b + k < e ? in[b + k] : kNoRow;
-            // two frontier probes per round, next round only for rows still unresolved
+                for (int k = 0; k < 8; k++) u[k] = b + k < e ? in[b + k] : kNoRow;
 #pragma unroll
-            for (int k = 0; k < kPullProbe; k += 2) {
-                if (found) break;
-                const bool h0 = u[k] != kNoRow && a.cur[u[k]] == a.curEp;
-                const bool h1 = u[k + 1] != kNoRow && a.cur[u[k + 1]] == a.curEp;
-                found = h0 || h1;
+                for (int k = 0; k < 8; k += 2) {
+                    if (found) break;
+                    const bool h0 = u[k] != kNoRow && a.cur[u[k]] == a.curEp;
+                    const bool h1 = u[k + 1] != kNoRow && a.cur[u[k + 1]] == a.curEp;
+                    found = h0 || h1;
+                }
             }
         }
         if (found) {
@@ -469,7 +470,6 @@ __global__ __launch_bounds__(WG) void k_pull(PullArgs a) {
             }
         }
     }
-    // rows with longer in-lists: reserve queue words for their remaining segments
     if (__syncthreads_or(nseg != 0)) {
         uint64_t tot;
         const uint64_t pre = blockExScan(nseg, tot, sm);
@@ -481,68 +481,53 @@ __global__ __launch_bounds__(WG) void k_pull(PullArgs a) {
                 if (re[s] <= rb[s] + kPullProbe) continue;
                 const uint64_t cnt = (re[s] - rb[s] - kPullProbe + kPullSeg - 1) / kPullSeg;
                 for (uint64_t k = 0; k < cnt; k++, at++) {
-                    if (at < a.segCap) __hip_atomic_store(a.seg + at, pullSegWord(static_cast<uint32_t>(r), s, k),
-                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (at < a.segCap) a.seg[at] = pullSegWord(static_cast<uint32_t>(r), s, k);
                     else atomicOr(a.err + 3, 1u);
                 }
             }
         }
     }
-    // drain the queue: take segments while any are reserved and not yet taken
-    for (;;) {
-        if (threadIdx.x == 0) {
-            uint64_t w = 0;
-            uint32_t nx = __hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (;;) {
-                const uint32_t rs = __hip_atomic_load(&a.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (nx >= rs || nx >= a.segCap) break;
-                if (__hip_atomic_compare_exchange_strong(&a.ctl[1], &nx, nx + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT)) {
-                    // its producer has reserved it and is writing it
-                    uint64_t* p = a.seg + nx;
-                    uint32_t spins = 0;
-                    while ((w = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
-                        if (++spins > (1u << 24)) { atomicOr(a.err + 3, 1u); break; }
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-                    __hip_atomic_store(p, 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // zero for the next launch
-                    break;
-                }
-            }
-            sSeg = w;
-        }
-        __syncthreads();
-        const uint64_t w = sSeg;
-        if (w == 0) break;
+}
+
+// Segment pass (the next launch on the stream, so every segment word is visible): a workgroup per
+// segment of kPullSeg in-edges, grid-stride; any hit marks the row. The last workgroup out leaves
+// the counters zero for the next hop.
+__global__ __launch_bounds__(WG) void k_pull_segments(PullArgs a) {
+    const uint32_t nres = __hip_atomic_load(&a.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t n = nres < a.segCap ? nres : a.segCap;
+    for (uint64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const uint64_t w = a.seg[i];
         const uint32_t row = static_cast<uint32_t>(w);
         const int s = static_cast<int>((w >> 32) & 0xF);
-        const uint64_t k = (w >> 36) & ((1ULL << 27) - 1);
+        const uint64_t k = w >> 36;
         const uint64_t e = a.ioff[s][row + 1];
         const uint64_t b = a.ioff[s][row] + kPullProbe + k * kPullSeg;
         const uint64_t be = b + kPullSeg < e ? b + kPullSeg : e;
         const uint32_t* in = a.isrc[s];
-        bool hit = false;
         uint32_t u[kPullSeg / WG];
 #pragma unroll
         for (int j = 0; j < static_cast<int>(kPullSeg / WG); j++) {
             const uint64_t p = b + threadIdx.x + static_cast<uint64_t>(j) * WG;
             u[j] = p < be ? in[p] : kNoRow;
         }
+        bool hit = false;
 #pragma unroll
         for (int j = 0; j < static_cast<int>(kPullSeg / WG); j++) hit |= u[j] != kNoRow && a.cur[u[j]] == a.curEp;
         if (hit) a.out[row] = a.ep;
-        __syncthreads();                                  // sSeg is rewritten by the next take
     }
-    // the last workgroup out leaves the queue counters zero for the next launch (every segment is
-    // taken and finished by then: each workgroup drains after its own reservations)
+    __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t d = atomicAdd(&a.ctl[2], 1u);
         if (d == gridDim.x - 1) {
             __hip_atomic_store(&a.ctl[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&a.ctl[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+}
+
+__global__ void k_mark_rows(const uint32_t* F, uint64_t n, uint8_t* marks, uint8_t ep) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n && F[i] != kNoRow) marks[F[i]] = ep;
 }
 
 // 16-byte units of a batch of arrays, grid-stride; unit u of array k covers bytes [16 (u - start[k]) ..)
@@ -564,10 +549,6 @@ __global__ __launch_bounds__(256) void k_copy_batch(CopyBatch b) {
     }
 }
 
-__global__ void k_mark_rows(const uint32_t* F, uint64_t n, uint8_t* marks, uint8_t ep) {
-    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i < n && F[i] != kNoRow) marks[F[i]] = ep;
-}
 
 // ------------------------------------------------------------------------------ final hop (interpreter)
 struct VmEv {
@@ -874,6 +855,8 @@ int launchPull(const PullArgs& a, hipStream_t s) {
     dim3 grid(static_cast<unsigned>((a.V + WG - 1) / WG));
     if (a.n == 1) hipLaunchKernelGGL((k_pull<true>), grid, dim3(WG), 0, s, a);
     else hipLaunchKernelGGL((k_pull<false>), grid, dim3(WG), 0, s, a);
+    // long unresolved in-lists: at most a.segCap segments, 2 workgroups per CU striding over them
+    hipLaunchKernelGGL(k_pull_segments, dim3(512), dim3(WG), 0, s, a);
     return static_cast<int>(hipGetLastError());
 }
 
