@@ -116,6 +116,7 @@ struct ngx_ctx {
     int cmpPar = 0;
     DBuf oSrc, oDst, oRank, oType, oEntry, progBuf, sendBits, recvBits, vcells, misc, oColDesc, edgeMask;
     DBuf oFlags, rowCols, rowLen, rowOff, rowBytes;     // GetNeighbors response rows (encode_rows)
+    DBuf dkTable, dkKeep, dkPre, dSrc, dDst, dRank, dType;   // YIELD DISTINCT (table, marks, compacted rows)
     int64_t maxEdgesPerVertex = INT32_MAX;             // storaged FLAGS_max_edge_returned_per_vertex (GO hops)
     struct ColBuf { DBuf x, len, t; };
     struct PinBuf {                                     // page-locked host staging for result D2H
@@ -143,6 +144,7 @@ struct ngx_ctx {
     } hostStage, inStage;
     size_t progStageBytes = 0;                          // bytes of inStage holding this call's programs                               // results D2H / query inputs H2D (programs, seeds)
     std::vector<ColBuf> oCols;                          // result columns (columnar, HBM)
+    std::vector<ColBuf> dCols;                          // DISTINCT: the other half of each column's double buffer
     std::vector<OutCol> oColView;                       // their device pointers, as uploaded to oColDesc
     uint64_t visitedSize = 0;
     uint8_t epoch = 0;
@@ -175,8 +177,10 @@ struct ngx_ctx {
         for (DBuf* b : {&visited, &F0, &F1, &estart, &tileSums, &counters, &lbStatus, &seedPart, &seedVid, &oSrc,
                         &oDst, &oRank, &oType, &oEntry, &chunkFirst, &oColDesc, &progBuf, &sendBits, &recvBits,
                         &vcells, &misc, &edgeMask, &cmpStatus[0], &cmpStatus[1], &oFlags, &rowCols, &rowLen,
-                        &rowOff, &rowBytes, &pullSeg, &pullCtl}) b->release();
+                        &rowOff, &rowBytes, &pullSeg, &pullCtl, &dkTable, &dkKeep, &dkPre, &dSrc, &dDst, &dRank,
+                        &dType}) b->release();
         for (auto& cb : oCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
+        for (auto& cb : dCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         hostStage.release();
         inStage.release();
         for (auto e : eventPool) (void)hipEventDestroy(e);
@@ -1597,7 +1601,6 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         kfBytes += 8 * (wr.srcTag.size() + wr.dstTag.size());
     }
 
-    if (p.result_on_device && p.distinct) return fail(c, NGX_E_UNSUPPORTED, "YIELD DISTINCT needs host results");
     // ---- seeds (starts_), routed by ID_HASH; duplicates kept unless DISTINCT (:123-129)
     std::vector<int64_t> starts(p.starts, p.starts + p.nstarts);
     if (p.distinct) {
@@ -1949,6 +1952,83 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     if (flags[2]) return fail(c, NGX_E_QUERY, "YIELD value does not match its column type (boost::get)");
 
     int32_t nY = static_cast<int32_t>(progs.yOff.size());
+    if (p.distinct && totalRows) {
+        // YIELD DISTINCT (processFinalResult, GoExecutor.cpp:1298-1305) on the device: mark one row of
+        // every group of equal YIELD rows, then move the kept rows of every result array together
+        if (nY > kMaxDistinctCols || totalRows >= (1ULL << 32)) return fail(c, NGX_E_UNSUPPORTED, "DISTINCT over this result");
+        const uint64_t n = totalRows;
+        uint64_t cap = 1024;
+        while (cap < 2 * n) cap <<= 1;
+        DistinctArgs da{};
+        da.n = n;
+        da.nY = nY;
+        OutCol* colsDev = c->oColDesc.get<OutCol>(std::max<int32_t>(nY, 1));
+        HIP_OK(hipMemcpyAsync(colsDev, c->oColView.data(), nY * sizeof(OutCol), hipMemcpyHostToDevice, c->stream));
+        da.cols = colsDev;
+        for (int32_t y = 0; y < nY; y++) {
+            ColView cv;
+            cv.colType = gp.colTypes[y];
+            da.vt[y] = cv.typeAt(0);
+        }
+        da.table = c->dkTable.get<uint64_t>(cap);
+        HIP_OK(hipMemsetAsync(da.table, 0, cap * 8, c->stream));
+        da.mask = cap - 1;
+        da.keep = c->dkKeep.get<uint64_t>(n + 1);
+        uint64_t* pre = c->dkPre.get<uint64_t>(n + 1);
+        uint64_t* tiles = c->tileSums.get<uint64_t>((n + kTile - 1) / kTile + 1);
+        c->timed("distinct", n * 8 * static_cast<uint64_t>(nY), [&] {
+            if (launchDistinctMark(da, c->stream)) throw Error{NGX_E_DEVICE, "distinct"};
+            if (launchScanU64(da.keep, n, pre, tiles, c->stream)) throw Error{NGX_E_DEVICE, "distinct scan"};
+        });
+        const uint64_t kept = readScalar(c, pre + n);
+        ScatterArgs sa{};
+        sa.n = n;
+        sa.keep = da.keep;
+        sa.pre = pre;
+        auto move = [&](DBuf& from, DBuf& to, uint8_t esz) {
+            if (!from.p) return;
+            sa.src[sa.k] = static_cast<const uint8_t*>(from.p);
+            sa.dst[sa.k] = to.get<uint8_t>(std::max<uint64_t>(kept, 1) * esz);
+            sa.esz[sa.k] = esz;
+            sa.k++;
+        };
+        move(c->oSrc, c->dSrc, 8);
+        move(c->oDst, c->dDst, 8);
+        move(c->oRank, c->dRank, 8);
+        if (!constType) move(c->oType, c->dType, 4);
+        if (c->dCols.size() < static_cast<size_t>(nY)) c->dCols.resize(nY);
+        for (int32_t y = 0; y < nY; y++) {
+            if (y < static_cast<int32_t>(yAlias.size()) && yAlias[y] >= 0) continue;
+            if (sa.k + 3 > kMaxScatter) {
+                if (launchScatterKept(sa, c->stream)) throw Error{NGX_E_DEVICE, "distinct scatter"};
+                sa.k = 0;
+            }
+            move(c->oCols[y].x, c->dCols[y].x, 8);
+            if (c->oColView[y].len) move(c->oCols[y].len, c->dCols[y].len, 4);
+            if (c->oColView[y].t) move(c->oCols[y].t, c->dCols[y].t, 1);
+        }
+        if (launchScatterKept(sa, c->stream)) throw Error{NGX_E_DEVICE, "distinct scatter"};
+        // the compacted arrays become the result arrays (the old ones are scratch for the next DISTINCT)
+        std::swap(c->oSrc, c->dSrc);
+        std::swap(c->oDst, c->dDst);
+        std::swap(c->oRank, c->dRank);
+        if (!constType) std::swap(c->oType, c->dType);
+        for (int32_t y = 0; y < nY; y++) {
+            OutCol& v = c->oColView[y];
+            if (y < static_cast<int32_t>(yAlias.size()) && yAlias[y] >= 0) {
+                v.x = static_cast<int64_t*>((yAlias[y] == 0 ? c->oSrc : yAlias[y] == 1 ? c->oDst : c->oRank).p);
+                continue;
+            }
+            const bool hasLen = v.len != nullptr, hasT = v.t != nullptr;
+            std::swap(c->oCols[y].x, c->dCols[y].x);
+            if (hasLen) std::swap(c->oCols[y].len, c->dCols[y].len);
+            if (hasT) std::swap(c->oCols[y].t, c->dCols[y].t);
+            v.x = static_cast<int64_t*>(c->oCols[y].x.p);
+            v.len = hasLen ? static_cast<uint32_t*>(c->oCols[y].len.p) : nullptr;
+            v.t = hasT ? static_cast<uint8_t*>(c->oCols[y].t.p) : nullptr;
+        }
+        totalRows = kept;
+    }
     if (p.result_on_device) {                                 // rows stay in HBM (valid until the next call)
         R.r.nrows = totalRows;
         R.r.dev_src = static_cast<const int64_t*>(c->oSrc.p);
@@ -2030,43 +2110,6 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     R.strings = progs.pool;                                    // string literals of YIELD, kept with the result
     StrMap sm{&d, reinterpret_cast<uint64_t>(dp.pool), &R.strings};
     uint64_t nOut = n;
-    if (p.distinct && n) {                                     // processFinalResult DISTINCT (:1298-1305)
-        // key = every column's value type and bits (string bytes), before the ColumnValue typing, as
-        // boost::hash_range over the VariantType record does
-        std::unordered_set<std::string> seen;
-        seen.reserve(static_cast<size_t>(std::min<uint64_t>(n, 1u << 24)));
-        std::string key;
-        uint64_t w = 0;
-        for (uint64_t r = 0; r < n; r++) {
-            key.clear();
-            for (int32_t y = 0; y < nY; y++) {
-                const ColView& cv = cols[y];
-                uint8_t t = cv.typeAt(r);
-                key.push_back(static_cast<char>(t));
-                if (t == V_STR) {
-                    uint32_t len = cv.len ? cv.len[r] : 0;
-                    key.append(reinterpret_cast<const char*>(&len), 4);
-                    key.append(sm.host(static_cast<uint64_t>(cv.x[r]), len), len);
-                } else {
-                    key.append(reinterpret_cast<const char*>(&cv.x[r]), 8);
-                }
-            }
-            if (!seen.insert(key).second) continue;
-            if (w != r) {                                      // compact in place (w < r)
-                hSrc[w] = hSrc[r]; hDst[w] = hDst[r]; hRank[w] = hRank[r];
-                if (hType) hType[w] = hType[r];
-                for (int32_t y = 0; y < nY; y++) {
-                    ColView& cv = cols[y];
-                    if (y < static_cast<int32_t>(yAlias.size()) && yAlias[y] >= 0) continue;
-                    cv.x[w] = cv.x[r];
-                    if (cv.len) cv.len[w] = cv.len[r];
-                    if (cv.t) cv.t[w] = cv.t[r];
-                }
-            }
-            w++;
-        }
-        nOut = w;
-    }
     R.r.nrows = nOut;
     R.r.dev_type_const = constType ? hs.etype[0] : 0;
     if (p.host_columnar) {

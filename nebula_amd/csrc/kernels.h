@@ -160,6 +160,37 @@ struct PullArgs {
 int launchPull(const PullArgs& a, hipStream_t s);
 // marks[F[i]] = ep for the rows of a frontier list (kNoRow entries skipped)
 int launchMarkRows(const uint32_t* F, uint64_t n, uint8_t* marks, uint8_t ep, hipStream_t s);
+// YIELD DISTINCT on the device (GoExecutor::processFinalResult, GoExecutor.cpp:1298-1305): one row of
+// every group of rows with equal YIELD values is kept. Values are equal when their value types are
+// equal and their bits are, doubles by value (0.0 == -0.0, NaN == NaN: what the reference's
+// boost::hash_range key makes equal), strings by bytes. An open-addressing table (capacity a power of
+// two >= 2n, zeroed) holds (hash high 32 bits << 32 | row + 1); a row either claims an empty slot
+// (keep[r] = 1) or meets an equal row's slot (keep[r] = 0). Which of equal rows is kept is not fixed
+// (GO rows have no fixed order; only the values are returned).
+constexpr int kMaxDistinctCols = 64;
+struct DistinctArgs {
+    uint64_t n;
+    int32_t nY;
+    const OutCol* cols;                 // nY result columns (device array)
+    uint8_t vt[kMaxDistinctCols];       // V_* of column y's rows when cols[y].t is null
+    uint64_t* table;
+    uint64_t mask;
+    uint64_t* keep;                     // n entries
+};
+int launchDistinctMark(const DistinctArgs& a, hipStream_t s);
+// rows r with keep[r] move to pre[r] (exclusive scan of keep) in every array: k arrays of esz-byte
+// elements, src -> dst
+constexpr int kMaxScatter = 48;
+struct ScatterArgs {
+    uint64_t n;
+    const uint64_t* keep;
+    const uint64_t* pre;
+    int32_t k;
+    const uint8_t* src[kMaxScatter];
+    uint8_t* dst[kMaxScatter];
+    uint8_t esz[kMaxScatter];
+};
+int launchScatterKept(const ScatterArgs& a, hipStream_t s);
 // Batched device -> host copy by a kernel: every array is streamed with 16-byte loads and stores into
 // page-locked host memory mapped into the device address space (dst = hipHostGetDevicePointer), so
 // the copy runs at the PCIe write rate on all CUs instead of on one DMA engine.

