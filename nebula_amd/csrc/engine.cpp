@@ -126,7 +126,9 @@ struct ngx_ctx {
             if (bytes > cap) {
                 if (p) (void)hipHostFree(p);
                 p = nullptr;
-                size_t c = std::max(bytes, cap * 3 / 2);
+                // 25 % headroom: result sizes vary from query to query, and re-pinning a GB-sized
+                // staging block costs more than the copy itself
+                size_t c = std::max(bytes + bytes / 4, cap * 3 / 2);
                 HIP_OK(hipHostMalloc(&p, c, hipHostMallocDefault));
                 cap = c;
             }
@@ -1892,10 +1894,20 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             ca.estart = c->estart.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
             ca.chunkFirst = c->chunkFirst.get<uint64_t>(cfCap);
             ca.cfCap = cfCap;
-            ca.status = static_cast<uint64_t*>(c->cmpStatus[c->cmpPar].p);
-            ca.nextStatus = static_cast<uint64_t*>(c->cmpStatus[c->cmpPar ^ 1].p);
-            ca.nNext = c->cmpWords;
-            c->cmpPar ^= 1;
+            // frontier order: tile-reservation order (a set needs none); NGX_COMPACT=ordered keeps row
+            // order through the decoupled look-back (A/B)
+            static const bool ordered = [] { const char* e = std::getenv("NGX_COMPACT"); return e && std::string(e) == "ordered"; }();
+            ca.ordered = ordered;
+            if (ordered) {
+                ca.status = static_cast<uint64_t*>(c->cmpStatus[c->cmpPar].p);
+                ca.nextStatus = static_cast<uint64_t*>(c->cmpStatus[c->cmpPar ^ 1].p);
+                ca.nNext = c->cmpWords;
+                c->cmpPar ^= 1;
+            } else {
+                ca.status = static_cast<uint64_t*>(c->cmpStatus[0].p);   // counter + done, left zero by each launch
+                ca.nextStatus = nullptr;
+                ca.nNext = 0;
+            }
             ca.total = counters + 2;
             ca.pub = nextPub(c);
             ca.zero = lbw;
@@ -2063,9 +2075,9 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     size_t total = 0;
     for (auto& a : arrs) total += (a.bytes + 63) & ~size_t(63);
     char* stage = c->hostStage.get(std::max<size_t>(total, 64));
-    // the copy: a kernel streaming into the mapped staging (all CUs, PCIe write rate; default) or the
-    // DMA engine (NGX_D2H=dma)
-    static const bool dmaCopy = [] { const char* e = std::getenv("NGX_D2H"); return e && std::string(e) == "dma"; }();
+    // the copy: the DMA engine (default; 57 GB/s into page-locked memory, tools/mb_d2h.hip) or a kernel
+    // streaming into the mapped staging (NGX_D2H=kernel, 55 GB/s, occupies the CUs)
+    static const bool dmaCopy = [] { const char* e = std::getenv("NGX_D2H"); return !(e && std::string(e) == "kernel"); }();
     char* stageDev = nullptr;
     if (!dmaCopy && hipHostGetDevicePointer(reinterpret_cast<void**>(&stageDev), c->hostStage.p, 0) != hipSuccess)
         stageDev = nullptr;

@@ -89,6 +89,7 @@ struct CompactArgs {
     uint32_t nzero;
     uint32_t* err;
     uint8_t epoch;
+    bool ordered;                       // frontier in row order (look-back) instead of tile-reservation order
 };
 constexpr uint64_t kCompactLbMaxV = 1ULL << (62 - kFdShift);
 // GO final kernel words: [0] rows reserved (one atomicAdd per chunk), [kDoneOff] chunks finished. Kept

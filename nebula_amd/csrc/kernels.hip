@@ -339,16 +339,25 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
 // shard's segment of visited[] is 16-byte aligned). The tile's packed (rows << kFdShift | degrees) sum
 // goes through the decoupled look-back of final_kernels.h (tiles by ticket, dispatch order), so the
 // marks and offsets are read once (the 3-phase scan read them twice and took three launches).
-template <bool ONE, bool AL>
+//
+// ORD = false (default): the next frontier is a SET (getDstIdsFromResp collects distinct dsts into an
+// unordered set, GoExecutor.cpp:675-718), so tiles need no prefix order: each tile reserves its rows
+// and edges with ONE packed 64-bit atomicAdd (rows << kFdShift | degrees; frontier slots and edge
+// offsets advance together, so estart stays monotonic along the frontier) and the last workgroup out
+// publishes the totals. No look-back chain across the 8 XCDs. status[0] = counter, status[1] = done,
+// zero between launches (the last workgroup resets them).
+template <bool ONE, bool AL, bool ORD>
 __global__ __launch_bounds__(WG) void k_compact_lb(CompactArgs a) {
     __shared__ uint64_t sm[NW + 1];
     __shared__ uint32_t sTile;
     __shared__ uint64_t sPrefix;
-    if (threadIdx.x == 0) sTile = atomicAdd(reinterpret_cast<uint32_t*>(a.status), 1u);
-    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * WG;
-    for (uint64_t z = static_cast<uint64_t>(blockIdx.x) * WG + threadIdx.x; z < a.nNext; z += stride) a.nextStatus[z] = 0;
-    __syncthreads();
-    const uint32_t tile = sTile;
+    if (ORD && threadIdx.x == 0) sTile = atomicAdd(reinterpret_cast<uint32_t*>(a.status), 1u);
+    if (ORD) {
+        const uint64_t stride = static_cast<uint64_t>(gridDim.x) * WG;
+        for (uint64_t z = static_cast<uint64_t>(blockIdx.x) * WG + threadIdx.x; z < a.nNext; z += stride) a.nextStatus[z] = 0;
+        __syncthreads();
+    }
+    const uint32_t tile = ORD ? sTile : blockIdx.x;
     const uint64_t base = static_cast<uint64_t>(tile) * TILE + static_cast<uint64_t>(threadIdx.x) * ITEMS;
     uint32_t flags = 0;
     if (AL && base + ITEMS <= a.V) {
@@ -378,9 +387,15 @@ __global__ __launch_bounds__(WG) void k_compact_lb(CompactArgs a) {
     const uint64_t v = (static_cast<uint64_t>(__popc(flags)) << kFdShift) | dsum;
     uint64_t tot;
     const uint64_t pre = blockExScan(v, tot, sm);
-    if (threadIdx.x < 64) {
-        const uint64_t excl = lookBack(a.status + 1, tile, tot, a.err);
-        if (threadIdx.x == 0) sPrefix = excl;
+    if (ORD) {
+        if (threadIdx.x < 64) {
+            const uint64_t excl = lookBack(a.status + 1, tile, tot, a.err);
+            if (threadIdx.x == 0) sPrefix = excl;
+        }
+    } else if (threadIdx.x == 0) {
+        sPrefix = tot ? static_cast<uint64_t>(atomicAdd(reinterpret_cast<unsigned long long*>(a.status),
+                                                       static_cast<unsigned long long>(tot)))
+                      : 0;
     }
     __syncthreads();
     const uint64_t excl = sPrefix;
@@ -406,7 +421,23 @@ __global__ __launch_bounds__(WG) void k_compact_lb(CompactArgs a) {
         f++;
     }
     if (tile == 0 && threadIdx.x < a.nzero) a.zero[threadIdx.x * kDoneOff] = 0;
-    if (tile == gridDim.x - 1 && threadIdx.x == 0) {
+    if (!ORD) {
+        if (threadIdx.x == 0) {
+            const uint32_t d = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(a.status + 1), 1u, __ATOMIC_ACQ_REL,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            if (d == gridDim.x - 1) {                       // every tile has reserved: the counter is the total
+                const uint64_t incl = __hip_atomic_load(a.status, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                a.estart[(incl >> kFdShift) * static_cast<uint64_t>(ns)] = incl & kFdMask;
+                *a.total = incl;
+                __hip_atomic_store(a.status, 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(a.status + 1, 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (a.pub.slot) {
+                    __hip_atomic_store(a.pub.slot, incl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(a.pub.slot + 1, a.pub.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            }
+        }
+    } else if (tile == gridDim.x - 1 && threadIdx.x == 0) {
         const uint64_t incl = excl + tot;
         a.estart[(incl >> kFdShift) * static_cast<uint64_t>(ns)] = incl & kFdMask;
         *a.total = incl;
@@ -899,12 +930,20 @@ int launchCompactLb(const CompactArgs& a, hipStream_t s) {
     const uint64_t nt = std::max<uint64_t>((a.V + TILE - 1) / TILE, 1);
     const bool al = (reinterpret_cast<uintptr_t>(a.visited) & 15) == 0;
     dim3 grid(static_cast<unsigned>(nt));
-    if (a.hs.n == 1) {
-        if (al) hipLaunchKernelGGL((k_compact_lb<true, true>), grid, dim3(WG), 0, s, a);
-        else hipLaunchKernelGGL((k_compact_lb<true, false>), grid, dim3(WG), 0, s, a);
+    if (a.ordered) {
+        if (a.hs.n == 1) {
+            if (al) hipLaunchKernelGGL((k_compact_lb<true, true, true>), grid, dim3(WG), 0, s, a);
+            else hipLaunchKernelGGL((k_compact_lb<true, false, true>), grid, dim3(WG), 0, s, a);
+        } else {
+            if (al) hipLaunchKernelGGL((k_compact_lb<false, true, true>), grid, dim3(WG), 0, s, a);
+            else hipLaunchKernelGGL((k_compact_lb<false, false, true>), grid, dim3(WG), 0, s, a);
+        }
+    } else if (a.hs.n == 1) {
+        if (al) hipLaunchKernelGGL((k_compact_lb<true, true, false>), grid, dim3(WG), 0, s, a);
+        else hipLaunchKernelGGL((k_compact_lb<true, false, false>), grid, dim3(WG), 0, s, a);
     } else {
-        if (al) hipLaunchKernelGGL((k_compact_lb<false, true>), grid, dim3(WG), 0, s, a);
-        else hipLaunchKernelGGL((k_compact_lb<false, false>), grid, dim3(WG), 0, s, a);
+        if (al) hipLaunchKernelGGL((k_compact_lb<false, true, false>), grid, dim3(WG), 0, s, a);
+        else hipLaunchKernelGGL((k_compact_lb<false, false, false>), grid, dim3(WG), 0, s, a);
     }
     return static_cast<int>(hipGetLastError());
 }
