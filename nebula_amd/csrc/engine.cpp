@@ -1671,7 +1671,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     c->chunkFirst.get<uint64_t>(cfCap);
     uint64_t* lbw = lookBack(c, std::max<uint64_t>(cfCap, kDoneOff));   // GO final words: [0] rows, [kDoneOff] done
     if (lbCompact) {
-        const uint64_t words = (d.V + kTile - 1) / kTile + 2;
+        const uint64_t words = (d.V + kCompactTile - 1) / kCompactTile + 2;
         if (c->cmpWords < words) {
             for (DBuf& b : c->cmpStatus) {
                 b.get<uint64_t>(words);
@@ -1894,20 +1894,10 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             ca.estart = c->estart.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
             ca.chunkFirst = c->chunkFirst.get<uint64_t>(cfCap);
             ca.cfCap = cfCap;
-            // frontier order: tile-reservation order (a set needs none); NGX_COMPACT=ordered keeps row
-            // order through the decoupled look-back (A/B)
-            static const bool ordered = [] { const char* e = std::getenv("NGX_COMPACT"); return e && std::string(e) == "ordered"; }();
-            ca.ordered = ordered;
-            if (ordered) {
-                ca.status = static_cast<uint64_t*>(c->cmpStatus[c->cmpPar].p);
-                ca.nextStatus = static_cast<uint64_t*>(c->cmpStatus[c->cmpPar ^ 1].p);
-                ca.nNext = c->cmpWords;
-                c->cmpPar ^= 1;
-            } else {
-                ca.status = static_cast<uint64_t*>(c->cmpStatus[0].p);   // counter + done, left zero by each launch
-                ca.nextStatus = nullptr;
-                ca.nNext = 0;
-            }
+            ca.status = static_cast<uint64_t*>(c->cmpStatus[c->cmpPar].p);
+            ca.nextStatus = static_cast<uint64_t*>(c->cmpStatus[c->cmpPar ^ 1].p);
+            ca.nNext = c->cmpWords;
+            c->cmpPar ^= 1;
             ca.total = counters + 2;
             ca.pub = nextPub(c);
             ca.zero = lbw;

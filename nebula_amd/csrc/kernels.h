@@ -67,7 +67,7 @@ int launchCompactDegrees(const uint8_t* visited, uint64_t gbase, uint64_t V, uin
                          Publish pub = Publish{nullptr, 0});
 // Single-pass compaction of an intermediate hop (kernels.hip k_compact_lb): visited[row] == epoch ->
 // next frontier outF, its entries' estart (|F| * hs.n + 1 entries, the last = E) and the next hop's
-// chunk heads chunkFirst (what k_chunk_first computes), in ONE launch: tiles of kTile rows taken by
+// chunk heads chunkFirst (what k_chunk_first computes), in ONE launch: tiles of kCompactTile rows taken by
 // ticket, prefix by decoupled look-back over packed (count << kFdShift | degree) aggregates.
 // status: [0] ticket + one word per tile, zero at launch; the launch clears nextStatus[0 .. nNext)
 // for the launch after it (double buffer, no memset between hops). zero[0 .. nzero): words the next
@@ -89,9 +89,9 @@ struct CompactArgs {
     uint32_t nzero;
     uint32_t* err;
     uint8_t epoch;
-    bool ordered;                       // frontier in row order (look-back) instead of tile-reservation order
 };
 constexpr uint64_t kCompactLbMaxV = 1ULL << (62 - kFdShift);
+constexpr uint64_t kCompactTile = 16384;    // rows per compaction tile (256 threads x 64 rows)
 // GO final kernel words: [0] rows reserved (one atomicAdd per chunk), [kDoneOff] chunks finished. Kept
 // 8 KiB apart: two per-chunk atomics on one cache line serialize at the memory side (+300 us/launch).
 // The seed / compaction kernels clear zero[k * kDoneOff] for k < nzero.
