@@ -91,7 +91,7 @@ struct CompactArgs {
     uint8_t epoch;
 };
 constexpr uint64_t kCompactLbMaxV = 1ULL << (62 - kFdShift);
-constexpr uint64_t kCompactTile = 16384;    // rows per compaction tile (256 threads x 64 rows)
+constexpr uint64_t kCompactTile = 4096;     // rows per compaction tile (256 threads x 16 rows)
 // GO final kernel words: [0] rows reserved (one atomicAdd per chunk), [kDoneOff] chunks finished. Kept
 // 8 KiB apart: two per-chunk atomics on one cache line serialize at the memory side (+300 us/launch).
 // The seed / compaction kernels clear zero[k * kDoneOff] for k < nzero.

@@ -335,15 +335,13 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
 
 // ------------------------------------------------------------------------------ single-pass compaction
 // visited[row] == epoch -> next frontier + its entries' estart + the next hop's chunk heads, one launch.
-// A tile is kCompactTile rows: 64 consecutive rows per thread (four 16-byte loads of their marks when
-// the shard's segment of visited[] is 16-byte aligned). The tile's packed (rows << kFdShift | degrees)
-// sum goes through the decoupled look-back of final_kernels.h (tiles by ticket, dispatch order). The
-// tile is 16 K rows so the look-back chain is short: at 4 K rows the 489 tiles of a 2 M-row shard
-// spent most of the launch in look-back rounds (a frontier of 25 K rows took 20 us); the offsets of a
-// thread's flagged rows are read twice (sum, then write), the second time from cache.
+// A tile is kTile rows (16 consecutive rows per thread; one 16-byte load of their marks when the
+// shard's segment of visited[] is 16-byte aligned). The tile's packed (rows << kFdShift | degrees) sum
+// goes through the decoupled look-back of final_kernels.h (tiles by ticket, dispatch order), so the
+// marks and offsets are read once (the 3-phase scan read them twice and took three launches).
 // (A/B, r02: reserving each tile's range with one packed 64-bit atomicAdd instead — the frontier is a
-// set — ran 113 vs 65 us per step: 489 same-address atomics serialize at the memory side.)
-constexpr int CI = 64;
+// set — ran 113 vs 65 us per step: 489 same-address atomics serialize at the memory side; 16 K-row
+// tiles with 64 rows per thread ran 28 + 47 vs 20 + 38 us for the two compactions of a C2 step.)
 template <bool ONE, bool AL>
 __global__ __launch_bounds__(WG) void k_compact_lb(CompactArgs a) {
     __shared__ uint64_t sm[NW + 1];
@@ -354,35 +352,33 @@ __global__ __launch_bounds__(WG) void k_compact_lb(CompactArgs a) {
     for (uint64_t z = static_cast<uint64_t>(blockIdx.x) * WG + threadIdx.x; z < a.nNext; z += stride) a.nextStatus[z] = 0;
     __syncthreads();
     const uint32_t tile = sTile;
-    const uint64_t base = static_cast<uint64_t>(tile) * kCompactTile + static_cast<uint64_t>(threadIdx.x) * CI;
-    uint64_t flags = 0;
-    if (AL && base + CI <= a.V) {
+    const uint64_t base = static_cast<uint64_t>(tile) * TILE + static_cast<uint64_t>(threadIdx.x) * ITEMS;
+    uint32_t flags = 0;
+    if (AL && base + ITEMS <= a.V) {
+        const uint4 w = *reinterpret_cast<const uint4*>(a.visited + base);
+        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-        for (int q = 0; q < CI / 16; q++) {
-            const uint4 w = *reinterpret_cast<const uint4*>(a.visited + base + 16 * q);
-            const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-            for (int k = 0; k < 16; k++)
-                flags |= static_cast<uint64_t>(((ws[k >> 2] >> (8 * (k & 3))) & 0xFFu) == a.epoch ? 1u : 0u) << (16 * q + k);
-        }
+        for (int k = 0; k < ITEMS; k++) flags |= (((ws[k >> 2] >> (8 * (k & 3))) & 0xFFu) == a.epoch ? 1u : 0u) << k;
     } else {
-        for (int k = 0; k < CI; k++) flags |= static_cast<uint64_t>(base + k < a.V && a.visited[base + k] == a.epoch ? 1u : 0u) << k;
+#pragma unroll
+        for (int k = 0; k < ITEMS; k++) flags |= (base + k < a.V && a.visited[base + k] == a.epoch ? 1u : 0u) << k;
     }
     const int ns = a.hs.n;
+    uint64_t deg[ONE ? ITEMS : 1];
     uint64_t dsum = 0;
-    if (flags) {
-        for (int s = 0; s < (ONE ? 1 : ns); s++) {
-            const uint64_t* off = a.hs.off[s];
-            uint64_t o0 = off[base];
-            for (int k = 0; k < CI; k++) {
-                if (base + k >= a.V) break;
-                const uint64_t o1 = off[base + k + 1];
-                if (flags >> k & 1ULL) dsum += o1 - o0;
-                o0 = o1;
-            }
+#pragma unroll
+    for (int k = 0; k < ITEMS; k++) {
+        if (ONE) deg[k] = 0;
+        if (!(flags >> k & 1u)) continue;
+        const uint64_t r = base + k;
+        if (ONE) {
+            deg[k] = a.hs.off[0][r + 1] - a.hs.off[0][r];
+            dsum += deg[k];
+        } else {
+            for (int s = 0; s < ns; s++) dsum += a.hs.off[s][r + 1] - a.hs.off[s][r];
         }
     }
-    const uint64_t v = (static_cast<uint64_t>(__popcll(flags)) << kFdShift) | dsum;
+    const uint64_t v = (static_cast<uint64_t>(__popc(flags)) << kFdShift) | dsum;
     uint64_t tot;
     const uint64_t pre = blockExScan(v, tot, sm);
     if (threadIdx.x < 64) {
@@ -393,26 +389,24 @@ __global__ __launch_bounds__(WG) void k_compact_lb(CompactArgs a) {
     const uint64_t excl = sPrefix;
     const uint64_t at = excl + pre;
     uint64_t f = at >> kFdShift, e = at & kFdMask;
-    if (flags) {
-        for (int k = 0; k < CI; k++) {
-            if (!(flags >> k & 1ULL)) continue;
-            const uint64_t r = base + k;
-            a.outF[f] = static_cast<uint32_t>(r);
-            if (ONE) {
-                const uint64_t d = a.hs.off[0][r + 1] - a.hs.off[0][r];
-                a.estart[f] = e;
-                writeChunkHeads(a.chunkFirst, a.cfCap, f, e, d, a.err);
+#pragma unroll
+    for (int k = 0; k < ITEMS; k++) {
+        if (!(flags >> k & 1u)) continue;
+        const uint64_t r = base + k;
+        a.outF[f] = static_cast<uint32_t>(r);
+        if (ONE) {
+            a.estart[f] = e;
+            writeChunkHeads(a.chunkFirst, a.cfCap, f, e, deg[k], a.err);
+            e += deg[k];
+        } else {
+            for (int s = 0; s < ns; s++) {
+                const uint64_t d = a.hs.off[s][r + 1] - a.hs.off[s][r];
+                a.estart[f * ns + s] = e;
+                writeChunkHeads(a.chunkFirst, a.cfCap, f * ns + s, e, d, a.err);
                 e += d;
-            } else {
-                for (int s = 0; s < ns; s++) {
-                    const uint64_t d = a.hs.off[s][r + 1] - a.hs.off[s][r];
-                    a.estart[f * ns + s] = e;
-                    writeChunkHeads(a.chunkFirst, a.cfCap, f * ns + s, e, d, a.err);
-                    e += d;
-                }
             }
-            f++;
         }
+        f++;
     }
     if (tile == 0 && threadIdx.x < a.nzero) a.zero[threadIdx.x * kDoneOff] = 0;
     if (tile == gridDim.x - 1 && threadIdx.x == 0) {
@@ -905,7 +899,7 @@ int launchCompactDegrees(const uint8_t* visited, uint64_t gbase, uint64_t V, uin
 
 int launchCompactLb(const CompactArgs& a, hipStream_t s) {
     if (a.V >= kCompactLbMaxV || a.nzero > WG) return 1;
-    const uint64_t nt = std::max<uint64_t>((a.V + kCompactTile - 1) / kCompactTile, 1);
+    const uint64_t nt = std::max<uint64_t>((a.V + TILE - 1) / TILE, 1);
     const bool al = (reinterpret_cast<uintptr_t>(a.visited) & 15) == 0;
     dim3 grid(static_cast<unsigned>(nt));
     if (a.hs.n == 1) {
