@@ -155,6 +155,9 @@ struct ngx_ctx {
     uint64_t pullSegWords = 0;
     int64_t pullFactor = 200;                           // pull when 100 x hop edges >= pullFactor x shard rows (0: never)
     uint64_t pullHops = 0;
+    bool dynHops = true;                                // device-driven hops (no host round trip per hop)
+    DBuf dynStats;                                      // per hop: packed (|F|, E) written by seed / compaction
+    int cus = 256;                                      // compute units of the device
     // RCCL watchdog: collective work must finish within this; else the communicator is aborted
     int64_t rcclTimeoutMs = 120000;
     bool broken = false;                                // communicator aborted: every later call fails
@@ -180,7 +183,7 @@ struct ngx_ctx {
                         &oDst, &oRank, &oType, &oEntry, &chunkFirst, &oColDesc, &progBuf, &sendBits, &recvBits,
                         &vcells, &misc, &edgeMask, &cmpStatus[0], &cmpStatus[1], &oFlags, &rowCols, &rowLen,
                         &rowOff, &rowBytes, &pullSeg, &pullCtl, &dkTable, &dkKeep, &dkPre, &dSrc, &dDst, &dRank,
-                        &dType}) b->release();
+                        &dType, &dynStats}) b->release();
         for (auto& cb : oCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         for (auto& cb : dCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         hostStage.release();
@@ -906,6 +909,8 @@ int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return NGX_E_DEVICE;
     if (hipSetDevice(c->device) != hipSuccess) return NGX_E_DEVICE;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return NGX_E_DEVICE;
+    if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->cus < 1) c->cus = 256;
+    if (const char* dh = std::getenv("NGX_DYN_HOPS")) c->dynHops = std::string(dh) != "0";
     if (hipHostMalloc(reinterpret_cast<void**>(&c->pin), 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
         std::memset(c->pin, 0, 64);
         if (hipHostGetDevicePointer(reinterpret_cast<void**>(&c->pinDev), c->pin, 0) != hipSuccess) c->pinDev = nullptr;
@@ -1188,6 +1193,7 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
     if (n == "jit_cache_capacity") { c->jit.capacity = value < 1 ? 1 : static_cast<size_t>(value); return NGX_OK; }
     if (n == "pull_factor") { c->pullFactor = value < 0 ? 0 : value; return NGX_OK; }
     if (n == "jit_async") { c->jit.async = value != 0; c->jit.device = c->device; return NGX_OK; }
+    if (n == "dyn_hops") { c->dynHops = value != 0; return NGX_OK; }
     if (n == "jit_wait") { c->jit.drain(); return NGX_OK; }
     return fail(c, NGX_E_BAD_ARGUMENT, "unknown flag " + n);
 }
@@ -1200,6 +1206,7 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "max_edge_returned_per_vertex") *value = c->maxEdgesPerVertex;
     else if (n == "pull_factor") *value = c->pullFactor;
     else if (n == "jit_async") *value = c->jit.async ? 1 : 0;
+    else if (n == "dyn_hops") *value = c->dynHops ? 1 : 0;
     else if (n == "pull_hops") *value = static_cast<int64_t>(c->pullHops);
     else if (n == "jit_compiled") *value = static_cast<int64_t>(c->jit.compiled);
     else if (n == "jit_hits") *value = static_cast<int64_t>(c->jit.hits);
@@ -1680,6 +1687,47 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             c->cmpWords = std::min(c->cmpStatus[0].cap, c->cmpStatus[1].cap) / 8;
         }
     }
+    // storage-side request of each hop (getStepOutProps): props only on record hops, TTL info always
+    uint32_t recordPropsMask = 0, ttlMask = 0;
+    int32_t ttlCol[kMaxSlots];
+    int64_t ttlDur[kMaxSlots];
+    for (int s = 0; s < hs.n; s++) {
+        if (gctx.respSchema.count(hs.etype[s]) && !gctx.respSchema[hs.etype[s]].empty()) recordPropsMask |= 1u << s;
+        if (ttlInfo(sp.edge(std::abs(hs.etype[s])), ttlCol[s], ttlDur[s])) ttlMask |= 1u << s;
+    }
+    const int64_t edgeCap = c->maxEdgesPerVertex;              // FLAGS_max_edge_returned_per_vertex
+    const bool capped = edgeCap < INT32_MAX;
+    // Device-driven hops: every kernel reads the frontier size and E that the previous kernel wrote
+    // (dynStats), grids are upper bounds striding over the real work, pull-or-push is decided on the
+    // device; the host enqueues the whole query without waiting (no round trip per hop) and reads the
+    // hop totals once at the end. Single shard, fused seed hop, one record hop, no storage mask.
+    bool intermediateChecks = false;
+    for (int s = 0; s < hs.n; s++) {
+        if ((ttlMask >> s & 1u) && (hs.eflags[s] != nullptr || ttlCol[s] >= 0)) intermediateChecks = true;
+    }
+    const bool dyn = c->dynHops && c->world == 1 && lbCompact && hs.n > 0 && !capped && recordFrom == steps && !pushInvalid &&
+                     !intermediateChecks && !svids.empty() && svids.size() <= kSeedFuseMax &&
+                     svids.size() * static_cast<uint64_t>(hs.n) <= kSeedFuseMax && d.vindex.slots != nullptr;
+    uint64_t* dynStats = dyn ? c->dynStats.get<uint64_t>(steps + 2) : nullptr;
+    const uint64_t pullMinE = pullable ? (static_cast<uint64_t>(c->pullFactor) * d.V + 99) / 100 : ~0ULL;
+    if (dyn && c->epoch + 2 * static_cast<uint64_t>(steps) + 4 > 255) {   // no epoch wrap inside the query
+        HIP_OK(hipMemsetAsync(c->visited.p, 0, c->visitedSize, c->stream));
+        c->epoch = 0;
+    }
+    if (dyn) {
+        // every buffer a hop's kernels use is sized for the whole query before the first launch: a
+        // DBuf that grew later would free memory still read by kernels already enqueued
+        uint64_t mult = 1;
+        {
+            std::unordered_map<int64_t, uint64_t> m;
+            for (int64_t v : svids) mult = std::max<uint64_t>(mult, ++m[v]);
+        }
+        const uint64_t rowsCap = std::max<uint64_t>(d.V, svids.size());
+        c->F0.get<uint32_t>(rowsCap);
+        c->F1.get<uint32_t>(rowsCap);
+        c->estart.get<uint64_t>(rowsCap * static_cast<uint64_t>(hs.n) + 1);
+        c->chunkFirst.get<uint64_t>(std::max<uint64_t>((slotEdges * mult + kChunk - 1) / kChunk + 1, cfCap));
+    }
     bool haveHeads = false;                                    // chunkFirst of the next hop already built
     hipEvent_t t0 = c->ev(), t1 = c->ev();
     R.tLaunch = std::chrono::steady_clock::now();
@@ -1711,10 +1759,10 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             uint64_t* cf = c->chunkFirst.get<uint64_t>(std::max(cf0, cfCap));
             c->timed("seed", nF * 12 + nEnt0 * 24, [&] {
                 if (launchSeedFrontierCf(dp_, dv, nF, d.vindex, hs, F, est0, pub, cf, std::max(cf0, cfCap), lbw, 2, errFlag,
-                                         c->stream))
+                                         c->stream, dynStats))
                     throw Error{NGX_E_DEVICE, "seed"};
             });
-            fusedE = awaitPub(c, pub, est0 + nEnt0);
+            fusedE = dyn ? slotEdges * mult : awaitPub(c, pub, est0 + nEnt0);   // dyn: an upper bound
             haveEstart = true;
             haveHeads = true;
         } else {
@@ -1729,16 +1777,6 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     std::vector<ColSpec> colSpec;
     for (int32_t ct : gp.colTypes) colSpec.push_back(ColSpec{ct == T_UNKNOWN || ct == T_STRING, ct == T_UNKNOWN});
 
-    // storage-side request of each hop (getStepOutProps): props only on record hops, TTL info always
-    uint32_t recordPropsMask = 0, ttlMask = 0;
-    int32_t ttlCol[kMaxSlots];
-    int64_t ttlDur[kMaxSlots];
-    for (int s = 0; s < hs.n; s++) {
-        if (gctx.respSchema.count(hs.etype[s]) && !gctx.respSchema[hs.etype[s]].empty()) recordPropsMask |= 1u << s;
-        if (ttlInfo(sp.edge(std::abs(hs.etype[s])), ttlCol[s], ttlDur[s])) ttlMask |= 1u << s;
-    }
-    const int64_t edgeCap = c->maxEdgesPerVertex;              // FLAGS_max_edge_returned_per_vertex
-    const bool capped = edgeCap < INT32_MAX;
     for (uint32_t h = 1; h <= steps; h++) {
         bool isRecord = h >= recordFrom;
         bool isFinal = h == steps;
@@ -1757,8 +1795,11 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
         }
         haveEstart = false;
         if (isFinal && pushInvalid && nF) return fail(c, NGX_E_QUERY, "Get neighbors failed");
-        R.hopFrontier.push_back(nF);
-        R.hopEdges.push_back(E);
+        if (!dyn) {                                              // dyn: read back after the last hop
+            R.hopFrontier.push_back(nF);
+            R.hopEdges.push_back(E);
+        }
+        const uint64_t* dynTotal = dyn ? dynStats + (h - 1) : nullptr;   // this hop's (|F|, E), device side
         uint64_t chunks = (E + kChunk - 1) / kChunk;
         uint64_t* chunkFirst = c->chunkFirst.get<uint64_t>(std::max<uint64_t>(chunks, 1));
         uint64_t* lb = (isRecord && E) ? lbw : nullptr;        // GO final: [0] rows reserved, [kDoneOff] chunks done
@@ -1823,29 +1864,41 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             a.oEntry = nullptr;
             a.lbStatus = lb;
             a.done = reinterpret_cast<uint32_t*>(lb + kDoneOff);
-            Publish rowsPub = nextPub(c);                       // the last chunk publishes the row count
+            Publish rowsPub = dyn ? Publish{nullptr, 0} : nextPub(c);   // the last chunk publishes the row count
             a.rowsPub = rowsPub.slot;
             a.rowsSeq = rowsPub.seq;
-            c->timed("final", E * (16 + kfBytes), [&] {
+            a.dynTotal = dynTotal;
+            // dyn: as many workgroups as stay resident, striding over the real chunks
+            unsigned grid = static_cast<unsigned>(chunks);
+            if (dyn) {
+                int perCU = 0;
+                if (kj) (void)hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kj->final, 256, 0);
+                else perCU = finalOccupancy(a);
+                grid = static_cast<unsigned>(std::min<uint64_t>(chunks, static_cast<uint64_t>(std::max(perCU, 1)) * c->cus));
+            }
+            c->timed("final", dyn ? 0 : E * (16 + kfBytes), [&] {
                 if (kj) {
                     void* args[] = {&a};
-                    HIP_OK(hipModuleLaunchKernel(kj->final, static_cast<unsigned>(chunks), 1, 1, 256, 1, 1, 0, c->stream, args, nullptr));
-                } else if (launchFinal(a, c->stream)) {
+                    HIP_OK(hipModuleLaunchKernel(kj->final, grid, 1, 1, 256, 1, 1, 0, c->stream, args, nullptr));
+                } else if (launchFinal(a, c->stream, grid)) {
                     throw Error{NGX_E_DEVICE, "final"};
                 }
             });
-            uint64_t nrows = awaitPub(c, rowsPub, a.lbStatus);   // GO: rows reserved by atomicAdd
-            c->addBytes("final", nrows * (24 + 8 * ky));
-            totalRows += nrows;
+            if (!dyn) {
+                uint64_t nrows = awaitPub(c, rowsPub, a.lbStatus);   // GO: rows reserved by atomicAdd
+                c->addBytes("final", nrows * (24 + 8 * ky));
+                totalRows += nrows;
+            }
         }
         if (isFinal) break;
         // ---- expand to the next frontier (set of distinct dsts)
         // pull when the hop's edges outnumber the shard's rows pullFactor/100 times (every row's in-list is
         // probed instead of every frontier edge storing a mark); push otherwise, or when a storage mask
         // (TTL / max-edges) decides which edges count
-        const bool pull = pullable && !mask && E && E * 100 >= static_cast<uint64_t>(c->pullFactor) * d.V;
+        // dyn: both expansions are enqueued and the device takes the one its E selects (pullMinE)
+        const bool pull = dyn ? pullable : pullable && !mask && E && E * 100 >= static_cast<uint64_t>(c->pullFactor) * d.V;
         uint8_t* marks = marksA;
-        if (pull && (curMarks == nullptr || c->epoch >= 254)) {
+        if (pull && (curMarks == nullptr || (!dyn && c->epoch >= 254))) {
             // the seed frontier has no marks yet, or the epoch counter would wrap (clearing every mark)
             // between the frontier's epoch and the pull's: re-mark F after the clear
             if (c->epoch >= 254) {
@@ -1857,6 +1910,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             if (launchMarkRows(F, nF, marksA, curEp, c->stream)) throw Error{NGX_E_DEVICE, "mark rows"};
         }
         uint8_t ep = nextEpoch(c);
+        if (dyn) marks = curMarks == marksA ? marksB : marksA;  // pull and push write the same array
         if (pull) {
             marks = curMarks == marksA ? marksB : marksA;
             pa.cur = curMarks;
@@ -1864,13 +1918,17 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             pa.out = marks + d.gbase;
             pa.ep = ep;
             pa.err = errFlag;
-            c->timed("pull", d.V * (16 * static_cast<uint64_t>(hs.n) + 1), [&] {
+            pa.dyn = dynTotal;
+            pa.minE = pullMinE;
+            c->timed("pull", dyn ? 0 : d.V * (16 * static_cast<uint64_t>(hs.n) + 1), [&] {
                 if (launchPull(pa, c->stream)) throw Error{NGX_E_DEVICE, "pull"};
             });
-            c->pullHops++;
-        } else if (E) {
-            c->timed("expand", E * 8, [&] {
-                if (launchExpandMark(F, estart, chunkFirst, nEnt, E, hs, marksA, ep, pos32, c->stream, mask))
+            if (!dyn) c->pullHops++;
+        }
+        if ((!pull || dyn) && E) {
+            c->timed("expand", dyn ? 0 : E * 8, [&] {
+                if (launchExpandMark(F, estart, chunkFirst, nEnt, E, hs, dyn ? marks : marksA, ep, pos32, c->stream, mask,
+                                     dynTotal, dyn ? pullMinE : ~0ULL))
                     throw Error{NGX_E_DEVICE, "expand"};
             });
         }
@@ -1898,8 +1956,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             ca.nextStatus = static_cast<uint64_t*>(c->cmpStatus[c->cmpPar ^ 1].p);
             ca.nNext = c->cmpWords;
             c->cmpPar ^= 1;
-            ca.total = counters + 2;
-            ca.pub = nextPub(c);
+            ca.total = dyn ? dynStats + h : counters + 2;
+            ca.pub = dyn ? Publish{nullptr, 0} : nextPub(c);
             ca.zero = lbw;
             ca.nzero = 2;
             ca.err = errFlag;
@@ -1907,12 +1965,17 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             c->timed("compact_degrees", 0, [&] {
                 if (launchCompactLb(ca, c->stream)) throw Error{NGX_E_DEVICE, "compact"};
             });
-            uint64_t packed = awaitPub(c, ca.pub, counters + 2);
-            nF = packed >> kFdShift;
-            fusedE = packed & kFdMask;
             haveEstart = true;
             haveHeads = true;
-            c->addBytes("compact_degrees", nF * 8 + nF * static_cast<uint64_t>(hs.n) * 24);
+            if (dyn) {                                          // upper bounds; the device has the real ones
+                nF = d.V;
+                fusedE = slotEdges;
+            } else {
+                uint64_t packed = awaitPub(c, ca.pub, counters + 2);
+                nF = packed >> kFdShift;
+                fusedE = packed & kFdMask;
+                c->addBytes("compact_degrees", nF * 8 + nF * static_cast<uint64_t>(hs.n) * 24);
+            }
         } else if (fuseDeg) {
             // estart sized for any next frontier (every row of the shard) so the next hop's get() keeps it
             uint64_t* est = c->estart.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
@@ -1935,12 +1998,35 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             nF = readScalar(c, counters + 2);
             c->addBytes("compact", nF * 8);
         }
-        R.hopNext.push_back(nF);
+        if (!dyn) R.hopNext.push_back(nF);
         F = Fn;
-        if (nF == 0 && c->world == 1) break;                    // GO_EXIT: empty frontier
+        if (!dyn && nF == 0 && c->world == 1) break;            // GO_EXIT: empty frontier
     }
     HIP_OK(hipEventRecord(t1, c->stream));
     HIP_OK(hipEventSynchronize(t1));
+    if (dyn) {
+        // the hop totals the kernels passed along, and the final kernel's row count
+        std::vector<uint64_t> st(steps);
+        HIP_OK(hipMemcpy(st.data(), dynStats, steps * 8, hipMemcpyDeviceToHost));
+        uint64_t rows = 0;
+        HIP_OK(hipMemcpy(&rows, lbw, 8, hipMemcpyDeviceToHost));
+        for (uint32_t h = 1; h <= steps; h++) {
+            const uint64_t nf = st[h - 1] >> kFdShift, e = st[h - 1] & kFdMask;
+            if (h > 1 && nf == 0) break;                        // GO_EXIT: empty frontier (the kernels idled)
+            R.hopFrontier.push_back(nf);
+            R.hopEdges.push_back(e);
+            if (h < steps) {
+                R.hopNext.push_back(st[h] >> kFdShift);
+                if (pullable && e >= pullMinE) c->pullHops++;
+                c->addBytes(pullable && e >= pullMinE ? "pull" : "expand",
+                            pullable && e >= pullMinE ? d.V * (16 * static_cast<uint64_t>(hs.n) + 1) : e * 8);
+                c->addBytes("compact_degrees", (st[h] >> kFdShift) * (8 + 24 * static_cast<uint64_t>(hs.n)));
+            } else {
+                c->addBytes("final", e * (16 + kfBytes) + rows * (24 + 8 * ky));
+            }
+        }
+        totalRows = rows;
+    }
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, t0, t1));
     c->collectTimings();

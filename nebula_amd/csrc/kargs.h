@@ -81,7 +81,13 @@ struct FinalArgs {
                                         // path); when set, replaces the storage checks. nullptr: none
     int64_t kc[kJitConsts];             // generated kernels: literal bits (string: pool offset)
     uint32_t kl[kJitConsts];            // string literal lengths
+    const uint64_t* dynTotal;           // device-driven hop: packed (frontier rows << kDynShift | E) written by
+                                        // the kernel that built the frontier; nullptr: E / nEnt above
 };
+
+// packed (frontier rows, hop edges) totals of the compaction / seed kernels
+constexpr int kDynShift = 36;
+constexpr uint64_t kDynMask = (1ULL << kDynShift) - 1;
 
 struct VertexCellArgs {
     const uint32_t* rows;

@@ -47,9 +47,12 @@ int launchDegreeScan(const uint32_t* F, uint64_t nEnt, const HopSlots& hs, uint6
 int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst, hipStream_t s, uint64_t* zero = nullptr,
                      uint64_t nzero = 0);
 // mask (nullptr: every edge): only hop edges e with mask[e] != 0 are expanded
+// dyn != nullptr (device-driven hop): E / nEnt are upper bounds, the real ones are read from *dyn; the
+// kernel does nothing when the real E >= pullMinE (the pull kernels take that hop)
+constexpr uint64_t kDynGrid = 2048;                // workgroups of a device-driven (grid-stride) launch
 int launchExpandMark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst, uint64_t nEnt, uint64_t E,
                      const HopSlots& hs, uint8_t* visited, uint8_t epoch, bool pos32, hipStream_t s,
-                     const uint8_t* mask = nullptr);
+                     const uint8_t* mask = nullptr, const uint64_t* dyn = nullptr, uint64_t pullMinE = ~0ULL);
 // storage outcome per hop edge (a.E entries of out: 1 = emitted) for the max-edges / TTL mask path;
 // a's F / estart / chunkFirst / hs / env / P / propsMask / ttl fields are read
 int launchStoragePass(const FinalArgs& a, uint8_t* out, hipStream_t s);
@@ -60,8 +63,8 @@ int launchCompact(const uint8_t* visited, uint64_t gbase, uint64_t V, uint8_t ep
 // fused compaction + next-hop degree scan (kernels.hip FlagDegIn): outF gets the next frontier,
 // estart its entries' edge offsets (|F| * hs.n + 1 entries, the last = E), *packedTotal = |F| << kFdShift | E.
 // Requires V < 2^(64 - kFdShift) and the slots' total edges < 2^kFdShift.
-constexpr int kFdShift = 36;
-constexpr uint64_t kFdMask = (1ULL << kFdShift) - 1;
+constexpr int kFdShift = kDynShift;
+constexpr uint64_t kFdMask = kDynMask;
 int launchCompactDegrees(const uint8_t* visited, uint64_t gbase, uint64_t V, uint8_t epoch, const HopSlots& hs,
                          uint32_t* outF, uint64_t* estart, uint64_t* tileSums, uint64_t* packedTotal, hipStream_t s,
                          Publish pub = Publish{nullptr, 0});
@@ -100,7 +103,7 @@ int launchCompactLb(const CompactArgs& a, hipStream_t s);
 // seed hop variant that also writes chunkFirst (cfCap entries) and clears zero[0 .. nzero)
 int launchSeedFrontierCf(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, const HopSlots& hs,
                          uint32_t* F, uint64_t* estart, Publish pub, uint64_t* chunkFirst, uint64_t cfCap,
-                         uint64_t* zero, uint32_t nzero, uint32_t* err, hipStream_t s);
+                         uint64_t* zero, uint32_t nzero, uint32_t* err, hipStream_t s, uint64_t* packedOut = nullptr);
 // QueryResponse rows of GetNeighbors (storage.thrift IdAndProp.props): per returned edge, the RowWriter
 // row of its type's response edge schema (QueryBoundProcessor.cpp:38-43 with collectProps,
 // QueryBaseProcessor.inl:325-399). Two launches: write == false stores each row's length in rowLen,
@@ -130,7 +133,9 @@ int launchScanU64(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tileS
 // final hop, one pass (interpreter kernel): a.lbStatus zeroed, ceil(E / kChunk) + 1 words; outputs
 // sized for a.oBase + a.E rows. a.oEntry set (GetNeighbors): rows in edge order, rows written = the
 // inclusive status of the last chunk; else (GO) chunks in completion order, rows written = lbStatus[0]
-int launchFinal(const FinalArgs& a, hipStream_t s);
+int launchFinal(const FinalArgs& a, hipStream_t s, unsigned grid = 0);   // grid 0: one workgroup per chunk of a.E
+// resident workgroups per CU of the interpreter final kernel launchFinal would run for `a`
+int finalOccupancy(const FinalArgs& a);
 
 // Direction-optimizing ("pull", Beamer et al. SC'12) intermediate hop, one shard holding every row:
 // row r joins the next frontier iff one of its in-neighbours over a hop slot's MIRROR slot (-t for t,
@@ -156,6 +161,8 @@ struct PullArgs {
     uint32_t* ctl;                         // [0] segments reserved, [2] segment-pass workgroups done
     uint32_t* err;                         // [3] queue overflow / spin limit (device fault)
     uint8_t curEp, ep;
+    const uint64_t* dyn;                   // device-driven hop: packed totals; the row pass does nothing when
+    uint64_t minE;                         // the hop's E < minE (the push expansion takes it)
 };
 // worst-case queue words for in-degrees over the mirror slots: V * n + in-edges / kPullSeg + 1
 int launchPull(const PullArgs& a, hipStream_t s);

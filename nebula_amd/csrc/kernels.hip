@@ -214,7 +214,7 @@ template <bool CF>
 __global__ __launch_bounds__(1024) void k_seed_frontier(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx,
                                                         HopSlots hs, uint32_t* F, uint64_t* estart, Publish pub,
                                                         uint64_t* chunkFirst, uint64_t cfCap, uint64_t* zero,
-                                                        uint32_t nzero, uint32_t* err) {
+                                                        uint32_t nzero, uint32_t* err, uint64_t* packedOut) {
     if (CF && threadIdx.x < nzero) zero[threadIdx.x * kDoneOff] = 0;
     __shared__ uint64_t sm[1024 / 64 + 1];
     constexpr int kPer = static_cast<int>(kSeedFuseMax / 1024);
@@ -265,6 +265,7 @@ __global__ __launch_bounds__(1024) void k_seed_frontier(const int32_t* qpart, co
     }
     if (threadIdx.x == 0) {
         estart[n * hs.n] = sm[16];
+        if (packedOut) *packedOut = (n << kDynShift) | sm[16];       // device-driven hops read this
         if (pub.slot) {
             __hip_atomic_store(pub.slot, sm[16], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(pub.slot + 1, pub.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -290,19 +291,32 @@ __global__ void k_chunk_first(const uint64_t* estart, uint64_t nEnt, uint64_t* c
 // The store is unconditional: a byte store needs no read and duplicates write the same value.
 // P32: CSR positions fit 32 bits (20 KiB chunk map instead of 28, see ChunkMap)
 // MASK: only edges with mask[e] != 0 (the storage outcome of a hop with TTL or a max-edges cap)
+// dyn (device-driven hop): E and the frontier size come from *dyn (packed, written by the kernel that
+// built the frontier); the fixed grid strides over the chunks; a hop with E >= pullMinE is the pull
+// kernels' (they run instead).
 template <bool ONE, bool P32, bool MASK>
 __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst,
                                                     uint64_t nEnt, uint64_t E, HopSlots hs, uint8_t* visited,
-                                                    uint8_t epoch, const uint8_t* mask, int mode) {
+                                                    uint8_t epoch, const uint8_t* mask, int mode, const uint64_t* dyn,
+                                                    uint64_t pullMinE) {
     __shared__ ChunkMap<ONE, false, P32> m;
     // direct-mapped LDS filter of the rows this workgroup already marked: a repeated destination
     // (hubs of a power-law graph) costs an LDS probe instead of another L2 byte-store transaction
     constexpr int kSeenBits = 11;
     __shared__ uint32_t seen[1 << kSeenBits];
+    uint32_t nChunks = gridDim.x;
+    if (dyn != nullptr) {
+        const uint64_t t = *dyn;
+        E = t & kDynMask;
+        if (E >= pullMinE) return;
+        nEnt = (t >> kDynShift) * static_cast<uint64_t>(hs.n);
+        nChunks = static_cast<uint32_t>((E + CE - 1) / CE);
+    }
     for (int p = threadIdx.x; p < (1 << kSeenBits); p += WG) seen[p] = kNoRow;
-    const uint64_t base = static_cast<uint64_t>(blockIdx.x) * CE;
+    for (uint32_t chunk = blockIdx.x; chunk < nChunks; chunk += gridDim.x) {
+    const uint64_t base = static_cast<uint64_t>(chunk) * CE;
     const uint32_t cnt = static_cast<uint32_t>(E - base < CE ? E - base : CE);
-    buildMap<ONE, false, P32>(estart, chunkFirst, nEnt, blockIdx.x, gridDim.x, base, cnt, F, hs, m);
+    buildMap<ONE, false, P32>(estart, chunkFirst, nEnt, chunk, nChunks, base, cnt, F, hs, m);
     uint32_t g[CITEMS];
 #pragma unroll
     for (int k = 0; k < CITEMS; k++) {
@@ -330,6 +344,9 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
         if (seen[h] == g[k]) continue;                  // marked by this workgroup already (its store is issued)
         seen[h] = g[k];
         visited[g[k]] = epoch;
+    }
+    if (dyn == nullptr) break;
+    __syncthreads();                                    // the chunk map is rebuilt for the next chunk
     }
 }
 
@@ -434,7 +451,9 @@ __global__ __launch_bounds__(WG) void k_pull(PullArgs a) {
     __shared__ uint64_t sm[NW + 1];
     __shared__ uint32_t sBase;
     const int ns = ONE ? 1 : a.n;
-    const uint64_t r = static_cast<uint64_t>(blockIdx.x) * WG + threadIdx.x;
+    if (a.dyn != nullptr && (*a.dyn & kDynMask) < a.minE) return;   // a push hop (k_expand_mark takes it)
+    for (uint64_t r0 = static_cast<uint64_t>(blockIdx.x) * WG; r0 < a.V; r0 += static_cast<uint64_t>(gridDim.x) * WG) {
+    const uint64_t r = r0 + threadIdx.x;
     uint64_t rb[kPullMaxSlots], re[kPullMaxSlots];
     uint32_t nseg = 0;
     if (r < a.V) {
@@ -489,6 +508,8 @@ __global__ __launch_bounds__(WG) void k_pull(PullArgs a) {
                 }
             }
         }
+        __syncthreads();                                 // sBase reused by the next rows
+    }
     }
 }
 
@@ -831,16 +852,16 @@ int launchSeedFrontier(const int32_t* qpart, const int64_t* qvid, uint64_t n, VI
                        uint32_t* F, uint64_t* estart, Publish pub, hipStream_t s) {
     if (n * static_cast<uint64_t>(hs.n) > kSeedFuseMax || n > kSeedFuseMax || idx.slots == nullptr) return 1;
     hipLaunchKernelGGL(k_seed_frontier<false>, dim3(1), dim3(1024), 0, s, qpart, qvid, n, idx, hs, F, estart, pub,
-                       nullptr, 0, nullptr, 0u, nullptr);
+                       nullptr, 0, nullptr, 0u, nullptr, nullptr);
     return static_cast<int>(hipGetLastError());
 }
 
 int launchSeedFrontierCf(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, const HopSlots& hs,
                          uint32_t* F, uint64_t* estart, Publish pub, uint64_t* chunkFirst, uint64_t cfCap,
-                         uint64_t* zero, uint32_t nzero, uint32_t* err, hipStream_t s) {
+                         uint64_t* zero, uint32_t nzero, uint32_t* err, hipStream_t s, uint64_t* packedOut) {
     if (n * static_cast<uint64_t>(hs.n) > kSeedFuseMax || n > kSeedFuseMax || idx.slots == nullptr || nzero > 1024) return 1;
     hipLaunchKernelGGL(k_seed_frontier<true>, dim3(1), dim3(1024), 0, s, qpart, qvid, n, idx, hs, F, estart, pub,
-                       chunkFirst, cfCap, zero, nzero, err);
+                       chunkFirst, cfCap, zero, nzero, err, packedOut);
     return static_cast<int>(hipGetLastError());
 }
 
@@ -854,12 +875,14 @@ int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst
 }
 
 int launchExpandMark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst, uint64_t nEnt, uint64_t E,
-                     const HopSlots& hs, uint8_t* visited, uint8_t epoch, bool pos32, hipStream_t s, const uint8_t* mask) {
+                     const HopSlots& hs, uint8_t* visited, uint8_t epoch, bool pos32, hipStream_t s, const uint8_t* mask,
+                     const uint64_t* dyn, uint64_t pullMinE) {
     if (E == 0) return 0;
-    dim3 grid(static_cast<unsigned>((E + CE - 1) / CE));
+    // dyn: E is an upper bound here; the grid strides (kDynGrid workgroups at most)
+    dim3 grid(static_cast<unsigned>(std::min<uint64_t>((E + CE - 1) / CE, dyn ? kDynGrid : ~0u)));
     static const int mode = getenv("NGX_EXPAND_MODE") ? atoi(getenv("NGX_EXPAND_MODE")) : 0;
 #define NGX_EXPAND(ONE, P32, MASK) hipLaunchKernelGGL((k_expand_mark<ONE, P32, MASK>), grid, dim3(WG), 0, s, F, estart, \
-                                                    chunkFirst, nEnt, E, hs, visited, epoch, mask, mode)
+                                                    chunkFirst, nEnt, E, hs, visited, epoch, mask, mode, dyn, pullMinE)
     if (mask) {
         if (hs.n == 1) NGX_EXPAND(true, false, true);
         else NGX_EXPAND(false, false, true);
@@ -922,9 +945,21 @@ int launchScanU64(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tileS
     return scan3(ArrIn{in}, n, WriteArr{out}, tileSums, out + n, s);
 }
 
-int launchFinal(const FinalArgs& a, hipStream_t s) {
+int finalOccupancy(const FinalArgs& a) {
+    int n = 0;
+    if (a.oEntry != nullptr) {
+        if (a.hs.n == 1) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_final<true, true>, WG, 0);
+        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_final<false, true>, WG, 0);
+    } else {
+        if (a.hs.n == 1) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_final<true, false>, WG, 0);
+        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_final<false, false>, WG, 0);
+    }
+    return n > 0 ? n : 1;
+}
+
+int launchFinal(const FinalArgs& a, hipStream_t s, unsigned g) {
     if (a.E == 0) return 0;
-    dim3 grid(static_cast<unsigned>((a.E + CE - 1) / CE));
+    dim3 grid(g ? g : static_cast<unsigned>((a.E + CE - 1) / CE));
     if (a.oEntry != nullptr) {
         if (a.hs.n == 1) hipLaunchKernelGGL((k_final<true, true>), grid, dim3(WG), 0, s, a);
         else hipLaunchKernelGGL((k_final<false, true>), grid, dim3(WG), 0, s, a);
@@ -938,7 +973,7 @@ int launchFinal(const FinalArgs& a, hipStream_t s) {
 int launchPull(const PullArgs& a, hipStream_t s) {
     if (a.V == 0) return 0;
     if (a.n < 1 || a.n > kPullMaxSlots || a.V >= (1ULL << 32)) return 1;
-    dim3 grid(static_cast<unsigned>((a.V + WG - 1) / WG));
+    dim3 grid(static_cast<unsigned>(std::min<uint64_t>((a.V + WG - 1) / WG, a.dyn ? kDynGrid : ~0u)));
     if (a.n == 1) hipLaunchKernelGGL((k_pull<true>), grid, dim3(WG), 0, s, a);
     else hipLaunchKernelGGL((k_pull<false>), grid, dim3(WG), 0, s, a);
     // long unresolved in-lists: at most a.segCap segments, 2 workgroups per CU striding over them

@@ -43,13 +43,16 @@ def _run(e, o, space, q, factor, pushdown=True, mirrored=True):
     return pulled
 
 
-@pytest.fixture(scope="module")
-def rmat12():
+@pytest.fixture(scope="module", params=["dyn", "host"])
+def rmat12(request):
+    """dyn: device-driven hops (the kernels pass |F| and E along, pull-or-push decided on the device);
+    host: the host reads every hop's totals and launches exact grids."""
     ds = fixtures.RmatDataset(12, with_in=True, with_tag=True)
     o = oracle.Oracle()
     o.set_flags(threads=8)
     ds.load_oracle(o)
     e = engine.Engine(0)
+    e.set_flag("dyn_hops", 1 if request.param == "dyn" else 0)
     ds.load_engine(e)
     yield ds, o, e
     e.close()
