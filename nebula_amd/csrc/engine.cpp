@@ -1868,14 +1868,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             a.rowsPub = rowsPub.slot;
             a.rowsSeq = rowsPub.seq;
             a.dynTotal = dynTotal;
-            // dyn: as many workgroups as stay resident, striding over the real chunks
-            unsigned grid = static_cast<unsigned>(chunks);
-            if (dyn) {
-                int perCU = 0;
-                if (kj) (void)hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kj->final, 256, 0);
-                else perCU = finalOccupancy(a);
-                grid = static_cast<unsigned>(std::min<uint64_t>(chunks, static_cast<uint64_t>(std::max(perCU, 1)) * c->cus));
-            }
+            // dyn: chunks of the upper bound E; the workgroups past the real chunks return at once
+            const unsigned grid = static_cast<unsigned>(chunks);
             c->timed("final", dyn ? 0 : E * (16 + kfBytes), [&] {
                 if (kj) {
                     void* args[] = {&a};
