@@ -207,10 +207,23 @@ struct ngx_ctx {
         stats.push_back(Stat{name});
         return static_cast<int>(stats.size()) - 1;
     }
+    // host timeline of a query (NGX_HOST_TRACE=1): launches and publication waits, printed per query
+    bool htrace = false;
+    std::vector<std::pair<std::string, std::chrono::steady_clock::time_point>> hmarks;
+    void hmark(const std::string& what) { if (htrace) hmarks.emplace_back(what, std::chrono::steady_clock::now()); }
+    void hflush() {
+        if (!htrace || hmarks.empty()) return;
+        std::string line = "[ngx host]";
+        for (auto& m : hmarks)
+            line += " " + m.first + "@" + std::to_string(std::chrono::duration<double, std::micro>(m.second - hmarks[0].second).count()).substr(0, 7);
+        std::fprintf(stderr, "%s\n", line.c_str());
+        hmarks.clear();
+    }
     // bracket a launch group with events when profiling
     template <typename F>
     void timed(const char* name, uint64_t algoBytes, F&& f) {
-        if (!prof) { f(); return; }
+        if (htrace) hmark(std::string("L:") + name);
+        if (!prof) { f(); if (htrace) hmark(std::string("l:") + name); return; }
         int k = statIndex(name);
         hipEvent_t a = ev(), b = ev();
         HIP_OK(hipEventRecord(a, stream));
@@ -641,7 +654,10 @@ uint64_t awaitPub(ngx_ctx* c, const Publish& p, const uint64_t* devCopy) {
     if (!p.slot) return readScalar(c, devCopy);
     auto t0 = std::chrono::steady_clock::now();
     for (uint32_t i = 0;; i++) {
-        if (__atomic_load_n(&c->pin[1], __ATOMIC_ACQUIRE) == p.seq) return __atomic_load_n(&c->pin[0], __ATOMIC_RELAXED);
+        if (__atomic_load_n(&c->pin[1], __ATOMIC_ACQUIRE) == p.seq) {
+            c->hmark("pub");
+            return __atomic_load_n(&c->pin[0], __ATOMIC_RELAXED);
+        }
         __builtin_ia32_pause();
         if ((i & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
     }
@@ -911,6 +927,7 @@ int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return NGX_E_DEVICE;
     if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->cus < 1) c->cus = 256;
     if (const char* dh = std::getenv("NGX_DYN_HOPS")) c->dynHops = std::string(dh) != "0";
+    if (const char* ht = std::getenv("NGX_HOST_TRACE")) c->htrace = std::string(ht) == "1";
     if (hipHostMalloc(reinterpret_cast<void**>(&c->pin), 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
         std::memset(c->pin, 0, 64);
         if (hipHostGetDevicePointer(reinterpret_cast<void**>(&c->pinDev), c->pin, 0) != hipSuccess) c->pinDev = nullptr;
@@ -1456,6 +1473,7 @@ std::vector<OutCell> downloadCells(ngx_ctx* c, const std::vector<ColSpec>& spec,
 }
 
 int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
+    c->hmark("in");
     DeviceGraph& d = *sp.dev;
     const int64_t now = p.now_sec > 0 ? p.now_sec : static_cast<int64_t>(std::time(nullptr));   // WallClock
     GoPlan gp;
@@ -1731,6 +1749,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     bool haveHeads = false;                                    // chunkFirst of the next hop already built
     hipEvent_t t0 = c->ev(), t1 = c->ev();
     R.tLaunch = std::chrono::steady_clock::now();
+    c->hmark("start");
     HIP_OK(hipEventRecord(t0, c->stream));
     uint64_t* counters = c->counters.get<uint64_t>(8);
     uint32_t* errFlag = reinterpret_cast<uint32_t*>(counters + 4);
@@ -1998,6 +2017,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     }
     HIP_OK(hipEventRecord(t1, c->stream));
     HIP_OK(hipEventSynchronize(t1));
+    c->hmark("sync");
     if (dyn) {
         // the hop totals the kernels passed along, and the final kernel's row count
         std::vector<uint64_t> st(steps);
@@ -2026,6 +2046,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     c->collectTimings();
     R.r.device_ms = ms;
     R.tDone = std::chrono::steady_clock::now();
+    c->hmark("done");
+    c->hflush();
     uint32_t flags[4];
     HIP_OK(hipMemcpy(flags, errFlag, 16, hipMemcpyDeviceToHost));
     if (flags[3]) return fail(c, NGX_E_DEVICE, "final-hop look-back did not complete (device fault)");
