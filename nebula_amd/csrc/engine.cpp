@@ -155,7 +155,10 @@ struct ngx_ctx {
     uint64_t pullSegWords = 0;
     int64_t pullFactor = 200;                           // pull when 100 x hop edges >= pullFactor x shard rows (0: never)
     uint64_t pullHops = 0;
-    bool dynHops = true;                                // device-driven hops (no host round trip per hop)
+    // device-driven hops (no host round trip per hop). Off by default: on MI355X the upper-bound grids
+    // and the idle launch of the expansion not taken cost what the round trips saved (C2 step: device
+    // 680 vs 656 us, profiles/r02_dyn_*); kept as an option ("dyn_hops", NGX_DYN_HOPS=1)
+    bool dynHops = false;
     DBuf dynStats;                                      // per hop: packed (|F|, E) written by seed / compaction
     int cus = 256;                                      // compute units of the device
     // RCCL watchdog: collective work must finish within this; else the communicator is aborted
@@ -431,6 +434,26 @@ DevPrograms uploadPrograms(ngx_ctx* c, const Programs& pr, const std::vector<int
 }
 
 // seeds (part, vid) to the device through the page-locked input stage, after the programs in it
+// largest number of times one vid appears among the seeds (open addressing; a std::unordered_map
+// took ~30 us for 1000 seeds, on the query's critical path)
+uint64_t maxMultiplicity(const std::vector<int64_t>& v) {
+    size_t cap = 16;
+    while (cap < 2 * v.size()) cap <<= 1;
+    std::vector<int64_t> key(cap);
+    std::vector<uint32_t> cnt(cap, 0);
+    uint64_t best = v.empty() ? 0 : 1;
+    for (int64_t x : v) {
+        uint64_t h = (static_cast<uint64_t>(x) * 0x9E3779B97F4A7C15ULL) >> 20;
+        for (;; h++) {
+            const size_t i = h & (cap - 1);
+            if (cnt[i] == 0) { key[i] = x; cnt[i] = 1; break; }
+            if (key[i] == x) { best = std::max<uint64_t>(best, ++cnt[i]); break; }
+        }
+    }
+    return best;
+}
+
+// seeds (vids then parts) into one device block with one copy; dvid holds n * 12 bytes
 void stageSeeds(ngx_ctx* c, const std::vector<int32_t>& parts, const std::vector<int64_t>& vids, int32_t* dpart,
                 int64_t* dvid) {
     const size_t n = vids.size();
@@ -441,8 +464,12 @@ void stageSeeds(ngx_ctx* c, const std::vector<int32_t>& parts, const std::vector
     char* hp = host + progBytes;
     std::memcpy(hp, vids.data(), n * 8);
     std::memcpy(hp + n * 8, parts.data(), n * 4);
-    HIP_OK(hipMemcpyAsync(dvid, hp, n * 8, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(dpart, hp + n * 8, n * 4, hipMemcpyHostToDevice, c->stream));
+    if (reinterpret_cast<char*>(dpart) == reinterpret_cast<char*>(dvid) + n * 8) {
+        HIP_OK(hipMemcpyAsync(dvid, hp, n * 12, hipMemcpyHostToDevice, c->stream));
+    } else {
+        HIP_OK(hipMemcpyAsync(dvid, hp, n * 8, hipMemcpyHostToDevice, c->stream));
+        HIP_OK(hipMemcpyAsync(dpart, hp + n * 8, n * 4, hipMemcpyHostToDevice, c->stream));
+    }
 }
 
 // VM string pointer -> host bytes
@@ -1735,11 +1762,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     if (dyn) {
         // every buffer a hop's kernels use is sized for the whole query before the first launch: a
         // DBuf that grew later would free memory still read by kernels already enqueued
-        uint64_t mult = 1;
-        {
-            std::unordered_map<int64_t, uint64_t> m;
-            for (int64_t v : svids) mult = std::max<uint64_t>(mult, ++m[v]);
-        }
+        const uint64_t mult = std::max<uint64_t>(maxMultiplicity(svids), 1);
         const uint64_t rowsCap = std::max<uint64_t>(d.V, svids.size());
         c->F0.get<uint32_t>(rowsCap);
         c->F1.get<uint32_t>(rowsCap);
@@ -1759,8 +1782,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     bool haveEstart = false;                                   // estart[] / E of the next hop already built
     uint64_t fusedE = 0;
     if (nF) {
-        int32_t* dp_ = c->seedPart.get<int32_t>(nF);
-        int64_t* dv = c->seedVid.get<int64_t>(nF);
+        int64_t* dv = reinterpret_cast<int64_t*>(c->seedVid.get<uint8_t>(nF * 12));   // vids, then parts
+        int32_t* dp_ = reinterpret_cast<int32_t*>(dv + nF);
         stageSeeds(c, sparts, svids, dp_, dv);
         const uint64_t nEnt0 = nF * static_cast<uint64_t>(hs.n);
         if (hs.n > 0 && nF <= kSeedFuseMax && nEnt0 <= kSeedFuseMax && d.vindex.slots) {
@@ -1769,11 +1792,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
             uint64_t* est0 = c->estart.get<uint64_t>(nEnt0 + 1);
             Publish pub = nextPub(c);
             // seeds may repeat (no DISTINCT): E <= slot edges x the largest multiplicity
-            uint64_t mult = 1;
-            {
-                std::unordered_map<int64_t, uint64_t> m;
-                for (int64_t v : svids) mult = std::max<uint64_t>(mult, ++m[v]);
-            }
+            const uint64_t mult = std::max<uint64_t>(maxMultiplicity(svids), 1);
             const uint64_t cf0 = (slotEdges * mult + kChunk - 1) / kChunk + 1;
             uint64_t* cf = c->chunkFirst.get<uint64_t>(std::max(cf0, cfCap));
             c->timed("seed", nF * 12 + nEnt0 * 24, [&] {
