@@ -513,98 +513,6 @@ __global__ __launch_bounds__(WG) void k_pull(PullArgs a) {
     }
 }
 
-// Row pass for a hop with ONE slot: every thread takes kPullRows rows (strided by the workgroup size,
-// so offset loads stay coalesced) and interleaves their probes: each step issues the loads of all its
-// still-unresolved rows before waiting on any, so a wave keeps kPullRows x more requests in flight
-// (the one-row pass was latency-bound: ~5 dependent round trips per row, 4.6 generations of waves).
-constexpr int kPullRows = 4;
-__global__ __launch_bounds__(WG) void k_pull1(PullArgs a) {
-    __shared__ uint64_t sm[NW + 1];
-    __shared__ uint32_t sBase;
-    if (a.dyn != nullptr && (*a.dyn & kDynMask) < a.minE) return;
-    const uint64_t* ioff = a.ioff[0];
-    const uint32_t* in = a.isrc[0];
-    for (uint64_t r0 = static_cast<uint64_t>(blockIdx.x) * WG * kPullRows; r0 < a.V;
-         r0 += static_cast<uint64_t>(gridDim.x) * WG * kPullRows) {
-        uint64_t b[kPullRows], e[kPullRows];
-        bool live[kPullRows];
-#pragma unroll
-        for (int k = 0; k < kPullRows; k++) {
-            const uint64_t r = r0 + static_cast<uint64_t>(k) * WG + threadIdx.x;
-            live[k] = r < a.V;
-            b[k] = live[k] ? ioff[r] : 0;
-            e[k] = live[k] ? ioff[r + 1] : 0;
-            live[k] = live[k] && e[k] > b[k];
-        }
-        bool found[kPullRows];
-#pragma unroll
-        for (int k = 0; k < kPullRows; k++) found[k] = false;
-        for (int round = 0; round < kPullProbe / 8; round++) {
-            bool any = false;
-#pragma unroll
-            for (int k = 0; k < kPullRows; k++) any |= live[k] && !found[k] && b[k] + 8 * round < e[k];
-            if (!any) break;
-            uint32_t u[kPullRows][8];
-#pragma unroll
-            for (int k = 0; k < kPullRows; k++) {
-                const uint64_t p = b[k] + 8 * round;
-                const bool want = live[k] && !found[k];
-#pragma unroll
-                for (int j = 0; j < 8; j++) u[k][j] = want && p + j < e[k] ? in[p + j] : kNoRow;
-            }
-#pragma unroll
-            for (int j = 0; j < 8; j += 2) {
-                bool h[kPullRows];
-#pragma unroll
-                for (int k = 0; k < kPullRows; k++) {
-                    const bool h0 = u[k][j] != kNoRow && a.cur[u[k][j]] == a.curEp;
-                    const bool h1 = u[k][j + 1] != kNoRow && a.cur[u[k][j + 1]] == a.curEp;
-                    h[k] = h0 || h1;
-                }
-                bool pending = false;
-#pragma unroll
-                for (int k = 0; k < kPullRows; k++) {
-                    found[k] = found[k] || h[k];
-                    pending |= live[k] && !found[k];
-                }
-                if (!pending) break;
-#pragma unroll
-                for (int k = 0; k < kPullRows; k++)           // resolved rows probe nothing more this round
-                    if (found[k]) {
-#pragma unroll
-                        for (int q = 0; q < 8; q++) u[k][q] = kNoRow;
-                    }
-            }
-        }
-        uint32_t nseg = 0;
-#pragma unroll
-        for (int k = 0; k < kPullRows; k++) {
-            const uint64_t r = r0 + static_cast<uint64_t>(k) * WG + threadIdx.x;
-            if (found[k]) a.out[r] = a.ep;
-            else if (live[k] && e[k] > b[k] + kPullProbe)
-                nseg += static_cast<uint32_t>((e[k] - b[k] - kPullProbe + kPullSeg - 1) / kPullSeg);
-        }
-        if (__syncthreads_or(nseg != 0)) {
-            uint64_t tot;
-            const uint64_t pre = blockExScan(nseg, tot, sm);
-            if (threadIdx.x == 0) sBase = atomicAdd(&a.ctl[0], static_cast<uint32_t>(tot));
-            __syncthreads();
-            uint64_t at = sBase + pre;
-#pragma unroll
-            for (int k = 0; k < kPullRows; k++) {
-                if (found[k] || !live[k] || e[k] <= b[k] + kPullProbe) continue;
-                const uint64_t r = r0 + static_cast<uint64_t>(k) * WG + threadIdx.x;
-                const uint64_t cnt = (e[k] - b[k] - kPullProbe + kPullSeg - 1) / kPullSeg;
-                for (uint64_t q = 0; q < cnt; q++, at++) {
-                    if (at < a.segCap) a.seg[at] = pullSegWord(static_cast<uint32_t>(r), 0, q);
-                    else atomicOr(a.err + 3, 1u);
-                }
-            }
-            __syncthreads();
-        }
-    }
-}
-
 // Segment pass (the next launch on the stream, so every segment word is visible): a workgroup per
 // segment of kPullSeg in-edges, grid-stride; any hit marks the row. The last workgroup out leaves
 // the counters zero for the next hop.
@@ -1065,20 +973,11 @@ int launchFinal(const FinalArgs& a, hipStream_t s, unsigned g) {
 int launchPull(const PullArgs& a, hipStream_t s) {
     if (a.V == 0) return 0;
     if (a.n < 1 || a.n > kPullMaxSlots || a.V >= (1ULL << 32)) return 1;
-    if (a.n == 1) {
-        static const bool oneRow = getenv("NGX_PULL_ROWS1") != nullptr;       // A/B: one row per thread
-        if (oneRow) {
-            dim3 grid(static_cast<unsigned>(std::min<uint64_t>((a.V + WG - 1) / WG, a.dyn ? kDynGrid : ~0u)));
-            hipLaunchKernelGGL((k_pull<true>), grid, dim3(WG), 0, s, a);
-        } else {
-            const uint64_t per = static_cast<uint64_t>(WG) * kPullRows;
-            dim3 grid(static_cast<unsigned>(std::min<uint64_t>((a.V + per - 1) / per, a.dyn ? kDynGrid : ~0u)));
-            hipLaunchKernelGGL(k_pull1, grid, dim3(WG), 0, s, a);
-        }
-    } else {
-        dim3 grid(static_cast<unsigned>(std::min<uint64_t>((a.V + WG - 1) / WG, a.dyn ? kDynGrid : ~0u)));
-        hipLaunchKernelGGL((k_pull<false>), grid, dim3(WG), 0, s, a);
-    }
+    // (A/B, r02: four rows per thread with interleaved probes ran 96 vs 76 us per step: the pass is
+    // not short of requests in flight)
+    dim3 grid(static_cast<unsigned>(std::min<uint64_t>((a.V + WG - 1) / WG, a.dyn ? kDynGrid : ~0u)));
+    if (a.n == 1) hipLaunchKernelGGL((k_pull<true>), grid, dim3(WG), 0, s, a);
+    else hipLaunchKernelGGL((k_pull<false>), grid, dim3(WG), 0, s, a);
     // long unresolved in-lists: at most a.segCap segments, 2 workgroups per CU striding over them
     hipLaunchKernelGGL(k_pull_segments, dim3(512), dim3(WG), 0, s, a);
     return static_cast<int>(hipGetLastError());
