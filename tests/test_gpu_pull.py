@@ -212,7 +212,7 @@ def test_pull_needs_exact_mirror(variant):
 
 
 def test_pull_epoch_wrap(rmat12):
-    """300 pulled queries in a row: the one-byte mark epoch wraps (marks cleared, the frontier
+    """140 pulled queries in a row: the one-byte mark epoch wraps (marks cleared, the frontier
     re-marked) several times without losing a frontier."""
     ds, o, e = rmat12
     seeds = datagen.sample_vids(4242, 1 << ds.scale, 8)
@@ -220,6 +220,6 @@ def test_pull_epoch_wrap(rmat12):
     s = ngql.parse_go(q)
     ref = fixtures.normalize_cells(o.go(ds.space, s).rows)
     e.set_flag("pull_factor", 1)
-    for i in range(300):
+    for i in range(140):
         got = e.go(ds.space, s)
         assert got.ok and fixtures.normalize_cells(got.rows) == ref, i
