@@ -180,6 +180,29 @@ def main():
     stats = eng.kernel_stats()
     eng.set_profiling(False)
 
+    # GetNeighbors, the storage boundary (QueryBoundProcessor, the final-hop request GoExecutor sends):
+    # one step's 1000 seeds grouped by part, return columns _dst, p0, p1, pushed filter e.p0 < 50, rows
+    # and typed cells delivered to host memory (reported beside `value`)
+    gn_stats = None
+    if world == 1:
+        seeds0 = [int(v) for v in datagen.rmat_seeds(scale, args.seeds, args.ef, 42, 42, threads=args.threads)]
+        by_part = {}
+        for v in seeds0:
+            by_part.setdefault(v % args.parts + 1, []).append(v)
+        gparts = sorted(by_part.items())
+        gcols = [(engine.EDGE, 1, "_dst"), (engine.EDGE, 1, "p0"), (engine.EDGE, 1, "p1")]
+        gfilt = ngql.Binary(ngql.K_REL, ngql.REL_OPS["<"], ngql.Prop(ngql.K_ALIAS, "", "e", "p0"), ngql.Prim(50)).encode()
+        for _ in range(3):
+            eng.get_neighbors(datagen.RMAT_SPACE, gparts, [1], gcols, gfilt, decode=False)
+        reps = 20
+        t_g = time.perf_counter()
+        for _ in range(reps):
+            gr = eng.get_neighbors(datagen.RMAT_SPACE, gparts, [1], gcols, gfilt, decode=False)
+        g_ms = (time.perf_counter() - t_g) * 1e3 / reps
+        gn_stats = {"request": "1000 vids by part, return _dst/p0/p1, filter e.p0 < 50, cells to host",
+                    "ms_per_request": round(g_ms, 3), "edges_returned": gr.total_edges,
+                    "returned_edges_per_s": round(gr.total_edges / (g_ms / 1e3), 1)}
+
     # the same steps with the rows delivered to host memory (reported, never `value`): columnar arrays
     # in page-locked staging (host_columnar), and typed cells (ColumnValue) built on host threads
     host_steps = min(2, args.steps)
@@ -270,6 +293,7 @@ def main():
                                  "note": "inside ngx_go: before the first launch (plan, programs, seeds) / after the "
                                          "device finished; the rest of ms_per_step - device_ms is the Python caller"},
             "timed_region": "seeds on host -> result rows + YIELD columns in HBM (result_on_device)",
+            "get_neighbors": gn_stats,
             "host_delivery": {"ms_per_step_columnar": round(host_col_ms, 3), "ms_per_step_cells": round(host_cell_ms, 3),
                               "columnar_library_tail_ms": round(col_tail, 3), "columnar_device_ms": round(col_dev, 3),
                               "columnar_row_bytes": col_bytes,

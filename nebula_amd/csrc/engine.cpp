@@ -1470,32 +1470,43 @@ void prepareCols(ngx_ctx* c, FinalArgs& a, const std::vector<ColSpec>& spec, uin
 // result columns rows [first, first + n) -> host OutCells (row-major); a typed column's rows carry its static type
 std::vector<OutCell> downloadCells(ngx_ctx* c, const std::vector<ColSpec>& spec, const std::vector<int32_t>& colTypes,
                                    uint64_t n, uint64_t first) {
+    // every column's arrays in one batch of copies into the page-locked stage, one synchronisation
     size_t nY = spec.size();
     std::vector<OutCell> raw(n * nY);
-    std::vector<int64_t> x(n);
-    std::vector<uint32_t> len(n);
-    std::vector<uint8_t> t(n);
+    if (n == 0 || nY == 0) { HIP_OK(hipStreamSynchronize(c->stream)); return raw; }
+    const size_t per = (n * 13 + 63) & ~size_t(63);
+    char* stage = c->hostStage.get(per * nY);
     for (size_t y = 0; y < nY; y++) {
         const OutCol& v = c->oColView[y];
-        HIP_OK(hipMemcpyAsync(x.data(), v.x + first, n * 8, hipMemcpyDeviceToHost, c->stream));
-        if (v.len) HIP_OK(hipMemcpyAsync(len.data(), v.len + first, n * 4, hipMemcpyDeviceToHost, c->stream));
-        if (v.t) HIP_OK(hipMemcpyAsync(t.data(), v.t + first, n, hipMemcpyDeviceToHost, c->stream));
-        HIP_OK(hipStreamSynchronize(c->stream));
-        uint8_t st = V_ERR;
-        switch (y < colTypes.size() ? colTypes[y] : T_UNKNOWN) {
-            case T_BOOL: st = V_BOOL; break;
-            case T_INT: case T_VID: case T_TIMESTAMP: st = V_INT; break;
-            case T_FLOAT: case T_DOUBLE: st = V_DBL; break;
-            case T_STRING: st = V_STR; break;
-            default: break;
-        }
-        for (uint64_t r = 0; r < n; r++) {
-            OutCell& o = raw[r * nY + y];
-            o.x = x[r];
-            o.len = v.len ? len[r] : 0;
-            o.t = v.t ? t[r] : st;
-        }
+        char* h = stage + per * y;
+        HIP_OK(hipMemcpyAsync(h, v.x + first, n * 8, hipMemcpyDeviceToHost, c->stream));
+        if (v.len) HIP_OK(hipMemcpyAsync(h + n * 8, v.len + first, n * 4, hipMemcpyDeviceToHost, c->stream));
+        if (v.t) HIP_OK(hipMemcpyAsync(h + n * 12, v.t + first, n, hipMemcpyDeviceToHost, c->stream));
     }
+    HIP_OK(hipStreamSynchronize(c->stream));
+    parallelRows(n, [&](uint64_t lo, uint64_t hi, int) {
+        for (size_t y = 0; y < nY; y++) {
+            const OutCol& v = c->oColView[y];
+            const char* h = stage + per * y;
+            const int64_t* x = reinterpret_cast<const int64_t*>(h);
+            const uint32_t* len = reinterpret_cast<const uint32_t*>(h + n * 8);
+            const uint8_t* t = reinterpret_cast<const uint8_t*>(h + n * 12);
+            uint8_t st = V_ERR;
+            switch (y < colTypes.size() ? colTypes[y] : T_UNKNOWN) {
+                case T_BOOL: st = V_BOOL; break;
+                case T_INT: case T_VID: case T_TIMESTAMP: st = V_INT; break;
+                case T_FLOAT: case T_DOUBLE: st = V_DBL; break;
+                case T_STRING: st = V_STR; break;
+                default: break;
+            }
+            for (uint64_t r = lo; r < hi; r++) {
+                OutCell& o = raw[r * nY + y];
+                o.x = x[r];
+                o.len = v.len ? len[r] : 0;
+                o.t = v.t ? t[r] : st;
+            }
+        }
+    });
     return raw;
 }
 
@@ -2587,8 +2598,9 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
     uint64_t* estart = c->estart.get<uint64_t>(nEnt + 1);
     if (nEnt) {
         uint64_t* tiles = c->tileSums.get<uint64_t>((nEnt + kTile - 1) / kTile + 1);
-        if (launchDegreeScan(F, nEnt, hs, estart, tiles, c->stream)) throw Error{NGX_E_DEVICE, "degree"};
-        E = readScalar(c, estart + nEnt);
+        Publish pub = nextPub(c);                                 // E published to host-mapped memory
+        if (launchDegreeScan(F, nEnt, hs, estart, tiles, c->stream, pub)) throw Error{NGX_E_DEVICE, "degree"};
+        E = awaitPub(c, pub, estart + nEnt);
     }
     uint64_t nrows = 0;
     int32_t nY = q.ncols;
@@ -2679,7 +2691,19 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
     if (flags[3]) throw Error{NGX_E_DEVICE, "final-hop look-back did not complete (device fault)"};
     if (flags[1]) throw Error{NGX_E_UNSUPPORTED, "a return column needs a host-only construct"};
     R.edgeCells.resize(nrows * nY);
-    for (uint64_t i = 0; i < nrows * nY; i++) rawCell(raw[i], R.edgeCells[i], R.strings, d, dp, progs.pool);
+    {
+        // typed cells on host threads, per-thread string arenas appended in order afterwards
+        const int T = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(hostThreads(), (nrows * nY) / 65536 + 1)));
+        std::vector<std::string> arena(T);
+        parallelRows(nrows, [&](uint64_t lo, uint64_t hi, int t) {
+            for (uint64_t i = lo * nY; i < hi * nY; i++) rawCell(raw[i], R.edgeCells[i], arena[t], d, dp, progs.pool);
+        }, T);
+        std::vector<uint64_t> base(T);
+        for (int t = 0; t < T; t++) { base[t] = R.strings.size(); R.strings += arena[t]; }
+        parallelRows(nrows, [&](uint64_t lo, uint64_t hi, int t) {
+            for (uint64_t i = lo * nY; i < hi * nY; i++) if (R.edgeCells[i].kind == NGX_CELL_STR) R.edgeCells[i].v.str_off += base[t];
+        }, T);
+    }
     R.vertexCells.resize(nF * nY);
     R.vertexHasTag.assign(nF * nY, 0);
     for (uint64_t i = 0; i < nF * static_cast<uint64_t>(nY); i++) {

@@ -359,7 +359,8 @@ class Engine:
     def get_neighbors(self, space, parts: Sequence[Tuple[int, Sequence[int]]], edge_types: Optional[Sequence[int]],
                       return_columns: Sequence[Tuple[int, int, str]], filter_bytes: bytes = b"",
                       max_edges_per_vertex: int = 2**31 - 1, now_sec: int = 0,
-                      encode_rows: bool = False) -> NeighborsResult:
+                      encode_rows: bool = False, decode: bool = True) -> NeighborsResult:
+        """decode=False: counts and failed codes only (no Python cells; the bench's latency loop)."""
         pid = np.array([p for p, _ in parts], dtype=np.int32)
         nv = np.array([len(v) for _, v in parts], dtype=np.uint32)
         vids = np.array([x for _, v in parts for x in v], dtype=np.int64)
@@ -376,6 +377,10 @@ class Engine:
             if rc and rc not in (NGX_OK,) and r.nfailed == 0:
                 raise EngineError(rc, self.L.ngx_last_error(self.h).decode())
             failed = [(r.failed_codes[2 * i], r.failed_codes[2 * i + 1]) for i in range(r.nfailed)]
+            if not decode:
+                return NeighborsResult(code=r.code, failed_codes=failed, total_edges=r.nedges, edge_vertex=None,
+                                       edge_type=None, edge_dst=None, edge_cells=[], vertex_cells=[],
+                                       vertex_has_tag=None)
             strings = ctypes.string_at(r.strings, r.strings_len) if r.strings_len else b""
             nc = r.ncols
             enc = {}
