@@ -248,6 +248,20 @@ typedef struct {
     int64_t now_sec;                   /* clock for TTL; <= 0: the current time */
     int32_t result_on_device;          /* 1: leave rows in HBM (dev_* below), no host cells / DISTINCT */
     int32_t host_columnar;             /* 1 (host results): columnar host arrays (host_cols), no cells */
+    /* FROM $-.col / $var.col: the interim result of the previous sentence (pipe, GoExecutor fromType_
+     * kPipe / kVariable, GoExecutor.cpp:149-180, :471-509). input_vid_col == NULL: FROM takes `starts'.
+     * The rows are the InterimResult's rows (InterimResult.cpp:178-280); `$-.x' / `$var.x' in WHERE and
+     * YIELD read the input row(s) behind each edge row (getRoots + rowsOfVids, GoExecutor.cpp:1317-1330):
+     * one output row per (edge row, input row whose FROM column holds a root of the edge). Results come
+     * back as host cells (result_on_device and host_columnar are refused). */
+    const char* input_vid_col;         /* the FROM column */
+    const char* input_var;             /* variable name for FROM $var.col; NULL / "" for $- */
+    int32_t input_ncols;
+    const char* const* input_names;    /* column names (YIELD aliases or expression text) */
+    const int32_t* input_types;        /* NGX_T_* column types of the interim schema */
+    uint64_t input_nrows;
+    const ngx_cell* input_cells;       /* [row * input_ncols + col]; NGX_CELL_STR: str_off into input_strings */
+    const char* input_strings;
 } ngx_go_plan;
 
 /* One YIELD column of a device-resident result (result_on_device), columnar in HBM, nrows entries:

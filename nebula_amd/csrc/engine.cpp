@@ -16,6 +16,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <ctime>
+#include <functional>
+#include <set>
+#include <unordered_map>
 #include <thread>
 #include <unordered_set>
 
@@ -1292,7 +1295,53 @@ struct GoPlan {
     std::vector<int32_t> colTypes;
 };
 
-int32_t prepareGo(ngx_ctx* c, const Space& sp, const ngx_go_plan& p, GoPlan& gp) {
+// FROM $-.col / $var.col: the interim result the sentence reads and, during one sub-run, the input
+// row whose values `$-.x' / `$var.x' take (InterimResultIndex::getColumnWithRow,
+// src/graph/InterimResult.cpp:282-297)
+struct InputBind {
+    bool isVar = false;
+    std::string var;
+    std::map<std::string, int32_t> colIdx;                  // columnToIndex_: the last column of a name
+    const ngx_go_plan* p = nullptr;
+    const ngx_cell* row = nullptr;                          // bound row, or none (prepare only)
+    // calculateExprType of kInputProp / kVariableProp (TraverseExecutor.cpp:141-158): the column's
+    // type, UNKNOWN without data or for a column the schema lacks
+    int32_t typeOf(const std::string& col) const {
+        if (!p || p->input_nrows == 0) return T_UNKNOWN;
+        auto it = colIdx.find(col);
+        return it == colIdx.end() ? T_UNKNOWN : p->input_types[it->second];
+    }
+};
+
+// `$-.x' / `$var.x' -> the bound row's value as a constant of its variant type; graphd evaluates them
+// per input row, never at storage (they are not pushable: TraverseExecutor.cpp:512-516)
+int32_t bindRow(ExprNode& n, const InputBind& b, std::string& err) {
+    if (n.kind == K_INPUT_PROP || n.kind == K_VAR_PROP) {
+        auto it = b.colIdx.find(n.prop);
+        if (it == b.colIdx.end()) { err = "Prop `" + n.prop + "' not found"; return NGX_E_QUERY; }
+        const ngx_cell& v = b.row[it->second];
+        n.kind = K_PRIMARY;
+        n.ref.clear(); n.alias.clear(); n.prop.clear();
+        switch (v.kind) {
+            case NGX_CELL_BOOL: n.vtype = 2; n.i = v.v.i != 0; break;
+            case NGX_CELL_INT: case NGX_CELL_ID: case NGX_CELL_TIMESTAMP: n.vtype = 0; n.i = v.v.i; break;
+            case NGX_CELL_FLOAT: case NGX_CELL_DOUBLE: n.vtype = 1; n.d = v.v.d; break;
+            case NGX_CELL_STR:
+                n.vtype = 3;
+                n.s.assign(b.p->input_strings + v.v.str_off, static_cast<size_t>(v.str_len));
+                break;
+            default: err = "Unknown VariantType in the input row"; return NGX_E_BAD_ARGUMENT;
+        }
+        return NGX_OK;
+    }
+    for (auto& k : n.kids) {
+        int32_t rc = bindRow(*k, b, err);
+        if (rc) return rc;
+    }
+    return NGX_OK;
+}
+
+int32_t prepareGo(ngx_ctx* c, const Space& sp, const ngx_go_plan& p, GoPlan& gp, const InputBind* in = nullptr) {
     auto addTypes = [&](int32_t t) {                         // GoExecutor.cpp:297-319
         if (p.direction == NGX_DIR_FORWARD) gp.edgeTypes.push_back(t);
         else if (p.direction == NGX_DIR_REVERSELY) gp.edgeTypes.push_back(-t);
@@ -1341,8 +1390,14 @@ int32_t prepareGo(ngx_ctx* c, const Space& sp, const ngx_go_plan& p, GoPlan& gp)
             gp.yields.push_back(std::move(n));
         }
     }
-    if (gp.refs.variable) return fail(c, NGX_E_QUERY, "A variable must be referred in FROM before used in WHERE or YIELD");
-    if (gp.refs.input) return fail(c, NGX_E_QUERY, "`$-' must be referred in FROM before used in WHERE or YIELD");
+    // prepareNeededProps (GoExecutor.cpp:367-392)
+    if (gp.refs.variable) {
+        if (!in || !in->isVar) return fail(c, NGX_E_QUERY, "A variable must be referred in FROM before used in WHERE or YIELD");
+        if (gp.refs.vars.size() > 1) return fail(c, NGX_E_QUERY, "Only one variable allowed to use");
+        if (*gp.refs.vars.begin() != in->var)
+            return fail(c, NGX_E_QUERY, "Variable name not match: `" + *gp.refs.vars.begin() + "' vs. `" + in->var + "'");
+    }
+    if (gp.refs.input && (!in || in->isVar)) return fail(c, NGX_E_QUERY, "`$-' must be referred in FROM before used in WHERE or YIELD");
     for (auto& tp : gp.refs.srcTag) if (!sp.tagByName.count(tp.first)) return fail(c, NGX_E_QUERY, "Tag `" + tp.first + "' not found.");
     for (auto& tp : gp.refs.dstTag) if (!sp.tagByName.count(tp.first)) return fail(c, NGX_E_QUERY, "Tag `" + tp.first + "' not found.");
     // checkNeededProps (GoExecutor.cpp:422-468)
@@ -1362,7 +1417,21 @@ int32_t prepareGo(ngx_ctx* c, const Space& sp, const ngx_go_plan& p, GoPlan& gp)
         if (es->latest().index(ap.second) < 0) return fail(c, NGX_E_QUERY, "`" + ap.second + "' is not a prop of `" + ap.first + "'");
     }
     for (auto& f : gp.refs.funcs) (void)f;
-    for (auto& y : gp.yields) gp.colTypes.push_back(exprType(*y, sp));
+    for (auto& y : gp.yields) {
+        bool inputCol = in && (y->kind == K_INPUT_PROP || y->kind == K_VAR_PROP);
+        gp.colTypes.push_back(inputCol ? in->typeOf(y->prop) : exprType(*y, sp));
+    }
+    if (in && in->row && (gp.refs.input || gp.refs.variable)) {
+        // the pushed copy was rewritten before binding: input props never reach storage
+        if (gp.where) {
+            int32_t rc = bindRow(*gp.where, *in, err);
+            if (rc) return fail(c, rc, err);
+        }
+        for (auto& y : gp.yields) {
+            int32_t rc = bindRow(*y, *in, err);
+            if (rc) return fail(c, rc, err);
+        }
+    }
     return NGX_OK;
 }
 
@@ -1510,12 +1579,12 @@ std::vector<OutCell> downloadCells(ngx_ctx* c, const std::vector<ColSpec>& spec,
     return raw;
 }
 
-int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
+int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, const InputBind* in = nullptr) {
     c->hmark("in");
     DeviceGraph& d = *sp.dev;
     const int64_t now = p.now_sec > 0 ? p.now_sec : static_cast<int64_t>(std::time(nullptr));   // WallClock
     GoPlan gp;
-    int32_t rc = prepareGo(c, sp, p, gp);
+    int32_t rc = prepareGo(c, sp, p, gp, in);
     if (rc) return rc;
     R.colTypes = gp.colTypes;
     uint32_t recordFrom = p.record_from, steps = p.record_to;
@@ -2295,6 +2364,152 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
     return NGX_OK;
 }
 
+// One YIELD row as a DISTINCT key: boost::hash_range over the record (GoExecutor.cpp:1298-1305), which
+// treats 0.0 and -0.0 as one value; every NaN alike, as the device DISTINCT (kernels.hip dBits)
+void rowKey(const GoResultHolder& S, uint64_t r, int32_t nY, std::string& key) {
+    key.clear();
+    for (int32_t y = 0; y < nY; y++) {
+        const ngx_cell& v = S.cells[r * nY + y];
+        key.push_back(static_cast<char>(v.kind));
+        if (v.kind == NGX_CELL_STR) {
+            uint32_t n = static_cast<uint32_t>(v.str_len);
+            key.append(reinterpret_cast<const char*>(&n), 4);
+            key.append(S.strings.data() + v.v.str_off, n);
+            continue;
+        }
+        uint64_t bits = static_cast<uint64_t>(v.v.i);
+        if (v.kind == NGX_CELL_DOUBLE || v.kind == NGX_CELL_FLOAT) {
+            if (v.v.d == 0.0) bits = 0;
+            else if (v.v.d != v.v.d) bits = 0x7FF8000000000000ULL;
+        }
+        key.append(reinterpret_cast<const char*>(&bits), 8);
+    }
+}
+
+// GO FROM $-.col / $var.col (GoExecutor fromType_ kPipe / kVariable). The reference walks once from the
+// distinct input vids, records per hop which roots reach each vertex (VertexBackTracker,
+// GoExecutor.h:189-207, getDstIdsFromRespWithBackTrack :675-718) and emits each edge row once per input
+// row whose vid is one of the edge's roots (getRoots + rowsOfVids, :1317-1330), evaluating `$-.x' with
+// that row. Per root that is exactly a GO from the root alone: the hop-k frontier of root r is the set
+// of vertices r reaches in k hops, so the rows of root r are the rows of `GO ... FROM r'. The device
+// runs:
+//   - one walk from all distinct vids when no expression reads the input and the sentence has one
+//     step: the root of an edge row is its src, and each row is repeated once per input row of that
+//     vid (the multimap order of rowsOfVid is irrelevant: results are sets of rows);
+//   - one walk per distinct vid when no expression reads the input (rows repeated per input row);
+//   - one walk per input row otherwise, `$-.x' bound to that row's values as constants (device
+//     kernels for the query shape are reused across rows: literals travel in launch slots).
+// DISTINCT (one uniqResult over the whole result, :1298-1305) is the device DISTINCT of every walk,
+// then the union deduplicated here.
+int32_t runPipe(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) {
+    if (p.result_on_device || p.host_columnar)
+        return fail(c, NGX_E_BAD_ARGUMENT, "FROM $-/$var: the result comes back as host cells (no result_on_device / host_columnar)");
+    if (p.input_nrows && (p.input_ncols <= 0 || !p.input_names || !p.input_types || !p.input_cells))
+        return fail(c, NGX_E_BAD_ARGUMENT, "input rows without columns");
+    if (std::string(p.input_vid_col) == "*")                     // prepareFrom (GoExecutor.cpp:175-178)
+        return fail(c, NGX_E_QUERY, "Can not use `*' to reference a vertex id column.");
+    InputBind b;
+    b.p = &p;
+    b.isVar = p.input_var && p.input_var[0];
+    if (b.isVar) b.var = p.input_var;
+    for (int32_t i = 0; i < p.input_ncols; i++) b.colIdx[p.input_names[i] ? p.input_names[i] : ""] = i;
+    // prepareClauses first: its errors come before any about the input (GoExecutor.cpp:92-97)
+    GoPlan probe;
+    int32_t rc = prepareGo(c, sp, p, probe, &b);
+    if (rc) return rc;
+    R.colTypes = probe.colTypes;
+    if (p.input_nrows == 0 || p.record_to == 0) return NGX_OK;      // no data: onEmptyInputs (:119-122)
+    // setupStarts (:471-509): checkIfDuplicateColumn, getDistinctVIDs (a VID or INT column,
+    // RowReader::getVid), buildIndex
+    if (!b.isVar && static_cast<int32_t>(b.colIdx.size()) != p.input_ncols) {    // inputs_ only
+        std::set<std::string> seen;
+        for (int32_t i = 0; i < p.input_ncols; i++)
+            if (!seen.insert(p.input_names[i]).second) return fail(c, NGX_E_QUERY, std::string("Duplicate column `") + p.input_names[i] + "'");
+    }
+    const std::string col = p.input_vid_col;
+    auto ci = b.colIdx.find(col);
+    if (ci == b.colIdx.end() || (p.input_types[ci->second] != T_INT && p.input_types[ci->second] != T_VID))
+        return fail(c, NGX_E_QUERY, "Column `" + col + "' not found");
+    const int32_t vc = ci->second, nc = p.input_ncols;
+    std::vector<int64_t> vids;                                   // distinct, first-seen order
+    std::vector<std::vector<uint64_t>> rowsOf;
+    std::unordered_map<int64_t, uint32_t> group;
+    for (uint64_t r = 0; r < p.input_nrows; r++) {
+        int64_t v = p.input_cells[r * nc + vc].v.i;
+        auto [it, fresh] = group.emplace(v, static_cast<uint32_t>(vids.size()));
+        if (fresh) { vids.push_back(v); rowsOf.emplace_back(); }
+        rowsOf[it->second].push_back(r);
+    }
+    const bool perRow = probe.refs.input || probe.refs.variable;
+    const bool oneWalk = !perRow && p.record_to == 1;
+    const int32_t nY = static_cast<int32_t>(R.colTypes.size());
+    std::unordered_set<std::string> seen;
+    std::string key;
+    bool first = true;
+    // append a walk's rows, each `times(r)' times (DISTINCT: once, and only if new)
+    auto absorb = [&](GoResultHolder& S, const std::function<uint64_t(uint64_t)>& times) {
+        if (first) { R.tLaunch = S.tLaunch; first = false; }
+        R.tDone = S.tDone;
+        R.r.device_ms += S.r.device_ms;
+        auto addv = [](std::vector<uint64_t>& a, const std::vector<uint64_t>& x) {
+            if (a.size() < x.size()) a.resize(x.size(), 0);
+            for (size_t i = 0; i < x.size(); i++) a[i] += x[i];
+        };
+        addv(R.hopFrontier, S.hopFrontier); addv(R.hopEdges, S.hopEdges); addv(R.hopNext, S.hopNext);
+        const uint64_t base = R.strings.size();
+        R.strings += S.strings;
+        for (uint64_t r = 0; r < S.r.nrows; r++) {
+            uint64_t k = times(r);
+            if (p.distinct) {
+                rowKey(S, r, nY, key);
+                k = (k && seen.insert(key).second) ? 1 : 0;
+            }
+            for (uint64_t j = 0; j < k; j++) {
+                for (int32_t y = 0; y < nY; y++) {
+                    ngx_cell cl = S.cells[r * nY + y];
+                    if (cl.kind == NGX_CELL_STR) cl.v.str_off += base;
+                    R.cells.push_back(cl);
+                }
+                R.src.push_back(S.src[r]); R.dst.push_back(S.dst[r]);
+                R.rank.push_back(S.rank[r]); R.type.push_back(S.type[r]);
+            }
+        }
+    };
+    ngx_go_plan sub = p;
+    sub.input_vid_col = nullptr;
+    sub.input_nrows = 0;
+    auto walk = [&](const int64_t* starts, uint64_t n, const ngx_cell* row, GoResultHolder& S) {
+        sub.starts = starts;
+        sub.nstarts = n;
+        b.row = row;
+        S.tIn = std::chrono::steady_clock::now();
+        S.tLaunch = S.tDone = S.tIn;
+        return runGo(c, sp, sub, S, &b);
+    };
+    if (oneWalk) {
+        GoResultHolder S;
+        if ((rc = walk(vids.data(), vids.size(), nullptr, S))) return rc;
+        absorb(S, [&](uint64_t r) { return rowsOf[group.at(S.src[r])].size(); });
+    } else if (!perRow) {
+        for (size_t g = 0; g < vids.size(); g++) {
+            GoResultHolder S;
+            if ((rc = walk(&vids[g], 1, nullptr, S))) return rc;
+            const uint64_t m = rowsOf[g].size();
+            absorb(S, [&](uint64_t) { return m; });
+        }
+    } else {
+        for (size_t g = 0; g < vids.size(); g++) {
+            for (uint64_t r : rowsOf[g]) {
+                GoResultHolder S;
+                if ((rc = walk(&vids[g], 1, p.input_cells + r * nc, S))) return rc;
+                absorb(S, [](uint64_t) { return uint64_t(1); });
+            }
+        }
+    }
+    R.r.nrows = R.src.size();
+    return NGX_OK;
+}
+
 }  // namespace
 
 extern "C" int32_t ngx_go(ngx_ctx* c, const ngx_go_plan* p, ngx_go_result** out) {
@@ -2308,6 +2523,7 @@ extern "C" int32_t ngx_go(ngx_ctx* c, const ngx_go_plan* p, ngx_go_result** out)
         HIP_OK(hipSetDevice(c->device));
         Space* sp = findSpace(c, p->space);
         if (!sp || !sp->dev) rc = fail(c, NGX_E_NOT_LOADED, "space not committed");
+        else if (p->input_vid_col) rc = runPipe(c, *sp, *p, *R);
         else rc = runGo(c, *sp, *p, *R);
     } catch (const Error& e) {
         rc = fail(c, e.code, e.msg);

@@ -143,7 +143,7 @@ void collectRefs(const ExprNode& n, PropRefs& r) {
         case K_SRC_PROP: r.srcTag.emplace(n.alias, n.prop); break;
         case K_DST_PROP: r.dstTag.emplace(n.alias, n.prop); break;
         case K_INPUT_PROP: r.input = true; break;
-        case K_VAR_PROP: r.variable = true; break;
+        case K_VAR_PROP: r.variable = true; r.vars.insert(n.alias); break;
         case K_ALIAS: case K_EDGE_RANK: case K_EDGE_DST: case K_EDGE_SRC: case K_EDGE_TYPE:
             r.alias.emplace(n.alias, n.prop); break;
         case K_FUNC: r.funcs.insert(n.name); break;

@@ -47,6 +47,7 @@ bool rewritePushdown(ExprNode& n);
 struct PropRefs {
     std::set<std::pair<std::string, std::string>> srcTag, dstTag, alias;
     bool input = false, variable = false;
+    std::set<std::string> vars;                  // $var names (ExpressionContext::variables())
     std::set<std::string> funcs;
 };
 void collectRefs(const ExprNode& n, PropRefs& r);

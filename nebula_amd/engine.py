@@ -101,7 +101,35 @@ class GoPlan(ctypes.Structure):
                 ("where", ctypes.c_char_p), ("where_len", c_u32), ("nyields", c_i32),
                 ("yields", P(ctypes.c_char_p)), ("yield_lens", P(c_u32)), ("distinct", c_i32),
                 ("filter_pushdown", c_i32), ("now_sec", c_i64), ("result_on_device", c_i32),
-                ("host_columnar", c_i32)]
+                ("host_columnar", c_i32), ("input_vid_col", ctypes.c_char_p), ("input_var", ctypes.c_char_p),
+                ("input_ncols", c_i32), ("input_names", P(ctypes.c_char_p)), ("input_types", P(c_i32)),
+                ("input_nrows", c_u64), ("input_cells", P(Cell)), ("input_strings", ctypes.c_char_p)]
+
+
+_CELL_KIND = {"empty": 0, "bool": 1, "int": 2, "id": 3, "float": 4, "double": 5, "str": 6, "timestamp": 21}
+
+
+def _input_arrays(inp):
+    """An Interim (nebula_amd.pipeline) as the plan's input_* arrays; the tuple keeps them alive."""
+    nc, nr = len(inp.names), len(inp.rows)
+    names = (ctypes.c_char_p * max(1, nc))(*[n.encode() for n in inp.names])
+    types = (c_i32 * max(1, nc))(*(list(inp.types) + [0] * (nc - len(inp.types))))
+    cells = (Cell * max(1, nr * nc))()
+    strings = bytearray()
+    for r, row in enumerate(inp.rows):
+        for c, (kind, v) in enumerate(row):
+            cl = cells[r * nc + c]
+            cl.kind = _CELL_KIND[kind]
+            if kind == "str":
+                b = v.encode("utf-8", "surrogateescape")
+                cl.v.str_off = len(strings)
+                cl.str_len = len(b)
+                strings += b
+            elif kind in ("float", "double"):
+                cl.v.d = v
+            elif kind != "empty":
+                cl.v.i = int(v)
+    return names, types, cells, bytes(strings) + b"\0", nc, nr
 
 
 class GoResultC(ctypes.Structure):
@@ -411,14 +439,15 @@ class Engine:
     # ---- GO
     def go(self, space: int, s: Union[str, ngql.GoSentence], pushdown: bool = True, now_sec: int = 0,
            raise_on_error: bool = False, rows: bool = True, on_device: bool = False, fetch: bool = False,
-           columnar: bool = False, digest_fn=None, arrays: bool = True) -> GoResult:
+           columnar: bool = False, digest_fn=None, arrays: bool = True, input=None) -> GoResult:
         """Run one GO. rows=False skips decoding cells into Python tuples; on_device=True leaves the
         result rows in HBM (GoResult.nrows and the statistics only); with fetch=True the HBM arrays
         (src/dst/rank/type and the columnar YIELD columns) are copied back into the result.
         columnar=True asks for host_columnar results: no cells; with rows=True they are rebuilt here
         from the columns (ColumnValue typing by col_types) so they compare with the cell path.
         digest_fn(col_types, nrows, x_ptrs, len_ptrs, type_ptrs) is called on the host columns
-        before the result is freed (tests: large-result comparison)."""
+        before the result is freed (tests: large-result comparison). FROM $-.col / $var.col reads
+        `input' (a nebula_amd.pipeline.Interim; None: no input, no rows)."""
         if isinstance(s, str):
             s = ngql.parse_go(s)
         # the sentence's encoded form (expressions in Expression::encode bytes, vids as int64) is built once
@@ -442,6 +471,15 @@ class Engine:
                       names, aliases, 1 if s.over_all else 0, s.direction, where if where else None, len(where),
                       len(yb), yarr, ylen, 1 if s.distinct else 0, 1 if pushdown else 0, now_sec,
                       1 if on_device else 0, 1 if columnar else 0)
+        if s.from_type:
+            from .pipeline import Interim
+            keep = _input_arrays(input if input is not None else Interim([]))
+            names_a, types_a, cells_a, strings_a, nc, nr = keep
+            plan.input_vid_col = s.from_col.encode()
+            plan.input_var = s.from_var.encode() if s.from_type == 2 else None
+            plan.input_ncols, plan.input_nrows = nc, nr
+            plan.input_names, plan.input_types, plan.input_cells = names_a, types_a, cells_a
+            plan.input_strings = strings_a
         out = P(GoResultC)()
         rc = self.L.ngx_go(self.h, ctypes.byref(plan), ctypes.byref(out))
         try:

@@ -40,6 +40,11 @@ class Expr:
         """(kind, alias, prop) of every property reference, in traversal order."""
         return []
 
+    def to_string(self) -> str:
+        """Expression::toString (Expressions.cpp): the column name of an un-aliased YIELD column
+        (GoExecutor::getResultColumnNames, GoExecutor.cpp:976-987)."""
+        raise NotImplementedError
+
 
 @dataclass
 class Prim(Expr):
@@ -56,6 +61,16 @@ class Prim(Expr):
             return bytes([K_PRIMARY, 1]) + struct.pack("<d", v)
         return bytes([K_PRIMARY, 3]) + _s16(v)
 
+    def to_string(self):
+        v = self.value
+        if isinstance(v, bool):
+            return "true" if v else "false"
+        if isinstance(v, int):
+            return str(v)
+        if isinstance(v, float):
+            return "%.15f" % v
+        return v
+
 
 @dataclass
 class Prop(Expr):
@@ -71,6 +86,15 @@ class Prop(Expr):
     def props(self):
         return [(self.kind, self.alias, self.prop)]
 
+    def to_string(self):                                          # Expressions.cpp:118-137
+        out = self.ref
+        if self.ref not in ("", "$"):
+            out += "."
+        out += self.alias
+        if self.alias:
+            out += "."
+        return out + self.prop
+
 
 @dataclass
 class Func(Expr):
@@ -85,6 +109,9 @@ class Func(Expr):
     def props(self):
         return [p for a in self.args for p in a.props()]
 
+    def to_string(self):
+        return self.name + "(" + ",".join(a.to_string() for a in self.args) + ")"
+
 
 @dataclass
 class Unary(Expr):
@@ -97,6 +124,9 @@ class Unary(Expr):
 
     def props(self):
         return self.operand.props()
+
+    def to_string(self):
+        return "+-!"[self.op] + "(" + self.operand.to_string() + ")"
 
 
 @dataclass
@@ -111,6 +141,9 @@ class Cast(Expr):
     def props(self):
         return self.operand.props()
 
+    def to_string(self):
+        return "(" + ("int", "string", "double", "bool", "timestamp")[self.ctype % 5] + ")" + self.operand.to_string()
+
 
 @dataclass
 class Binary(Expr):
@@ -124,6 +157,12 @@ class Binary(Expr):
 
     def props(self):
         return self.left.props() + self.right.props()
+
+    def to_string(self):
+        names = {K_ARITH: ("+", "-", "*", "/", "%", "^"), K_REL: ("<", "<=", ">", ">=", "==", "!=", " CONTAINS "),
+                 K_LOGIC: ("&&", "||", "XOR")}[self.kind]
+        o = names[self.op] if self.op < len(names) else "?"
+        return "(" + self.left.to_string() + o + self.right.to_string() + ")"
 
 
 # ------------------------------------------------------------------------------ std::hash
@@ -455,6 +494,17 @@ class GoSentence:
     where: Optional[Expr] = None
     distinct: bool = False
     yields: List[YieldCol] = field(default_factory=list)
+    # FROM $-.col / $var.col (GoExecutor fromType_, GoExecutor.cpp:149-180): 0 literal vids, 1 $-, 2 $var
+    from_type: int = 0
+    from_var: str = ""
+    from_col: str = ""
+
+    def column_names(self, edge_names: Sequence[str] = ()) -> List[str]:
+        """getResultColumnNames (GoExecutor.cpp:976-987): alias, else the expression text. OVER *
+        without YIELD yields `<edge>._dst' per edge of the space (`edge_names', schema order)."""
+        if not self.yields and self.over_all:
+            return [n + "._dst" for n in edge_names]
+        return [y.alias if y.alias else y.expr.to_string() for y in self.yields]
 
 
 def parse_go(src: str) -> GoSentence:
@@ -474,9 +524,15 @@ def parse_go(src: str) -> GoSentence:
         p.expect("kw", "STEPS")
     # from_clause (:626-656)
     p.expect("kw", "FROM")
-    while True:
+    t = p.peek()
+    if t.kind == "ref" and t.text == "$-" or t.kind == "var":      # from_clause: input_ref / var_ref
+        p.take()
+        p.expect("op", ".")
+        col = "*" if p.accept("op", "*") else p.label()
+        s.from_type, s.from_var, s.from_col = (1, "", col) if t.kind == "ref" else (2, t.text[1:], col)
+    while s.from_type == 0:
         if p.peek().kind in ("ref", "var"):
-            raise SyntaxError("FROM $-/$var input is outside this path")
+            raise SyntaxError("FROM accepts vids, $-.col or $var.col")
         e = p.primary() if p.is_op("-") or p.is_op("+") else p.base()
         if isinstance(e, Unary) and e.op == UNARY_OPS["+"]:
             e = e.operand

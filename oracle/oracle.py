@@ -237,6 +237,7 @@ class GoResult:
     seconds: float = 0.0                 # wall time of the restated GoExecutor run (no serialisation)
     nrows: int = 0
     digests: Optional[np.ndarray] = None  # digest=True: sorted 16-byte row digests
+    column_names: List[str] = field(default_factory=list)   # getResultColumnNames
 
 
 def _cell(r: _Rd):
@@ -350,7 +351,7 @@ class Oracle:
             verts.append({"vid": vid, "tags": tags, "edges": edata})
         return NeighborsResponse(failed, vs, es, verts, r.get("i"))
 
-    def go(self, space: int, s, pushdown=True, rows=True, digest=False) -> GoResult:
+    def go(self, space: int, s, pushdown=True, rows=True, digest=False, input=None) -> GoResult:
         """Run a parsed nebula_amd.ngql.GoSentence through the restated GoExecutor. digest=True
         returns the rows as sorted 128-bit digests of their serialized cells (digest_columns())."""
         b = struct.pack("<IIi", s.record_from, s.record_to, len(s.vids)) + struct.pack(f"<{len(s.vids)}q", *s.vids)
@@ -363,6 +364,25 @@ class Oracle:
         for y in s.yields:
             b += _s(y.expr.encode()) + _s(y.alias)
         b += struct.pack("<BB", 1 if pushdown else 0, 2 if digest else (0 if rows else 1))
+        ft = getattr(s, "from_type", 0)
+        b += struct.pack("<B", ft) + _s(getattr(s, "from_var", "")) + _s(getattr(s, "from_col", ""))
+        names = input.names if (ft and input is not None) else []
+        types = input.types if (ft and input is not None) else []
+        rws = input.rows if (ft and input is not None) else []
+        b += struct.pack("<i", len(names))
+        for i, n in enumerate(names):
+            b += _s(n) + struct.pack("<i", types[i] if i < len(types) else 0)
+        b += struct.pack("<q", len(rws))
+        for row in rws:
+            for kind, v in row:
+                if kind == "str":
+                    b += struct.pack("<B", 3) + _s(v.encode("utf-8", "surrogateescape"))
+                elif kind in ("float", "double"):
+                    b += struct.pack("<Bd", 1, v)
+                elif kind == "bool":
+                    b += struct.pack("<BB", 2, 1 if v else 0)
+                else:
+                    b += struct.pack("<Bq", 0, int(v))
         r = _Rd(_call(self.L.orc_go, self.h, space, b, len(b)))
         ok = r.get("B") == 1
         err = r.str().decode()
@@ -379,4 +399,6 @@ class Oracle:
         for _ in range(hops):
             fr.append(r.get("q"))
             sc.append(r.get("q"))
-        return GoResult(ok, err, types, out, fr, sc, r.get("d"), nrows, dig)
+        secs = r.get("d")
+        names_out = [r.str().decode() for _ in range(r.get("i"))]
+        return GoResult(ok, err, types, out, fr, sc, secs, nrows, dig, names_out)

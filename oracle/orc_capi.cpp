@@ -290,6 +290,29 @@ char* orc_go(void* e, int32_t space, const uint8_t* blob, uint64_t len, uint64_t
     f.filter_pushdown = r.get<uint8_t>() != 0;
     uint8_t mode = r.p < r.e ? r.get<uint8_t>() : 0;        // 0 cells, 1 count only, 2 row digests
     bool countOnly = mode != 0;
+    if (r.p < r.e) {                                        // FROM $-.col / $var.col and the input
+        s.fromType = r.get<uint8_t>();
+        s.fromVar = r.str();
+        s.fromCol = r.str();
+        int32_t nc = r.get<int32_t>();
+        for (int32_t i = 0; i < nc; i++) {
+            s.inputNames.push_back(r.str());
+            s.inputTypes.push_back(static_cast<SupportedType>(r.get<int32_t>()));
+        }
+        int64_t nr = r.get<int64_t>();
+        for (int64_t i = 0; i < nr; i++) {
+            std::vector<Variant> row;
+            for (int32_t j = 0; j < nc; j++) {
+                switch (r.get<uint8_t>()) {
+                    case VAR_INT64: row.emplace_back(r.get<int64_t>()); break;
+                    case VAR_DOUBLE: row.emplace_back(r.get<double>()); break;
+                    case VAR_BOOL: row.emplace_back(r.get<uint8_t>() != 0); break;
+                    default: row.emplace_back(r.str()); break;
+                }
+            }
+            s.inputRows.push_back(std::move(row));
+        }
+    }
     auto t0 = std::chrono::steady_clock::now();
     auto res = runGo(*eng, space, s, f);
     double seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -323,6 +346,8 @@ char* orc_go(void* e, int32_t space, const uint8_t* blob, uint64_t len, uint64_t
         w.put<int64_t>(res.hopScanned[i]);
     }
     w.put<double>(seconds);
+    w.put<int32_t>(static_cast<int32_t>(res.columnNames.size()));
+    for (auto& n : res.columnNames) w.str(n);
     return toHeap(w.b, outLen);
 }
 

@@ -82,6 +82,56 @@ struct GoExec {
     // VertexHolder (GoExecutor.cpp:1337-1412): (vid, tag) -> (row, schema)
     std::map<std::pair<VertexID, TagID>, std::pair<std::string, std::shared_ptr<Schema>>> vertexHolder;
     std::map<TagID, std::shared_ptr<Schema>> vertexHolderSchemas;
+    // VertexBackTracker (GoExecutor.h:189-207): (step, dst) -> root
+    std::multimap<std::pair<uint32_t, VertexID>, VertexID> backTracker;
+    // InterimResultIndex (InterimResult.h:80-114): column index, rows, vid -> row multimap
+    std::map<std::string, uint32_t> columnToIndex;
+    std::multimap<VertexID, uint32_t> vidToRowIndex;
+
+    std::vector<VertexID> getRoots(VertexID srcId, size_t record) const {      // GoExecutor.h:218-230
+        std::vector<VertexID> ids;
+        if (record == 1) { ids.push_back(srcId); return ids; }
+        auto range = backTracker.equal_range({static_cast<uint32_t>(record - 1), srcId});
+        for (auto i = range.first; i != range.second; ++i) ids.push_back(i->second);
+        return ids;
+    }
+    std::vector<uint32_t> rowsOfVids(const std::vector<VertexID>& ids) const {  // InterimResult.h:95-104
+        std::vector<uint32_t> rows;
+        for (auto v : ids) {
+            auto range = vidToRowIndex.equal_range(v);
+            for (auto i = range.first; i != range.second; ++i) rows.push_back(i->second);
+        }
+        return rows;
+    }
+    OptVariant getColumnWithRow(size_t row, const std::string& col) const {   // InterimResult.cpp:282-297
+        if (row >= s.inputRows.size()) return Status::Error("Out of range");
+        auto it = columnToIndex.find(col);
+        if (it == columnToIndex.end()) return Status::Error("Prop `" + col + "' not found");
+        return OptVariant(s.inputRows[row][it->second]);
+    }
+
+    // setupStarts (GoExecutor.cpp:471-509): checkIfDuplicateColumn (TraverseExecutor.cpp:167-181),
+    // getDistinctVIDs (InterimResult.cpp:51-72, RowReader::getVid: INT or VID columns), buildIndex
+    // (:178-280)
+    bool setupStarts() {
+        if (s.inputRows.empty()) return true;
+        std::unordered_set<std::string> uniq;
+        // checkIfDuplicateColumn reads inputs_: the pipe input, not a variable
+        if (s.fromType == 1)
+            for (auto& n : s.inputNames)
+                if (!uniq.insert(n).second) return fail("Duplicate column `" + n + "'");
+        int vidCol = -1;
+        for (size_t i = 0; i < s.inputNames.size(); i++) if (s.inputNames[i] == s.fromCol) vidCol = static_cast<int>(i);
+        // RowReader::getVid by name reads the first field of that name; names are unique here
+        if (vidCol < 0 || (s.inputTypes[vidCol] != INT && s.inputTypes[vidCol] != VID))
+            return fail("Column `" + s.fromCol + "' not found");
+        std::unordered_set<VertexID> u;
+        for (auto& r : s.inputRows) u.insert(std::get<int64_t>(r[vidCol]));
+        starts.assign(u.begin(), u.end());
+        for (size_t i = 0; i < s.inputNames.size(); i++) columnToIndex[s.inputNames[i]] = static_cast<uint32_t>(i);
+        for (uint32_t r = 0; r < s.inputRows.size(); r++) vidToRowIndex.emplace(std::get<int64_t>(s.inputRows[r][vidCol]), r);
+        return true;
+    }
 
     GoExec(const StorageEngine& e, GraphSpaceID sp, const GoSentence& sent, GoFlags f)
         : eng(e), sm(e.schemas), space(sp), s(sent), flags(f) {}
@@ -100,6 +150,7 @@ struct GoExec {
     bool prepareClauses() {                                            // :38-89
         recordFrom = s.recordFrom;
         steps = s.recordTo;
+        if (s.fromType != 0 && s.fromCol == "*") return fail("Can not use `*' to reference a vertex id column.");   // :175-178
         // prepareOver (:254-295) / prepareOverAll (:225-252)
         if (s.overAll) {
             ctx.overAll = true;
@@ -142,8 +193,14 @@ struct GoExec {
             auto st = y->prepare(&ctx);
             if (!st.ok()) return fail(st.msg_);
         }
-        if (ctx.hasVariableProp()) return fail("A variable must be referred in FROM before used in WHERE or YIELD");
-        if (ctx.hasInputProp()) return fail("`$-' must be referred in FROM before used in WHERE or YIELD");
+        if (ctx.hasVariableProp()) {                                   // :367-384
+            if (s.fromType != 2) return fail("A variable must be referred in FROM before used in WHERE or YIELD");
+            if (ctx.variables.size() > 1) return fail("Only one variable allowed to use");
+            if (*ctx.variables.begin() != s.fromVar)
+                return fail("Variable name not match: `" + *ctx.variables.begin() + "' vs. `" + s.fromVar + "'");
+        }
+        if (ctx.hasInputProp() && s.fromType != 1)                    // :386-392
+            return fail("`$-' must be referred in FROM before used in WHERE or YIELD");
         for (auto& e : ctx.tagMap) {
             auto id = sm.toTagID(space, e.first);
             if (!id.ok()) return fail("Tag `" + e.first + "' not found.");
@@ -237,11 +294,26 @@ struct GoExec {
             auto resp = eng.getBound(req);
             if (!resp.failed_codes.empty()) return fail("Get neighbors failed");
             records.push_back(std::move(resp));
-            // getDstIdsFromRespWithBackTrack (:675-718) — the frontier is the set of distinct dsts
+            // getDstIdsFromRespWithBackTrack (:675-718) — the frontier is the set of distinct dsts;
+            // for steps > 1 the back tracker records (step, dst) -> root for non-final steps, all
+            // pairs of the step read before any is inserted
             std::unordered_set<VertexID> set;
+            std::set<std::pair<VertexID, VertexID>> curBackTrace;
             for (auto& vd : records.back().vertices)
                 for (auto& ed : vd.edge_data)
-                    for (auto& e : ed.edges) set.insert(e.dst);
+                    for (auto& e : ed.edges) {
+                        if (!isFinalStep() && steps != 1) {
+                            if (curStep == 1) {
+                                curBackTrace.emplace(e.dst, vd.vertex_id);
+                            } else {
+                                auto pre = backTracker.equal_range({curStep - 1, vd.vertex_id});
+                                for (auto t = pre.first; t != pre.second; ++t) curBackTrace.emplace(e.dst, t->second);
+                            }
+                        }
+                        set.insert(e.dst);
+                    }
+            if (!isFinalStep() && steps != 1)
+                for (auto& t : curBackTrace) backTracker.emplace(std::make_pair(curStep, t.first), t.second);
             if (isFinalStep()) return true;
             starts.assign(set.begin(), set.end());
             if (starts.empty()) {
@@ -298,6 +370,14 @@ struct GoExec {
             }
             case Expression::kEdgeDstId: case Expression::kEdgeSrcId: return VID;
             case Expression::kEdgeRank: case Expression::kEdgeType: return INT;
+            case Expression::kVariableProp: case Expression::kInputProp: {
+                // the interim result's column type; UNKNOWN without data (:141-158)
+                if (s.inputRows.empty()) return UNKNOWN;
+                auto* a = static_cast<const AliasPropertyExpression*>(e);
+                for (size_t i = 0; i < s.inputNames.size(); i++)
+                    if (s.inputNames[i] == a->prop()) return s.inputTypes[i];
+                return UNKNOWN;
+            }
             case Expression::kAliasProp: {
                 auto* a = static_cast<const AliasPropertyExpression*>(e);
                 auto et = sm.toEdgeType(space, a->alias());
@@ -397,34 +477,50 @@ struct GoExec {
             return OptVariant(r.v);
         };
 
+        size_t inputRow = 0;
+        g.getInputProp = [&](const std::string& prop) { return getColumnWithRow(inputRow, prop); };
+        g.getVariableProp = [&](const std::string& prop) { return getColumnWithRow(inputRow, prop); };
+
         std::set<std::vector<Variant>> uniq;
-        for (size_t ri = recordFrom - 1; ri < records.size(); ri++) {
+        size_t recordIn = recordFrom;                                   // :1089
+        for (size_t ri = recordFrom - 1; ri < records.size(); ri++, recordIn++) {
             auto& resp = records[ri];
             for (auto& kv : resp.vertex_schema) tagSchema.emplace(kv.first, kv.second);
             for (auto& kv : resp.edge_schema) edgeSchema.emplace(kv.first, kv.second);
             for (auto& vd : resp.vertices) {
                 tagData = &vd.tag_data;
                 srcId = vd.vertex_id;
-                for (auto& ed : vd.edge_data) {
-                    edgeType = ed.type;
-                    auto sit = edgeSchema.find(edgeType);
-                    for (auto& e : ed.edges) {
-                        dstId = e.dst;
-                        rowBytes = &e.props;
-                        reader = sit != edgeSchema.end() ? RowReader::make(*rowBytes, sit->second) : nullptr;
-                        if (filter) {
-                            auto v = filter->eval(g);
-                            if (!v.ok()) return fail(v.status().msg_);
-                            if (!Expression::asBool(v.value())) continue;
+                auto func = [&]() -> bool {
+                    for (auto& ed : vd.edge_data) {
+                        edgeType = ed.type;
+                        auto sit = edgeSchema.find(edgeType);
+                        for (auto& e : ed.edges) {
+                            dstId = e.dst;
+                            rowBytes = &e.props;
+                            reader = sit != edgeSchema.end() ? RowReader::make(*rowBytes, sit->second) : nullptr;
+                            if (filter) {
+                                auto v = filter->eval(g);
+                                if (!v.ok()) return fail(v.status().msg_);
+                                if (!Expression::asBool(v.value())) continue;
+                            }
+                            std::vector<Variant> record;
+                            for (auto& y : yields) {
+                                auto v = y->eval(g);
+                                if (!v.ok()) return fail(v.status().msg_);
+                                record.push_back(v.value());
+                            }
+                            if (s.distinct && !uniq.insert(record).second) continue;
+                            res.rows.push_back(std::move(record));
                         }
-                        std::vector<Variant> record;
-                        for (auto& y : yields) {
-                            auto v = y->eval(g);
-                            if (!v.ok()) return fail(v.status().msg_);
-                            record.push_back(v.value());
-                        }
-                        if (s.distinct && !uniq.insert(record).second) continue;
-                        res.rows.push_back(std::move(record));
+                    }
+                    return true;
+                };
+                if (s.fromType == 0) {
+                    if (!func()) return false;
+                } else {                                               // :1321-1330
+                    for (auto row : rowsOfVids(getRoots(srcId, recordIn))) {
+                        inputRow = row;
+                        if (!func()) return false;
                     }
                 }
             }
@@ -439,7 +535,8 @@ struct GoExec {
         }
         if (steps == 0) return res;                                    // :99-104
         if (recordFrom == 0) recordFrom = 1;
-        starts = s.vids;
+        if (s.fromType == 0) starts = s.vids;
+        else if (!setupStarts()) return res;
         if (starts.empty()) return res;
         if (s.distinct) {
             std::unordered_set<VertexID> u(starts.begin(), starts.end());
@@ -454,6 +551,7 @@ struct GoExec {
                 auto e = std::make_shared<AliasPropertyExpression>("", a, "_dst");
                 e->setKind(Expression::kEdgeDstId);
                 yields.push_back(e);
+                res.columnNames.push_back(e->toString());             // getResultColumnNames
             }
         }
         processFinalResult();

@@ -72,6 +72,13 @@ struct GoSentence {
     std::string where;                                        // encoded Expression
     bool distinct = false;
     std::vector<GoYield> yields;                              // the parser's default is <edge>._dst
+    // FROM $-.col / $var.col (fromType_ kPipe / kVariable, GoExecutor.cpp:149-180): the interim
+    // result of the previous sentence (InterimResult: column names, schema types, rows)
+    int fromType = 0;                                         // 0 literal vids, 1 $-, 2 $var
+    std::string fromVar, fromCol;
+    std::vector<std::string> inputNames;
+    std::vector<SupportedType> inputTypes;
+    std::vector<std::vector<Variant>> inputRows;
 };
 struct GoResult {
     bool ok = true;

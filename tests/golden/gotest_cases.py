@@ -321,3 +321,122 @@ CASES = [
     dict(line=648, query="GO FROM {P:LaMarcus Aldridge} OVER * YIELD $$.team.name, $$.player.name",
          rows=[("Trail Blazers", ""), ("", "Tim Duncan"), ("", "Tony Parker"), ("Spurs", "")]),
 ]
+
+# Pipes and variables (GoTest.cpp): `names' is verifyColNames' list when the test checks it.
+# Not transcribed: GoTest.cpp:146 (`A | (B | C)' from Boris Diaw expects 4 rows, while the same
+# nesting at :667 / :688 and the flat pipe at :120 give the 7 rows the PipeExecutor / back-tracker
+# semantics produce; the executor sources show no path to 4 rows), :3095 and :55 (YIELD sentences).
+_SPURS7 = [("T:Spurs",)] * 5 + [("T:Hornets",), ("T:Trail Blazers",)]
+_REF_PIPE = [("Tim Duncan", "Manu Ginobili", "Tim Duncan"), ("Tim Duncan", "Tony Parker", "LaMarcus Aldridge"),
+             ("Tim Duncan", "Tony Parker", "Manu Ginobili"), ("Tim Duncan", "Tony Parker", "Tim Duncan"),
+             ("Chris Paul", "LeBron James", "Ray Allen"), ("Chris Paul", "Carmelo Anthony", "Chris Paul"),
+             ("Chris Paul", "Carmelo Anthony", "LeBron James"), ("Chris Paul", "Carmelo Anthony", "Dwyane Wade"),
+             ("Chris Paul", "Dwyane Wade", "Chris Paul"), ("Chris Paul", "Dwyane Wade", "LeBron James"),
+             ("Chris Paul", "Dwyane Wade", "Carmelo Anthony")]
+_REF_PIPE_WHERE = [r for r in _REF_PIPE if r[0] != r[2]]
+_REF_PIPE_STAR = [(a, "P:" + b, b, c) for a, b, c in _REF_PIPE]
+_REV_LEBRON = ([("Cavaliers", n) for n in ("Kyrie Irving", "Dwyane Wade", "Shaquile O'Neal", "Danny Green",
+                                          "LeBron James", "LeBron James")] * 2 +
+               [("Heat", n) for n in ("Dwyane Wade", "Dwyane Wade", "LeBron James", "Ray Allen",
+                                     "Shaquile O'Neal", "Amar'e Stoudemire")] +
+               [("Lakers", n) for n in ("Kobe Bryant", "LeBron James", "Rajon Rondo", "Steve Nash", "Paul Gasol",
+                                       "Shaquile O'Neal", "JaVale McGee", "Dwight Howard")])
+_MANU_REV = [("T:Spurs",), ("T:Spurs",), ("T:Hornets",), ("T:Spurs",), ("T:Hawks",), ("T:76ers",), ("T:Spurs",)]
+_TD = "P:Tim Duncan"
+_TD12 = ([(_TD, "P:Tony Parker"), (_TD, "P:Manu Ginobili")] * 2 +
+         [(_TD, _TD)] * 4 + [(_TD, "P:Manu Ginobili")] * 2 + [(_TD, "P:LaMarcus Aldridge")] * 2)
+_TD12_PROPS = [(_TD, "P:Tony Parker", "P:Tony Parker", 95), (_TD, "P:Tony Parker", "P:Manu Ginobili", 95),
+               (_TD, "P:Manu Ginobili", "P:Tony Parker", 95), (_TD, "P:Manu Ginobili", "P:Manu Ginobili", 95),
+               (_TD, "P:Tony Parker", _TD, 95), (_TD, "P:Tony Parker", "P:Manu Ginobili", 95),
+               (_TD, "P:Tony Parker", "P:LaMarcus Aldridge", 90), (_TD, "P:Tony Parker", _TD, 90),
+               (_TD, "P:Manu Ginobili", _TD, 95), (_TD, "P:Manu Ginobili", "P:Manu Ginobili", 95),
+               (_TD, "P:Manu Ginobili", "P:LaMarcus Aldridge", 90), (_TD, "P:Manu Ginobili", _TD, 90)]
+_DG = [("P:Danny Green", _TD, "P:" + n) for n in ("Tony Parker", "Manu Ginobili", "LaMarcus Aldridge", "Danny Green")]
+_TP, _MG, _LA = "P:Tony Parker", "P:Manu Ginobili", "P:LaMarcus Aldridge"
+_OVERLAP = [(_TP, x, a, b) for x in (_TD, _MG, _LA)
+            for a, b in ((_TD, _MG), (_TD, _TP), (_LA, _TP), (_MG, _TD), (_LA, _TD))]
+_TMG = "P:Tracy McGrady"
+
+PIPE_CASES = [
+    dict(line=118, query="GO FROM {P:Boris Diaw} OVER like YIELD like._dst as id | GO FROM $-.id OVER like "
+                         "YIELD like._dst as id | GO FROM $-.id OVER serve", names=["serve._dst"], rows=_SPURS7),
+    dict(line=176, query="$var = GO FROM {P:Tracy McGrady} OVER like YIELD like._dst as id; "
+                         "GO FROM $var.id OVER like", names=["like._dst"], rows=[(_TMG,), (_LA,)]),
+    dict(line=198, query="$var = (GO FROM {P:Tracy McGrady} OVER like YIELD like._dst as id | GO FROM $-.id OVER "
+                         "like YIELD like._dst as id); GO FROM $var.id OVER like", names=["like._dst"],
+         rows=[("P:Kobe Bryant",), ("P:Grant Hill",), ("P:Rudy Gay",), (_TP,), (_TD,)]),
+    dict(line=226, query="GO FROM $var OVER like", error=True),
+    dict(line=236, query="$var = GO FROM -1 OVER like YIELD like._dst as id; GO FROM $var.id OVER like", empty=True),
+    dict(line=304, query="GO FROM {P:Boris Diaw} OVER like YIELD like._dst as id | GO FROM $-.id OVER like "
+                         "YIELD like._dst as id | GO FROM $-.id OVER serve YIELD DISTINCT serve._dst, $$.team.name",
+         names=["serve._dst", "$$.team.name"],
+         rows=[("T:Spurs", "Spurs"), ("T:Hornets", "Hornets"), ("T:Trail Blazers", "Trail Blazers")]),
+    dict(line=398, query="GO FROM {P:Nobody} OVER serve | GO FROM $-.serve_id OVER serve", empty=True),
+    dict(line=405, query="GO FROM {P:Nobody} OVER like YIELD like._dst as id | GO FROM $-.id OVER like "
+                         "YIELD like._dst as id | GO FROM $-.id OVER serve", empty=True),
+    dict(line=414, query="GO FROM {P:Nobody} OVER like YIELD like._dst as id | (GO FROM $-.id OVER like "
+                         "YIELD like._dst as id | GO FROM $-.id OVER serve)", empty=True),
+    dict(line=665, query="GO FROM {P:Boris Diaw} OVER like, serve YIELD like._dst as id | ( GO FROM $-.id OVER "
+                         "like YIELD like._dst as id | GO FROM $-.id OVER serve )", rows=_SPURS7),
+    dict(line=686, query="GO FROM {P:Boris Diaw} OVER * YIELD like._dst as id | ( GO FROM $-.id OVER like "
+                         "YIELD like._dst as id | GO FROM $-.id OVER serve )", rows=_SPURS7),
+    dict(line=708, query="GO FROM hash('Tim Duncan'),hash('Chris Paul') OVER like YIELD $^.player.name AS name, "
+                         "like._dst AS id | GO FROM $-.id OVER like YIELD $-.name, $^.player.name, $$.player.name",
+         names=["$-.name", "$^.player.name", "$$.player.name"], rows=_REF_PIPE),
+    dict(line=737, query="GO FROM hash('Tim Duncan'),hash('Chris Paul') OVER like YIELD $^.player.name AS name, "
+                         "like._dst AS id | GO FROM $-.id OVER like WHERE $-.name != $$.player.name "
+                         "YIELD $-.name, $^.player.name, $$.player.name",
+         names=["$-.name", "$^.player.name", "$$.player.name"], rows=_REF_PIPE_WHERE),
+    dict(line=763, query="GO FROM hash('Tim Duncan'),hash('Chris Paul') OVER like YIELD $^.player.name AS name, "
+                         "like._dst AS id | GO FROM $-.id OVER like YIELD $-.*, $^.player.name, $$.player.name",
+         rows=_REF_PIPE_STAR),
+    dict(line=795, query="$var = GO FROM hash('Tim Duncan'),hash('Chris Paul') OVER like YIELD $^.player.name AS "
+                         "name, like._dst AS id; GO FROM $var.id OVER like YIELD $var.name, $^.player.name, "
+                         "$$.player.name", names=["$var.name", "$^.player.name", "$$.player.name"], rows=_REF_PIPE),
+    dict(line=824, query="$var = GO FROM hash('Tim Duncan'),hash('Chris Paul') OVER like YIELD $^.player.name AS "
+                         "name, like._dst AS id; GO FROM $var.id OVER like WHERE $var.name != $$.player.name "
+                         "YIELD $var.name, $^.player.name, $$.player.name",
+         names=["$var.name", "$^.player.name", "$$.player.name"], rows=_REF_PIPE_WHERE),
+    dict(line=850, query="$var = GO FROM hash('Tim Duncan'),hash('Chris Paul') OVER like YIELD $^.player.name AS "
+                         "name, like._dst AS id; GO FROM $var.id OVER like YIELD $var.*, $^.player.name, "
+                         "$$.player.name", rows=_REF_PIPE_STAR),
+    dict(line=925, query="GO FROM {P:Tim Duncan} OVER like YIELD like._dst AS id | GO FROM $-.id OVER serve "
+                         "WHERE udf_is_in($-.id, {P:Tony Parker}, 123)", names=["serve._dst"],
+         rows=[("T:Spurs",), ("T:Hornets",)]),
+    dict(line=945, query="GO FROM {P:Tim Duncan} OVER like YIELD like._dst AS id | GO FROM $-.id OVER serve "
+                         "WHERE udf_is_in($-.id, {P:Tony Parker}, 123) && 1 == 1", names=["serve._dst"],
+         rows=[("T:Spurs",), ("T:Hornets",)]),
+    dict(line=1223, query="GO FROM hash('LeBron James') OVER serve YIELD serve._dst AS id | GO FROM $-.id OVER "
+                          "serve REVERSELY YIELD $^.team.name, $$.player.name", rows=_REV_LEBRON),
+    dict(line=1258, query="GO FROM hash('LeBron James') OVER serve YIELD serve._dst AS id | GO FROM $-.id OVER "
+                          "serve REVERSELY WHERE $$.player.name != 'LeBron James' YIELD $^.team.name, "
+                          "$$.player.name", rows=[r for r in _REV_LEBRON if r[1] != "LeBron James"]),
+    dict(line=1291, query="GO FROM hash('Manu Ginobili') OVER like REVERSELY YIELD like._dst AS id | "
+                          "GO FROM $-.id OVER serve", rows=_MANU_REV),
+    dict(line=1309, query="GO FROM hash('Manu Ginobili') OVER * REVERSELY YIELD like._dst AS id | "
+                          "GO FROM $-.id OVER serve", rows=_MANU_REV),
+    dict(line=2063, query="GO FROM {P:Tim Duncan} OVER like YIELD like._dst AS id | GO FROM $-.id OVER serve "
+                          "WHERE $^.player.name == \"Tony Parker\" && serve.start_year > 2013",
+         names=["serve._dst"], rows=[("T:Hornets",)]),
+    dict(line=2297, query="GO FROM {P:Tim Duncan} OVER like YIELD like._dst AS id, like.likeness AS id | "
+                          "GO FROM $-.id OVER serve", error=True),
+    dict(line=2888, query="GO FROM {P:Tim Duncan} OVER like YIELD like._src as src, like._dst as dst | GO FROM "
+                          "$-.src OVER like YIELD $-.src as src, like._dst as dst, $^.player.name, $$.player.name",
+         rows=[(_TD, _TP, "Tim Duncan", "Tony Parker"), (_TD, _MG, "Tim Duncan", "Manu Ginobili")] * 2),
+    dict(line=2911, query="$a = GO FROM {P:Tim Duncan} OVER like YIELD like._src as src, like._dst as dst; "
+                          "GO FROM $a.src OVER like YIELD $a.src as src, like._dst as dst",
+         rows=[(_TD, _TP), (_TD, _MG)] * 2),
+    dict(line=2930, query="GO FROM {P:Tim Duncan} OVER like YIELD like._src as src, like._dst as dst | GO 1 TO 2 "
+                          "STEPS FROM $-.src OVER like YIELD $-.src as src, like._dst as dst", rows=_TD12),
+    dict(line=2957, query="GO FROM {P:Tim Duncan} OVER like YIELD like._src as src, like._dst as dst | GO 1 TO 2 "
+                          "STEPS FROM $-.src OVER like YIELD $-.src as src, $-.dst, like._dst as dst, like.likeness",
+         rows=_TD12_PROPS),
+    dict(line=2986, query="GO FROM {P:Danny Green} OVER like YIELD like._src AS src, like._dst AS dst | GO FROM "
+                          "$-.dst OVER teammate YIELD $-.src AS src, $-.dst, teammate._dst AS dst", rows=_DG),
+    dict(line=3004, query="$a = GO FROM {P:Danny Green} OVER like YIELD like._src AS src, like._dst AS dst; GO FROM "
+                          "$a.dst OVER teammate YIELD $a.src AS src, $a.dst, teammate._dst AS dst", rows=_DG),
+    dict(line=3047, query="GO FROM {P:Tony Parker} OVER like YIELD like._src as src, like._dst as dst | GO 2 STEPS "
+                          "FROM $-.src OVER like YIELD $-.src, $-.dst, like._src, like._dst", rows=_OVERLAP),
+    dict(line=3057, query="$a = GO FROM {P:Tony Parker} OVER like YIELD like._src as src, like._dst as dst; GO 2 "
+                          "STEPS FROM $a.src OVER like YIELD $a.src, $a.dst, like._src, like._dst", rows=_OVERLAP),
+]
