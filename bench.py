@@ -49,6 +49,7 @@ def parse():
     p.add_argument("--cpu-budget", type=float, default=20.0, help="target seconds of oracle GO work (0: skip)")
     p.add_argument("--threads", type=int, default=16, help="host threads for datagen / oracle")
     p.add_argument("--out-only", action="store_true", help="store out-edges only (no -e in-edge slot)")
+    p.add_argument("--row-arrays", action="store_true", help="also write the src / dst / rank row arrays in the timed step")
     p.add_argument("--host-exchange", action="store_true",
                    help="rehearsal of the N > 1 path on one GPU: every rank on device 0, frontier exchange "
                         "through the host collective (gloo) instead of RCCL")
@@ -140,7 +141,8 @@ def main():
     plans = [sentence(i, args.seeds) for i in range(args.warmup + args.steps)]
 
     def step(s, on_device=True, columnar=False, rows_=False):
-        r = eng.go(datagen.RMAT_SPACE, s, rows=rows_, on_device=on_device, columnar=columnar, arrays=False)
+        r = eng.go(datagen.RMAT_SPACE, s, rows=rows_, on_device=on_device, columnar=columnar, arrays=False,
+                   yield_only=on_device and not args.row_arrays)
         if not r.ok:
             raise RuntimeError(r.error)
         return r
@@ -292,7 +294,10 @@ def main():
             "host_ms_per_step": {"library_prep": round(prep_ms / args.steps, 3), "library_tail": round(tail_ms / args.steps, 3),
                                  "note": "inside ngx_go: before the first launch (plan, programs, seeds) / after the "
                                          "device finished; the rest of ms_per_step - device_ms is the Python caller"},
-            "timed_region": "seeds on host -> result rows + YIELD columns in HBM (result_on_device)",
+            "timed_region": ("seeds on host -> the YIELD columns of every result row in HBM (result_on_device; "
+                             + ("src/dst/rank row arrays too" if args.row_arrays else
+                                "yield_only: e._dst / e._rank alias the dst / rank row arrays, no src array — the "
+                                "reference response holds the YIELD columns only") + ")"),
             "get_neighbors": gn_stats,
             "host_delivery": {"ms_per_step_columnar": round(host_col_ms, 3), "ms_per_step_cells": round(host_cell_ms, 3),
                               "columnar_library_tail_ms": round(col_tail, 3), "columnar_device_ms": round(col_dev, 3),

@@ -262,6 +262,10 @@ typedef struct {
     uint64_t input_nrows;
     const ngx_cell* input_cells;       /* [row * input_ncols + col]; NGX_CELL_STR: str_off into input_strings */
     const char* input_strings;
+    /* result_on_device without DISTINCT: 1 = write only the row arrays a YIELD column aliases
+     * (dev_src / dev_dst / dev_rank NULL otherwise). The reference's response holds the YIELD
+     * columns alone (GoExecutor::toThriftResponse); the row arrays are this library's extra. */
+    int32_t yield_only;
 } ngx_go_plan;
 
 /* One YIELD column of a device-resident result (result_on_device), columnar in HBM, nrows entries:

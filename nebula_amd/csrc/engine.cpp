@@ -1661,6 +1661,12 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     // one OVER type: every row's type is hs.etype[0], so the final hop writes no per-row type column
     const bool constType = hs.n == 1;
     const std::vector<int32_t> yAlias = keyAliases(progs, gp.colTypes, hs);
+    // yield_only: the row arrays no YIELD column aliases are not written (bit k: src, dst, rank)
+    int32_t rowMask = 7;
+    if (p.yield_only && p.result_on_device && !p.distinct) {
+        rowMask = 0;
+        for (int32_t al : yAlias) if (al >= 0) rowMask |= 1 << al;
+    }
     // per-query straight-line kernels (jit.cpp); the interpreter kernels otherwise
     const JitKernels* jk = nullptr;
     const JitKernels* jkNoP = nullptr;                       // record hops before the last (no pushdown)
@@ -1685,6 +1691,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         }
         jq.etype0 = hs.n == 1 ? hs.etype[0] : 0;
         jq.dstReplica = dstReplica;
+        jq.rowMask = rowMask;
         jq.dstW = hs.n ? hs.dstW[0] : 0;
         jq.rankW = hs.n ? hs.rankW[0] : 0;
         for (int s = 1; s < hs.n; s++) {
@@ -1975,9 +1982,9 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             growKeep(c, c->oType, cap * 4, totalRows * 4);
             prepareCols(c, a, colSpec, cap, totalRows, yAlias);
             a.oBase = totalRows;
-            a.oSrc = static_cast<int64_t*>(c->oSrc.p);
-            a.oDst = static_cast<int64_t*>(c->oDst.p);
-            a.oRank = static_cast<int64_t*>(c->oRank.p);
+            a.oSrc = (rowMask & 1) ? static_cast<int64_t*>(c->oSrc.p) : nullptr;
+            a.oDst = (rowMask & 2) ? static_cast<int64_t*>(c->oDst.p) : nullptr;
+            a.oRank = (rowMask & 4) ? static_cast<int64_t*>(c->oRank.p) : nullptr;
             a.oType = constType ? nullptr : static_cast<int32_t*>(c->oType.p);
             a.oEntry = nullptr;
             a.lbStatus = lb;
@@ -1998,7 +2005,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             });
             if (!dyn) {
                 uint64_t nrows = awaitPub(c, rowsPub, a.lbStatus);   // GO: rows reserved by atomicAdd
-                c->addBytes("final", nrows * (24 + 8 * ky));
+                c->addBytes("final", nrows * (8 * __builtin_popcount(rowMask) + 8 * ky));
                 totalRows += nrows;
             }
         }
@@ -2135,7 +2142,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                             pullable && e >= pullMinE ? d.V * (16 * static_cast<uint64_t>(hs.n) + 1) : e * 8);
                 c->addBytes("compact_degrees", (st[h] >> kFdShift) * (8 + 24 * static_cast<uint64_t>(hs.n)));
             } else {
-                c->addBytes("final", e * (16 + kfBytes) + rows * (24 + 8 * ky));
+                c->addBytes("final", e * (16 + kfBytes) + rows * (8 * __builtin_popcount(rowMask) + 8 * ky));
             }
         }
         totalRows = rows;
@@ -2234,9 +2241,9 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     }
     if (p.result_on_device) {                                 // rows stay in HBM (valid until the next call)
         R.r.nrows = totalRows;
-        R.r.dev_src = static_cast<const int64_t*>(c->oSrc.p);
-        R.r.dev_dst = static_cast<const int64_t*>(c->oDst.p);
-        R.r.dev_rank = static_cast<const int64_t*>(c->oRank.p);
+        R.r.dev_src = (rowMask & 1) ? static_cast<const int64_t*>(c->oSrc.p) : nullptr;
+        R.r.dev_dst = (rowMask & 2) ? static_cast<const int64_t*>(c->oDst.p) : nullptr;
+        R.r.dev_rank = (rowMask & 4) ? static_cast<const int64_t*>(c->oRank.p) : nullptr;
         R.r.dev_type = constType ? nullptr : static_cast<const int32_t*>(c->oType.p);
         R.r.dev_type_const = constType ? hs.etype[0] : 0;
         R.devCols.clear();

@@ -47,6 +47,7 @@ struct JitQuery {
     bool ttl = false;               // some slot's edge type has TTL info
     int32_t etype0 = 0;             // the only slot's signed type (0: several slots)
     bool dstReplica = false;        // $$ props read the cross-shard replicas (8-byte, may lack values)
+    int32_t rowMask = 7;            // row arrays written: 1 src, 2 dst, 4 rank (ngx_go_plan::yield_only)
 };
 
 class JitCache {

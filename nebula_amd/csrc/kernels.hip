@@ -667,6 +667,7 @@ struct VmEv {
     static constexpr bool kFlat = false;              // branchy passes(): programs evaluated only when needed
     static constexpr bool kEflags = true, kTtl = true; // per-edge flags / TTL read when the slot has them
     static constexpr int kEtype = 0;                  // edge type read per slot
+    static constexpr int kRowMask = 7;                // row arrays: written where FinalArgs::o* is set
     static __device__ __forceinline__ void YV(const FinalArgs&, const EdgeCtx&, Val*) {}
     static __device__ __forceinline__ void YS(const FinalArgs&, const Val*, uint64_t, uint32_t&) {}
     static __device__ __forceinline__ bool hasP(const FinalArgs& a) { return a.P != nullptr; }

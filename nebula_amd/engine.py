@@ -103,7 +103,8 @@ class GoPlan(ctypes.Structure):
                 ("filter_pushdown", c_i32), ("now_sec", c_i64), ("result_on_device", c_i32),
                 ("host_columnar", c_i32), ("input_vid_col", ctypes.c_char_p), ("input_var", ctypes.c_char_p),
                 ("input_ncols", c_i32), ("input_names", P(ctypes.c_char_p)), ("input_types", P(c_i32)),
-                ("input_nrows", c_u64), ("input_cells", P(Cell)), ("input_strings", ctypes.c_char_p)]
+                ("input_nrows", c_u64), ("input_cells", P(Cell)), ("input_strings", ctypes.c_char_p),
+                ("yield_only", c_i32)]
 
 
 _CELL_KIND = {"empty": 0, "bool": 1, "int": 2, "id": 3, "float": 4, "double": 5, "str": 6, "timestamp": 21}
@@ -439,7 +440,8 @@ class Engine:
     # ---- GO
     def go(self, space: int, s: Union[str, ngql.GoSentence], pushdown: bool = True, now_sec: int = 0,
            raise_on_error: bool = False, rows: bool = True, on_device: bool = False, fetch: bool = False,
-           columnar: bool = False, digest_fn=None, arrays: bool = True, input=None) -> GoResult:
+           columnar: bool = False, digest_fn=None, arrays: bool = True, input=None,
+           yield_only: bool = False) -> GoResult:
         """Run one GO. rows=False skips decoding cells into Python tuples; on_device=True leaves the
         result rows in HBM (GoResult.nrows and the statistics only); with fetch=True the HBM arrays
         (src/dst/rank/type and the columnar YIELD columns) are copied back into the result.
@@ -447,7 +449,8 @@ class Engine:
         from the columns (ColumnValue typing by col_types) so they compare with the cell path.
         digest_fn(col_types, nrows, x_ptrs, len_ptrs, type_ptrs) is called on the host columns
         before the result is freed (tests: large-result comparison). FROM $-.col / $var.col reads
-        `input' (a nebula_amd.pipeline.Interim; None: no input, no rows)."""
+        `input' (a nebula_amd.pipeline.Interim; None: no input, no rows). yield_only (with on_device):
+        only the YIELD columns are materialised; src / dst / rank arrays only where a column aliases them."""
         if isinstance(s, str):
             s = ngql.parse_go(s)
         # the sentence's encoded form (expressions in Expression::encode bytes, vids as int64) is built once
@@ -471,6 +474,7 @@ class Engine:
                       names, aliases, 1 if s.over_all else 0, s.direction, where if where else None, len(where),
                       len(yb), yarr, ylen, 1 if s.distinct else 0, 1 if pushdown else 0, now_sec,
                       1 if on_device else 0, 1 if columnar else 0)
+        plan.yield_only = 1 if yield_only else 0
         if s.from_type:
             from .pipeline import Interim
             keep = _input_arrays(input if input is not None else Interim([]))
@@ -498,9 +502,9 @@ class Engine:
                                hop_xchg=[r.hop_exchange_bytes[i] for i in range(r.nhops)] if r.hop_exchange_bytes else [],
                                device_ms=r.device_ms)
                 if fetch and rc == 0:
-                    res.src = self._d2h(r.dev_src, n, np.int64)
-                    res.dst = self._d2h(r.dev_dst, n, np.int64)
-                    res.rank = self._d2h(r.dev_rank, n, np.int64)
+                    res.src = self._d2h(r.dev_src, n, np.int64) if r.dev_src else None
+                    res.dst = self._d2h(r.dev_dst, n, np.int64) if r.dev_dst else None
+                    res.rank = self._d2h(r.dev_rank, n, np.int64) if r.dev_rank else None
                     res.etype = (self._d2h(r.dev_type, n, np.int32) if r.dev_type
                                  else np.full(n, r.dev_type_const, np.int32))   # one OVER type: no column
                     cols = ctypes.cast(r.dev_cols, P(DevColumn)) if r.dev_cols else None
