@@ -1537,46 +1537,133 @@ void prepareCols(ngx_ctx* c, FinalArgs& a, const std::vector<ColSpec>& spec, uin
 }
 
 // result columns rows [first, first + n) -> host OutCells (row-major); a typed column's rows carry its static type
-std::vector<OutCell> downloadCells(ngx_ctx* c, const std::vector<ColSpec>& spec, const std::vector<int32_t>& colTypes,
-                                   uint64_t n, uint64_t first) {
-    // every column's arrays in one batch of copies into the page-locked stage, one synchronisation
-    size_t nY = spec.size();
-    std::vector<OutCell> raw(n * nY);
-    if (n == 0 || nY == 0) { HIP_OK(hipStreamSynchronize(c->stream)); return raw; }
-    const size_t per = (n * 13 + 63) & ~size_t(63);
-    char* stage = c->hostStage.get(per * nY);
-    for (size_t y = 0; y < nY; y++) {
-        const OutCol& v = c->oColView[y];
-        char* h = stage + per * y;
-        HIP_OK(hipMemcpyAsync(h, v.x + first, n * 8, hipMemcpyDeviceToHost, c->stream));
-        if (v.len) HIP_OK(hipMemcpyAsync(h + n * 8, v.len + first, n * 4, hipMemcpyDeviceToHost, c->stream));
-        if (v.t) HIP_OK(hipMemcpyAsync(h + n * 12, v.t + first, n, hipMemcpyDeviceToHost, c->stream));
-    }
-    HIP_OK(hipStreamSynchronize(c->stream));
-    parallelRows(n, [&](uint64_t lo, uint64_t hi, int) {
-        for (size_t y = 0; y < nY; y++) {
-            const OutCol& v = c->oColView[y];
-            const char* h = stage + per * y;
-            const int64_t* x = reinterpret_cast<const int64_t*>(h);
-            const uint32_t* len = reinterpret_cast<const uint32_t*>(h + n * 8);
-            const uint8_t* t = reinterpret_cast<const uint8_t*>(h + n * 12);
-            uint8_t st = V_ERR;
-            switch (y < colTypes.size() ? colTypes[y] : T_UNKNOWN) {
-                case T_BOOL: st = V_BOOL; break;
-                case T_INT: case T_VID: case T_TIMESTAMP: st = V_INT; break;
-                case T_FLOAT: case T_DOUBLE: st = V_DBL; break;
-                case T_STRING: st = V_STR; break;
-                default: break;
-            }
-            for (uint64_t r = lo; r < hi; r++) {
-                OutCell& o = raw[r * nY + y];
-                o.x = x[r];
-                o.len = v.len ? len[r] : 0;
-                o.t = v.t ? t[r] : st;
-            }
+// device arrays -> the context's page-locked staging, one synchronisation. Small batches go through one
+// copy kernel storing into the mapped staging: each DMA copy costs ~8 us of latency, which made a
+// GetNeighbors response's dozen arrays take 166 us (tools/gn_trace.py). Large batches use the DMA
+// engine (57 GB/s vs 55 GB/s for the kernel, tools/mb_d2h.hip, and the CUs stay free);
+// NGX_D2H=kernel / dma forces one.
+struct HostArr { const void* dev; size_t bytes; char* host; };
+void stageArrays(ngx_ctx* c, std::vector<HostArr>& arrs) {
+    constexpr size_t kKernelCopyMax = size_t(32) << 20;
+    size_t total = 0;
+    for (auto& a : arrs) total += (a.bytes + 63) & ~size_t(63);
+    char* stage = c->hostStage.get(std::max<size_t>(total, 64));
+    static const int mode = [] {
+        const char* e = std::getenv("NGX_D2H");
+        return e && std::string(e) == "kernel" ? 1 : e && std::string(e) == "dma" ? 2 : 0;
+    }();
+    const bool useKernel = mode == 1 || (mode == 0 && total <= kKernelCopyMax);
+    char* stageDev = nullptr;
+    if (useKernel && hipHostGetDevicePointer(reinterpret_cast<void**>(&stageDev), c->hostStage.p, 0) != hipSuccess)
+        stageDev = nullptr;
+    CopyBatch cb{};
+    for (auto& a : arrs) {
+        const size_t at = stage - static_cast<char*>(c->hostStage.p);
+        a.host = stage;
+        stage += (a.bytes + 63) & ~size_t(63);
+        if (!a.bytes) continue;
+        if (stageDev == nullptr) {
+            HIP_OK(hipMemcpyAsync(a.host, a.dev, a.bytes, hipMemcpyDeviceToHost, c->stream));
+            continue;
         }
-    });
-    return raw;
+        if (cb.n == kMaxCopies) {
+            if (launchCopyBatch(cb, c->stream)) throw Error{NGX_E_DEVICE, "copy to host"};
+            cb = CopyBatch{};
+        }
+        cb.src[cb.n] = static_cast<const uint8_t*>(a.dev);
+        cb.dst[cb.n] = reinterpret_cast<uint8_t*>(stageDev + at);
+        cb.bytes[cb.n] = a.bytes;
+        cb.start[cb.n + 1] = cb.start[cb.n] + (a.bytes + 15) / 16;
+        cb.n++;
+    }
+    if (cb.n && launchCopyBatch(cb, c->stream)) throw Error{NGX_E_DEVICE, "copy to host"};
+    HIP_OK(hipStreamSynchronize(c->stream));
+}
+
+// the result columns (and `extra` device arrays, staged alongside: their host copies come back in
+// extra[i].host), read in place from the page-locked staging as raw typed cells
+struct StagedCells {
+    std::vector<const int64_t*> x;
+    std::vector<const uint32_t*> len;
+    std::vector<const uint8_t*> t;
+    std::vector<uint8_t> st;                                     // value type of a column without types
+    OutCell at(uint64_t r, size_t y) const {
+        OutCell o;
+        o.x = x[y][r];
+        o.len = len[y] ? len[y][r] : 0;
+        o.t = t[y] ? t[y][r] : st[y];
+        return o;
+    }
+};
+StagedCells stageCells(ngx_ctx* c, const std::vector<ColSpec>& spec, const std::vector<int32_t>& colTypes,
+                       uint64_t n, uint64_t first, std::vector<HostArr>& extra) {
+    size_t nY = spec.size();
+    std::vector<HostArr> arrs(extra);
+    std::vector<size_t> iX(nY, SIZE_MAX), iLen(nY, SIZE_MAX), iT(nY, SIZE_MAX);
+    for (size_t y = 0; y < nY && n; y++) {
+        const OutCol& v = c->oColView[y];
+        iX[y] = arrs.size(); arrs.push_back(HostArr{v.x + first, n * 8, nullptr});
+        if (v.len) { iLen[y] = arrs.size(); arrs.push_back(HostArr{v.len + first, n * 4, nullptr}); }
+        if (v.t) { iT[y] = arrs.size(); arrs.push_back(HostArr{v.t + first, n, nullptr}); }
+    }
+    stageArrays(c, arrs);
+    for (size_t i = 0; i < extra.size(); i++) extra[i].host = arrs[i].host;
+    StagedCells sc;
+    for (size_t y = 0; y < nY && n; y++) {
+        sc.x.push_back(reinterpret_cast<const int64_t*>(arrs[iX[y]].host));
+        sc.len.push_back(iLen[y] == SIZE_MAX ? nullptr : reinterpret_cast<const uint32_t*>(arrs[iLen[y]].host));
+        sc.t.push_back(iT[y] == SIZE_MAX ? nullptr : reinterpret_cast<const uint8_t*>(arrs[iT[y]].host));
+        uint8_t st = V_ERR;
+        switch (y < colTypes.size() ? colTypes[y] : T_UNKNOWN) {
+            case T_BOOL: st = V_BOOL; break;
+            case T_INT: case T_VID: case T_TIMESTAMP: st = V_INT; break;
+            case T_FLOAT: case T_DOUBLE: st = V_DBL; break;
+            case T_STRING: st = V_STR; break;
+            default: break;
+        }
+        sc.st.push_back(st);
+    }
+    return sc;
+}
+
+// the hop's side of a generated final-hop kernel's shape: slots, widths, TTL, programs
+JitQuery jitHopQuery(const Space& sp, const HopSlots& hs, const Programs& progs) {
+    JitQuery jq;
+    jq.oneSlot = hs.n == 1;
+    jq.pos32 = true;
+    for (int s = 0; s < hs.n; s++) jq.pos32 = jq.pos32 && sp.host->slots[hs.slotIdx[s]].dst.size() < (1ULL << 32);
+    jq.P = JitProgram{progs.P >= 0 ? progs.code.data() + progs.P : nullptr, progs.P >= 0};
+    jq.W = JitProgram{progs.W >= 0 ? progs.code.data() + progs.W : nullptr, progs.W >= 0};
+    for (int32_t off : progs.yOff) jq.Y.push_back(JitProgram{progs.code.data() + off, true});
+    for (int s = 0; s < hs.n; s++) {
+        jq.slots.push_back(hs.slotIdx[s]);
+        int32_t tc;
+        int64_t td;
+        jq.ttl = jq.ttl || ttlInfo(sp.edge(std::abs(hs.etype[s])), tc, td);
+    }
+    jq.etype0 = hs.n == 1 ? hs.etype[0] : 0;
+    jq.dstW = hs.n ? hs.dstW[0] : 0;
+    jq.rankW = hs.n ? hs.rankW[0] : 0;
+    for (int s = 1; s < hs.n; s++) {
+        if (hs.dstW[s] != jq.dstW) jq.dstW = 0;
+        if (hs.rankW[s] != jq.rankW) jq.rankW = 0;
+    }
+    return jq;
+}
+
+// literals -> launch-time constant slots (one kernel per query shape)
+void jitSlotConsts(JitQuery& jq, std::vector<int64_t>& kc, std::vector<uint32_t>& kl) {
+    auto slotConsts = [&](const Insn* code) {
+        for (const Insn* in = code; in && in->op != OP_END; in++) {
+            if (in->op != OP_PUSH || static_cast<int>(kc.size()) >= kJitConsts) continue;
+            jq.constSlot[in] = static_cast<int32_t>(kc.size());
+            kc.push_back(in->imm);
+            kl.push_back(static_cast<uint32_t>(in->a));
+        }
+    };
+    if (jq.P.present) slotConsts(jq.P.code);
+    if (jq.W.present) slotConsts(jq.W.code);
+    for (auto& y : jq.Y) slotConsts(y.code);
 }
 
 int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, const InputBind* in = nullptr) {
@@ -1674,42 +1761,12 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     std::vector<uint32_t> jitKl;
     c->jitNote.clear();
     if (c->jitOn) {
-        JitQuery jq;
-        jq.oneSlot = hs.n == 1;
-        jq.pos32 = true;
-        for (int s = 0; s < hs.n; s++) jq.pos32 = jq.pos32 && sp.host->slots[hs.slotIdx[s]].dst.size() < (1ULL << 32);
-        jq.P = JitProgram{progs.P >= 0 ? progs.code.data() + progs.P : nullptr, progs.P >= 0};
-        jq.W = JitProgram{progs.W >= 0 ? progs.code.data() + progs.W : nullptr, progs.W >= 0};
-        for (int32_t off : progs.yOff) jq.Y.push_back(JitProgram{progs.code.data() + off, true});
+        JitQuery jq = jitHopQuery(sp, hs, progs);
         jq.yColType = gp.colTypes;
         jq.yKey = yAlias;
-        for (int s = 0; s < hs.n; s++) {
-            jq.slots.push_back(hs.slotIdx[s]);
-            int32_t tc;
-            int64_t td;
-            jq.ttl = jq.ttl || ttlInfo(sp.edge(std::abs(hs.etype[s])), tc, td);
-        }
-        jq.etype0 = hs.n == 1 ? hs.etype[0] : 0;
         jq.dstReplica = dstReplica;
         jq.rowMask = rowMask;
-        jq.dstW = hs.n ? hs.dstW[0] : 0;
-        jq.rankW = hs.n ? hs.rankW[0] : 0;
-        for (int s = 1; s < hs.n; s++) {
-            if (hs.dstW[s] != jq.dstW) jq.dstW = 0;
-            if (hs.rankW[s] != jq.rankW) jq.rankW = 0;
-        }
-        // literals -> launch-time constant slots (one kernel per query shape)
-        auto slotConsts = [&](const Insn* code) {
-            for (const Insn* in = code; in && in->op != OP_END; in++) {
-                if (in->op != OP_PUSH || static_cast<int>(jitKc.size()) >= kJitConsts) continue;
-                jq.constSlot[in] = static_cast<int32_t>(jitKc.size());
-                jitKc.push_back(in->imm);
-                jitKl.push_back(static_cast<uint32_t>(in->a));
-            }
-        };
-        if (jq.P.present) slotConsts(jq.P.code);
-        if (jq.W.present) slotConsts(jq.W.code);
-        for (auto& y : jq.Y) slotConsts(y.code);
+        jitSlotConsts(jq, jitKc, jitKl);
         std::string jerr;
         // kernels cached by query shape: the source is generated only on a miss
         jk = c->jit.get(jitShapeKey(sp, jq), [&] { return jitSource(sp, jq); }, jerr);
@@ -2257,7 +2314,6 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     }
     // ---- results to the host: every array in one batch of D2H copies into page-locked staging
     const uint64_t n = totalRows;
-    struct HostArr { const void* dev; size_t bytes; char* host; };
     std::vector<HostArr> arrs;
     auto want = [&](const void* dev, size_t bytes) { arrs.push_back(HostArr{dev, bytes, nullptr}); return arrs.size() - 1; };
     size_t iSrc = want(c->oSrc.p, n * 8), iDst = want(c->oDst.p, n * 8), iRank = want(c->oRank.p, n * 8);
@@ -2270,37 +2326,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         if (v.len) iLen[y] = want(v.len, n * 4);
         if (v.t) iT[y] = want(v.t, n);
     }
-    size_t total = 0;
-    for (auto& a : arrs) total += (a.bytes + 63) & ~size_t(63);
-    char* stage = c->hostStage.get(std::max<size_t>(total, 64));
-    // the copy: the DMA engine (default; 57 GB/s into page-locked memory, tools/mb_d2h.hip) or a kernel
-    // streaming into the mapped staging (NGX_D2H=kernel, 55 GB/s, occupies the CUs)
-    static const bool dmaCopy = [] { const char* e = std::getenv("NGX_D2H"); return !(e && std::string(e) == "kernel"); }();
-    char* stageDev = nullptr;
-    if (!dmaCopy && hipHostGetDevicePointer(reinterpret_cast<void**>(&stageDev), c->hostStage.p, 0) != hipSuccess)
-        stageDev = nullptr;
-    CopyBatch cb{};
-    for (auto& a : arrs) {
-        const size_t at = stage - static_cast<char*>(c->hostStage.p);
-        a.host = stage;
-        stage += (a.bytes + 63) & ~size_t(63);
-        if (!a.bytes) continue;
-        if (stageDev == nullptr) {
-            HIP_OK(hipMemcpyAsync(a.host, a.dev, a.bytes, hipMemcpyDeviceToHost, c->stream));
-            continue;
-        }
-        if (cb.n == kMaxCopies) {
-            if (launchCopyBatch(cb, c->stream)) throw Error{NGX_E_DEVICE, "copy to host"};
-            cb = CopyBatch{};
-        }
-        cb.src[cb.n] = static_cast<const uint8_t*>(a.dev);
-        cb.dst[cb.n] = reinterpret_cast<uint8_t*>(stageDev + at);
-        cb.bytes[cb.n] = a.bytes;
-        cb.start[cb.n + 1] = cb.start[cb.n] + (a.bytes + 15) / 16;
-        cb.n++;
-    }
-    if (cb.n && launchCopyBatch(cb, c->stream)) throw Error{NGX_E_DEVICE, "copy to host"};
-    HIP_OK(hipStreamSynchronize(c->stream));
+    stageArrays(c, arrs);
     int64_t* hSrc = reinterpret_cast<int64_t*>(arrs[iSrc].host);
     int64_t* hDst = reinterpret_cast<int64_t*>(arrs[iDst].host);
     int64_t* hRank = reinterpret_cast<int64_t*>(arrs[iRank].host);
@@ -2669,6 +2695,7 @@ void encodeTagRows(const ngx_gn_request& q, const std::vector<int32_t>& tagOrder
 }
 
 int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResultHolder& R) {
+    c->hmark("gn");
     DeviceGraph& d = *sp.dev;
     auto failAll = [&](int32_t code) {
         R.r.code = code;
@@ -2787,6 +2814,7 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
         progs.yOff.push_back(progs.add(yp));
     }
     DevPrograms dp = uploadPrograms(c, progs, ySlotType);
+    c->hmark("progs");
     // seeds in request order; a part this shard does not hold fails with E_PART_NOT_FOUND (NebulaStore::
     // prefix -> ERR_PART_NOT_FOUND, BaseProcessor::to; QueryBaseProcessor.inl:835-851) and its vids match
     // no vertex row
@@ -2816,6 +2844,28 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
     uint64_t* counters = c->counters.get<uint64_t>(8);
     uint32_t* errFlag = reinterpret_cast<uint32_t*>(counters + 4);
     HIP_OK(hipMemsetAsync(counters, 0, 64, c->stream));
+    // per-vertex tag columns (k_vertex_cells), launched now; their cells come back with the edge arrays
+    const int32_t nY = q.ncols;
+    OutCell* vcellsDev = nullptr;
+    if (nF && nY) {
+        std::vector<int32_t> tslot(nY, -1), tcol(nY, 0);
+        for (int32_t i = 0; i < nY; i++) {
+            if (q.cols[i].owner == 1 || q.cols[i].owner == 2) {
+                tslot[i] = sp.tagSlotOf(q.cols[i].id);
+                tcol[i] = sp.tag(q.cols[i].id)->latest().index(q.cols[i].name);
+            }
+        }
+        int32_t* dts = c->misc.get<int32_t>(2 * nY);
+        std::vector<int32_t> both(tslot);
+        both.insert(both.end(), tcol.begin(), tcol.end());
+        HIP_OK(hipMemcpyAsync(dts, both.data(), both.size() * 4, hipMemcpyHostToDevice, c->stream));
+        VertexCellArgs va{};
+        va.rows = F; va.n = nF; va.ncols = nY; va.tagSlot = dts; va.col = dts + nY;
+        va.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1, now, d.dtags, d.dcols};
+        va.out = vcellsDev = c->vcells.get<OutCell>(nF * nY);
+        if (launchVertexCells(va, c->stream)) throw Error{NGX_E_DEVICE, "vertex cells"};
+    }
+
     uint64_t nEnt = nF * static_cast<uint64_t>(hs.n);
     uint64_t E = 0;
     uint64_t* estart = c->estart.get<uint64_t>(nEnt + 1);
@@ -2825,9 +2875,11 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
         if (launchDegreeScan(F, nEnt, hs, estart, tiles, c->stream, pub)) throw Error{NGX_E_DEVICE, "degree"};
         E = awaitPub(c, pub, estart + nEnt);
     }
+    c->hmark("E");
     uint64_t nrows = 0;
-    int32_t nY = q.ncols;
-    std::vector<OutCell> raw;
+    StagedCells staged;
+    std::vector<char*> vhost;                                     // staged flags / vertex cells, if rows came back
+    uint32_t flagsHost[4];
     if (E) {
         uint64_t chunks = (E + kChunk - 1) / kChunk;
         uint64_t* chunkFirst = c->chunkFirst.get<uint64_t>(chunks);
@@ -2867,18 +2919,52 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
         std::vector<ColSpec> spec(nY, ColSpec{true, true});   // raw value cells: every column typed per row
         prepareCols(c, a, spec, E, 0);
         a.lbStatus = lb;
-        if (launchFinal(a, c->stream)) throw Error{NGX_E_DEVICE, "final"};
+        // a generated kernel for the request shape (the interpreter's per-instruction loads serialize a
+        // chunk's edges: 170 us for 25 K edges); a masked request (max-edges cap) stays on the interpreter
+        const JitKernels* jk = nullptr;
+        if (c->jitOn && !a.mask) {
+            JitQuery jq = jitHopQuery(sp, hs, progs);
+            jq.fidx = true;
+            jq.yColType.assign(nY, 0);
+            jq.yKey.assign(nY, -1);
+            for (int32_t y = 0; y < nY; y++) {
+                int32_t st = ySlotType[y];
+                if (hs.n == 1 && st == hs.etype[0]) st = 0;   // every edge is of the column's type
+                if (st != INT32_MIN && hs.n == 1 && st != 0) st = INT32_MIN;   // a type this request skips
+                jq.ySlot.push_back(st);
+            }
+            std::vector<int64_t> kc;
+            std::vector<uint32_t> kl;
+            jitSlotConsts(jq, kc, kl);
+            for (size_t k = 0; k < kc.size(); k++) { a.kc[k] = kc[k]; a.kl[k] = kl[k]; }
+            std::string jerr;
+            jk = c->jit.get(jitShapeKey(sp, jq), [&] { return jitSource(sp, jq); }, jerr);
+        }
+        if (jk) {
+            void* args[] = {&a};
+            HIP_OK(hipModuleLaunchKernel(jk->final, static_cast<unsigned>(chunks), 1, 1, 256, 1, 1, 0, c->stream, args, nullptr));
+        } else if (launchFinal(a, c->stream)) {
+            throw Error{NGX_E_DEVICE, "final"};
+        }
         nrows = readScalar(c, a.lbStatus + chunks) & ((1ULL << 62) - 1);
+        c->hmark("rows");
         R.edgeVertex.resize(nrows);
         R.edgeType.resize(nrows);
         R.edgeDst.resize(nrows);
         if (nrows) {
-            HIP_OK(hipMemcpyAsync(R.edgeVertex.data(), a.oEntry, nrows * 4, hipMemcpyDeviceToHost, c->stream));
-            HIP_OK(hipMemcpyAsync(R.edgeType.data(), a.oType, nrows * 4, hipMemcpyDeviceToHost, c->stream));
-            HIP_OK(hipMemcpyAsync(R.edgeDst.data(), a.oDst, nrows * 8, hipMemcpyDeviceToHost, c->stream));
-            raw = downloadCells(c, spec, std::vector<int32_t>(nY, T_UNKNOWN), nrows, 0);
+            // the per-edge arrays staged with the cells (a pageable destination makes each copy a
+            // synchronous staged transfer)
+            std::vector<HostArr> ex{{a.oEntry, nrows * 4, nullptr}, {a.oType, nrows * 4, nullptr}, {a.oDst, nrows * 8, nullptr},
+                                    {errFlag, 16, nullptr}};
+            if (vcellsDev) ex.push_back(HostArr{vcellsDev, nF * nY * sizeof(OutCell), nullptr});
+            staged = stageCells(c, spec, std::vector<int32_t>(nY, T_UNKNOWN), nrows, 0, ex);
+            for (size_t i = 3; i < ex.size(); i++) vhost.push_back(ex[i].host);
+            std::memcpy(R.edgeVertex.data(), ex[0].host, nrows * 4);
+            std::memcpy(R.edgeType.data(), ex[1].host, nrows * 4);
+            std::memcpy(R.edgeDst.data(), ex[2].host, nrows * 8);
             if (q.encode_rows) encodeEdgeRows(c, a, nrows, respCols, R);
             HIP_OK(hipStreamSynchronize(c->stream));
+            c->hmark("d2h");
             // IdAndProp.dst is set only by a `_dst` return column of the edge type (PropsCollector::
             // collectDstId, Collector.h:77-82); without one the reference leaves it 0
             std::set<int32_t> withDst;
@@ -2887,30 +2973,23 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
             for (uint64_t i = 0; i < nrows; i++) if (!withDst.count(R.edgeType[i])) R.edgeDst[i] = 0;
         }
     }
-    // per-vertex tag columns
+    // per-vertex tag cells and the error flags: staged with the edge arrays when there are rows,
+    // otherwise on their own (one synchronisation either way)
     std::vector<OutCell> vraw(nF * std::max(nY, 1));
-    if (nF && nY) {
-        std::vector<int32_t> tslot(nY, -1), tcol(nY, 0);
-        for (int32_t i = 0; i < nY; i++) {
-            if (q.cols[i].owner == 1 || q.cols[i].owner == 2) {
-                tslot[i] = sp.tagSlotOf(q.cols[i].id);
-                tcol[i] = sp.tag(q.cols[i].id)->latest().index(q.cols[i].name);
-            }
+    {
+        std::vector<HostArr> tail{{errFlag, 16, nullptr}};
+        if (vcellsDev) tail.push_back(HostArr{vcellsDev, nF * nY * sizeof(OutCell), nullptr});
+        if (!vhost.empty()) {
+            for (size_t i = 0; i < tail.size(); i++) tail[i].host = vhost[i];
+        } else {
+            stageArrays(c, tail);
         }
-        int32_t* dts = c->misc.get<int32_t>(2 * nY);
-        std::vector<int32_t> both(tslot);
-        both.insert(both.end(), tcol.begin(), tcol.end());
-        HIP_OK(hipMemcpyAsync(dts, both.data(), both.size() * 4, hipMemcpyHostToDevice, c->stream));
-        VertexCellArgs va{};
-        va.rows = F; va.n = nF; va.ncols = nY; va.tagSlot = dts; va.col = dts + nY;
-        va.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1, now, d.dtags, d.dcols};
-        va.out = c->vcells.get<OutCell>(nF * nY);
-        if (launchVertexCells(va, c->stream)) throw Error{NGX_E_DEVICE, "vertex cells"};
-        HIP_OK(hipMemcpyAsync(vraw.data(), va.out, nF * nY * sizeof(OutCell), hipMemcpyDeviceToHost, c->stream));
+        std::memcpy(flagsHost, tail[0].host, 16);
+        if (vcellsDev) std::memcpy(vraw.data(), tail[1].host, nF * nY * sizeof(OutCell));
     }
-    HIP_OK(hipStreamSynchronize(c->stream));
+    c->hmark("vcells");
     uint32_t flags[4];
-    HIP_OK(hipMemcpy(flags, errFlag, 16, hipMemcpyDeviceToHost));
+    std::memcpy(flags, flagsHost, 16);
     if (flags[3]) throw Error{NGX_E_DEVICE, "final-hop look-back did not complete (device fault)"};
     if (flags[1]) throw Error{NGX_E_UNSUPPORTED, "a return column needs a host-only construct"};
     R.edgeCells.resize(nrows * nY);
@@ -2919,7 +2998,20 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
         const int T = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(hostThreads(), (nrows * nY) / 65536 + 1)));
         std::vector<std::string> arena(T);
         parallelRows(nrows, [&](uint64_t lo, uint64_t hi, int t) {
-            for (uint64_t i = lo * nY; i < hi * nY; i++) rawCell(raw[i], R.edgeCells[i], arena[t], d, dp, progs.pool);
+            // column by column: each staged array is read front to back
+            for (int32_t y = 0; y < nY; y++) {
+                const int64_t* x = staged.x[y];
+                const uint32_t* ln = staged.len[y];
+                const uint8_t* ty = staged.t[y];
+                const uint8_t st = staged.st[y];
+                for (uint64_t r = lo; r < hi; r++) {
+                    OutCell v;
+                    v.x = x[r];
+                    v.len = ln ? ln[r] : 0;
+                    v.t = ty ? ty[r] : st;
+                    rawCell(v, R.edgeCells[r * nY + y], arena[t], d, dp, progs.pool);
+                }
+            }
         }, T);
         std::vector<uint64_t> base(T);
         for (int t = 0; t < T; t++) { base[t] = R.strings.size(); R.strings += arena[t]; }
@@ -2933,6 +3025,7 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
         rawCell(vraw[i], R.vertexCells[i], R.strings, d, dp, progs.pool);
         R.vertexHasTag[i] = vraw[i].t != 0xFF ? 1 : 0;
     }
+    c->hmark("cells");
     R.r.nvertices = static_cast<uint32_t>(nF);
     R.r.nedges = nrows;
     if (q.encode_rows) {
@@ -2956,6 +3049,8 @@ extern "C" int32_t ngx_get_neighbors(ngx_ctx* c, const ngx_gn_request* q, ngx_gn
     } catch (const Error& e) {
         rc = fail(c, e.code, e.msg);
     }
+    c->hmark("end");
+    c->hflush();
     if (rc != NGX_OK) R->r.code = rc;
     R->r.nfailed = static_cast<int32_t>(R->failed.size() / 2);
     R->r.failed_codes = R->failed.data();
