@@ -150,7 +150,9 @@ int32_t ngx_graph_info_get(ngx_ctx* ctx, int32_t space, ngx_graph_info* out);
 #define NGX_CELL_TIMESTAMP 21
 typedef struct {
     int32_t kind;                 /* NGX_CELL_* */
-    int32_t str_len;              /* for NGX_CELL_STR */
+    int32_t str_len;              /* for NGX_CELL_STR; 1 on an EMPTY cell that holds a bool in v.i (a bool
+                                   * of an UNKNOWN-typed YIELD column: toThriftResponse leaves it unset,
+                                   * the interim result of a pipe keeps it) */
     union { int64_t i; double d; uint64_t str_off; } v;   /* str_off indexes the result's strings */
 } ngx_cell;
 

@@ -619,7 +619,9 @@ bool toCell(const OutCell& v, int32_t colType, ngx_cell& out, std::string& strin
             switch (v.t) {
                 case V_INT: out.kind = NGX_CELL_INT; out.v.i = v.x; return true;
                 case V_DBL: out.kind = NGX_CELL_DOUBLE; out.v.i = v.x; return true;
-                case V_BOOL: out.kind = NGX_CELL_EMPTY; return true;          // left unset by the reference
+                // left unset by toThriftResponse; the value stays in v.i (str_len 1 marks it) for an
+                // interim result and for DISTINCT over pipe walks
+                case V_BOOL: out.kind = NGX_CELL_EMPTY; out.v.i = v.x; out.str_len = 1; return true;
                 case V_STR: str(); return true;
                 default: out.kind = NGX_CELL_EMPTY; return true;
             }

@@ -120,7 +120,7 @@ def _input_arrays(inp):
     for r, row in enumerate(inp.rows):
         for c, (kind, v) in enumerate(row):
             cl = cells[r * nc + c]
-            cl.kind = _CELL_KIND[kind]
+            cl.kind = _CELL_KIND[kind] if not (kind == "empty" and v is not None) else 1
             if kind == "str":
                 b = v.encode("utf-8", "surrogateescape")
                 cl.v.str_off = len(strings)
@@ -128,7 +128,7 @@ def _input_arrays(inp):
                 strings += b
             elif kind in ("float", "double"):
                 cl.v.d = v
-            elif kind != "empty":
+            elif v is not None:                                   # ints, bools (an unset bool too)
                 cl.v.i = int(v)
     return names, types, cells, bytes(strings) + b"\0", nc, nr
 
@@ -247,7 +247,7 @@ def _cells(cells, n, ncols, strings: bytes):
             cl = cells[r * ncols + c]
             k = kinds.get(cl.kind, str(cl.kind))
             if cl.kind == 0:
-                row.append(("empty", None))
+                row.append(("empty", bool(cl.v.i) if cl.str_len == 1 else None))
             elif cl.kind == 1:
                 row.append(("bool", bool(cl.v.i)))
             elif cl.kind in (4, 5):
@@ -575,7 +575,7 @@ class Engine:
                     elif vt == 2:
                         row.append((kinds.get(types[c], "double"), float(np.int64(v).view(np.float64))))
                     elif vt == 3:
-                        row.append(("bool", bool(v)) if types[c] == 1 else ("empty", None))
+                        row.append(("bool", bool(v)) if types[c] == 1 else ("empty", bool(v)))
                     elif vt == 1:
                         row.append((kinds.get(types[c], "int"), v))
                     else:

@@ -41,7 +41,8 @@ class Interim:
         types = []
         for i, t in enumerate(col_types):
             if t == T_UNKNOWN:                                    # GoExecutor.cpp:1008-1026
-                t = _KIND_TYPE[rows[0][i][0]]
+                kind, v = rows[0][i]
+                t = T_BOOL if kind == "empty" and v is not None else _KIND_TYPE.get(kind, T_UNKNOWN)
             types.append(t)
         return Interim(list(names), types, list(rows))
 

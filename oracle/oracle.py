@@ -254,6 +254,8 @@ def _cell(r: _Rd):
         return ("str", r.str().decode("utf-8", "surrogateescape"))
     if t == 0xFE:
         return ("type_error", None)
+    if t == 0xFD:                        # a bool of an UNKNOWN column: unset in the response
+        return ("empty", bool(r.get("B")))
     raise ValueError(t)
 
 
@@ -379,7 +381,7 @@ class Oracle:
                     b += struct.pack("<B", 3) + _s(v.encode("utf-8", "surrogateescape"))
                 elif kind in ("float", "double"):
                     b += struct.pack("<Bd", 1, v)
-                elif kind == "bool":
+                elif kind == "bool" or (kind == "empty" and v is not None):
                     b += struct.pack("<BB", 2, 1 if v else 0)
                 else:
                     b += struct.pack("<Bq", 0, int(v))

@@ -71,7 +71,8 @@ void cell(Writer& w, SupportedType t, const Variant& v) {
             switch (which(v)) {
                 case VAR_INT64: w.put<uint8_t>(2); w.put<int64_t>(std::get<int64_t>(v)); return;
                 case VAR_DOUBLE: w.put<uint8_t>(5); w.put<double>(std::get<double>(v)); return;
-                case VAR_BOOL: w.put<uint8_t>(0); return;               // left unset by the reference
+                // left unset by toThriftResponse; the value travels on for an interim result (pipe)
+                case VAR_BOOL: w.put<uint8_t>(0xFD); w.put<uint8_t>(std::get<bool>(v)); return;
                 default: w.put<uint8_t>(6); w.str(std::get<std::string>(v)); return;
             }
     }
@@ -145,7 +146,7 @@ void orc_digest_columns(int32_t ncols, const int32_t* colTypes, uint64_t nrows, 
                 default:
                     if (vt == 1) { w.put<uint8_t>(2); w.put<int64_t>(v); }
                     else if (vt == 2) { w.put<uint8_t>(5); w.put<double>(d); }
-                    else if (vt == 3) { w.put<uint8_t>(0); }
+                    else if (vt == 3) { w.put<uint8_t>(0xFD); w.put<uint8_t>(v != 0); }
                     else str();
             }
         }

@@ -64,6 +64,10 @@ RMAT_PIPES = [
     "GO FROM {S} OVER e YIELD e._dst AS id | GO 2 STEPS FROM $-.id OVER e YIELD DISTINCT e._dst",
     # variables
     "$v = GO FROM {S} OVER e YIELD e._dst AS id, e.p0 AS w; GO FROM $v.id OVER e WHERE e.p0 < $v.w YIELD $v.*, e.p0",
+    # a bool of an UNKNOWN-typed column: unset in the response, kept in the interim result and as a
+    # DISTINCT key (true and false rows stay apart)
+    "GO FROM {S} OVER e YIELD e._dst AS id, !(e.p0 > 50) AS b | GO FROM $-.id OVER e WHERE $-.b YIELD DISTINCT $-.b, e.p1 % 3",
+    "GO FROM {S} OVER e YIELD e._dst AS id | GO 2 STEPS FROM $-.id OVER e YIELD DISTINCT !(e.p0 > 50), e.p1 % 2",
 ]
 
 
