@@ -250,7 +250,8 @@ def main():
         name, (launches, ms, algo) = dom
         achieved = algo / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         traffic = None
-        if os.path.exists(args.traffic):
+        # the committed PMC bytes were measured on the N = 1 C2 step: other workloads report none
+        if os.path.exists(args.traffic) and world == 1 and scale == 22 and not args.yield_only:
             try:
                 tj = json.load(open(args.traffic))
                 if tj.get("kernel_class") == name:
