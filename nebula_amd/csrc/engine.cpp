@@ -42,6 +42,10 @@ struct DeviceGraph {
     VIndex vindex{nullptr, 0};                          // (part, vid) -> row hash index (seed lookup)
     std::vector<DSlot> slots;
     std::vector<int32_t> mirror;                        // per slot: the slot holding its exact transpose, or -1
+    // per slot with a mirror: the pull hop's head image of the in-lists (kernels.h PullArgs)
+    struct PullHead { const uint32_t* perm = nullptr; const uint32_t* head = nullptr; const uint8_t* nk = nullptr;
+                      uint64_t slices = 0, longRows = 0; };
+    std::vector<PullHead> pullHead;
     // $$ props across shards: every tag table over ALL global rows (replicas of the other shards'
     // rows), gathered on the first query that reads a $$ prop, kept until the next commit
     bool replicas = false;
@@ -107,16 +111,17 @@ struct ngx_ctx {
     ngx_exchange_fn xchg = nullptr;                    // host collective instead of RCCL (tests)
     uint64_t* pin = nullptr;                           // host-mapped [value, seq]: scan totals published by
     uint64_t* pinDev = nullptr;                        // k_scan_tiles (kernels.h Publish)
-    uint64_t pinSeq = 0;
+    uint64_t pinSeq = 0;                               // words [0, 2): scan totals; [kTailOff ..): query tail
+    static constexpr size_t kPinBytes = 1024;
+    static constexpr size_t kTailOff = 8;               // k_publish_tail: seq, error bits, extra words
     void* xchgUser = nullptr;
     std::map<int32_t, std::unique_ptr<Space>> spaces;
     std::string lastError;
     std::mutex mu;
     // scratch
     DBuf visited, F0, F1, estart, chunkFirst, tileSums, counters, lbStatus, seedPart, seedVid;
-    DBuf cmpStatus[2];                                  // k_compact_lb look-back words (double buffer, kept zeroed)
-    uint64_t cmpWords = 0;                              // capacity of each cmpStatus buffer, in words
-    int cmpPar = 0;
+    DBuf cmpStatus[2];                                  // compaction tile / wave totals (kernels.h CompactArgs)
+    DBuf frontierBits;                                  // the pull's frontier bitmap over global rows
     DBuf oSrc, oDst, oRank, oType, oEntry, progBuf, sendBits, recvBits, vcells, misc, oColDesc, edgeMask;
     DBuf oFlags, rowCols, rowLen, rowOff, rowBytes;     // GetNeighbors response rows (encode_rows)
     DBuf dkTable, dkKeep, dkPre, dSrc, dDst, dRank, dType;   // YIELD DISTINCT (table, marks, compacted rows)
@@ -187,7 +192,7 @@ struct ngx_ctx {
         spaces.clear();
         for (DBuf* b : {&visited, &F0, &F1, &estart, &tileSums, &counters, &lbStatus, &seedPart, &seedVid, &oSrc,
                         &oDst, &oRank, &oType, &oEntry, &chunkFirst, &oColDesc, &progBuf, &sendBits, &recvBits,
-                        &vcells, &misc, &edgeMask, &cmpStatus[0], &cmpStatus[1], &oFlags, &rowCols, &rowLen,
+                        &vcells, &misc, &edgeMask, &cmpStatus[0], &cmpStatus[1], &frontierBits, &oFlags, &rowCols, &rowLen,
                         &rowOff, &rowBytes, &pullSeg, &pullCtl, &dkTable, &dkKeep, &dkPre, &dSrc, &dDst, &dRank,
                         &dType, &dynStats}) b->release();
         for (auto& cb : oCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
@@ -475,6 +480,24 @@ void stageSeeds(ngx_ctx* c, const std::vector<int32_t>& parts, const std::vector
     }
 }
 
+// seeds (vids then parts) into the page-locked input stage after the programs, returned as device-visible
+// pointers into that (mapped) stage: the seed kernel reads them over the bus, no copy launch. False when
+// the stage cannot be mapped (the caller copies instead).
+bool stageSeedsMapped(ngx_ctx* c, const std::vector<int32_t>& parts, const std::vector<int64_t>& vids, const int32_t*& hpart,
+                      const int64_t*& hvid) {
+    const size_t n = vids.size();
+    const size_t progBytes = (c->progStageBytes + 63) & ~size_t(63);
+    if (c->inStage.cap < progBytes + n * 12 + 64) HIP_OK(hipStreamSynchronize(c->stream));
+    char* host = c->inStage.getKeep(progBytes + n * 12 + 64, progBytes);
+    char* dev = nullptr;
+    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&dev), c->inStage.p, 0) != hipSuccess || dev == nullptr) return false;
+    std::memcpy(host + progBytes, vids.data(), n * 8);
+    std::memcpy(host + progBytes + n * 8, parts.data(), n * 4);
+    hvid = reinterpret_cast<const int64_t*>(dev + progBytes);
+    hpart = reinterpret_cast<const int32_t*>(dev + progBytes + n * 8);
+    return true;
+}
+
 // VM string pointer -> host bytes
 std::string hostString(const DeviceGraph& d, const DevPrograms& dp, const std::string& pool, uint64_t ptr, uint32_t len) {
     if (len == 0) return std::string();
@@ -580,9 +603,65 @@ PairDigest slotDigest(const HostSlot& s, bool transpose) {
     return out;
 }
 
+// The pull hop's head image of hop slot `s` whose mirror is `m` (kernels.h PullArgs): the in-list of
+// row r over s is r's adjacency in m (dgid = the in-neighbour's row). Rows are ordered inside windows
+// of kPullWindow rows by min(in-degree, kPullK) descending, so the lanes of a slice need similar
+// numbers of rounds; each row's first kPullK in-neighbours are the ones with the largest out-degree
+// over s (a frontier reached by expansion holds the hubs first, so most reached rows hit on their
+// first probe). Which in-neighbours are probed first changes nothing but the probe count: the pull
+// computes set membership.
+void buildPullHead(const HostGraph& g, int32_t s, int32_t m, DeviceGraph& d) {
+    const HostSlot& out = g.slots[s];
+    const HostSlot& in = g.slots[m];
+    const uint64_t V = g.vid.size();
+    const uint64_t slices = (V + 63) / 64;
+    std::vector<uint32_t> perm(slices * 64, kNoRow), head(slices * 64 * kPullK, kNoRow);
+    std::vector<uint8_t> nk(slices, 0);
+    const uint64_t windows = (V + kPullWindow - 1) / kPullWindow;
+    std::vector<uint64_t> longRows(hostThreads() + 1, 0);
+    auto outDeg = [&](uint32_t u) -> uint64_t { return u < V ? out.off[u + 1] - out.off[u] : 0; };
+    parallelRows(windows, [&](uint64_t lo, uint64_t hi, int t) {
+        std::vector<std::pair<uint32_t, uint32_t>> rows;        // (head length, row)
+        std::vector<uint32_t> nb;
+        for (uint64_t w = lo; w < hi; w++) {
+            const uint64_t r0 = w * kPullWindow, r1 = std::min<uint64_t>(V, r0 + kPullWindow);
+            rows.clear();
+            for (uint64_t r = r0; r < r1; r++) {
+                const uint64_t deg = in.off[r + 1] - in.off[r];
+                rows.emplace_back(static_cast<uint32_t>(std::min<uint64_t>(deg, kPullK)), static_cast<uint32_t>(r));
+            }
+            std::stable_sort(rows.begin(), rows.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+            for (uint64_t i = 0; i < rows.size(); i++) {
+                const uint64_t at = r0 + i, slice = at / 64, lane = at % 64;
+                const uint32_t r = rows[i].second;
+                const uint64_t deg = in.off[r + 1] - in.off[r];
+                nb.assign(in.dgid.begin() + in.off[r], in.dgid.begin() + in.off[r + 1]);
+                nb.erase(std::remove(nb.begin(), nb.end(), kNoRow), nb.end());
+                const size_t keep = std::min<size_t>(nb.size(), kPullK);
+                std::partial_sort(nb.begin(), nb.begin() + keep, nb.end(), [&](uint32_t a, uint32_t b) {
+                    const uint64_t da = outDeg(a), db = outDeg(b);
+                    return da != db ? da > db : a < b;
+                });
+                for (size_t k = 0; k < keep; k++) head[(slice * kPullK + k) * 64 + lane] = nb[k];
+                const bool isLong = deg > static_cast<uint64_t>(kPullK);
+                perm[at] = r | (isLong ? kPullLong : 0u);
+                longRows[t] += isLong;
+                nk[slice] = std::max<uint8_t>(nk[slice], static_cast<uint8_t>(keep));
+            }
+        }
+    }, windows < 64 ? 1 : hostThreads());
+    DeviceGraph::PullHead ph;
+    ph.perm = d.upload(perm.data(), perm.size());
+    ph.head = d.upload(head.data(), head.size());
+    ph.nk = d.upload(nk.data(), nk.size());
+    ph.slices = slices;
+    for (uint64_t x : longRows) ph.longRows += x;
+    d.pullHead[s] = ph;
+}
+
 std::vector<int32_t> findMirrors(const HostGraph& g) {
     std::vector<int32_t> m(g.slots.size(), -1);
-    if (g.vid.size() >= (1ULL << 32)) return m;
+    if (g.vid.size() >= (1ULL << 31)) return m;
     for (size_t i = 0; i < g.slots.size(); i++) {
         if (m[i] >= 0 || g.slots[i].etype <= 0) continue;
         for (size_t j = 0; j < g.slots.size(); j++) {
@@ -594,6 +673,14 @@ std::vector<int32_t> findMirrors(const HostGraph& g) {
         }
     }
     return m;
+}
+
+// mirror slots and, for every slot with one, its pull head image (world 1: one shard holds every row)
+void attachMirrors(ngx_ctx* c, const HostGraph& g, DeviceGraph& d) {
+    d.mirror = c->world == 1 ? findMirrors(g) : std::vector<int32_t>(g.slots.size(), -1);
+    d.pullHead.assign(g.slots.size(), DeviceGraph::PullHead());
+    for (size_t s = 0; s < g.slots.size(); s++)
+        if (d.mirror[s] >= 0) buildPullHead(g, static_cast<int32_t>(s), d.mirror[s], d);
 }
 
 // ColumnValue per calculateExprType (GoExecutor::toThriftResponse, GoExecutor.cpp:775-829); string
@@ -681,21 +768,50 @@ Publish nextPub(ngx_ctx* c) {
 }
 
 // the published scan total: poll the host-mapped slot (no stream round trip); after ~50 ms block on
-// the stream, and read the device copy if the slot still disagrees
-uint64_t awaitPub(ngx_ctx* c, const Publish& p, const uint64_t* devCopy) {
-    if (!p.slot) return readScalar(c, devCopy);
+// the stream, and read the device copy if the slot still disagrees. extra (final-hop publications):
+// the word published beside the value (the query's error bits), or read from errDev on the fallback.
+uint64_t awaitPub(ngx_ctx* c, const Publish& p, const uint64_t* devCopy, uint64_t* extra = nullptr,
+                  const uint32_t* errDev = nullptr) {
+    auto errBits = [&] {
+        if (!extra) return;
+        uint32_t f[4];
+        HIP_OK(hipMemcpy(f, errDev, 16, hipMemcpyDeviceToHost));
+        *extra = 0;
+        for (int k = 0; k < 4; k++) *extra |= static_cast<uint64_t>(f[k] != 0) << k;
+    };
+    if (!p.slot) { errBits(); return readScalar(c, devCopy); }
     auto t0 = std::chrono::steady_clock::now();
     for (uint32_t i = 0;; i++) {
         if (__atomic_load_n(&c->pin[1], __ATOMIC_ACQUIRE) == p.seq) {
             c->hmark("pub");
+            if (extra) *extra = __atomic_load_n(&c->pin[2], __ATOMIC_RELAXED);
             return __atomic_load_n(&c->pin[0], __ATOMIC_RELAXED);
         }
         __builtin_ia32_pause();
         if ((i & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
     }
     HIP_OK(hipStreamSynchronize(c->stream));
-    if (__atomic_load_n(&c->pin[1], __ATOMIC_ACQUIRE) == p.seq) return __atomic_load_n(&c->pin[0], __ATOMIC_RELAXED);
+    if (__atomic_load_n(&c->pin[1], __ATOMIC_ACQUIRE) == p.seq) {
+        if (extra) *extra = __atomic_load_n(&c->pin[2], __ATOMIC_RELAXED);
+        return __atomic_load_n(&c->pin[0], __ATOMIC_RELAXED);
+    }
+    errBits();
     return readScalar(c, devCopy);
+}
+
+// the query tail published by k_publish_tail: out[0] = error bits, out[1 ..] the extra words; false
+// if it did not arrive within ~50 ms of polling (the caller synchronises and copies instead)
+bool awaitTail(ngx_ctx* c, uint64_t seq, uint64_t* out, int n) {
+    volatile uint64_t* slot = c->pin + ngx_ctx::kTailOff;
+    auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0;; i++) {
+        if (__atomic_load_n(const_cast<uint64_t*>(slot), __ATOMIC_ACQUIRE) == seq) {
+            for (int k = 0; k < n; k++) out[k] = __atomic_load_n(const_cast<uint64_t*>(slot + 1 + k), __ATOMIC_RELAXED);
+            return true;
+        }
+        __builtin_ia32_pause();
+        if ((i & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) return false;
+    }
 }
 
 struct ColSpec { bool len, t; };
@@ -960,8 +1076,8 @@ int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
     if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->cus < 1) c->cus = 256;
     if (const char* dh = std::getenv("NGX_DYN_HOPS")) c->dynHops = std::string(dh) != "0";
     if (const char* ht = std::getenv("NGX_HOST_TRACE")) c->htrace = std::string(ht) == "1";
-    if (hipHostMalloc(reinterpret_cast<void**>(&c->pin), 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
-        std::memset(c->pin, 0, 64);
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->pin), ngx_ctx::kPinBytes, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+        std::memset(c->pin, 0, ngx_ctx::kPinBytes);
         if (hipHostGetDevicePointer(reinterpret_cast<void**>(&c->pinDev), c->pin, 0) != hipSuccess) c->pinDev = nullptr;
     } else {
         c->pin = nullptr;
@@ -1118,7 +1234,7 @@ int32_t ngx_open_snapshot(ngx_ctx* c, int32_t space, const char* path, char* tag
         Error e = readSnapshotFile(*sp, path, c->rank, c->world, *hg, tag);
         if (e.code) return fail(c, e.code, e.msg);
         auto dev = upload(*hg, *sp);
-        dev->mirror = c->world == 1 ? findMirrors(*hg) : std::vector<int32_t>(hg->slots.size(), -1);
+        attachMirrors(c, *hg, *dev);
         HIP_OK(hipDeviceSynchronize());
         sp->dev = std::move(dev);
         sp->gen = nextGeneration();
@@ -1180,7 +1296,7 @@ int32_t ngx_commit(ngx_ctx* c, int32_t space) {
         if (hg->shardBase.empty()) { hg->shardBase = {0, hg->vid.size()}; hg->vglobal = hg->vid.size(); }
         hg->gbase = hg->shardBase[c->rank];
         sp->dev = upload(*hg, *sp);
-        sp->dev->mirror = c->world == 1 ? findMirrors(*hg) : std::vector<int32_t>(hg->slots.size(), -1);
+        attachMirrors(c, *hg, *sp->dev);
         sp->gen = nextGeneration();
         sp->host = std::move(hg);
         sp->staged = StagedRows();
@@ -1675,6 +1791,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     GoPlan gp;
     int32_t rc = prepareGo(c, sp, p, gp, in);
     if (rc) return rc;
+    c->hmark("prep");
     R.colTypes = gp.colTypes;
     uint32_t recordFrom = p.record_from, steps = p.record_to;
     if (steps == 0) return NGX_OK;                               // GoExecutor.cpp:99-104
@@ -1742,7 +1859,9 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     const DTag* dstTags = dstReplica ? d.rtags : d.dtags;
     const DCol* dstCols = dstReplica ? d.rcols : d.dcols;
     std::vector<int32_t> ySlotType(progs.yOff.size(), 0);
+    c->hmark("compile");
     DevPrograms dp = uploadPrograms(c, progs, ySlotType, gp.colTypes);
+    c->hmark("upload");
     // WHERE fully pushed: for edges whose storage filter ran, graphd's re-evaluation is implied
     bool wIsP = pushHere && gp.where && encodeExpr(*gp.pushed) == encodeExpr(*gp.where);
     std::vector<int32_t> hopTypes;
@@ -1780,6 +1899,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             jkNoP = jk;
         }
         if (!jk) c->jitNote = jerr.empty() ? "jit: unsupported program" : jerr;
+        c->hmark("jit");
     }
     // algorithmic-byte model inputs: k_f prop columns read by the filter, k_y yielded
     uint64_t ky = 0, kfBytes = 0;
@@ -1820,24 +1940,28 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     const uint64_t vAl = (d.vglobal + 15) & ~15ULL;
     ensureVisited(c, 2 * vAl);
     uint8_t* const marksA = c->visited.get<uint8_t>(2 * vAl);
-    uint8_t* const marksB = marksA + vAl;
-    const uint8_t* curMarks = nullptr;                          // current frontier F: curMarks[g] == curEp
-    uint8_t curEp = 0;
     PullArgs pa{};                                              // pull expansion (kernels.h launchPull)
     bool pullable = c->pullFactor > 0 && c->world == 1 && hs.n >= 1 && hs.n <= kPullMaxSlots && d.V < (1ULL << 32) &&
                     d.mirror.size() == d.slots.size();
     if (pullable) {
-        uint64_t inEdges = 0;
+        uint64_t inEdges = 0, longRows = 0, slices = 0;
         pa.n = hs.n;
         for (int s = 0; s < hs.n && pullable; s++) {
             const int32_t m = d.mirror[hs.slotIdx[s]];
-            if (m < 0) { pullable = false; break; }
+            if (m < 0 || d.pullHead.size() != d.slots.size() || !d.pullHead[hs.slotIdx[s]].perm) { pullable = false; break; }
+            const DeviceGraph::PullHead& ph = d.pullHead[hs.slotIdx[s]];
             pa.ioff[s] = d.slots[m].off;
             pa.isrc[s] = d.slots[m].dgid;
+            pa.perm[s] = ph.perm;
+            pa.head[s] = ph.head;
+            pa.nk[s] = ph.nk;
+            slices += ph.slices;
+            pa.sliceEnd[s] = slices;
+            longRows += ph.longRows;
             inEdges += sp.host->slots[m].dst.size();
         }
         if (pullable) {
-            pa.segCap = d.V * static_cast<uint64_t>(hs.n) + inEdges / kPullSeg + 1;
+            pa.segCap = longRows + inEdges / kPullSeg + 1;
             if (c->pullSegWords < pa.segCap) {
                 c->pullSeg.get<uint64_t>(pa.segCap);
                 HIP_OK(hipMemsetAsync(c->pullSeg.p, 0, c->pullSeg.cap, c->stream));
@@ -1868,16 +1992,21 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     const uint64_t cfCap = slotEdges / kChunk + 2;
     c->chunkFirst.get<uint64_t>(cfCap);
     uint64_t* lbw = lookBack(c, std::max<uint64_t>(cfCap, kDoneOff));   // GO final words: [0] rows, [kDoneOff] done
+    // compaction tile / wave totals (kernels.h CompactArgs)
+    uint64_t* cmpTile = nullptr;
+    uint64_t* cmpWave = nullptr;
     if (lbCompact) {
-        const uint64_t words = (d.V + kCompactTile - 1) / kCompactTile + 2;
-        if (c->cmpWords < words) {
-            for (DBuf& b : c->cmpStatus) {
-                b.get<uint64_t>(words);
-                HIP_OK(hipMemsetAsync(b.p, 0, b.cap, c->stream));
-            }
-            c->cmpWords = std::min(c->cmpStatus[0].cap, c->cmpStatus[1].cap) / 8;
-        }
+        const uint64_t tiles = (d.V + kCompactTile - 1) / kCompactTile + 1;
+        cmpTile = c->cmpStatus[0].get<uint64_t>(tiles);
+        cmpWave = c->cmpStatus[1].get<uint64_t>(tiles * (kCompactTile / 1024));
     }
+    // the pull reads the frontier as a bitmap over global rows, written by the compaction that built it
+    // (or from the frontier list for the seed frontier); the pull's segment counter is cleared by the
+    // compaction after it
+    if (!lbCompact) pullable = false;
+    uint64_t* fbits = pullable ? c->frontierBits.get<uint64_t>(vAl / 64 + 1) : nullptr;
+    bool haveBits = false;
+    pa.curBits = fbits;
     // storage-side request of each hop (getStepOutProps): props only on record hops, TTL info always
     uint32_t recordPropsMask = 0, ttlMask = 0;
     int32_t ttlCol[kMaxSlots];
@@ -1916,23 +2045,37 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         c->chunkFirst.get<uint64_t>(std::max<uint64_t>((slotEdges * mult + kChunk - 1) / kChunk + 1, cfCap));
     }
     bool haveHeads = false;                                    // chunkFirst of the next hop already built
-    hipEvent_t t0 = c->ev(), t1 = c->ev();
+    uint64_t finalErrBits = 0;                                 // error bits published by the last final kernel
+    bool haveFinalErrs = false;
+    // device time of the query (HIP events) only while profiling: an event query costs ~10 us of host
+    // time per call (ngx_set_profiling; bench.py reads device time from its profiled pass)
+    hipEvent_t t0 = c->prof ? c->ev() : nullptr, t1 = c->prof ? c->ev() : nullptr;
     R.tLaunch = std::chrono::steady_clock::now();
     c->hmark("start");
-    HIP_OK(hipEventRecord(t0, c->stream));
+    if (t0) HIP_OK(hipEventRecord(t0, c->stream));
     uint64_t* counters = c->counters.get<uint64_t>(8);
     uint32_t* errFlag = reinterpret_cast<uint32_t*>(counters + 4);
-    HIP_OK(hipMemsetAsync(counters, 0, 64, c->stream));           // before the seed hop: no bubble
     uint64_t nF = svids.size();
+    // the fused seed hop clears the counters itself (no memset launch); every other start clears them here
+    const bool fusedSeed = nF && hs.n > 0 && nF <= kSeedFuseMax && nF * static_cast<uint64_t>(hs.n) <= kSeedFuseMax &&
+                           d.vindex.slots != nullptr;
+    if (!fusedSeed) HIP_OK(hipMemsetAsync(counters, 0, 64, c->stream));
     uint32_t* F = c->F0.get<uint32_t>(std::max<uint64_t>(nF, 1));
     bool haveEstart = false;                                   // estart[] / E of the next hop already built
     uint64_t fusedE = 0;
     if (nF) {
-        int64_t* dv = reinterpret_cast<int64_t*>(c->seedVid.get<uint8_t>(nF * 12));   // vids, then parts
-        int32_t* dp_ = reinterpret_cast<int32_t*>(dv + nF);
-        stageSeeds(c, sparts, svids, dp_, dv);
+        // the fused seed kernel reads the seeds from the mapped page-locked stage; else a device copy
+        const int64_t* dv = nullptr;
+        const int32_t* dp_ = nullptr;
+        if (!fusedSeed || !stageSeedsMapped(c, sparts, svids, dp_, dv)) {
+            int64_t* cv = reinterpret_cast<int64_t*>(c->seedVid.get<uint8_t>(nF * 12));   // vids, then parts
+            int32_t* cp = reinterpret_cast<int32_t*>(cv + nF);
+            stageSeeds(c, sparts, svids, cp, cv);
+            dv = cv;
+            dp_ = cp;
+        }
         const uint64_t nEnt0 = nF * static_cast<uint64_t>(hs.n);
-        if (hs.n > 0 && nF <= kSeedFuseMax && nEnt0 <= kSeedFuseMax && d.vindex.slots) {
+        if (fusedSeed) {
             // lookup + degrees + scan + chunk heads of the seed hop in one workgroup; E published (no
             // stream round trip); the first hop's final-kernel words cleared on the way
             uint64_t* est0 = c->estart.get<uint64_t>(nEnt0 + 1);
@@ -1943,7 +2086,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             uint64_t* cf = c->chunkFirst.get<uint64_t>(std::max(cf0, cfCap));
             c->timed("seed", nF * 12 + nEnt0 * 24, [&] {
                 if (launchSeedFrontierCf(dp_, dv, nF, d.vindex, hs, F, est0, pub, cf, std::max(cf0, cfCap), lbw, 2, errFlag,
-                                         c->stream, dynStats))
+                                         c->stream, dynStats, counters))
                     throw Error{NGX_E_DEVICE, "seed"};
             });
             fusedE = dyn ? slotEdges * mult : awaitPub(c, pub, est0 + nEnt0);   // dyn: an upper bound
@@ -2063,7 +2206,9 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                 }
             });
             if (!dyn) {
-                uint64_t nrows = awaitPub(c, rowsPub, a.lbStatus);   // GO: rows reserved by atomicAdd
+                // GO: rows reserved by atomicAdd, and the query's error bits so far (final_kernels.h)
+                uint64_t nrows = awaitPub(c, rowsPub, a.lbStatus, &finalErrBits, errFlag);
+                haveFinalErrs = true;
                 c->addBytes("final", nrows * (8 * __builtin_popcount(rowMask) + 8 * ky));
                 totalRows += nrows;
             }
@@ -2075,43 +2220,31 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         // (TTL / max-edges) decides which edges count
         // dyn: both expansions are enqueued and the device takes the one its E selects (pullMinE)
         const bool pull = dyn ? pullable : pullable && !mask && E && E * 100 >= static_cast<uint64_t>(c->pullFactor) * d.V;
-        uint8_t* marks = marksA;
-        if (pull && (curMarks == nullptr || (!dyn && c->epoch >= 254))) {
-            // the seed frontier has no marks yet, or the epoch counter would wrap (clearing every mark)
-            // between the frontier's epoch and the pull's: re-mark F after the clear
-            if (c->epoch >= 254) {
-                HIP_OK(hipMemsetAsync(c->visited.p, 0, c->visitedSize, c->stream));
-                c->epoch = 0;
-            }
-            curEp = nextEpoch(c);
-            curMarks = marksA;
-            if (launchMarkRows(F, nF, marksA, curEp, c->stream)) throw Error{NGX_E_DEVICE, "mark rows"};
+        // the hop's output marks (pull and push alike; the pull reads the frontier from the bitmap)
+        uint8_t* const marks = marksA;
+        if (pull && !haveBits) {                                // the seed frontier: bitmap from its list
+            HIP_OK(hipMemsetAsync(fbits, 0, (d.V + 63) / 64 * 8, c->stream));
+            if (launchMarkBits(F, nF, fbits, c->stream)) throw Error{NGX_E_DEVICE, "mark bits"};
         }
         uint8_t ep = nextEpoch(c);
-        if (dyn) marks = curMarks == marksA ? marksB : marksA;  // pull and push write the same array
         if (pull) {
-            marks = curMarks == marksA ? marksB : marksA;
-            pa.cur = curMarks;
-            pa.curEp = curEp;
             pa.out = marks + d.gbase;
             pa.ep = ep;
             pa.err = errFlag;
             pa.dyn = dynTotal;
             pa.minE = pullMinE;
-            c->timed("pull", dyn ? 0 : d.V * (16 * static_cast<uint64_t>(hs.n) + 1), [&] {
+            c->timed("pull", dyn ? 0 : d.V * 9 * static_cast<uint64_t>(hs.n), [&] {
                 if (launchPull(pa, c->stream)) throw Error{NGX_E_DEVICE, "pull"};
             });
             if (!dyn) c->pullHops++;
         }
         if ((!pull || dyn) && E) {
             c->timed("expand", dyn ? 0 : E * 8, [&] {
-                if (launchExpandMark(F, estart, chunkFirst, nEnt, E, hs, dyn ? marks : marksA, ep, pos32, c->stream, mask,
+                if (launchExpandMark(F, estart, chunkFirst, nEnt, E, hs, marks, ep, pos32, c->stream, mask,
                                      dynTotal, dyn ? pullMinE : ~0ULL))
                     throw Error{NGX_E_DEVICE, "expand"};
             });
         }
-        curMarks = marks;
-        curEp = ep;
         if (c->world > 1) {
             c->timed("exchange", 0, [&] { exchangeFrontier(c, d, ep); });
             c->addBytes("exchange", c->lastXchgBytes);
@@ -2130,10 +2263,11 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             ca.estart = c->estart.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
             ca.chunkFirst = c->chunkFirst.get<uint64_t>(cfCap);
             ca.cfCap = cfCap;
-            ca.status = static_cast<uint64_t*>(c->cmpStatus[c->cmpPar].p);
-            ca.nextStatus = static_cast<uint64_t*>(c->cmpStatus[c->cmpPar ^ 1].p);
-            ca.nNext = c->cmpWords;
-            c->cmpPar ^= 1;
+            ca.tileSum = cmpTile;
+            ca.waveSum = cmpWave;
+            ca.clear32 = pullable ? pa.ctl : nullptr;
+            ca.bits = fbits;
+            haveBits = fbits != nullptr;
             ca.total = dyn ? dynStats + h : counters + 2;
             ca.pub = dyn ? Publish{nullptr, 0} : nextPub(c);
             ca.zero = lbw;
@@ -2180,15 +2314,37 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         F = Fn;
         if (!dyn && nF == 0 && c->world == 1) break;            // GO_EXIT: empty frontier
     }
-    HIP_OK(hipEventRecord(t1, c->stream));
-    HIP_OK(hipEventSynchronize(t1));
+    if (t1) HIP_OK(hipEventRecord(t1, c->stream));
+    // the outcome (error words; dyn: the hop totals and the row count) published to host-mapped memory
+    // by one last kernel and polled; the event / copy route is the fallback
+    uint64_t tail[1 + 64];
+    const int nExtra = dyn ? static_cast<int>(steps) + 1 : 0;
+    bool tailOk = false;
+    if (dyn) {                                                   // the row count next to the hop totals
+        HIP_OK(hipMemcpyAsync(dynStats + steps, lbw, 8, hipMemcpyDeviceToDevice, c->stream));
+    }
+    if (!dyn && haveFinalErrs) {                                 // the last final kernel published them
+        tail[0] = finalErrBits;
+        tailOk = true;
+    } else if (c->pinDev && nExtra <= 64) {
+        const uint64_t seq = ++c->pinSeq;
+        if (launchPublishTail(errFlag, dynStats, nExtra, c->pinDev + ngx_ctx::kTailOff, seq, c->stream))
+            throw Error{NGX_E_DEVICE, "publish tail"};
+        tailOk = awaitTail(c, seq, tail, 1 + nExtra);
+    }
+    if (!tailOk) {
+        HIP_OK(hipStreamSynchronize(c->stream));
+        uint32_t f[4];
+        HIP_OK(hipMemcpy(f, errFlag, 16, hipMemcpyDeviceToHost));
+        tail[0] = 0;
+        for (int k = 0; k < 4; k++) tail[0] |= static_cast<uint64_t>(f[k] != 0) << k;
+        if (nExtra) HIP_OK(hipMemcpy(tail + 1, dynStats, nExtra * 8, hipMemcpyDeviceToHost));
+    }
     c->hmark("sync");
     if (dyn) {
         // the hop totals the kernels passed along, and the final kernel's row count
-        std::vector<uint64_t> st(steps);
-        HIP_OK(hipMemcpy(st.data(), dynStats, steps * 8, hipMemcpyDeviceToHost));
-        uint64_t rows = 0;
-        HIP_OK(hipMemcpy(&rows, lbw, 8, hipMemcpyDeviceToHost));
+        std::vector<uint64_t> st(tail + 1, tail + 1 + steps);
+        uint64_t rows = tail[1 + steps];
         for (uint32_t h = 1; h <= steps; h++) {
             const uint64_t nf = st[h - 1] >> kFdShift, e = st[h - 1] & kFdMask;
             if (h > 1 && nf == 0) break;                        // GO_EXIT: empty frontier (the kernels idled)
@@ -2198,7 +2354,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                 R.hopNext.push_back(st[h] >> kFdShift);
                 if (pullable && e >= pullMinE) c->pullHops++;
                 c->addBytes(pullable && e >= pullMinE ? "pull" : "expand",
-                            pullable && e >= pullMinE ? d.V * (16 * static_cast<uint64_t>(hs.n) + 1) : e * 8);
+                            pullable && e >= pullMinE ? d.V * 9 * static_cast<uint64_t>(hs.n) : e * 8);
                 c->addBytes("compact_degrees", (st[h] >> kFdShift) * (8 + 24 * static_cast<uint64_t>(hs.n)));
             } else {
                 c->addBytes("final", e * (16 + kfBytes) + rows * (8 * __builtin_popcount(rowMask) + 8 * ky));
@@ -2207,18 +2363,20 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         totalRows = rows;
     }
     float ms = 0;
-    HIP_OK(hipEventElapsedTime(&ms, t0, t1));
+    if (t1) {
+        HIP_OK(hipEventSynchronize(t1));
+        HIP_OK(hipEventElapsedTime(&ms, t0, t1));
+    }
     c->collectTimings();
     R.r.device_ms = ms;
     R.tDone = std::chrono::steady_clock::now();
     c->hmark("done");
     c->hflush();
-    uint32_t flags[4];
-    HIP_OK(hipMemcpy(flags, errFlag, 16, hipMemcpyDeviceToHost));
-    if (flags[3]) return fail(c, NGX_E_DEVICE, "final-hop look-back did not complete (device fault)");
-    if (flags[1]) return fail(c, NGX_E_UNSUPPORTED, "an expression needs a host-only construct (string building or parsing)");
-    if (flags[0]) return fail(c, NGX_E_QUERY, "an expression of WHERE / YIELD failed to evaluate");
-    if (flags[2]) return fail(c, NGX_E_QUERY, "YIELD value does not match its column type (boost::get)");
+    const uint64_t flags = tail[0];
+    if (flags & 8u) return fail(c, NGX_E_DEVICE, "final-hop look-back did not complete (device fault)");
+    if (flags & 2u) return fail(c, NGX_E_UNSUPPORTED, "an expression needs a host-only construct (string building or parsing)");
+    if (flags & 1u) return fail(c, NGX_E_QUERY, "an expression of WHERE / YIELD failed to evaluate");
+    if (flags & 4u) return fail(c, NGX_E_QUERY, "YIELD value does not match its column type (boost::get)");
 
     int32_t nY = static_cast<int32_t>(progs.yOff.size());
     if (p.distinct && totalRows) {

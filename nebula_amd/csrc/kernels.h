@@ -68,13 +68,15 @@ constexpr uint64_t kFdMask = kDynMask;
 int launchCompactDegrees(const uint8_t* visited, uint64_t gbase, uint64_t V, uint8_t epoch, const HopSlots& hs,
                          uint32_t* outF, uint64_t* estart, uint64_t* tileSums, uint64_t* packedTotal, hipStream_t s,
                          Publish pub = Publish{nullptr, 0});
-// Single-pass compaction of an intermediate hop (kernels.hip k_compact_lb): visited[row] == epoch ->
-// next frontier outF, its entries' estart (|F| * hs.n + 1 entries, the last = E) and the next hop's
-// chunk heads chunkFirst (what k_chunk_first computes), in ONE launch: tiles of kCompactTile rows taken by
-// ticket, prefix by decoupled look-back over packed (count << kFdShift | degree) aggregates.
-// status: [0] ticket + one word per tile, zero at launch; the launch clears nextStatus[0 .. nNext)
-// for the launch after it (double buffer, no memset between hops). zero[0 .. nzero): words the next
-// hop's final kernel needs cleared. Requires V < 2^(62 - kFdShift) (look-back words carry 62 bits).
+// Compaction of an intermediate hop (kernels.hip k_compact_count + k_compact_write): visited[row] ==
+// epoch -> next frontier outF (row order), its entries' estart (|F| * hs.n + 1 entries, the last = E)
+// and the next hop's chunk heads chunkFirst (what k_chunk_first computes). Two launches over tiles of
+// kCompactTile rows: the first writes each tile's and each wave's packed (count << kFdShift | degree)
+// total, the second sums the totals before its tile (no inter-workgroup waiting: the r02 single-pass
+// look-back spent most of its 20-38 us on tickets and polling) and writes the rows. Wave w of a tile
+// owns rows w * 1024 + k * 64 + lane (k < 16): every mark / offset load of a wave is one coalesced
+// access. bits != nullptr: also the frontier bitmap (one 64-bit word per 64 rows, every word of the
+// shard written) for the next hop's pull.
 struct CompactArgs {
     const uint8_t* visited;             // this shard's rows (visited + gbase)
     uint64_t V;
@@ -83,15 +85,16 @@ struct CompactArgs {
     uint64_t* estart;
     uint64_t* chunkFirst;
     uint64_t cfCap;                     // entries of chunkFirst (overflow sets err[3])
-    uint64_t* status;
-    uint64_t* nextStatus;
-    uint64_t nNext;
+    uint64_t* tileSum;                  // one word per tile (written by the count launch)
+    uint64_t* waveSum;                  // NW words per tile
     uint64_t* total;                    // device copy of the packed total
     Publish pub;
-    uint64_t* zero;
+    uint64_t* zero;                     // words the next final kernel needs cleared (zero[k * kDoneOff], k < nzero)
     uint32_t nzero;
+    uint32_t* clear32;                  // optional word cleared by the count launch (the pull's segment counter)
     uint32_t* err;
     uint8_t epoch;
+    uint64_t* bits;                     // optional frontier bitmap of this shard's rows (V / 64 words, rounded up)
 };
 constexpr uint64_t kCompactLbMaxV = 1ULL << (62 - kFdShift);
 constexpr uint64_t kCompactTile = 4096;     // rows per compaction tile (256 threads x 16 rows)
@@ -103,7 +106,8 @@ int launchCompactLb(const CompactArgs& a, hipStream_t s);
 // seed hop variant that also writes chunkFirst (cfCap entries) and clears zero[0 .. nzero)
 int launchSeedFrontierCf(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, const HopSlots& hs,
                          uint32_t* F, uint64_t* estart, Publish pub, uint64_t* chunkFirst, uint64_t cfCap,
-                         uint64_t* zero, uint32_t nzero, uint32_t* err, hipStream_t s, uint64_t* packedOut = nullptr);
+                         uint64_t* zero, uint32_t nzero, uint32_t* err, hipStream_t s, uint64_t* packedOut = nullptr,
+                         uint64_t* zero8 = nullptr);     // zero8: 8 words cleared first (the query's counters)
 // QueryResponse rows of GetNeighbors (storage.thrift IdAndProp.props): per returned edge, the RowWriter
 // row of its type's response edge schema (QueryBoundProcessor.cpp:38-43 with collectProps,
 // QueryBaseProcessor.inl:325-399). Two launches: write == false stores each row's length in rowLen,
@@ -141,33 +145,51 @@ int finalOccupancy(const FinalArgs& a);
 // row r joins the next frontier iff one of its in-neighbours over a hop slot's MIRROR slot (-t for t,
 // verified at commit to be the exact transpose of t) is in the current frontier (cur[g] == curEp).
 // Same set as the push expansion (getDstIdsFromResp, GoExecutor.cpp:675-718), fewer random accesses
-// when the frontier's edges outnumber the shard's rows. Two launches: a row pass (a thread per row,
-// up to kPullProbe in-neighbours per slot with early exit) and a segment pass over the longer in-lists
-// still unresolved (kPullSeg in-edges per segment, a workgroup each), so a supernode spreads over many
-// workgroups. Reached rows get out[r] = ep. ctl[0..3) is zero between launches (the segment pass's
-// last workgroup leaves it so).
+// when the frontier's edges outnumber the shard's rows.
+//
+// Row pass over a per-slot "head" image built at commit (sliced ELLPACK, SELL-64-sigma): rows are
+// taken in slices of 64 (one wave each); inside windows of kPullWindow rows the rows are ordered by
+// min(in-degree, kPullK) descending (perm), and the first kPullK in-neighbours of every row are stored
+// column-major per slice (head[slice][k][lane]), largest source out-degree first, so one probe round
+// of a wave is ONE coalesced 256-byte load and most reached rows hit on their first probe (a frontier
+// reached by expansion is hub-heavy). The old row-per-thread pass loaded 8 in-neighbours of its own
+// in-list per lane: ~54 distinct cache lines per wave load, address-unit bound (r02: 60 us at C2).
+// Rows still open after their kPullK head entries (in-degree > kPullK) reserve segment words; the
+// segment pass probes their whole in-list in the mirror CSR (kPullSeg in-edges per workgroup, so a
+// supernode spreads over many workgroups). Reached rows get out[r] = ep. ctl[0..3) is zero between
+// launches (the segment pass's last workgroup leaves it so).
 constexpr int kPullMaxSlots = 4;
-constexpr int kPullProbe = 32;
+constexpr int kPullK = 16;                  // head entries per row (a multiple of 4)
+constexpr uint64_t kPullWindow = 2048;      // rows sorted by head length inside windows of this size
+constexpr uint32_t kPullLong = 0x80000000u; // perm word flag: in-degree > kPullK (row = word & ~flag)
 constexpr uint64_t kPullSeg = 1024;
 struct PullArgs {
     int32_t n;
     const uint64_t* ioff[kPullMaxSlots];   // mirror slot CSR offsets (V + 1)
     const uint32_t* isrc[kPullMaxSlots];   // mirror slot dgid: global row of each in-neighbour
-    const uint8_t* cur;                    // frontier marks over global rows
+    const uint32_t* perm[kPullMaxSlots];   // [slice * 64 + lane]: row | kPullLong, kNoRow past the rows
+    const uint32_t* head[kPullMaxSlots];   // [(slice * kPullK + k) * 64 + lane]: k-th in-neighbour or kNoRow
+    const uint8_t* nk[kPullMaxSlots];      // per slice: max over its rows of min(in-degree, kPullK)
+    uint64_t sliceEnd[kPullMaxSlots];      // inclusive prefix of the slots' slice counts
+    const uint64_t* curBits;               // frontier bitmap over global rows (bit g of word g / 64)
     uint8_t* out;                          // this shard's marks (marks + gbase)
     uint64_t V;
     uint64_t* seg;
     uint64_t segCap;
-    uint32_t* ctl;                         // [0] segments reserved, [2] segment-pass workgroups done
+    uint32_t* ctl;                         // [0] segments reserved (zero between hops: CompactArgs::clear32)
     uint32_t* err;                         // [3] queue overflow / spin limit (device fault)
     uint8_t curEp, ep;
     const uint64_t* dyn;                   // device-driven hop: packed totals; the row pass does nothing when
     uint64_t minE;                         // the hop's E < minE (the push expansion takes it)
 };
-// worst-case queue words for in-degrees over the mirror slots: V * n + in-edges / kPullSeg + 1
+// worst-case queue words: (rows with in-degree > kPullK) * n + in-edges / kPullSeg + 1
 int launchPull(const PullArgs& a, hipStream_t s);
 // marks[F[i]] = ep for the rows of a frontier list (kNoRow entries skipped)
 int launchMarkRows(const uint32_t* F, uint64_t n, uint8_t* marks, uint8_t ep, hipStream_t s);
+// end of a query: err[0..4) as bits and extra[0 .. nExtra) to host-mapped slot[1 ..], then slot[0] = seq
+int launchPublishTail(const uint32_t* err, const uint64_t* extra, int nExtra, uint64_t* slot, uint64_t seq, hipStream_t s);
+// bits of a frontier list's rows set in a bitmap (zeroed by the caller)
+int launchMarkBits(const uint32_t* F, uint64_t n, uint64_t* bits, hipStream_t s);
 // YIELD DISTINCT on the device (GoExecutor::processFinalResult, GoExecutor.cpp:1298-1305): one row of
 // every group of rows with equal YIELD values is kept. Values are equal when their value types are
 // equal and their bits are, doubles by value (0.0 == -0.0, NaN == NaN: what the reference's

@@ -214,8 +214,10 @@ template <bool CF>
 __global__ __launch_bounds__(1024) void k_seed_frontier(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx,
                                                         HopSlots hs, uint32_t* F, uint64_t* estart, Publish pub,
                                                         uint64_t* chunkFirst, uint64_t cfCap, uint64_t* zero,
-                                                        uint32_t nzero, uint32_t* err, uint64_t* packedOut) {
+                                                        uint32_t nzero, uint32_t* err, uint64_t* packedOut,
+                                                        uint64_t* zero8) {
     if (CF && threadIdx.x < nzero) zero[threadIdx.x * kDoneOff] = 0;
+    if (CF && zero8 != nullptr && threadIdx.x >= 64 && threadIdx.x < 72) zero8[threadIdx.x - 64] = 0;
     __shared__ uint64_t sm[1024 / 64 + 1];
     constexpr int kPer = static_cast<int>(kSeedFuseMax / 1024);
     const uint64_t per = (n + 1023) / 1024;
@@ -350,71 +352,156 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
     }
 }
 
-// ------------------------------------------------------------------------------ single-pass compaction
-// visited[row] == epoch -> next frontier + its entries' estart + the next hop's chunk heads, one launch.
-// A tile is kTile rows (16 consecutive rows per thread; one 16-byte load of their marks when the
-// shard's segment of visited[] is 16-byte aligned). The tile's packed (rows << kFdShift | degrees) sum
-// goes through the decoupled look-back of final_kernels.h (tiles by ticket, dispatch order), so the
-// marks and offsets are read once (the 3-phase scan read them twice and took three launches).
-// (A/B, r02: reserving each tile's range with one packed 64-bit atomicAdd instead — the frontier is a
-// set — ran 113 vs 65 us per step: 489 same-address atomics serialize at the memory side; 16 K-row
-// tiles with 64 rows per thread ran 28 + 47 vs 20 + 38 us for the two compactions of a C2 step.)
-template <bool ONE, bool AL>
-__global__ __launch_bounds__(WG) void k_compact_lb(CompactArgs a) {
-    __shared__ uint64_t sm[NW + 1];
-    __shared__ uint32_t sTile;
-    __shared__ uint64_t sPrefix;
-    if (threadIdx.x == 0) sTile = atomicAdd(reinterpret_cast<uint32_t*>(a.status), 1u);
-    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * WG;
-    for (uint64_t z = static_cast<uint64_t>(blockIdx.x) * WG + threadIdx.x; z < a.nNext; z += stride) a.nextStatus[z] = 0;
-    __syncthreads();
-    const uint32_t tile = sTile;
-    const uint64_t base = static_cast<uint64_t>(tile) * TILE + static_cast<uint64_t>(threadIdx.x) * ITEMS;
-    uint32_t flags = 0;
-    if (AL && base + ITEMS <= a.V) {
-        const uint4 w = *reinterpret_cast<const uint4*>(a.visited + base);
-        const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+// ------------------------------------------------------------------------------ compaction
+// visited[row] == epoch -> next frontier + its entries' estart + the next hop's chunk heads, two
+// launches (kernels.h CompactArgs). Wave w of tile t owns rows t * 4096 + w * 1024 + k * 64 + lane,
+// k < 16, so the marks (1 B per lane) and the CSR offsets (8 B per lane) of one k are one coalesced
+// wave access, and rows leave in row order (k-major, ballot prefix inside k).
+// (r02 gave each thread 16 consecutive rows: its offset loads put the 64 lanes of a wave on 64 cache
+// lines, 16 times, and the address unit bounded the pass; a single-pass decoupled look-back over
+// tiles taken by ticket then spent 20-38 us per launch on the 586 ticket atomics and the polling.)
+__device__ __forceinline__ uint64_t waveInclScan(uint64_t x, int lane) {
 #pragma unroll
-        for (int k = 0; k < ITEMS; k++) flags |= (((ws[k >> 2] >> (8 * (k & 3))) & 0xFFu) == a.epoch ? 1u : 0u) << k;
-    } else {
-#pragma unroll
-        for (int k = 0; k < ITEMS; k++) flags |= (base + k < a.V && a.visited[base + k] == a.epoch ? 1u : 0u) << k;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
     }
-    const int ns = a.hs.n;
-    uint64_t deg[ONE ? ITEMS : 1];
+    return x;
+}
+
+// Loads in these kernels are issued unconditionally (an unwanted lane reads a valid dummy address and
+// its value is discarded by a select): a load under a divergent branch gets its own `s_waitcnt
+// vmcnt(0)` at the branch's end, which serialized the 16 mark loads and 32 offset loads of a wave
+// into 48 round trips (r03 ISA; 7 + 13 us per compaction at C2 instead of ~3).
+template <bool ONE>
+__device__ __forceinline__ uint64_t rowDegree(const HopSlots& hs, uint64_t r) {
+    if (ONE) return hs.off[0][r + 1] - hs.off[0][r];
+    uint64_t d = 0;
+    for (int s = 0; s < hs.n; s++) d += hs.off[s][r + 1] - hs.off[s][r];
+    return d;
+}
+
+// the wave's 16 mark flags (bit k: row wbase + 64 k + lane)
+__device__ __forceinline__ uint32_t waveFlags(const CompactArgs& a, uint64_t wbase, int lane) {
+    uint8_t mk[ITEMS];
+#pragma unroll
+    for (int k = 0; k < ITEMS; k++) {
+        const uint64_t r = wbase + k * 64 + lane;
+        mk[k] = a.visited[r < a.V ? r : a.V - 1];
+    }
+    uint32_t flags = 0;
+#pragma unroll
+    for (int k = 0; k < ITEMS; k++) flags |= (mk[k] == a.epoch && wbase + k * 64 + lane < a.V ? 1u : 0u) << k;
+    return flags;
+}
+
+// degrees of the wave's flagged rows (0 elsewhere), every load issued before the first use
+template <bool ONE>
+__device__ __forceinline__ void waveDegrees(const CompactArgs& a, uint64_t wbase, int lane, uint32_t flags,
+                                            uint64_t (&deg)[ITEMS]) {
+#pragma unroll
+    for (int k = 0; k < ITEMS; k++) {
+        const bool m = (flags >> k) & 1u;
+        const uint64_t d = rowDegree<ONE>(a.hs, m ? wbase + k * 64 + lane : 0);
+        deg[k] = m ? d : 0;
+    }
+}
+
+// launch 1: per tile and per wave the packed (rows << kFdShift | degrees) total; the bitmap words
+template <bool ONE>
+__global__ __launch_bounds__(WG) void k_compact_count(CompactArgs a) {
+    __shared__ uint64_t sWave[NW];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t wbase = static_cast<uint64_t>(blockIdx.x) * TILE + static_cast<uint64_t>(wid) * (64 * ITEMS);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && a.clear32 != nullptr) *a.clear32 = 0;
+    const uint32_t flags = waveFlags(a, wbase, lane);
+    uint64_t deg[ITEMS];
+    waveDegrees<ONE>(a, wbase, lane, flags, deg);
     uint64_t dsum = 0;
 #pragma unroll
-    for (int k = 0; k < ITEMS; k++) {
-        if (ONE) deg[k] = 0;
-        if (!(flags >> k & 1u)) continue;
-        const uint64_t r = base + k;
-        if (ONE) {
-            deg[k] = a.hs.off[0][r + 1] - a.hs.off[0][r];
-            dsum += deg[k];
-        } else {
-            for (int s = 0; s < ns; s++) dsum += a.hs.off[s][r + 1] - a.hs.off[s][r];
+    for (int k = 0; k < ITEMS; k++) dsum += deg[k];
+    if (a.bits != nullptr) {
+        // word k of the wave = rows wbase + 64 k .. + 63; lane k stores it
+        uint64_t w = 0;
+#pragma unroll
+        for (int k = 0; k < ITEMS; k++) {
+            const uint64_t b = __ballot((flags >> k) & 1u);
+            if (lane == k) w = b;
         }
+        if (lane < ITEMS && wbase + static_cast<uint64_t>(lane) * 64 < a.V) a.bits[(wbase >> 6) + lane] = w;
     }
-    const uint64_t v = (static_cast<uint64_t>(__popc(flags)) << kFdShift) | dsum;
-    uint64_t tot;
-    const uint64_t pre = blockExScan(v, tot, sm);
-    if (threadIdx.x < 64) {
-        const uint64_t excl = lookBack(a.status + 1, tile, tot, a.err);
-        if (threadIdx.x == 0) sPrefix = excl;
+    uint64_t packed = (static_cast<uint64_t>(__popc(flags)) << kFdShift) | dsum;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) packed += __shfl_xor(packed, o, 64);
+    if (lane == 0) {
+        sWave[wid] = packed;
+        a.waveSum[static_cast<uint64_t>(blockIdx.x) * NW + wid] = packed;
     }
     __syncthreads();
-    const uint64_t excl = sPrefix;
-    const uint64_t at = excl + pre;
-    uint64_t f = at >> kFdShift, e = at & kFdMask;
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+#pragma unroll
+        for (int w = 0; w < NW; w++) t += sWave[w];
+        a.tileSum[blockIdx.x] = t;
+    }
+}
+
+// launch 2: the wave's start = the tiles before it + the waves before it in its tile (summed from
+// launch 1's words, nothing waited for), then the rows in order: positions from each k's ballot and a
+// wave scan of its degrees. The last tile writes the totals (estart[|F| * ns] = E, *total, publish).
+template <bool ONE>
+__global__ __launch_bounds__(WG) void k_compact_write(CompactArgs a) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t tile = blockIdx.x;
+    const uint64_t wbase = tile * TILE + static_cast<uint64_t>(wid) * (64 * ITEMS);
+    const int ns = a.hs.n;
+    const uint32_t flags = waveFlags(a, wbase, lane);
+    // the totals of the tiles before this one: 8 loads in flight per lane (a dependent loop of loads
+    // cost 10 us at C2's 586 tiles)
+    uint64_t pre = lane < wid ? a.waveSum[tile * NW + lane] : 0;
+    for (uint64_t t0 = 0; t0 < tile; t0 += 8 * 64) {
+        uint64_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint64_t t = t0 + j * 64 + lane;
+            v[j] = t < tile ? a.tileSum[t] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) pre += v[j];
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) pre += __shfl_xor(pre, o, 64);
+    if (tile == gridDim.x - 1 && wid == NW - 1 && lane == 0) {
+        const uint64_t incl = pre + a.waveSum[tile * NW + wid];
+        a.estart[(incl >> kFdShift) * static_cast<uint64_t>(ns)] = incl & kFdMask;
+        *a.total = incl;
+        if (a.pub.slot) {
+            __hip_atomic_store(a.pub.slot, incl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.pub.slot + 1, a.pub.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    if (tile == 0 && threadIdx.x < a.nzero) a.zero[threadIdx.x * kDoneOff] = 0;
+    if (__ballot(flags != 0) == 0) return;              // wave-uniform: every lane stays for the scans below
+    uint64_t deg[ITEMS];
+    waveDegrees<ONE>(a, wbase, lane, flags, deg);
+    uint64_t fk = pre >> kFdShift, ek = pre & kFdMask;     // running start of group k
+    const uint64_t below = (1ULL << lane) - 1;
 #pragma unroll
     for (int k = 0; k < ITEMS; k++) {
-        if (!(flags >> k & 1u)) continue;
-        const uint64_t r = base + k;
+        const bool m = (flags >> k) & 1u;
+        const uint64_t ball = __ballot(m);
+        if (ball == 0) continue;
+        const uint64_t r = wbase + k * 64 + lane;
+        const uint64_t incl = waveInclScan(deg[k], lane);
+        const uint64_t f = fk + static_cast<uint64_t>(__popcll(ball & below));
+        uint64_t e = ek + incl - deg[k];
+        fk += static_cast<uint64_t>(__popcll(ball));
+        ek += __shfl(incl, 63, 64);
+        if (!m) continue;
         a.outF[f] = static_cast<uint32_t>(r);
         if (ONE) {
             a.estart[f] = e;
             writeChunkHeads(a.chunkFirst, a.cfCap, f, e, deg[k], a.err);
-            e += deg[k];
         } else {
             for (int s = 0; s < ns; s++) {
                 const uint64_t d = a.hs.off[s][r + 1] - a.hs.off[s][r];
@@ -422,17 +509,6 @@ __global__ __launch_bounds__(WG) void k_compact_lb(CompactArgs a) {
                 writeChunkHeads(a.chunkFirst, a.cfCap, f * ns + s, e, d, a.err);
                 e += d;
             }
-        }
-        f++;
-    }
-    if (tile == 0 && threadIdx.x < a.nzero) a.zero[threadIdx.x * kDoneOff] = 0;
-    if (tile == gridDim.x - 1 && threadIdx.x == 0) {
-        const uint64_t incl = excl + tot;
-        a.estart[(incl >> kFdShift) * static_cast<uint64_t>(ns)] = incl & kFdMask;
-        *a.total = incl;
-        if (a.pub.slot) {
-            __hip_atomic_store(a.pub.slot, incl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(a.pub.slot + 1, a.pub.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
@@ -443,79 +519,118 @@ __device__ __forceinline__ uint64_t pullSegWord(uint32_t row, int s, uint64_t k)
     return (k << 36) | (static_cast<uint64_t>(s) << 32) | row;
 }
 
-// Row pass: one thread per row; up to kPullProbe in-neighbours per slot, loaded 8 at a time and
-// probed two per round, the next round only while the row is unresolved. Rows whose in-list is longer
-// and still unresolved reserve segment words (one atomicAdd per workgroup) for k_pull_segments.
+// Row pass over the head image (kernels.h PullArgs): one wave per 64-row slice, grid-stride over the
+// slices of every hop slot. Round k loads head[slice][k][*] (coalesced) and probes the frontier mark
+// of that in-neighbour for the lanes still open; the first kPullK / 2 rounds are loaded together. A
+// lane closes on a hit, on a kNoRow entry (its in-list ended) or after its last head entry; lanes of
+// rows with a longer in-list that are still open reserve segment words for k_pull_segments (their
+// whole in-list, from the mirror CSR).
+__device__ __forceinline__ bool inFrontier(const PullArgs& a, uint32_t g) {
+    return (a.curBits[g >> 6] >> (g & 63)) & 1ULL;
+}
+// the probe of a lane that may not need it: an unconditional load (row 0's word for the others) so the
+// probes of a round issue together (see rowDegree's note)
+__device__ __forceinline__ bool probe(const PullArgs& a, bool want, uint32_t g) {
+    const uint32_t x = want ? g : 0u;
+    const uint64_t w = a.curBits[x >> 6];
+    return static_cast<bool>(static_cast<uint32_t>(want) & static_cast<uint32_t>((w >> (x & 63)) & 1ULL));
+}
+
+// one slice's first loads: its rows, round count and first KH head rounds (independent loads; rounds
+// past the slice's count hold kNoRow: the image is kPullK rounds deep everywhere)
+constexpr int kPullKH = 4;
+struct PullSlice {
+    uint32_t pw;
+    int nk;
+    uint32_t u[kPullKH];
+};
 template <bool ONE>
-__global__ __launch_bounds__(WG) void k_pull(PullArgs a) {
-    __shared__ uint64_t sm[NW + 1];
-    __shared__ uint32_t sBase;
-    const int ns = ONE ? 1 : a.n;
+__device__ __forceinline__ void pullLoad(const PullArgs& a, uint64_t j, int lane, int& s, uint64_t& js, PullSlice& p) {
+    s = 0;
+    if (!ONE) while (j >= a.sliceEnd[s]) s++;
+    js = (ONE || s == 0) ? j : j - a.sliceEnd[s - 1];
+    const uint32_t* hp = a.head[s] + js * (kPullK * 64) + lane;
+    p.pw = a.perm[s][js * 64 + lane];
+    p.nk = a.nk[s][js];
+#pragma unroll
+    for (int k = 0; k < kPullKH; k++) p.u[k] = hp[k * 64];
+}
+
+// probes of N consecutive head rounds held in u[off .. off + N), for the lanes still open: every probe
+// issued before the first is resolved, then the rounds resolved in order
+template <int N>
+__device__ __forceinline__ void pullProbe(const PullArgs& a, const uint32_t* u, bool& open, bool& hit) {
+    // bit k of `ev`: round k ends the lane's search (a hit, or kNoRow: its in-list ended); straight-line
+    // selects, no branch per round (a branch would wait for each probe in turn)
+    uint32_t hits = 0, ends = 0;
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        hits |= static_cast<uint32_t>(probe(a, open && u[k] != kNoRow, u[k])) << k;
+        ends |= static_cast<uint32_t>(u[k] == kNoRow) << k;
+    }
+    const uint32_t ev = hits | ends;
+    const uint32_t first = ev & (0u - ev);                  // lowest set bit: the round that decides
+    hit = hit || (open && (first & hits) != 0);
+    open = open && ev == 0;
+}
+
+template <bool ONE>
+__global__ __launch_bounds__(WG) void k_pull_head(PullArgs a) {
     if (a.dyn != nullptr && (*a.dyn & kDynMask) < a.minE) return;   // a push hop (k_expand_mark takes it)
-    for (uint64_t r0 = static_cast<uint64_t>(blockIdx.x) * WG; r0 < a.V; r0 += static_cast<uint64_t>(gridDim.x) * WG) {
-    const uint64_t r = r0 + threadIdx.x;
-    uint64_t rb[kPullMaxSlots], re[kPullMaxSlots];
-    uint32_t nseg = 0;
-    if (r < a.V) {
-        bool found = false;
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = static_cast<uint64_t>(gridDim.x) * NW;
+    const uint64_t total = a.sliceEnd[ONE ? 0 : a.n - 1];
+    uint64_t j = (static_cast<uint64_t>(blockIdx.x) * WG + threadIdx.x) >> 6;
+    if (j >= total) return;
+    int s;
+    uint64_t js;
+    PullSlice cur;
+    pullLoad<ONE>(a, j, lane, s, js, cur);
+    while (true) {
+        // the next slice's loads go out before this slice's probes (software pipelining over the grid stride)
+        const uint64_t jn = j + nw;
+        int sn = 0;
+        uint64_t jsn = 0;
+        PullSlice nxt;
+        pullLoad<ONE>(a, jn < total ? jn : total - 1, lane, sn, jsn, nxt);   // unconditional: no branch wait
+        const uint32_t* hp = a.head[s] + js * (kPullK * 64) + lane;
+        // round 0 alone (most reached rows hit there), then the rest of the batch for the lanes still open
+        bool hit = probe(a, cur.u[0] != kNoRow, cur.u[0]);
+        bool open = cur.pw != kNoRow && !hit && cur.u[0] != kNoRow && cur.nk > 1;
+        if (__any(open)) {
+            pullProbe<kPullKH - 1>(a, cur.u + 1, open, hit);           // rounds 1 .. kPullKH - 1
+            uint32_t u[kPullKH];
+            for (int k0 = kPullKH; k0 < cur.nk && __any(open); k0 += kPullKH) {
 #pragma unroll
-        for (int s = 0; s < kPullMaxSlots; s++) {
-            if (s >= ns) break;
-            rb[s] = a.ioff[s][r];
-            re[s] = a.ioff[s][r + 1];
-        }
-#pragma unroll
-        for (int s = 0; s < kPullMaxSlots; s++) {
-            if (s >= ns || found) break;
-            const uint64_t e = re[s];
-            const uint32_t* in = a.isrc[s];
-            for (uint64_t b = rb[s]; b < e && b < rb[s] + kPullProbe && !found; b += 8) {
-                uint32_t u[8];
-#pragma unroll
-                for (int k = 0; k < 8; k++) u[k] = b + k < e ? in[b + k] : kNoRow;
-#pragma unroll
-                for (int k = 0; k < 8; k += 2) {
-                    if (found) break;
-                    const bool h0 = u[k] != kNoRow && a.cur[u[k]] == a.curEp;
-                    const bool h1 = u[k + 1] != kNoRow && a.cur[u[k + 1]] == a.curEp;
-                    found = h0 || h1;
-                }
+                for (int k = 0; k < kPullKH; k++) u[k] = hp[(k0 + k) * 64];
+                pullProbe<kPullKH>(a, u, open, hit);
             }
         }
-        if (found) {
-            a.out[r] = a.ep;
-        } else {
-#pragma unroll
-            for (int s = 0; s < kPullMaxSlots; s++) {
-                if (s >= ns) break;
-                if (re[s] > rb[s] + kPullProbe) nseg += static_cast<uint32_t>((re[s] - rb[s] - kPullProbe + kPullSeg - 1) / kPullSeg);
+        const uint32_t row = cur.pw & ~kPullLong;
+        if (hit) a.out[row] = a.ep;
+        // an open lane of a long row: its in-list continues past the head
+        const bool more = open && cur.pw != kNoRow && (cur.pw & kPullLong) != 0;
+        uint32_t nseg = 0;
+        if (more) nseg = static_cast<uint32_t>((a.ioff[s][row + 1] - a.ioff[s][row] + kPullSeg - 1) / kPullSeg);
+        if (__any(nseg != 0)) {
+            const uint64_t incl = waveInclScan(nseg, lane);
+            uint32_t base = 0;
+            if (lane == 63) base = atomicAdd(&a.ctl[0], static_cast<uint32_t>(incl));
+            base = __shfl(base, 63, 64);
+            uint64_t at = base + incl - nseg;
+            for (uint32_t k = 0; k < nseg; k++, at++) {
+                if (at < a.segCap) a.seg[at] = pullSegWord(row, s, k);
+                else atomicOr(a.err + 3, 1u);
             }
         }
-    }
-    if (__syncthreads_or(nseg != 0)) {
-        uint64_t tot;
-        const uint64_t pre = blockExScan(nseg, tot, sm);
-        if (threadIdx.x == 0) sBase = atomicAdd(&a.ctl[0], static_cast<uint32_t>(tot));
-        __syncthreads();
-        uint64_t at = sBase + pre;
-        if (nseg) {
-            for (int s = 0; s < ns; s++) {
-                if (re[s] <= rb[s] + kPullProbe) continue;
-                const uint64_t cnt = (re[s] - rb[s] - kPullProbe + kPullSeg - 1) / kPullSeg;
-                for (uint64_t k = 0; k < cnt; k++, at++) {
-                    if (at < a.segCap) a.seg[at] = pullSegWord(static_cast<uint32_t>(r), s, k);
-                    else atomicOr(a.err + 3, 1u);
-                }
-            }
-        }
-        __syncthreads();                                 // sBase reused by the next rows
-    }
+        if (jn >= total) break;
+        j = jn; s = sn; js = jsn; cur = nxt;
     }
 }
 
 // Segment pass (the next launch on the stream, so every segment word is visible): a workgroup per
-// segment of kPullSeg in-edges, grid-stride; any hit marks the row. The last workgroup out leaves
-// the counters zero for the next hop.
+// segment of kPullSeg in-edges of a long row's in-list, grid-stride; any hit marks the row. The
+// compaction's count launch after it clears the segment counter for the next hop (CompactArgs::clear32).
 __global__ __launch_bounds__(WG) void k_pull_segments(PullArgs a) {
     const uint32_t nres = __hip_atomic_load(&a.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t n = nres < a.segCap ? nres : a.segCap;
@@ -525,7 +640,7 @@ __global__ __launch_bounds__(WG) void k_pull_segments(PullArgs a) {
         const int s = static_cast<int>((w >> 32) & 0xF);
         const uint64_t k = w >> 36;
         const uint64_t e = a.ioff[s][row + 1];
-        const uint64_t b = a.ioff[s][row] + kPullProbe + k * kPullSeg;
+        const uint64_t b = a.ioff[s][row] + k * kPullSeg;
         const uint64_t be = b + kPullSeg < e ? b + kPullSeg : e;
         const uint32_t* in = a.isrc[s];
         uint32_t u[kPullSeg / WG];
@@ -536,17 +651,26 @@ __global__ __launch_bounds__(WG) void k_pull_segments(PullArgs a) {
         }
         bool hit = false;
 #pragma unroll
-        for (int j = 0; j < static_cast<int>(kPullSeg / WG); j++) hit |= u[j] != kNoRow && a.cur[u[j]] == a.curEp;
+        for (int j = 0; j < static_cast<int>(kPullSeg / WG); j++) hit |= u[j] != kNoRow && inFrontier(a, u[j]);
         if (hit) a.out[row] = a.ep;
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t d = atomicAdd(&a.ctl[2], 1u);
-        if (d == gridDim.x - 1) {
-            __hip_atomic_store(&a.ctl[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.ctl[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+}
+
+// the end of a GO query: the error words (bit k = err[k] != 0) and `nExtra` device words published to
+// host-mapped memory, sequence number last (system-scope release), so the host learns the outcome by
+// polling instead of an event synchronisation plus a copy (~20 us of host time per query)
+__global__ void k_publish_tail(const uint32_t* err, const uint64_t* extra, int nExtra, uint64_t* slot, uint64_t seq) {
+    if (threadIdx.x != 0) return;
+    uint64_t bits = 0;
+    for (int k = 0; k < 4; k++) bits |= static_cast<uint64_t>(err[k] != 0) << k;
+    __hip_atomic_store(slot + 1, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int i = 0; i < nExtra; i++) __hip_atomic_store(slot + 2 + i, extra[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(slot, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void k_mark_bits(const uint32_t* F, uint64_t n, uint64_t* bits) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n && F[i] != kNoRow) atomicOr(reinterpret_cast<unsigned long long*>(bits + (F[i] >> 6)), 1ULL << (F[i] & 63));
 }
 
 __global__ void k_mark_rows(const uint32_t* F, uint64_t n, uint8_t* marks, uint8_t ep) {
@@ -853,16 +977,17 @@ int launchSeedFrontier(const int32_t* qpart, const int64_t* qvid, uint64_t n, VI
                        uint32_t* F, uint64_t* estart, Publish pub, hipStream_t s) {
     if (n * static_cast<uint64_t>(hs.n) > kSeedFuseMax || n > kSeedFuseMax || idx.slots == nullptr) return 1;
     hipLaunchKernelGGL(k_seed_frontier<false>, dim3(1), dim3(1024), 0, s, qpart, qvid, n, idx, hs, F, estart, pub,
-                       nullptr, 0, nullptr, 0u, nullptr, nullptr);
+                       nullptr, 0, nullptr, 0u, nullptr, nullptr, nullptr);
     return static_cast<int>(hipGetLastError());
 }
 
 int launchSeedFrontierCf(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, const HopSlots& hs,
                          uint32_t* F, uint64_t* estart, Publish pub, uint64_t* chunkFirst, uint64_t cfCap,
-                         uint64_t* zero, uint32_t nzero, uint32_t* err, hipStream_t s, uint64_t* packedOut) {
-    if (n * static_cast<uint64_t>(hs.n) > kSeedFuseMax || n > kSeedFuseMax || idx.slots == nullptr || nzero > 1024) return 1;
+                         uint64_t* zero, uint32_t nzero, uint32_t* err, hipStream_t s, uint64_t* packedOut,
+                         uint64_t* zero8) {
+    if (n * static_cast<uint64_t>(hs.n) > kSeedFuseMax || n > kSeedFuseMax || idx.slots == nullptr || nzero > 64) return 1;
     hipLaunchKernelGGL(k_seed_frontier<true>, dim3(1), dim3(1024), 0, s, qpart, qvid, n, idx, hs, F, estart, pub,
-                       chunkFirst, cfCap, zero, nzero, err, packedOut);
+                       chunkFirst, cfCap, zero, nzero, err, packedOut, zero8);
     return static_cast<int>(hipGetLastError());
 }
 
@@ -924,14 +1049,13 @@ int launchCompactDegrees(const uint8_t* visited, uint64_t gbase, uint64_t V, uin
 int launchCompactLb(const CompactArgs& a, hipStream_t s) {
     if (a.V >= kCompactLbMaxV || a.nzero > WG) return 1;
     const uint64_t nt = std::max<uint64_t>((a.V + TILE - 1) / TILE, 1);
-    const bool al = (reinterpret_cast<uintptr_t>(a.visited) & 15) == 0;
     dim3 grid(static_cast<unsigned>(nt));
     if (a.hs.n == 1) {
-        if (al) hipLaunchKernelGGL((k_compact_lb<true, true>), grid, dim3(WG), 0, s, a);
-        else hipLaunchKernelGGL((k_compact_lb<true, false>), grid, dim3(WG), 0, s, a);
+        hipLaunchKernelGGL((k_compact_count<true>), grid, dim3(WG), 0, s, a);
+        hipLaunchKernelGGL((k_compact_write<true>), grid, dim3(WG), 0, s, a);
     } else {
-        if (al) hipLaunchKernelGGL((k_compact_lb<false, true>), grid, dim3(WG), 0, s, a);
-        else hipLaunchKernelGGL((k_compact_lb<false, false>), grid, dim3(WG), 0, s, a);
+        hipLaunchKernelGGL((k_compact_count<false>), grid, dim3(WG), 0, s, a);
+        hipLaunchKernelGGL((k_compact_write<false>), grid, dim3(WG), 0, s, a);
     }
     return static_cast<int>(hipGetLastError());
 }
@@ -973,14 +1097,17 @@ int launchFinal(const FinalArgs& a, hipStream_t s, unsigned g) {
 
 int launchPull(const PullArgs& a, hipStream_t s) {
     if (a.V == 0) return 0;
-    if (a.n < 1 || a.n > kPullMaxSlots || a.V >= (1ULL << 32)) return 1;
-    // (A/B, r02: four rows per thread with interleaved probes ran 96 vs 76 us per step: the pass is
-    // not short of requests in flight)
-    dim3 grid(static_cast<unsigned>(std::min<uint64_t>((a.V + WG - 1) / WG, a.dyn ? kDynGrid : ~0u)));
-    if (a.n == 1) hipLaunchKernelGGL((k_pull<true>), grid, dim3(WG), 0, s, a);
-    else hipLaunchKernelGGL((k_pull<false>), grid, dim3(WG), 0, s, a);
+    if (a.n < 1 || a.n > kPullMaxSlots || a.V >= (1ULL << 31)) return 1;
+    const uint64_t slices = a.sliceEnd[a.n - 1];
+    if (slices == 0) return 0;
+    // waves stride over the slices (8 resident workgroups per CU on 256 CUs), each prefetching its next
+    // slice while it probes the current one
+    static const uint64_t maxGrid = getenv("NGX_PULL_GRID") ? std::strtoull(getenv("NGX_PULL_GRID"), nullptr, 10) : kDynGrid;
+    dim3 grid(static_cast<unsigned>(std::min<uint64_t>((slices + NW - 1) / NW, maxGrid)));
+    if (a.n == 1) hipLaunchKernelGGL((k_pull_head<true>), grid, dim3(WG), 0, s, a);
+    else hipLaunchKernelGGL((k_pull_head<false>), grid, dim3(WG), 0, s, a);
     // long unresolved in-lists: at most a.segCap segments, 2 workgroups per CU striding over them
-    hipLaunchKernelGGL(k_pull_segments, dim3(512), dim3(WG), 0, s, a);
+    hipLaunchKernelGGL(k_pull_segments, dim3(256), dim3(WG), 0, s, a);
     return static_cast<int>(hipGetLastError());
 }
 
@@ -1008,6 +1135,17 @@ int launchScatterKept(const ScatterArgs& a, hipStream_t s) {
 int launchMarkRows(const uint32_t* F, uint64_t n, uint8_t* marks, uint8_t ep, hipStream_t s) {
     if (n == 0) return 0;
     hipLaunchKernelGGL(k_mark_rows, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, F, n, marks, ep);
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchPublishTail(const uint32_t* err, const uint64_t* extra, int nExtra, uint64_t* slot, uint64_t seq, hipStream_t s) {
+    hipLaunchKernelGGL(k_publish_tail, dim3(1), dim3(64), 0, s, err, extra, nExtra, slot, seq);
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchMarkBits(const uint32_t* F, uint64_t n, uint64_t* bits, hipStream_t s) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_mark_bits, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, F, n, bits);
     return static_cast<int>(hipGetLastError());
 }
 

@@ -40,6 +40,7 @@ def lib():
         L.orc_engine_free.argtypes = [vp]
         L.orc_buf_free.argtypes = [vp]
         L.orc_set_flags.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32]
+        L.orc_set_graph_threads.argtypes = [vp, ctypes.c_int32]
         L.orc_add_space.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
         L.orc_add_part.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
         L.orc_add_schema.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p,
@@ -275,8 +276,11 @@ class Oracle:
         except Exception:
             pass
 
-    def set_flags(self, max_handlers=10, min_vertices=3, max_edges=2**31 - 1, now_sec=0, threads=1):
+    def set_flags(self, max_handlers=10, min_vertices=3, max_edges=2**31 - 1, now_sec=0, threads=1, graph_threads=1):
+        """threads: the reader-pool threads that run a request's buckets; graph_threads (test harness, not a
+        reference flag): threads of the final evaluation of GO (rows in the sequential order)."""
         self.L.orc_set_flags(self.h, max_handlers, min_vertices, max_edges, now_sec, threads)
+        self.L.orc_set_graph_threads(self.h, graph_threads)
 
     def add_space(self, space: int, num_parts: int):
         self.L.orc_add_space(self.h, space, num_parts)

@@ -107,6 +107,14 @@ void rowDigest(const std::string& b, uint8_t* out16) {
     std::memcpy(out16 + 8, &h2, 8);
 }
 
+// GoFlags::digest: a result row serialized as its ColumnValue cells, then digested
+void digestRow(const std::vector<SupportedType>& colTypes, const std::vector<Variant>& row, uint8_t* out16) {
+    thread_local Writer w;
+    w.b.clear();
+    for (size_t c = 0; c < row.size(); c++) cell(w, c < colTypes.size() ? colTypes[c] : UNKNOWN, row[c]);
+    rowDigest(w.b, out16);
+}
+
 }  // namespace
 
 extern "C" {
@@ -167,6 +175,9 @@ void orc_set_flags(void* e, int32_t maxHandlers, int32_t minVertices, int32_t ma
     f.max_edge_returned_per_vertex = maxEdges;
     f.now_sec = nowSec;
     f.threads = threads;
+}
+void orc_set_graph_threads(void* e, int32_t threads) {
+    static_cast<StorageEngine*>(e)->flags.graph_threads = threads < 1 ? 1 : threads;
 }
 
 void orc_add_space(void* e, int32_t space, int32_t numParts) {
@@ -291,6 +302,8 @@ char* orc_go(void* e, int32_t space, const uint8_t* blob, uint64_t len, uint64_t
     f.filter_pushdown = r.get<uint8_t>() != 0;
     uint8_t mode = r.p < r.e ? r.get<uint8_t>() : 0;        // 0 cells, 1 count only, 2 row digests
     bool countOnly = mode != 0;
+    f.threads = eng->flags.graph_threads;
+    if (mode == 2) f.digest = digestRow;
     if (r.p < r.e) {                                        // FROM $-.col / $var.col and the input
         s.fromType = r.get<uint8_t>();
         s.fromVar = r.str();
@@ -322,19 +335,8 @@ char* orc_go(void* e, int32_t space, const uint8_t* blob, uint64_t len, uint64_t
     w.str(res.error);
     w.put<int32_t>(static_cast<int32_t>(res.colTypes.size()));
     for (auto t : res.colTypes) w.put<int32_t>(t);
-    w.put<int64_t>(static_cast<int64_t>(res.rows.size()));
-    if (mode == 2) {
-        std::string dig(16 * res.rows.size(), '\0');
-        parallelChunks(res.rows.size(), [&](uint64_t lo, uint64_t hi) {
-            Writer rw;
-            for (uint64_t i = lo; i < hi; i++) {
-                rw.b.clear();
-                for (size_t c = 0; c < res.rows[i].size(); c++) cell(rw, c < res.colTypes.size() ? res.colTypes[c] : UNKNOWN, res.rows[i][c]);
-                rowDigest(rw.b, reinterpret_cast<uint8_t*>(&dig[16 * i]));
-            }
-        });
-        w.b += dig;
-    }
+    w.put<int64_t>(static_cast<int64_t>(mode == 2 ? res.rowCount : res.rows.size()));
+    if (mode == 2) w.b += res.digests;
     if (countOnly) res.rows.clear();
     for (auto& row : res.rows) {
         for (size_t c = 0; c < row.size(); c++) {

@@ -4,6 +4,10 @@
 // pushdown rewrite (src/graph/TraverseExecutor.cpp:426-538), calculateExprType (:88-165) and the
 // StorageClient routing (vid -> part by ID_HASH, src/storage/client/StorageClient.cpp:439-449) for
 // a single storaged host (completeness is 0 as soon as any part fails, StorageClient.inl:134-151).
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <thread>
 #include <unordered_set>
 
 #include "orc_query.h"
@@ -136,8 +140,18 @@ struct GoExec {
     GoExec(const StorageEngine& e, GraphSpaceID sp, const GoSentence& sent, GoFlags f)
         : eng(e), sm(e.schemas), space(sp), s(sent), flags(f) {}
 
-    bool fail(const std::string& msg) { res.ok = false; res.error = msg; res.rows.clear(); return false; }
+    bool fail(const std::string& msg) {
+        res.ok = false; res.error = msg; res.rows.clear(); res.digests.clear(); res.rowCount = 0;
+        return false;
+    }
     bool isFinalStep() const { return curStep == steps; }
+    // ORC_TRACE=1: phase times on stderr (test harness diagnostics)
+    void trace(const char* what, std::chrono::steady_clock::time_point t0) const {
+        static const bool on = std::getenv("ORC_TRACE") != nullptr;
+        if (!on) return;
+        std::fprintf(stderr, "[orc] step %u %s %.3fs\n", curStep, what,
+                     std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+    }
     bool isRecord() const { return curStep >= recordFrom && curStep <= steps; }
 
     bool addToEdgeTypes(EdgeType t) {                                  // GoExecutor.cpp:297-319
@@ -291,18 +305,24 @@ struct GoExec {
             req.return_columns = returns;
             res.hopFrontier.push_back(static_cast<int64_t>(starts.size()));
             res.hopScanned.push_back(countScanned(starts));
+            auto tq = std::chrono::steady_clock::now();
             auto resp = eng.getBound(req);
+            trace("getBound", tq);
             if (!resp.failed_codes.empty()) return fail("Get neighbors failed");
             records.push_back(std::move(resp));
+            tq = std::chrono::steady_clock::now();
             // getDstIdsFromRespWithBackTrack (:675-718) — the frontier is the set of distinct dsts;
             // for steps > 1 the back tracker records (step, dst) -> root for non-final steps, all
             // pairs of the step read before any is inserted
+            // (the roots are read only by a sentence whose FROM is $- / $var (getRoots, :1317-1330): with
+            // literal vids the tracker changes no result, and this harness skips building it)
+            const bool track = !isFinalStep() && steps != 1 && s.fromType != 0;
             std::unordered_set<VertexID> set;
             std::set<std::pair<VertexID, VertexID>> curBackTrace;
             for (auto& vd : records.back().vertices)
                 for (auto& ed : vd.edge_data)
                     for (auto& e : ed.edges) {
-                        if (!isFinalStep() && steps != 1) {
+                        if (track) {
                             if (curStep == 1) {
                                 curBackTrace.emplace(e.dst, vd.vertex_id);
                             } else {
@@ -312,8 +332,9 @@ struct GoExec {
                         }
                         set.insert(e.dst);
                     }
-            if (!isFinalStep() && steps != 1)
+            if (track)
                 for (auto& t : curBackTrace) backTracker.emplace(std::make_pair(curStep, t.first), t.second);
+            trace("frontier", tq);
             if (isFinalStep()) return true;
             starts.assign(set.begin(), set.end());
             if (starts.empty()) {
@@ -391,139 +412,193 @@ struct GoExec {
         }
     }
 
+    // Evaluation state of processFinalResult (:1082-1335): the getters read the edge being evaluated.
+    // One per thread when the rows are split over threads (GoFlags::threads).
+    struct FinalEval {
+        GoExec& x;
+        const std::map<TagID, std::shared_ptr<Schema>>& tagSchema;
+        const std::map<EdgeType, std::shared_ptr<Schema>>& edgeSchema;
+        VertexID srcId = 0, dstId = 0;
+        EdgeType edgeType = 0;
+        const std::vector<TagData>* tagData = nullptr;
+        std::unique_ptr<RowReader> reader;
+        size_t inputRow = 0;
+        Getters g;
+        FinalEval(GoExec& ex, const std::map<TagID, std::shared_ptr<Schema>>& ts,
+                  const std::map<EdgeType, std::shared_ptr<Schema>>& es)
+            : x(ex), tagSchema(ts), edgeSchema(es) {
+            g.getEdgeDstId = [this](const std::string& edgeName) -> OptVariant {
+                if (x.edgeTypes.size() > 1) {
+                    EdgeType t;
+                    if (!x.ctx.getEdgeType(edgeName, t)) return Status::Error("Get edge type failed in getters.");
+                    if (t != std::abs(edgeType)) return OptVariant(int64_t(0));
+                }
+                return OptVariant(dstId);
+            };
+            g.getSrcTagProp = [this](const std::string& tag, const std::string& prop) -> OptVariant {
+                TagID tagId;
+                if (!x.ctx.getTagId(tag, tagId)) return Status::Error("Get tag id failed in getters.");
+                const TagData* found = nullptr;
+                for (auto& td : *tagData) if (td.tag_id == tagId) { found = &td; break; }
+                if (!found) {
+                    auto ts = x.sm.getTagSchema(x.space, tagId);
+                    if (!ts) return Status::Error("No tag schema");
+                    auto d = RowReader::getDefaultProp(ts.get(), prop);
+                    if (!d.ok()) return d.status();
+                    return OptVariant(d.value());
+                }
+                auto sit = tagSchema.find(tagId);
+                auto vr = RowReader::make(found->data, sit == tagSchema.end() ? nullptr : sit->second);
+                if (!vr) return Status::Error("bad tag row");
+                auto r = RowReader::getPropByName(vr.get(), prop);
+                if (!r.ok()) return Status::Error("get prop failed");
+                return OptVariant(r.v);
+            };
+            g.getDstTagProp = [this](const std::string& tag, const std::string& prop) -> OptVariant {
+                TagID tagId;
+                if (!x.ctx.getTagId(tag, tagId)) return Status::Error("Get tag id failed in getters.");
+                auto it = x.vertexHolder.find({dstId, tagId});
+                bool ok = false;
+                Variant v;
+                if (it != x.vertexHolder.end()) {
+                    auto vr = RowReader::make(it->second.first, it->second.second);
+                    if (vr) {
+                        auto r = RowReader::getPropByName(vr.get(), prop);
+                        if (r.ok()) { ok = true; v = r.v; }
+                    }
+                } else {
+                    // VertexHolder::getDefaultProp: the holder's response schema, else the latest one
+                    auto hs = x.vertexHolderSchemas.find(tagId);
+                    StatusOr<Variant> d = hs != x.vertexHolderSchemas.end()
+                        ? RowReader::getDefaultProp(hs->second.get(), prop)
+                        : (x.sm.getTagSchema(x.space, tagId) ? RowReader::getDefaultProp(x.sm.getTagSchema(x.space, tagId).get(), prop)
+                                                             : StatusOr<Variant>(Status::Error("No tag schema")));
+                    if (d.ok()) { ok = true; v = d.value(); }
+                }
+                if (!ok) {
+                    auto ts = x.sm.getTagSchema(x.space, tagId);
+                    if (!ts) return Status::Error("No tag schema");
+                    auto d = RowReader::getDefaultProp(ts.get(), prop);
+                    if (!d.ok()) return d.status();
+                    return OptVariant(d.value());
+                }
+                return OptVariant(v);
+            };
+            g.getAliasProp = [this](const std::string& edgeName, const std::string& prop) -> OptVariant {
+                EdgeType type;
+                if (!x.ctx.getEdgeType(edgeName, type)) return Status::Error("Get edge type failed in getters.");
+                if (std::abs(edgeType) != type) {
+                    auto sit = edgeSchema.find(x.s.direction == 1 ? -type : type);
+                    if (sit == edgeSchema.end()) return Status::Error("Can't find schema when get default.");
+                    auto d = RowReader::getDefaultProp(sit->second.get(), prop);
+                    if (!d.ok()) return d.status();
+                    return OptVariant(d.value());
+                }
+                if (prop == "_src") return OptVariant(srcId);
+                if (!reader) return Status::Error("null reader");
+                auto r = RowReader::getPropByName(reader.get(), prop);
+                if (!r.ok()) return Status::Error("get prop failed");
+                return OptVariant(r.v);
+            };
+            g.getInputProp = [this](const std::string& prop) { return x.getColumnWithRow(inputRow, prop); };
+            g.getVariableProp = [this](const std::string& prop) { return x.getColumnWithRow(inputRow, prop); };
+        }
+    };
+
+    // rows (or their digests) of one thread's vertex range, and the first evaluation error in it
+    struct FinalOut {
+        std::vector<std::vector<Variant>> rows;
+        std::string digests;
+        uint64_t count = 0;
+        bool ok = true;
+        std::string error;
+    };
+
     bool processFinalResult() {                                        // :1082-1335
         std::vector<SupportedType> colTypes;
         for (auto& y : yields) colTypes.push_back(calculateExprType(y.get()));
         res.colTypes = colTypes;
         std::map<TagID, std::shared_ptr<Schema>> tagSchema;
         std::map<EdgeType, std::shared_ptr<Schema>> edgeSchema;
-        VertexID srcId = 0, dstId = 0;
-        EdgeType edgeType = 0;
-        const std::vector<TagData>* tagData = nullptr;
-        std::unique_ptr<RowReader> reader;
-        const std::string* rowBytes = nullptr;
-
-        Getters g;
-        g.getEdgeDstId = [&](const std::string& edgeName) -> OptVariant {
-            if (edgeTypes.size() > 1) {
-                EdgeType t;
-                if (!ctx.getEdgeType(edgeName, t)) return Status::Error("Get edge type failed in getters.");
-                if (t != std::abs(edgeType)) return OptVariant(int64_t(0));
-            }
-            return OptVariant(dstId);
-        };
-        g.getSrcTagProp = [&](const std::string& tag, const std::string& prop) -> OptVariant {
-            TagID tagId;
-            if (!ctx.getTagId(tag, tagId)) return Status::Error("Get tag id failed in getters.");
-            const TagData* found = nullptr;
-            for (auto& td : *tagData) if (td.tag_id == tagId) { found = &td; break; }
-            if (!found) {
-                auto ts = sm.getTagSchema(space, tagId);
-                if (!ts) return Status::Error("No tag schema");
-                auto d = RowReader::getDefaultProp(ts.get(), prop);
-                if (!d.ok()) return d.status();
-                return OptVariant(d.value());
-            }
-            auto vr = RowReader::make(found->data, tagSchema[tagId]);
-            if (!vr) return Status::Error("bad tag row");
-            auto r = RowReader::getPropByName(vr.get(), prop);
-            if (!r.ok()) return Status::Error("get prop failed");
-            return OptVariant(r.v);
-        };
-        g.getDstTagProp = [&](const std::string& tag, const std::string& prop) -> OptVariant {
-            TagID tagId;
-            if (!ctx.getTagId(tag, tagId)) return Status::Error("Get tag id failed in getters.");
-            auto it = vertexHolder.find({dstId, tagId});
-            bool ok = false;
-            Variant v;
-            if (it != vertexHolder.end()) {
-                auto vr = RowReader::make(it->second.first, it->second.second);
-                if (vr) {
-                    auto r = RowReader::getPropByName(vr.get(), prop);
-                    if (r.ok()) { ok = true; v = r.v; }
-                }
-            } else {
-                // VertexHolder::getDefaultProp: the holder's response schema, else the latest one
-                auto hs = vertexHolderSchemas.find(tagId);
-                StatusOr<Variant> d = hs != vertexHolderSchemas.end()
-                    ? RowReader::getDefaultProp(hs->second.get(), prop)
-                    : (sm.getTagSchema(space, tagId) ? RowReader::getDefaultProp(sm.getTagSchema(space, tagId).get(), prop)
-                                                     : StatusOr<Variant>(Status::Error("No tag schema")));
-                if (d.ok()) { ok = true; v = d.value(); }
-            }
-            if (!ok) {
-                auto ts = sm.getTagSchema(space, tagId);
-                if (!ts) return Status::Error("No tag schema");
-                auto d = RowReader::getDefaultProp(ts.get(), prop);
-                if (!d.ok()) return d.status();
-                return OptVariant(d.value());
-            }
-            return OptVariant(v);
-        };
-        g.getAliasProp = [&](const std::string& edgeName, const std::string& prop) -> OptVariant {
-            EdgeType type;
-            if (!ctx.getEdgeType(edgeName, type)) return Status::Error("Get edge type failed in getters.");
-            if (std::abs(edgeType) != type) {
-                auto sit = edgeSchema.find(s.direction == 1 ? -type : type);
-                if (sit == edgeSchema.end()) return Status::Error("Can't find schema when get default.");
-                auto d = RowReader::getDefaultProp(sit->second.get(), prop);
-                if (!d.ok()) return d.status();
-                return OptVariant(d.value());
-            }
-            if (prop == "_src") return OptVariant(srcId);
-            if (!reader) return Status::Error("null reader");
-            auto r = RowReader::getPropByName(reader.get(), prop);
-            if (!r.ok()) return Status::Error("get prop failed");
-            return OptVariant(r.v);
-        };
-
-        size_t inputRow = 0;
-        g.getInputProp = [&](const std::string& prop) { return getColumnWithRow(inputRow, prop); };
-        g.getVariableProp = [&](const std::string& prop) { return getColumnWithRow(inputRow, prop); };
-
         std::set<std::vector<Variant>> uniq;
+        const bool par = flags.threads > 1 && s.fromType == 0 && !s.distinct;
+        // one vertex's edges (with the input row bound for pipes); false on an evaluation error
+        auto vertexRows = [&](FinalEval& ev, const VertexData& vd, FinalOut& out) -> bool {
+            for (auto& ed : vd.edge_data) {
+                ev.edgeType = ed.type;
+                auto sit = edgeSchema.find(ev.edgeType);
+                for (auto& e : ed.edges) {
+                    ev.dstId = e.dst;
+                    ev.reader = sit != edgeSchema.end() ? RowReader::make(e.props, sit->second) : nullptr;
+                    if (filter) {
+                        auto v = filter->eval(ev.g);
+                        if (!v.ok()) { out.ok = false; out.error = v.status().msg_; return false; }
+                        if (!Expression::asBool(v.value())) continue;
+                    }
+                    std::vector<Variant> record;
+                    for (auto& y : yields) {
+                        auto v = y->eval(ev.g);
+                        if (!v.ok()) { out.ok = false; out.error = v.status().msg_; return false; }
+                        record.push_back(v.value());
+                    }
+                    if (s.distinct && !uniq.insert(record).second) continue;
+                    out.count++;
+                    if (flags.digest) {
+                        const size_t at = out.digests.size();
+                        out.digests.resize(at + 16);
+                        flags.digest(colTypes, record, reinterpret_cast<uint8_t*>(&out.digests[at]));
+                    } else {
+                        out.rows.push_back(std::move(record));
+                    }
+                }
+            }
+            return true;
+        };
+        auto range = [&](FinalEval& ev, const QueryResponse& resp, size_t recordIn, size_t lo, size_t hi, FinalOut& out) {
+            for (size_t vi = lo; vi < hi; vi++) {
+                const VertexData& vd = resp.vertices[vi];
+                ev.tagData = &vd.tag_data;
+                ev.srcId = vd.vertex_id;
+                if (s.fromType == 0) {
+                    if (!vertexRows(ev, vd, out)) return;
+                } else {                                               // :1321-1330
+                    for (auto row : rowsOfVids(getRoots(ev.srcId, recordIn))) {
+                        ev.inputRow = row;
+                        if (!vertexRows(ev, vd, out)) return;
+                    }
+                }
+            }
+        };
+        auto absorb = [&](FinalOut& out) -> bool {
+            res.rowCount += out.count;
+            res.digests += out.digests;
+            for (auto& r : out.rows) res.rows.push_back(std::move(r));
+            if (!out.ok) return fail(out.error);
+            return true;
+        };
         size_t recordIn = recordFrom;                                   // :1089
         for (size_t ri = recordFrom - 1; ri < records.size(); ri++, recordIn++) {
             auto& resp = records[ri];
             for (auto& kv : resp.vertex_schema) tagSchema.emplace(kv.first, kv.second);
             for (auto& kv : resp.edge_schema) edgeSchema.emplace(kv.first, kv.second);
-            for (auto& vd : resp.vertices) {
-                tagData = &vd.tag_data;
-                srcId = vd.vertex_id;
-                auto func = [&]() -> bool {
-                    for (auto& ed : vd.edge_data) {
-                        edgeType = ed.type;
-                        auto sit = edgeSchema.find(edgeType);
-                        for (auto& e : ed.edges) {
-                            dstId = e.dst;
-                            rowBytes = &e.props;
-                            reader = sit != edgeSchema.end() ? RowReader::make(*rowBytes, sit->second) : nullptr;
-                            if (filter) {
-                                auto v = filter->eval(g);
-                                if (!v.ok()) return fail(v.status().msg_);
-                                if (!Expression::asBool(v.value())) continue;
-                            }
-                            std::vector<Variant> record;
-                            for (auto& y : yields) {
-                                auto v = y->eval(g);
-                                if (!v.ok()) return fail(v.status().msg_);
-                                record.push_back(v.value());
-                            }
-                            if (s.distinct && !uniq.insert(record).second) continue;
-                            res.rows.push_back(std::move(record));
-                        }
-                    }
-                    return true;
-                };
-                if (s.fromType == 0) {
-                    if (!func()) return false;
-                } else {                                               // :1321-1330
-                    for (auto row : rowsOfVids(getRoots(srcId, recordIn))) {
-                        inputRow = row;
-                        if (!func()) return false;
-                    }
+            const size_t nv = resp.vertices.size();
+            const int T = par && nv >= 1024 ? flags.threads : 1;
+            std::vector<FinalOut> outs(T);
+            if (T == 1) {
+                FinalEval ev(*this, tagSchema, edgeSchema);
+                range(ev, resp, recordIn, 0, nv, outs[0]);
+            } else {
+                std::vector<std::thread> ts;
+                for (int t = 0; t < T; t++) {
+                    ts.emplace_back([&, t] {
+                        FinalEval ev(*this, tagSchema, edgeSchema);
+                        range(ev, resp, recordIn, nv * t / T, nv * (t + 1) / T, outs[t]);
+                    });
                 }
+                for (auto& th : ts) th.join();
             }
+            // in sequential order: the first failing range's error is the first error of the record
+            for (auto& out : outs) if (!absorb(out)) return false;
         }
         return true;
     }
@@ -554,7 +629,9 @@ struct GoExec {
                 res.columnNames.push_back(e->toString());             // getResultColumnNames
             }
         }
+        auto tf = std::chrono::steady_clock::now();
         processFinalResult();
+        trace("final", tf);
         return res;
     }
 };

@@ -47,6 +47,7 @@ struct StorageFlags {                      // QueryBaseProcessor.cpp:9-13 defaul
     int32_t max_edge_returned_per_vertex = INT32_MAX;
     int64_t now_sec = 0;                   // WallClock::fastNowInSec() — fixed for determinism
     int32_t threads = 1;                   // reader-pool threads used to run buckets
+    int32_t graph_threads = 1;             // test harness: threads of processFinalResult (GoFlags::threads)
 };
 
 class StorageEngine {
@@ -88,8 +89,19 @@ struct GoResult {
     std::vector<std::vector<Variant>> rows;
     std::vector<int64_t> hopScanned;                          // edges scanned per hop (stats)
     std::vector<int64_t> hopFrontier;
+    // GoFlags::digest set: one 16-byte digest per result row instead of `rows' (rowCount rows)
+    std::string digests;
+    uint64_t rowCount = 0;
 };
-struct GoFlags { bool filter_pushdown = true; };
+// Test-harness knobs (not reference flags): `threads' > 1 splits processFinalResult's rows over threads
+// in contiguous vertex ranges, rows concatenated in the sequential order (no DISTINCT, literal FROM);
+// `digest' turns every result row into a 16-byte digest as it is produced (large-result comparison).
+using RowDigestFn = void (*)(const std::vector<SupportedType>& colTypes, const std::vector<Variant>& row, uint8_t* out16);
+struct GoFlags {
+    bool filter_pushdown = true;
+    int threads = 1;
+    RowDigestFn digest = nullptr;
+};
 
 GoResult runGo(const StorageEngine& eng, GraphSpaceID space, const GoSentence& s, const GoFlags& f);
 

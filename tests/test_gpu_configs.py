@@ -1,9 +1,10 @@
 """BASELINE.json configs at their stated sizes, HIP path (C ABI, device 0) against the oracle.
 
 * C1  NBA fixture (TraverseTestBase), GO 2 STEPS OVER like / serve WHERE ... YIELD ...
-* C2  RMAT scale 22, edge factor 16, 100 parts, e(p0 INT, p1 INT), the bench query
-      `GO 3 STEPS ... WHERE e.p0 < 50 YIELD e._dst, e._rank, e.p0, e.p1`: a seed subset row-for-row
-      against the oracle; the full 1000-seed batch through size-independent properties.
+* C2  RMAT scale 22, edge factor 16, 100 parts, e(p0 INT, p1 INT) with in-edges stored (bench.py's
+      graph), the bench query `GO 3 STEPS ... WHERE e.p0 < 50 YIELD e._dst, e._rank, e.p0, e.p1`: the
+      bench step itself (1000 seeds) row-for-row against the oracle with pull default / forced / off;
+      another 1000-seed batch through size-independent properties.
 * C4  power law with 4 supernodes of in-degree ~1e6 (one frontier entry spans ~470 chunks of 2048
       edges), GO 1/2 STEPS REVERSELY.
 * C5  LDBC-SNB-like (knows / likes / hasCreator, string + int props), a 10k-vid batch, GO 4 STEPS,
@@ -86,50 +87,53 @@ def c2(rmat22):
 
 
 @pytest.mark.timeout(600)
-def test_c2_bench_query_seed_subset(c2):
-    """The bench query at full scale 22 from 2 seeds (hop 3 scans ~30 M edges, ~15 M rows): every
-    row equal to the oracle's, and every hop's scanned edges, with the generated and the interpreter
-    final-hop kernels."""
+def test_c2_bench_step_vs_oracle(c2):
+    """The exact step bench.py times (its first plan: 1000 seeds, sample seed 42), on the graph bench.py
+    builds (in-edges stored, so hop 2 may pull), row for row against the oracle: sorted 128-bit row
+    digests and every hop's scanned edges, with pull at its default factor, forced on every
+    intermediate hop (factor 1) and off (factor 0), and once on the interpreter kernels."""
     ds, o, e = c2
-    seeds = datagen.rmat_seeds(22, 2, 16, 42, 4242, threads=16)
+    seeds = datagen.rmat_seeds(22, 1000, 16, 42, 42, threads=16)
     s = ngql.parse_go(C2_QUERY.replace("{S}", _seed_list(seeds)).replace("{K}", "50"))
     ref = o.go(ds.space, s, digest=True)
-    for mode in (1, 0):
-        e.set_flag("jit", mode)
-        got = _digest_go(e, ds.space, s)
-        assert got.hop_edges == ref.hop_scanned
-        assert sum(got.hop_edges) > 10_000_000
-        _same_digests(got, ref)
-    e.set_flag("jit", 1)
+    assert ref.ok and ref.nrows > 20_000_000 and sum(ref.hop_scanned) > 60_000_000
+    default = e.get_flag("pull_factor")
+    pulls = {}
+    try:
+        for factor, jit in ((default, 1), (1, 1), (0, 1), (default, 0)):
+            e.set_flag("pull_factor", factor)
+            e.set_flag("jit", jit)
+            before = e.get_flag("pull_hops")
+            got = _digest_go(e, ds.space, s)
+            pulls[(factor, jit)] = e.get_flag("pull_hops") - before
+            assert got.hop_edges == ref.hop_scanned, (factor, jit)
+            _same_digests(got, ref)
+    finally:
+        e.set_flag("pull_factor", default)
+        e.set_flag("jit", 1)
+    assert pulls[(1, 1)] == 2 and pulls[(0, 1)] == 0 and pulls[(default, 1)] >= 1
 
 
 @pytest.mark.timeout(600)
 def test_c2_full_batch_properties(c2):
-    """The bench step itself (1000 seeds, ~85 M scanned edges, ~32 M rows), checked through properties
-    that hold at any size:
-      * the precompiled interpreter kernels and the per-query generated kernels return the same rows;
+    """The bench step through properties that hold at any size, beside the oracle check above:
       * without WHERE every scanned edge of the last hop is a row;
       * WHERE p0 < 50 and WHERE p0 >= 50 partition those rows (filter linearity), and the rows of
         `p0 < 50` are exactly the p0 < 50 rows of the unfiltered result (p0 values counted)."""
     ds, o, e = c2
-    seeds = _seed_list(datagen.rmat_seeds(22, 1000, 16, 42, 42, threads=16))
+    seeds = _seed_list(datagen.rmat_seeds(22, 1000, 16, 42, 43, threads=16))
     q50 = ngql.parse_go(C2_QUERY.replace("{S}", seeds).replace("{K}", "50"))
-    e.set_flag("jit", 1)
-    jit = _digest_go(e, ds.space, q50)
-    e.set_flag("jit", 0)
-    vm = _digest_go(e, ds.space, q50)
-    e.set_flag("jit", 1)
-    assert jit.nrows > 20_000_000 and jit.hop_edges == vm.hop_edges
-    assert np.array_equal(jit.digests, vm.digests)
+    lt = e.go(ds.space, q50, on_device=True)
     everything = e.go(ds.space, ngql.parse_go(
-        f"GO 3 STEPS FROM {seeds} OVER e YIELD e._dst, e._rank, e.p0, e.p1"), columnar=True, rows=False)
+        f"GO 3 STEPS FROM {seeds} OVER e YIELD e._dst, e._rank, e.p0, e.p1"), on_device=True, fetch=True)
     ge = e.go(ds.space, ngql.parse_go(
         f"GO 3 STEPS FROM {seeds} OVER e WHERE e.p0 >= 50 YIELD e._dst"), on_device=True)
-    assert everything.ok and ge.ok
-    assert everything.nrows == everything.hop_edges[-1] == jit.hop_edges[-1]
-    assert jit.nrows + ge.nrows == everything.nrows
+    assert lt.ok and everything.ok and ge.ok
+    assert lt.nrows > 20_000_000
+    assert everything.nrows == everything.hop_edges[-1] == lt.hop_edges[-1]
+    assert lt.nrows + ge.nrows == everything.nrows
     p0 = everything.dev_cols[2][0]
-    assert int(np.count_nonzero(p0 < 50)) == jit.nrows
+    assert int(np.count_nonzero(p0 < 50)) == lt.nrows
 
 
 # ----------------------------------------------------------------------------------------- C4
