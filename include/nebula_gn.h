@@ -350,6 +350,12 @@ int32_t ngx_kernel_stats(ngx_ctx* ctx, const ngx_kernel_stat** out, int32_t* n);
  *          V rows pulls (probes every row's in-edges) when 100 * E >= pull_factor * V and the hop's
  *          in-edge slots mirror its out-edge slots exactly; default 200, 0 = never. Same results.
  * Read-only "pull_hops": intermediate hops that pulled so far.
+ *   "device_libm"  math functions of row values. abs/floor/ceil/round/sqrt are correctly rounded on the
+ *          device and always run there; calls of the others (sin, cos, tan, asin, acos, atan, exp, exp2,
+ *          log, log2, log10, cbrt, hypot, pow) whose arguments are literals are evaluated at compile
+ *          time with the host libm. With a row-dependent argument they compile to NGX_E_UNSUPPORTED
+ *          (default 0; the caller runs its CPU path) because the device libm may differ from glibc in
+ *          the last place; 1 accepts the device libm (within 2 ulp of glibc).
  *   "max_edge_returned_per_vertex"  storaged's flag for the storage requests of every GO hop: at most
  *          this many edges emitted per (vertex, edge type) in key order, counted after the storage
  *          checks and the pushed filter (QueryBaseProcessor.inl:501-505); <= 0: unlimited (default).

@@ -125,6 +125,7 @@ struct ngx_ctx {
     DBuf oSrc, oDst, oRank, oType, oEntry, progBuf, sendBits, recvBits, vcells, misc, oColDesc, edgeMask;
     DBuf oFlags, rowCols, rowLen, rowOff, rowBytes;     // GetNeighbors response rows (encode_rows)
     DBuf dkTable, dkKeep, dkPre, dSrc, dDst, dRank, dType;   // YIELD DISTINCT (table, marks, compacted rows)
+    std::vector<DBuf> strArena;                         // result string arenas, one per record hop (FinalArgs::strOut)
     int64_t maxEdgesPerVertex = INT32_MAX;             // storaged FLAGS_max_edge_returned_per_vertex (GO hops)
     struct ColBuf { DBuf x, len, t; };
     struct PinBuf {                                     // page-locked host staging for result D2H
@@ -167,6 +168,7 @@ struct ngx_ctx {
     // and the idle launch of the expansion not taken cost what the round trips saved (C2 step: device
     // 680 vs 656 us, profiles/r02_dyn_*); kept as an option ("dyn_hops", NGX_DYN_HOPS=1)
     bool dynHops = false;
+    bool deviceLibm = false;                            // inexact libm of row values on the device (exprc.cpp)
     DBuf dynStats;                                      // per hop: packed (|F|, E) written by seed / compaction
     int cus = 256;                                      // compute units of the device
     // RCCL watchdog: collective work must finish within this; else the communicator is aborted
@@ -514,12 +516,18 @@ std::string hostString(const DeviceGraph& d, const DevPrograms& dp, const std::s
 // device string pointer -> host bytes: the query's literal pool (copied to `pool`) or a snapshot
 // string column (DeviceGraph::strRanges)
 struct StrMap {
+    struct Range { uint64_t dev, len; const char* host; };
     const DeviceGraph* d;
     uint64_t poolDev;
     const std::string* pool;
+    const std::vector<Range>* built = nullptr;                  // result string arenas (host copies)
     const char* host(uint64_t ptr, uint32_t len) const {
         if (len == 0) return "";
         if (ptr >= poolDev && ptr + len <= poolDev + pool->size()) return pool->data() + (ptr - poolDev);
+        if (built) {
+            for (const Range& r : *built)
+                if (ptr >= r.dev && ptr + len <= r.dev + r.len) return r.host + (ptr - r.dev);
+        }
         auto it = std::upper_bound(d->strRanges.begin(), d->strRanges.end(), ptr,
                                    [](uint64_t v, const DeviceGraph::Range& r) { return v < r.dev; });
         if (it == d->strRanges.begin()) return "";
@@ -826,6 +834,7 @@ struct GoResultHolder {
     std::vector<int64_t> src, dst, rank;
     std::vector<int32_t> type;
     std::string strings;
+    std::vector<std::string> built;                             // host copies of the result string arenas
     std::vector<uint64_t> hopFrontier, hopEdges, hopNext, hopXchg;
     // host-side timing of the call (steady clock): entry, first launch, device done
     std::chrono::steady_clock::time_point tIn, tLaunch, tDone;
@@ -1232,6 +1241,19 @@ int32_t ngx_open_snapshot(ngx_ctx* c, int32_t space, const char* path, char* tag
         auto hg = std::make_unique<HostGraph>();
         std::string tag;
         Error e = readSnapshotFile(*sp, path, c->rank, c->world, *hg, tag);
+        if (c->world > 1) {
+            // collective: every rank's file must come from the same commit (the shards' global rows and
+            // destination rows encode each other's vertex tables); a rank whose file failed still takes
+            // part, so every rank reaches the same verdict and none waits in a later collective alone
+            uint64_t mine[2] = {e.code ? 0ULL : 1ULL, e.code ? 0ULL : hg->commitDigest};
+            std::vector<uint8_t> all = gatherHost(c, mine, sizeof(mine));
+            for (int w = 0; w < c->world && !e.code; w++) {
+                uint64_t other[2];
+                std::memcpy(other, all.data() + w * sizeof(mine), sizeof(mine));
+                if (!other[0]) e = Error{NGX_E_SNAPSHOT, std::string(path) + ": the snapshot of shard " + std::to_string(w) + " failed to open"};
+                else if (other[1] != mine[1]) e = Error{NGX_E_SNAPSHOT, std::string(path) + ": snapshots of different commits across shards"};
+            }
+        }
         if (e.code) return fail(c, e.code, e.msg);
         auto dev = upload(*hg, *sp);
         attachMirrors(c, *hg, *dev);
@@ -1293,6 +1315,7 @@ int32_t ngx_commit(ngx_ctx* c, int32_t space) {
             }
         }
         resolveDstRows(*sp, *hg, tables, c->world);
+        hg->commitDigest = tablesDigest(tables);
         if (hg->shardBase.empty()) { hg->shardBase = {0, hg->vid.size()}; hg->vglobal = hg->vid.size(); }
         hg->gbase = hg->shardBase[c->rank];
         sp->dev = upload(*hg, *sp);
@@ -1359,6 +1382,7 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
     if (n == "pull_factor") { c->pullFactor = value < 0 ? 0 : value; return NGX_OK; }
     if (n == "jit_async") { c->jit.async = value != 0; c->jit.device = c->device; return NGX_OK; }
     if (n == "dyn_hops") { c->dynHops = value != 0; return NGX_OK; }
+    if (n == "device_libm") { c->deviceLibm = value != 0; return NGX_OK; }
     if (n == "jit_wait") { c->jit.drain(); return NGX_OK; }
     return fail(c, NGX_E_BAD_ARGUMENT, "unknown flag " + n);
 }
@@ -1372,6 +1396,7 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "pull_factor") *value = c->pullFactor;
     else if (n == "jit_async") *value = c->jit.async ? 1 : 0;
     else if (n == "dyn_hops") *value = c->dynHops ? 1 : 0;
+    else if (n == "device_libm") *value = c->deviceLibm ? 1 : 0;
     else if (n == "pull_hops") *value = static_cast<int64_t>(c->pullHops);
     else if (n == "jit_compiled") *value = static_cast<int64_t>(c->jit.compiled);
     else if (n == "jit_hits") *value = static_cast<int64_t>(c->jit.hits);
@@ -1800,6 +1825,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     // ---- final-hop request (getStepOutProps for record hops)
     GraphdCtx gctx;
     gctx.sp = &sp;
+    gctx.deviceLibm = c->deviceLibm;
     gctx.aliasType = gp.aliasType;
     gctx.direction = p.direction;
     gctx.nEdgeTypes = gp.edgeTypes.size();
@@ -1816,6 +1842,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     }
     StorageCtx sctx;
     sctx.sp = &sp;
+    sctx.deviceLibm = c->deviceLibm;
     sctx.haveEdgeContexts = true;
     for (int32_t t : gp.edgeTypes) {
         const SchemaSet* es = sp.edge(std::abs(t));
@@ -1848,11 +1875,20 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     }
     for (auto& y : gp.yields) {
         Program yp;
-        if (builtStringAtRoot(*y)) return fail(c, NGX_E_UNSUPPORTED, "YIELD of a (string) cast: result strings are not built on the device");
         int32_t crc = compileGraphd(*y, gctx, yp, err);
         if (crc) return fail(c, crc, err);
         progs.yOff.push_back(progs.add(yp));
     }
+    // YIELD columns that build strings keep them in the result string arena (one slot per row)
+    uint32_t strOutMask = 0;
+    for (size_t y = 0; y < progs.yOff.size(); y++) {
+        if (!strBuffersOf(progs.code.data() + progs.yOff[y])) continue;
+        if (y >= 32) return fail(c, NGX_E_UNSUPPORTED, "a YIELD column past the 32nd that builds strings");
+        strOutMask |= 1u << y;
+    }
+    const uint32_t nStrOut = static_cast<uint32_t>(__builtin_popcount(strOutMask));
+    struct Arena { const char* dev; uint64_t rows; };
+    std::vector<Arena> arenas;                                   // this query's, in record-hop order
     // $$ props: tag tables over every global row (world > 1: replicas of the other shards' rows)
     const bool dstReplica = progs.usesDst && c->world > 1;
     if (dstReplica) ensureDstReplicas(c, sp);
@@ -1876,11 +1912,11 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         for (int32_t al : yAlias) if (al >= 0) rowMask |= 1 << al;
     }
     // per-query straight-line kernels (jit.cpp); the interpreter kernels otherwise
-    const JitKernels* jk = nullptr;
-    const JitKernels* jkNoP = nullptr;                       // record hops before the last (no pushdown)
+    std::shared_ptr<const JitKernels> jk, jkNoP;             // jkNoP: record hops before the last (no pushdown)
     std::vector<int64_t> jitKc;                              // their literal table (FinalArgs::kc/kl)
     std::vector<uint32_t> jitKl;
     c->jitNote.clear();
+    c->jit.releaseRetired(c->stream);                        // modules evicted by earlier queries
     if (c->jitOn) {
         JitQuery jq = jitHopQuery(sp, hs, progs);
         jq.yColType = gp.colTypes;
@@ -2175,7 +2211,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             a.wIsP = (isFinal && wIsP) ? 1u : 0u;
             for (size_t k = 0; k < jitKc.size(); k++) { a.kc[k] = jitKc[k]; a.kl[k] = jitKl[k]; }
             // a masked hop (max-edges cap) runs on the interpreter kernel: the generated ones skip the mask
-            const JitKernels* kj = mask ? nullptr : (isFinal ? jk : jkNoP);
+            const JitKernels* kj = mask ? nullptr : (isFinal ? jk.get() : jkNoP.get());
             // outputs sized for every edge passing (rows are written in the same launch)
             uint64_t cap = totalRows + E;
             growKeep(c, c->oSrc, cap * 8, totalRows * 8);
@@ -2195,6 +2231,14 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             a.rowsPub = rowsPub.slot;
             a.rowsSeq = rowsPub.seq;
             a.dynTotal = dynTotal;
+            a.strOut = nullptr;
+            a.nStrOut = nStrOut;
+            a.strOutMask = strOutMask;
+            if (nStrOut) {
+                if (c->strArena.size() <= arenas.size()) c->strArena.resize(arenas.size() + 1);
+                a.strOut = c->strArena[arenas.size()].get<char>(E * nStrOut * static_cast<uint64_t>(kStrBuildBytes));
+                arenas.push_back(Arena{a.strOut, 0});
+            }
             // dyn: chunks of the upper bound E; the workgroups past the real chunks return at once
             const unsigned grid = static_cast<unsigned>(chunks);
             c->timed("final", dyn ? 0 : E * (16 + kfBytes), [&] {
@@ -2211,6 +2255,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                 haveFinalErrs = true;
                 c->addBytes("final", nrows * (8 * __builtin_popcount(rowMask) + 8 * ky));
                 totalRows += nrows;
+                if (nStrOut) arenas.back().rows = nrows;
             }
         }
         if (isFinal) break;
@@ -2361,6 +2406,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             }
         }
         totalRows = rows;
+        if (nStrOut && !arenas.empty()) arenas.back().rows = rows;
     }
     float ms = 0;
     if (t1) {
@@ -2504,7 +2550,18 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         }
     }
     R.strings = progs.pool;                                    // string literals of YIELD, kept with the result
-    StrMap sm{&d, reinterpret_cast<uint64_t>(dp.pool), &R.strings};
+    // the strings YIELD columns built: each record hop's arena rows, copied next to the result
+    R.built.clear();
+    std::vector<StrMap::Range> builtRanges;
+    for (const Arena& ar : arenas) {
+        const uint64_t bytes = ar.rows * nStrOut * static_cast<uint64_t>(kStrBuildBytes);
+        if (!bytes) continue;
+        R.built.emplace_back(bytes, '\0');
+        HIP_OK(hipMemcpyAsync(&R.built.back()[0], ar.dev, bytes, hipMemcpyDeviceToHost, c->stream));
+        builtRanges.push_back(StrMap::Range{reinterpret_cast<uint64_t>(ar.dev), bytes, R.built.back().data()});
+    }
+    if (!builtRanges.empty()) HIP_OK(hipStreamSynchronize(c->stream));
+    StrMap sm{&d, reinterpret_cast<uint64_t>(dp.pool), &R.strings, &builtRanges};
     uint64_t nOut = n;
     R.r.nrows = nOut;
     R.r.dev_type_const = constType ? hs.etype[0] : 0;
@@ -2867,6 +2924,7 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
     std::set<int32_t> tagCols;
     StorageCtx sctx;
     sctx.sp = &sp;
+    sctx.deviceLibm = c->deviceLibm;
     for (int32_t i = 0; i < q.nedge_types; i++) edgeCols[q.edge_types[i]];
     for (int32_t i = 0; i < q.ncols; i++) {
         const ngx_prop_def& col = q.cols[i];
@@ -3081,7 +3139,7 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
         a.lbStatus = lb;
         // a generated kernel for the request shape (the interpreter's per-instruction loads serialize a
         // chunk's edges: 170 us for 25 K edges); a masked request (max-edges cap) stays on the interpreter
-        const JitKernels* jk = nullptr;
+        std::shared_ptr<const JitKernels> jk;
         if (c->jitOn && !a.mask) {
             JitQuery jq = jitHopQuery(sp, hs, progs);
             jq.fidx = true;
@@ -3098,6 +3156,7 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
             jitSlotConsts(jq, kc, kl);
             for (size_t k = 0; k < kc.size(); k++) { a.kc[k] = kc[k]; a.kl[k] = kl[k]; }
             std::string jerr;
+            c->jit.releaseRetired(c->stream);
             jk = c->jit.get(jitShapeKey(sp, jq), [&] { return jitSource(sp, jq); }, jerr);
         }
         if (jk) {

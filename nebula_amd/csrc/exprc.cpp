@@ -164,14 +164,19 @@ const std::map<std::string, FuncInfo>& functions() {          // FunctionManager
         {"tan", {F_TAN, 1, 1}}, {"atan", {F_ATAN, 1, 1}}, {"hypot", {F_HYPOT, 2, 2}},
         {"pow", {F_POW, 2, 2}}, {"strcasecmp", {F_STRCASECMP, 2, 2}}, {"length", {F_LENGTH, 1, 1}},
         {"hash", {F_HASH, 1, 1}}, {"udf_is_in", {F_UDF_IS_IN, 2, 1u << 20}},
+        {"lower", {F_LOWER, 1, 1}}, {"upper", {F_UPPER, 1, 1}}, {"trim", {F_TRIM, 1, 1}},
+        {"ltrim", {F_LTRIM, 1, 1}}, {"rtrim", {F_RTRIM, 1, 1}}, {"left", {F_LEFT, 2, 2}},
+        {"right", {F_RIGHT, 2, 2}}, {"lpad", {F_LPAD, 3, 3}}, {"rpad", {F_RPAD, 3, 3}},
+        {"substr", {F_SUBSTR, 3, 3}},
     };
     return m;
 }
-// functions the reference has but the device VM does not evaluate (string-producing or
-// nondeterministic): they compile to NGX_E_UNSUPPORTED rather than to a wrong answer
-const std::set<std::string> kHostOnlyFuncs = {"lower", "upper", "trim", "ltrim", "rtrim", "left", "right",
-                                              "lpad", "rpad", "substr", "rand32", "rand64", "now", "near",
-                                              "cos_similarity"};
+// functions the reference has but the device VM does not evaluate (nondeterministic, or geo / vector
+// helpers): they compile to NGX_E_UNSUPPORTED rather than to a wrong answer
+const std::set<std::string> kHostOnlyFuncs = {"rand32", "rand64", "now", "near", "cos_similarity"};
+// functions whose value is a string (views of an argument, or built in a buffer)
+bool stringFunc(int32_t fid) { return fid >= F_TRIM && fid <= F_RPAD; }
+bool builderFunc(int32_t fid) { return fid >= F_LOWER && fid <= F_RPAD; }
 }  // namespace
 
 bool rewritePushdown(ExprNode& n) {                            // TraverseExecutor.cpp:461-538
@@ -214,7 +219,11 @@ namespace {
 
 struct Emitter {
     Program& P;
-    int strCasts = 0;                   // (string) casts emitted (each takes one evaluation buffer)
+    bool deviceLibm = false;            // let inexact libm calls of row values run on the device libm
+    const Space* sp = nullptr;          // prop types (which string + can concatenate)
+    int builds = 0;                     // builder buffers handed out (Insn::mode)
+    // the next builder buffer, or kNoBuf when the program has used them all
+    uint8_t takeBuf() { return builds < kMaxStrBuilds ? static_cast<uint8_t>(builds++) : kNoBuf; }
     void emit(uint8_t op, int32_t a = 0, int32_t b = 0, uint8_t t1 = 0, uint8_t t2 = 0, uint8_t mode = 0, int64_t imm = 0) {
         Insn in{};
         in.op = op; in.a = a; in.b = b; in.t1 = t1; in.t2 = t2; in.mode = mode; in.imm = imm;
@@ -245,6 +254,99 @@ struct Emitter {
     }
 };
 
+// Math functions whose device (ocml) result is the correctly rounded one, so equal to glibc's bit for bit:
+// fabs, floor, ceil, round and sqrt (IEEE-754 requires sqrt correctly rounded; the gfx950 f64 sqrt
+// lowering refines to it). The rest are within an ulp or two of glibc but not always equal to it.
+bool libmExact(int32_t fid) {
+    return fid == F_ABS || fid == F_FLOOR || fid == F_CEIL || fid == F_ROUND || fid == F_SQRT;
+}
+bool libmFunc(int32_t fid) {
+    switch (fid) {
+        case F_ABS: case F_FLOOR: case F_CEIL: case F_ROUND: case F_SQRT: case F_CBRT: case F_EXP:
+        case F_EXP2: case F_LOG: case F_LOG2: case F_LOG10: case F_SIN: case F_ASIN: case F_COS:
+        case F_ACOS: case F_TAN: case F_ATAN: case F_HYPOT: case F_POW:
+            return true;
+        default:
+            return false;
+    }
+}
+
+// A numeric value known at compile time: a literal, its sign flip, or a math function of such values,
+// evaluated here with the host libm the reference evaluates it with (FunctionManager.cpp:20-120 calls
+// std::sin ... on graphd/storaged hosts). The value is the same for every row, so folding it is exact.
+bool constNumber(const ExprNode& n, double& d, bool& isInt, int64_t& i) {
+    if (n.kind == K_PRIMARY) {
+        if (n.vtype == 0) { isInt = true; i = n.i; d = static_cast<double>(n.i); return true; }
+        if (n.vtype == 1) { isInt = false; d = n.d; return true; }
+        return false;
+    }
+    if (n.kind == K_UNARY && (n.op == 0 || n.op == 1)) {           // +x, -x (Expressions.cpp:682-706)
+        if (!constNumber(*n.kids[0], d, isInt, i)) return false;
+        if (n.op == 0) return true;
+        if (isInt) {
+            if (i == INT64_MIN) return false;                       // leave the overflow to the evaluator
+            i = -i; d = static_cast<double>(i);
+        } else {
+            d = -d;
+        }
+        return true;
+    }
+    if (n.kind != K_FUNC) return false;
+    auto it = functions().find(n.name);
+    if (it == functions().end() || !libmFunc(it->second.id) || n.kids.size() < it->second.minA ||
+        n.kids.size() > it->second.maxA)
+        return false;
+    double a[2];
+    for (size_t k = 0; k < n.kids.size(); k++) {
+        bool ki; int64_t kv;
+        if (!constNumber(*n.kids[k], a[k], ki, kv)) return false;
+    }
+    switch (it->second.id) {
+        case F_ABS: d = std::fabs(a[0]); break;
+        case F_FLOOR: d = std::floor(a[0]); break;
+        case F_CEIL: d = std::ceil(a[0]); break;
+        case F_ROUND: d = std::round(a[0]); break;
+        case F_SQRT: d = std::sqrt(a[0]); break;
+        case F_CBRT: d = std::cbrt(a[0]); break;
+        case F_EXP: d = std::exp(a[0]); break;
+        case F_EXP2: d = std::exp2(a[0]); break;
+        case F_LOG: d = std::log(a[0]); break;
+        case F_LOG2: d = std::log2(a[0]); break;
+        case F_LOG10: d = std::log10(a[0]); break;
+        case F_SIN: d = std::sin(a[0]); break;
+        case F_ASIN: d = std::asin(a[0]); break;
+        case F_COS: d = std::cos(a[0]); break;
+        case F_ACOS: d = std::acos(a[0]); break;
+        case F_TAN: d = std::tan(a[0]); break;
+        case F_ATAN: d = std::atan(a[0]); break;
+        case F_HYPOT: d = std::hypot(a[0], a[1]); break;
+        case F_POW: d = std::pow(a[0], a[1]); break;
+        default: return false;
+    }
+    isInt = false;
+    return true;
+}
+
+// whether the expression's value can be a string (string + needs a builder buffer only then)
+bool mayBeString(const ExprNode& n, const Space* sp) {
+    switch (n.kind) {
+        case K_PRIMARY: return n.vtype == 3;
+        case K_CAST: return n.op == 1;
+        case K_UNARY: return n.op == 0 && mayBeString(*n.kids[0], sp);
+        case K_ARITH: return n.op == 0 && mayBeString(*n.kids[0], sp) && mayBeString(*n.kids[1], sp);
+        case K_REL: case K_LOGIC: return false;
+        case K_FUNC: {
+            auto it = functions().find(n.name);
+            return it == functions().end() || stringFunc(it->second.id);
+        }
+        default: {
+            if (sp == nullptr) return true;
+            const int32_t t = exprType(n, *sp);
+            return t == T_STRING || t == T_UNKNOWN;
+        }
+    }
+}
+
 int32_t compileCommon(const ExprNode& n, Emitter& em, std::string& err,
                       const std::function<int32_t(const ExprNode&)>& leaf,
                       const std::function<int32_t(const ExprNode&)>& rec) {
@@ -257,13 +359,14 @@ int32_t compileCommon(const ExprNode& n, Emitter& em, std::string& err,
             return NGX_OK;
         }
         case K_CAST: {
-            if (n.op == 1 && ++em.strCasts > kMaxStrCasts) {
-                err = "more (string) casts in one expression than the device evaluator buffers";
-                return NGX_E_UNSUPPORTED;
-            }
             int32_t rc = rec(*n.kids[0]);
             if (rc) return rc;
-            em.emit(OP_CAST, 0, 0, n.op);
+            uint8_t buf = kNoBuf;
+            if (n.op == 1 && (buf = em.takeBuf()) == kNoBuf) {
+                err = "more strings built in one expression than the device evaluator buffers";
+                return NGX_E_UNSUPPORTED;
+            }
+            em.emit(OP_CAST, 0, 0, n.op, 0, buf);
             return NGX_OK;
         }
         case K_ARITH: case K_REL: case K_LOGIC: {
@@ -275,10 +378,15 @@ int32_t compileCommon(const ExprNode& n, Emitter& em, std::string& err,
             if (n.kind == K_ARITH) {
                 static const uint8_t m[] = {OP_ADD, OP_SUB, OP_MUL, OP_DIV, OP_MOD, OP_AXOR};
                 if (n.op > 5) { em.emit(OP_ERR); return NGX_OK; }
-                if (n.op == 0) {
-                    // string + string concatenation builds a new string: detect statically where possible
-                }
                 op = m[n.op];
+                if (n.op == 0) {
+                    // string + string builds a string: a buffer when both sides can be strings; an ADD
+                    // without one flags a string operand pair as a host-only construct at run time
+                    const uint8_t buf = (mayBeString(*n.kids[0], em.sp) && mayBeString(*n.kids[1], em.sp))
+                                            ? em.takeBuf() : kNoBuf;
+                    em.emit(op, 0, 0, 0, 0, buf);
+                    return NGX_OK;
+                }
             } else if (n.kind == K_REL) {
                 static const uint8_t m[] = {OP_LT, OP_LE, OP_GT, OP_GE, OP_EQ, OP_NE, OP_CONTAINS};
                 if (n.op > 6) { em.emit(OP_ERR); return NGX_OK; }
@@ -300,11 +408,38 @@ int32_t compileCommon(const ExprNode& n, Emitter& em, std::string& err,
                 err = "Arity not match for function `" + n.name + "'";
                 return NGX_E_INVALID_FILTER;
             }
+            if (libmFunc(it->second.id)) {
+                double d; bool isInt; int64_t iv;
+                if (constNumber(n, d, isInt, iv)) {
+                    ExprNode c;
+                    c.kind = K_PRIMARY; c.vtype = 1; c.d = d;
+                    em.pushConst(c);
+                    return NGX_OK;
+                }
+                // a row-dependent argument: refuse rather than return a double that may differ from
+                // glibc's in the last place (the caller evaluates the query on its CPU path instead);
+                // constant non-numeric arguments go to the evaluator, which fails them without libm
+                bool rowDependent = false;
+                for (auto& k : n.kids) {
+                    double kd; bool ki; int64_t kv;
+                    if (k->kind != K_PRIMARY && !constNumber(*k, kd, ki, kv)) rowDependent = true;
+                }
+                if (rowDependent && !libmExact(it->second.id) && !em.deviceLibm) {
+                    err = "function `" + n.name + "' of a row value is not evaluated on the device (its libm "
+                          "is not glibc's bit for bit; set flag device_libm to accept it)";
+                    return NGX_E_UNSUPPORTED;
+                }
+            }
             for (auto& k : n.kids) {
                 int32_t rc = rec(*k);
                 if (rc) return rc;
             }
-            em.emit(OP_FUNC, it->second.id, static_cast<int32_t>(n.kids.size()));
+            uint8_t buf = kNoBuf;
+            if (builderFunc(it->second.id) && (buf = em.takeBuf()) == kNoBuf) {
+                err = "more strings built in one expression than the device evaluator buffers";
+                return NGX_E_UNSUPPORTED;
+            }
+            em.emit(OP_FUNC, it->second.id, static_cast<int32_t>(n.kids.size()), 0, 0, buf);
             return NGX_OK;
         }
         default:
@@ -324,6 +459,8 @@ int32_t keyIndex(const std::string& prop) {
 
 int32_t compileStorage(const ExprNode& root, StorageCtx& ctx, Program& out, std::string& err) {
     Emitter em{out};
+    em.deviceLibm = ctx.deviceLibm;
+    em.sp = ctx.sp;
     std::function<int32_t(const ExprNode&)> rec;
     auto leaf = [&](const ExprNode& n) -> int32_t {
         const Space& sp = *ctx.sp;
@@ -378,6 +515,8 @@ int32_t compileStorage(const ExprNode& root, StorageCtx& ctx, Program& out, std:
 
 int32_t compileGraphd(const ExprNode& root, GraphdCtx& ctx, Program& out, std::string& err) {
     Emitter em{out};
+    em.deviceLibm = ctx.deviceLibm;
+    em.sp = ctx.sp;
     std::function<int32_t(const ExprNode&)> rec;
     auto leaf = [&](const ExprNode& n) -> int32_t {
         const Space& sp = *ctx.sp;
@@ -470,14 +609,6 @@ int32_t exprType(const ExprNode& n, const Space& sp) {
         }
         default: return T_UNKNOWN;
     }
-}
-
-// a (string) cast at the root of an expression (through unary +): its value is a string built in
-// the evaluation's own buffer, which a YIELD would have to store
-bool builtStringAtRoot(const ExprNode& n) {
-    if (n.kind == K_CAST) return n.op == 1;
-    if (n.kind == K_UNARY && n.op == 0 && !n.kids.empty()) return builtStringAtRoot(*n.kids[0]);
-    return false;
 }
 
 }  // namespace ngx

@@ -66,6 +66,7 @@ struct StorageCtx {
     std::map<std::string, int32_t> edgeMap;      // edge NAME -> |type| of EDGE return columns
     bool haveEdgeContexts = false;
     std::set<int32_t> filterTags;                // tag ids referenced by $^ (checkExp adds contexts)
+    bool deviceLibm = false;                     // flag device_libm: inexact libm of row values allowed
 };
 
 // Graphd-side compile context for one GO
@@ -76,6 +77,7 @@ struct GraphdCtx {
     size_t nEdgeTypes = 0;
     // final-hop response schema per signed type: prop name -> type
     std::map<int32_t, std::map<std::string, int32_t>> respSchema;
+    bool deviceLibm = false;                     // flag device_libm: inexact libm of row values allowed
 };
 
 // Compile. Returns NGX_OK, NGX_E_INVALID_FILTER (storage checkExp failure), NGX_E_UNSUPPORTED, or
@@ -83,8 +85,6 @@ struct GraphdCtx {
 int32_t compileStorage(const ExprNode& n, StorageCtx& ctx, Program& out, std::string& err);
 int32_t compileGraphd(const ExprNode& n, GraphdCtx& ctx, Program& out, std::string& err);
 
-// the expression's value may be a string a (string) cast built (not storable as a YIELD column)
-bool builtStringAtRoot(const ExprNode& n);
 
 // TraverseExecutor::calculateExprType (src/graph/TraverseExecutor.cpp:88-165)
 int32_t exprType(const ExprNode& n, const Space& sp);

@@ -11,6 +11,7 @@
 #include <condition_variable>
 #include <functional>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -57,13 +58,19 @@ class JitCache {
 public:
     ~JitCache();
     // nullptr when compilation failed (err set). Kernels are cached by query shape (jitShapeKey), at most
-    // `capacity` modules (least recently used unloaded first; callers hold no kernel across queries);
+    // `capacity` modules, least recently used evicted first. An evicted module is retired, not unloaded:
+    // a query may still hold it (a later get() of the same query can evict an entry an earlier one
+    // returned), and releaseRetired() unloads the retired modules at the start of the next query, after
+    // the context's stream has drained; the returned handle keeps its descriptor alive meanwhile.
     // `source` generates the hipRTC source on a miss. With `async` set, a miss queues the compile on a
     // background thread and returns nullptr at once (err "jit: compiling"): the query runs on the
     // interpreter kernels and a later query of the same shape finds the module (hipRTC's ~170 ms stays
     // off the query's critical path). Finished modules enter the cache only inside get(), on the
     // caller's thread, so a module in use by the calling query is never evicted under it.
-    const JitKernels* get(const std::string& shape, const std::function<std::string()>& source, std::string& err);
+    std::shared_ptr<const JitKernels> get(const std::string& shape, const std::function<std::string()>& source,
+                                          std::string& err);
+    // unload the modules evicted since the last call (synchronises `s` first when there are any)
+    void releaseRetired(hipStream_t s);
     // block until every queued compile has finished (tests, warm-up)
     void drain();
     uint64_t compiled = 0, hits = 0, failed = 0, evicted = 0;
@@ -75,7 +82,8 @@ public:
     size_t size() const { return cache_.size(); }
 
 private:
-    struct Entry { JitKernels k; uint64_t used = 0; };
+    struct Entry { std::shared_ptr<JitKernels> k; uint64_t used = 0; };
+    std::vector<hipModule_t> retired_;
     struct Done { std::string shape; JitKernels k; std::string err; double seconds; int64_t regs, scratch; };
     void admit();                               // finished background compiles -> cache_ / failures_
     void insert(const std::string& shape, const JitKernels& k);

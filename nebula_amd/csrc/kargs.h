@@ -83,7 +83,16 @@ struct FinalArgs {
     uint32_t kl[kJitConsts];            // string literal lengths
     const uint64_t* dynTotal;           // device-driven hop: packed (frontier rows << kDynShift | E) written by
                                         // the kernel that built the frontier; nullptr: E / nEnt above
+    char* strOut;                       // result string arena: kStrBuildBytes per (row - oBase, string column),
+                                        // for the strings YIELD columns build; nullptr when none does
+    uint32_t nStrOut;                   // columns that build strings (bits of strOutMask, y < 32)
+    uint32_t strOutMask;
 };
+
+// the row's slot of the result string arena for the j-th column that builds strings
+__device__ __forceinline__ char* strSlot(const FinalArgs& a, uint64_t o, uint32_t j) {
+    return a.strOut == nullptr ? nullptr : a.strOut + ((o - a.oBase) * a.nStrOut + j) * kStrBuildBytes;
+}
 
 // packed (frontier rows, hop edges) totals of the compaction / seed kernels
 constexpr int kDynShift = 36;

@@ -805,7 +805,9 @@ struct VmEv {
             if (a.ySlotType != nullptr && a.ySlotType[y] != 0 && a.ySlotType[y] != ec.etype) {
                 v.t = 0xFF; v.len = 0; v.x = 0;              // column of another edge type (GetNeighbors)
             } else {
-                v = vmEval(a.yCode + a.yOff[y], a.env, ec);
+                const uint32_t sb = y < 32 ? (a.strOutMask >> y) & 1u : 0u;
+                v = vmEval(a.yCode + a.yOff[y], a.env, ec,
+                           sb ? strSlot(a, o, __popc(a.strOutMask & ((1u << y) - 1u))) : nullptr);
                 if (v.t == V_ERR) errs |= 1u;
                 else if (a.yColType != nullptr && !cellTypeOk(a.yColType[y], v.t)) errs |= 4u;
             }

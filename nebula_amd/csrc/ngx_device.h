@@ -12,8 +12,10 @@ namespace ngx {
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 constexpr int kMaxSlots = 16;
 constexpr int kMaxStack = 12;
-constexpr int kStrCastBytes = 24;           // buffer of one (string) cast (vm.h castToString)
-constexpr int kMaxStrCasts = 4;             // (string) casts per program (exprc.cpp refuses more)
+constexpr int kStrBuildBytes = 64;          // longest string a builder (lower, upper, lpad, rpad, string +,
+                                            // (string)) makes on the device; longer: host-only construct
+constexpr int kMaxStrBuilds = 4;            // builder buffers per program (exprc.cpp refuses more)
+constexpr uint8_t kNoBuf = 0xFF;            // Insn::mode of an OP_ADD / OP_FUNC / OP_CAST without a buffer
 
 // per-edge flags (HostSlot::eflags)
 enum : uint8_t {
@@ -73,17 +75,23 @@ enum Op : uint8_t {
     OP_SRCTAG,         // src tag column: a = column, b = tag slot; mode bit0: missing -> default
     OP_DSTTAG,         // dst tag column (graphd $$): a = column, b = tag slot; missing -> default
     OP_NEG, OP_PLUS, OP_NOT,
-    OP_CAST,           // t1 = ColumnType target (INT=0, STRING=1, DOUBLE=2, BOOL=3, TIMESTAMP=4)
-    OP_ADD, OP_SUB, OP_MUL, OP_DIV, OP_MOD, OP_AXOR,
+    OP_CAST,           // t1 = ColumnType target (INT=0, STRING=1, DOUBLE=2, BOOL=3, TIMESTAMP=4);
+                       // (string): mode = builder buffer
+    OP_ADD,            // mode = builder buffer for string + string (kNoBuf: none)
+    OP_SUB, OP_MUL, OP_DIV, OP_MOD, OP_AXOR,
     OP_LT, OP_LE, OP_GT, OP_GE, OP_EQ, OP_NE, OP_CONTAINS,
     OP_AND, OP_OR, OP_LXOR,
-    OP_FUNC,           // a = function id, b = argc
+    OP_FUNC,           // a = function id, b = argc, mode = builder buffer (kNoBuf: none)
 };
 
 enum Func : int32_t {
     F_ABS = 0, F_FLOOR, F_CEIL, F_ROUND, F_SQRT, F_CBRT, F_EXP, F_EXP2, F_LOG, F_LOG2, F_LOG10,
     F_SIN, F_ASIN, F_COS, F_ACOS, F_TAN, F_ATAN, F_HYPOT, F_POW, F_STRCASECMP, F_LENGTH, F_HASH,
     F_UDF_IS_IN,
+    // strings (FunctionManager.cpp:197-301): views of their argument
+    F_TRIM, F_LTRIM, F_RTRIM, F_LEFT, F_RIGHT, F_SUBSTR,
+    // ... and builders (Insn::mode = the evaluation buffer they write)
+    F_LOWER, F_UPPER, F_LPAD, F_RPAD,
 };
 
 struct Insn {
@@ -97,5 +105,18 @@ struct Insn {
     int64_t imm;
 };
 static_assert(sizeof(Insn) == 24, "Insn layout");
+
+#ifndef __HIPCC_RTC__
+// how many builder buffers (Insn::mode) the program's evaluation needs: a YIELD column whose program
+// uses any stores its built strings in the result string arena (FinalArgs::strOut)
+inline int strBuffersOf(const Insn* code) {
+    int n = 0;
+    for (const Insn* in = code; in->op != OP_END; in++) {
+        const bool builder = (in->op == OP_CAST && in->t1 == 1) || in->op == OP_ADD || in->op == OP_FUNC;
+        if (builder && in->mode < kMaxStrBuilds && in->mode + 1 > n) n = in->mode + 1;
+    }
+    return n;
+}
+#endif
 
 }  // namespace ngx

@@ -95,6 +95,7 @@ struct HostGraph {
     uint64_t vglobal = 0;               // rows over all shards
     std::vector<uint64_t> shardBase;    // world + 1
     uint64_t edges = 0;
+    uint64_t commitDigest = 0;          // digest of every shard's vertex table at commit (the commit set)
 };
 
 struct StagedRows {
@@ -137,6 +138,9 @@ inline int32_t idHash(int64_t vid, int32_t numParts) {        // ID_HASH (src/co
 Error exportSnapshot(Space& sp, int32_t rank, int32_t world, HostGraph& out);
 // snapshot.cpp: device snapshot files of a committed shard
 uint64_t schemaDigest(const Space& sp);
+// digest of the vertex tables of every shard, in rank order: equal on all ranks of one commit (the
+// global rows dgid / shardBase encode), different for tables of different commits
+uint64_t tablesDigest(const std::vector<std::vector<std::pair<int32_t, int64_t>>>& tables);
 Error writeSnapshotFile(const Space& sp, const HostGraph& g, int32_t rank, int32_t world, const std::string& path,
                         const std::string& tag);
 Error readSnapshotFile(const Space& sp, const std::string& path, int32_t rank, int32_t world, HostGraph& out,

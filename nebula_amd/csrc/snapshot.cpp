@@ -6,7 +6,9 @@
 //
 // Layout (little endian):
 //   header   magic "NGXSNAP\0", u32 format version, u32 reserved, i32 space, i32 num_parts, i32 rank,
-//            i32 world, u64 schema digest, char tag[64], u64 payload bytes, u64 payload hash, u64 reserved
+//            i32 world, u64 schema digest, char tag[64], u64 payload bytes, u64 payload hash,
+//            u64 commit digest (HostGraph::commitDigest: all shards' vertex tables; ngx_open_snapshot
+//            at world > 1 requires every rank's to agree)
 //   payload  the HostGraph fields in a fixed order; every array as [u64 count][count * sizeof(T)]
 // The payload hash (64-bit, 8 bytes a step) is checked before anything is replaced; the schema
 // digest covers every tag / edge schema version (names, types, TTL) registered for the space, so
@@ -22,7 +24,7 @@ namespace ngx {
 namespace {
 
 constexpr char kMagic[8] = {'N', 'G', 'X', 'S', 'N', 'A', 'P', '\0'};
-constexpr uint32_t kFormat = 1;
+constexpr uint32_t kFormat = 2;
 
 struct Header {
     char magic[8];
@@ -33,7 +35,7 @@ struct Header {
     char tag[64];
     uint64_t payloadBytes;
     uint64_t payloadHash;
-    uint64_t reserved2;
+    uint64_t commitDigest;
 };
 static_assert(sizeof(Header) == 128, "snapshot header layout");
 
@@ -208,32 +210,49 @@ bool getGraph(In& in, HostGraph& g) {
     return in.ok();
 }
 
-// structural checks of a decoded graph against itself (a bad file must not reach the kernels)
-bool consistent(const HostGraph& g) {
+// a column of n values: its arrays sized for n, string offsets 0-based and non-decreasing up to the bytes
+bool columnOk(const HostColumn& c, uint64_t n) {
+    if (!c.allValid && c.valid.size() != n) return false;
+    switch (c.type) {
+        case T_BOOL: return c.b.size() == n;
+        case T_FLOAT: case T_DOUBLE: return c.f64.size() == n;
+        case T_STRING: {
+            if (c.soff.size() != n + 1 || c.soff[0] != 0 || c.soff[n] != c.sbytes.size()) return false;
+            for (uint64_t i = 0; i < n; i++) if (c.soff[i] > c.soff[i + 1]) return false;
+            return true;
+        }
+        default: return c.i64.size() == n;
+    }
+}
+
+// structural checks of a decoded graph against itself and the space (a bad file must not reach the
+// kernels): array sizes, monotonic offsets, parts in range, the vertex table sorted by (part, vid) (the
+// seed lookup's binary search and index), destination rows inside the global table, shard bases
+bool consistent(const HostGraph& g, int32_t numParts, int32_t rank, int32_t world) {
     const uint64_t V = g.vid.size();
     if (g.vpart.size() != V || g.vglobal < V || g.gbase + V > g.vglobal) return false;
+    for (uint64_t r = 0; r < V; r++) {
+        if (numParts > 0 && (g.vpart[r] < 1 || g.vpart[r] > numParts)) return false;
+        if (r && !(g.vpart[r - 1] < g.vpart[r] || (g.vpart[r - 1] == g.vpart[r] && g.vid[r - 1] < g.vid[r]))) return false;
+    }
+    if (!g.shardBase.empty()) {
+        if (g.shardBase.size() != static_cast<size_t>(world) + 1 || g.shardBase[0] != 0) return false;
+        for (int32_t w = 0; w < world; w++) if (g.shardBase[w] > g.shardBase[w + 1]) return false;
+        if (g.gbase != g.shardBase[rank] || g.shardBase[rank + 1] - g.shardBase[rank] != V ||
+            g.vglobal != g.shardBase[world]) return false;
+    }
     for (const HostSlot& s : g.slots) {
-        if (s.off.size() != V + 1 || s.off.front() != 0) return false;
-        const uint64_t E = s.off.back();
+        if (s.off.size() != V + 1 || s.off[0] != 0) return false;
+        const uint64_t E = s.off[V];
         for (uint64_t r = 0; r < V; r++) if (s.off[r] > s.off[r + 1]) return false;
         if (s.dst.size() != E || s.rank.size() != E || s.dgid.size() != E) return false;
         if (s.anyFlags ? s.eflags.size() != E : !s.eflags.empty() && s.eflags.size() != E) return false;
         for (uint32_t x : s.dgid) if (x != kNoRow && x >= g.vglobal) return false;
-        for (const HostColumn& c : s.cols) {
-            const uint64_t n = c.type == T_BOOL ? c.b.size() : c.type == T_FLOAT || c.type == T_DOUBLE ? c.f64.size()
-                             : c.type == T_STRING ? (c.soff.empty() ? 0 : c.soff.size() - 1) : c.i64.size();
-            if (n != E || (!c.allValid && c.valid.size() != E)) return false;
-            if (c.type == T_STRING && (c.soff.back() != c.sbytes.size())) return false;
-        }
+        for (const HostColumn& c : s.cols) if (!columnOk(c, E)) return false;
     }
     for (const HostTag& t : g.tags) {
         if (t.present.size() != V) return false;
-        for (const HostColumn& c : t.cols) {
-            const uint64_t n = c.type == T_BOOL ? c.b.size() : c.type == T_FLOAT || c.type == T_DOUBLE ? c.f64.size()
-                             : c.type == T_STRING ? (c.soff.empty() ? 0 : c.soff.size() - 1) : c.i64.size();
-            if (n != V || (!c.allValid && c.valid.size() != V)) return false;
-            if (c.type == T_STRING && (c.soff.back() != c.sbytes.size())) return false;
-        }
+        for (const HostColumn& c : t.cols) if (!columnOk(c, V)) return false;
     }
     return true;
 }
@@ -263,6 +282,16 @@ uint64_t schemaDigest(const Space& sp) {
     return h.done();
 }
 
+uint64_t tablesDigest(const std::vector<std::vector<std::pair<int32_t, int64_t>>>& tables) {
+    StreamHash h;
+    for (auto& t : tables) {
+        uint64_t n = t.size();
+        h.add(&n, 8);
+        for (auto& pv : t) { h.add(&pv.first, 4); h.add(&pv.second, 8); }
+    }
+    return h.done();
+}
+
 Error writeSnapshotFile(const Space& sp, const HostGraph& g, int32_t rank, int32_t world, const std::string& path,
                         const std::string& tag) {
     if (tag.size() > 63) return Error{NGX_E_BAD_ARGUMENT, "snapshot tag longer than 63 bytes"};
@@ -279,6 +308,7 @@ Error writeSnapshotFile(const Space& sp, const HostGraph& g, int32_t rank, int32
     h.rank = rank;
     h.world = world;
     h.schemaDigest = schemaDigest(sp);
+    h.commitDigest = g.commitDigest;
     std::memcpy(h.tag, tag.data(), tag.size());
     bool ok = std::fwrite(&h, sizeof(h), 1, f.get()) == 1;
     Out o(f.get());
@@ -314,7 +344,8 @@ Error readSnapshotFile(const Space& sp, const std::string& path, int32_t rank, i
     const bool parsed = getGraph(in, g);
     if (!parsed || !in.ok() || in.left() != 0 || in.hash() != h.payloadHash)
         return Error{NGX_E_SNAPSHOT, path + ": snapshot payload corrupt"};
-    if (!consistent(g)) return Error{NGX_E_SNAPSHOT, path + ": snapshot arrays inconsistent"};
+    if (!consistent(g, sp.numParts, rank, world)) return Error{NGX_E_SNAPSHOT, path + ": snapshot arrays inconsistent"};
+    g.commitDigest = h.commitDigest;
     h.tag[63] = '\0';
     tag = h.tag;
     out = std::move(g);

@@ -303,11 +303,109 @@ __device__ __forceinline__ Val opNeg(Val v) {              // UnaryExpression NE
     return mkErr();
 }
 __device__ __forceinline__ Val opNot(Val v) { return v.t == V_ERR ? v : mkBool(!asBool(v)); }
+// ------------------------------------------------------------------------------ strings
+// Strings are (pointer, length) views: into a column's bytes, the program's literal pool, or one
+// kStrBuildBytes buffer of the evaluation that a builder (lower, upper, lpad, rpad, string +,
+// (string)) wrote (the compiler gives every builder its own buffer, Insn::mode). A result longer
+// than a buffer is a host-only construct (env.unsupported: the query returns NGX_E_UNSUPPORTED and
+// the caller runs its CPU path), never a truncated string. Bytes are read through flat pointers, so a
+// view of a private buffer reads like one of a column.
+__device__ __forceinline__ Val mkStr(const char* p, uint32_t n) { return Val{reinterpret_cast<int64_t>(p), n, V_STR}; }
+__device__ __forceinline__ const char* strPtr(const Val& v) { return reinterpret_cast<const char*>(v.x); }
+__device__ __forceinline__ Val hostOnly(const VmEnv& env) { atomicOr(env.unsupported, 1u); return mkErr(); }
+__device__ __forceinline__ bool isSpaceC(char c) { return c == ' ' || (c >= '\t' && c <= '\r'); }
+__device__ __forceinline__ bool isDigitC(char c) { return c >= '0' && c <= '9'; }
+
+// folly::to<int64_t>(string) as the oracle restates it (orc_expr.cpp toInt: strtoll base 10, the
+// whole C string consumed, no ERANGE): leading white space, one sign, digits, then the end or a NUL
+__device__ __forceinline__ Val strToInt(const Val& v) {
+    const char* p = strPtr(v);
+    const uint32_t n = v.len;
+    uint32_t k = 0;
+    while (k < n && isSpaceC(p[k])) k++;
+    bool neg = false;
+    if (k < n && (p[k] == '+' || p[k] == '-')) neg = p[k++] == '-';
+    if (k >= n || !isDigitC(p[k])) return mkErr();
+    const uint64_t limit = neg ? (1ULL << 63) : (1ULL << 63) - 1;
+    uint64_t acc = 0;
+    bool range = false;
+    for (; k < n && isDigitC(p[k]); k++) {
+        const uint64_t d = static_cast<uint64_t>(p[k] - '0');
+        if (acc > (limit - d) / 10) range = true;
+        else acc = acc * 10 + d;
+    }
+    if (range || (k < n && p[k] != '\0')) return mkErr();
+    return mkInt(neg ? static_cast<int64_t>(0ULL - acc) : static_cast<int64_t>(acc));
+}
+
+// folly::to<double>(string) (orc_expr.cpp toDouble: strtod, the whole C string consumed) for the
+// decimal forms strtod rounds with one IEEE operation (Clinger's fast path: at most 19 significant
+// digits, a mantissa <= 2^53 and a power of ten <= 1e22, all exact as doubles; or an integer mantissa
+// of up to 19 digits, converted once). Hex floats, inf / nan,
+// longer mantissas and larger exponents need strtod's big-number rounding: host-only constructs.
+__device__ __forceinline__ Val strToDouble(const Val& v, const VmEnv& env) {
+    const char* p = strPtr(v);
+    const uint32_t n = v.len;
+    uint32_t k = 0;
+    while (k < n && isSpaceC(p[k])) k++;
+    bool neg = false;
+    if (k < n && (p[k] == '+' || p[k] == '-')) neg = p[k++] == '-';
+    if (k < n && !isDigitC(p[k]) && p[k] != '.') {
+        const char c = p[k] | 0x20;
+        return (c == 'i' || c == 'n') ? hostOnly(env) : mkErr();        // inf / nan: strtod's spellings
+    }
+    uint64_t m = 0;
+    int sig = 0, exp10 = 0;
+    bool digits = false;
+    if (k + 1 < n && p[k] == '0' && (p[k + 1] | 0x20) == 'x') return hostOnly(env);
+    for (; k < n && isDigitC(p[k]); k++) {
+        digits = true;
+        if (m == 0 && p[k] == '0') continue;
+        if (sig < 19) { m = m * 10 + static_cast<uint64_t>(p[k] - '0'); sig++; }
+        else { if (p[k] != '0') return hostOnly(env); exp10++; }
+    }
+    if (k < n && p[k] == '.') {
+        k++;
+        for (; k < n && isDigitC(p[k]); k++) {
+            digits = true;
+            if (m == 0 && p[k] == '0') { exp10--; continue; }
+            if (sig < 19) { m = m * 10 + static_cast<uint64_t>(p[k] - '0'); sig++; exp10--; }
+            else if (p[k] != '0') return hostOnly(env);
+        }
+    }
+    if (!digits) return mkErr();
+    if (k < n && (p[k] | 0x20) == 'e') {                 // an exponent only with at least one digit
+        uint32_t j = k + 1;
+        bool eneg = false;
+        if (j < n && (p[j] == '+' || p[j] == '-')) eneg = p[j++] == '-';
+        if (j < n && isDigitC(p[j])) {
+            int64_t e = 0;
+            for (; j < n && isDigitC(p[j]); j++) if (e < 100000) e = e * 10 + (p[j] - '0');
+            exp10 += static_cast<int>(eneg ? -e : e);
+            k = j;
+        }
+    }
+    if (k < n && p[k] != '\0') return mkErr();
+    double d;
+    if (m == 0) {
+        d = 0.0;
+    } else if (exp10 == 0) {
+        d = static_cast<double>(m);                     // one correctly rounded conversion
+    } else {
+        if (m > (1ULL << 53) || exp10 > 22 || exp10 < -22) return hostOnly(env);
+        double pw = 1.0;
+        for (int i = 0; i < (exp10 < 0 ? -exp10 : exp10); i++) pw *= 10.0;   // 10^k, k <= 22: exact
+        d = exp10 < 0 ? static_cast<double>(m) / pw : static_cast<double>(m) * pw;
+    }
+    return mkDbl(neg ? -d : d);
+}
+
 // TypeCastingExpression::eval; t1 = ColumnType (INT 0, STRING 1, DOUBLE 2, BOOL 3, TIMESTAMP 4)
 __device__ __forceinline__ Val opCast(Val v, uint8_t t1, const VmEnv& env) {
     if (v.t == V_ERR) return v;
-    if (v.t == V_STR) {                                    // folly::to<int/double>(string): host only
-        if (t1 != 3) { atomicOr(env.unsupported, 1u); return mkErr(); }
+    if (v.t == V_STR) {
+        if (t1 == 0 || t1 == 4) return strToInt(v);
+        if (t1 == 2) return strToDouble(v, env);
         return mkBool(asBool(v));
     }
     if (t1 == 0 || t1 == 4) return mkInt(toInt(v));
@@ -315,13 +413,12 @@ __device__ __forceinline__ Val opCast(Val v, uint8_t t1, const VmEnv& env) {
     return mkBool(asBool(v));
 }
 
-// (string) cast, Expression::toString (Expressions.h:334-348), into a 24-byte buffer of the
-// evaluation (the caller's private memory: a WHERE / pushed filter consumes the string before the
-// program returns; a YIELD whose value is such a string is refused at compile time). int64 prints as
-// folly::to<std::string> (decimal, '-' sign), bool as "true" / "false"; a double needs folly's
-// shortest round-trip form: host only.
+// (string) cast, Expression::toString (Expressions.h:334-348), into the cast's builder buffer.
+// int64 prints as folly::to<std::string> (decimal, '-' sign), bool as "true" / "false"; a double needs
+// folly's shortest round-trip form: host only.
 __device__ __forceinline__ Val castToString(Val v, char* buf, const VmEnv& env) {
     if (v.t == V_ERR || v.t == V_STR) return v;
+    if (buf == nullptr) return hostOnly(env);
     uint32_t n = 0;
     if (v.t == V_BOOL) {
         const char* w = v.x ? "true" : "false";
@@ -337,14 +434,25 @@ __device__ __forceinline__ Val castToString(Val v, char* buf, const VmEnv& env) 
         }
         n += digits;
     } else {
-        atomicOr(env.unsupported, 1u);
-        return mkErr();
+        return hostOnly(env);
     }
-    return Val{reinterpret_cast<int64_t>(buf), n, V_STR};
+    return mkStr(buf, n);
+}
+
+// a YIELD value that is a view of the evaluation's builder buffers [lo, lo + bytes): copied to the
+// row's slot of the result string arena (out), which outlives the evaluation
+__device__ __forceinline__ Val copyOut(Val v, char* out, const char* lo, uint64_t bytes) {
+    if (out == nullptr || v.t != V_STR || v.len == 0) return v;
+    const uint64_t x = static_cast<uint64_t>(v.x), b = reinterpret_cast<uint64_t>(lo);
+    if (x < b || x >= b + bytes) return v;
+    const char* p = strPtr(v);
+    for (uint32_t k = 0; k < v.len; k++) out[k] = p[k];
+    v.x = reinterpret_cast<int64_t>(out);
+    return v;
 }
 
 // ------------------------------------------------------------------------------ arithmetic
-__device__ __forceinline__ Val opArith(uint8_t op, Val l, Val r, const VmEnv& env) {
+__device__ __forceinline__ Val opArith(uint8_t op, Val l, Val r, const VmEnv& env, char* buf = nullptr) {
     if (l.t == V_ERR) return l;
     if (r.t == V_ERR) return r;
     if ((l.t == V_INT || l.t == V_DBL) && (r.t == V_INT || r.t == V_DBL)) {
@@ -378,7 +486,14 @@ __device__ __forceinline__ Val opArith(uint8_t op, Val l, Val r, const VmEnv& en
             default: return mkInt(a ^ b);
         }
     }
-    if (op == OP_ADD && l.t == V_STR && r.t == V_STR) atomicOr(env.unsupported, 1u);   // builds a string
+    if (op == OP_ADD && l.t == V_STR && r.t == V_STR) {                // concatenation (Expressions.cpp:936)
+        if (buf == nullptr || l.len + r.len > static_cast<uint32_t>(kStrBuildBytes)) return hostOnly(env);
+        const char* p = strPtr(l);
+        const char* q = strPtr(r);
+        for (uint32_t k = 0; k < l.len; k++) buf[k] = p[k];
+        for (uint32_t k = 0; k < r.len; k++) buf[l.len + k] = q[k];
+        return mkStr(buf, l.len + r.len);
+    }
     return mkErr();
 }
 
@@ -419,7 +534,7 @@ __device__ __forceinline__ Val opLogic(uint8_t op, Val l, Val r) {
 }
 
 // ------------------------------------------------------------------------------ functions
-__device__ __forceinline__ Val opFunc(int32_t fid, const Val* args, int argc, const VmEnv& env) {
+__device__ __forceinline__ Val opFunc(int32_t fid, const Val* args, int argc, const VmEnv& env, char* buf = nullptr) {
     for (int k = 0; k < argc; k++) if (args[k].t == V_ERR) return args[k];
     bool num1 = args[0].t == V_INT || args[0].t == V_DBL;
     switch (fid) {
@@ -447,6 +562,68 @@ __device__ __forceinline__ Val opFunc(int32_t fid, const Val* args, int argc, co
             return mkDbl(fid == F_HYPOT ? hypot(a, b) : pow(a, b));
         }
         case F_LENGTH: return args[0].t == V_STR ? mkInt(args[0].len) : mkErr();
+        // FunctionManager.cpp:197-301 (std::tolower / toupper in the C locale, trims of ' ' only)
+        case F_LOWER: case F_UPPER: {
+            if (args[0].t != V_STR) return mkErr();
+            const uint32_t n = args[0].len;
+            if (buf == nullptr || n > static_cast<uint32_t>(kStrBuildBytes)) return hostOnly(env);
+            const char* p = strPtr(args[0]);
+            const char lo = fid == F_LOWER ? 'A' : 'a';
+            for (uint32_t k = 0; k < n; k++) {
+                const char ch = p[k];
+                buf[k] = (ch >= lo && ch <= lo + 25) ? static_cast<char>(ch ^ 0x20) : ch;
+            }
+            return mkStr(buf, n);
+        }
+        case F_TRIM: case F_LTRIM: case F_RTRIM: {
+            if (args[0].t != V_STR) return mkErr();
+            const char* p = strPtr(args[0]);
+            uint32_t b = 0, e = args[0].len;
+            if (fid != F_RTRIM) while (b < e && p[b] == ' ') b++;
+            if (fid != F_LTRIM) while (e > b && p[e - 1] == ' ') e--;
+            return mkStr(p + b, e - b);
+        }
+        case F_LEFT: case F_RIGHT: {
+            if (args[0].t != V_STR || args[1].t != V_INT) return mkErr();
+            const char* p = strPtr(args[0]);
+            const uint32_t n = args[0].len;
+            const int64_t k = args[1].x;
+            if (k <= 0) return mkStr(p, 0);
+            const uint32_t m = k < static_cast<int64_t>(n) ? static_cast<uint32_t>(k) : n;
+            return fid == F_LEFT ? mkStr(p, m) : mkStr(p + (n - m), m);
+        }
+        case F_SUBSTR: {
+            if (args[0].t != V_STR || args[1].t != V_INT || args[2].t != V_INT) return mkErr();
+            const char* p = strPtr(args[0]);
+            const uint64_t n = args[0].len;
+            const int64_t start = args[1].x, len = args[2].x;
+            // |start| > size (llabs(INT64_MIN) stays negative: a huge size_t), len <= 0 or start 0: ""
+            const uint64_t mag = start < 0 ? 0ULL - static_cast<uint64_t>(start) : static_cast<uint64_t>(start);
+            if (mag > n || len <= 0 || start == 0) return mkStr(p, 0);
+            const uint64_t pos = start > 0 ? static_cast<uint64_t>(start - 1) : n - mag;
+            const uint64_t cnt = static_cast<uint64_t>(len) < n - pos ? static_cast<uint64_t>(len) : n - pos;
+            return mkStr(p + pos, static_cast<uint32_t>(cnt));
+        }
+        case F_LPAD: case F_RPAD: {
+            if (args[0].t != V_STR || args[1].t != V_INT) return mkErr();
+            const char* p = strPtr(args[0]);
+            const uint64_t n = args[0].len;
+            const uint64_t size = static_cast<uint64_t>(args[1].x);         // static_cast<size_t>
+            if (size == 0) return mkStr(p, 0);
+            if (size < n) return mkStr(p, static_cast<uint32_t>(size));     // substr(0, size)
+            if (args[2].t != V_STR) return mkErr();                         // the pad is read only here
+            if (size == n) return args[0];
+            const uint32_t xl = args[2].len;
+            // an empty pad never reaches `size` (the reference loops): host-only like an oversize one
+            if (xl == 0 || buf == nullptr || size > static_cast<uint64_t>(kStrBuildBytes)) return hostOnly(env);
+            const char* x = strPtr(args[2]);
+            const uint32_t pad = static_cast<uint32_t>(size - n);
+            char* at = buf;
+            if (fid == F_RPAD) { for (uint32_t k = 0; k < n; k++) *at++ = p[k]; }
+            for (uint32_t k = 0, j = 0; k < pad; k++, j = (j + 1 == xl ? 0 : j + 1)) *at++ = x[j];
+            if (fid == F_LPAD) { for (uint32_t k = 0; k < n; k++) *at++ = p[k]; }
+            return mkStr(buf, static_cast<uint32_t>(size));
+        }
         case F_STRCASECMP: {
             if (!(args[0].t == V_STR && args[1].t == V_STR)) return mkErr();
             const unsigned char* p = reinterpret_cast<const unsigned char*>(args[0].x);     // C strings: stop at NUL
@@ -493,14 +670,15 @@ __device__ __forceinline__ Val opFunc(int32_t fid, const Val* args, int argc, co
 }
 
 // ------------------------------------------------------------------------------ interpreter
-static __device__ __noinline__ Val vmEval(const Insn* code, const VmEnv& env, const EdgeCtx& ec) {
+static __device__ __noinline__ Val vmEval(const Insn* code, const VmEnv& env, const EdgeCtx& ec, char* sout = nullptr) {
     Val st[kMaxStack];
-    char sbuf[kMaxStrCasts][kStrCastBytes];
-    int sp = 0, nsb = 0;
+    char sbuf[kMaxStrBuilds][kStrBuildBytes];
+    auto bufOf = [&](uint8_t m) -> char* { return m < kMaxStrBuilds ? sbuf[m] : nullptr; };
+    int sp = 0;
     for (int pc = 0;; pc++) {
         const Insn in = code[pc];
         switch (in.op) {
-            case OP_END: return sp > 0 ? st[sp - 1] : mkErr();
+            case OP_END: return copyOut(sp > 0 ? st[sp - 1] : mkErr(), sout, &sbuf[0][0], sizeof(sbuf));
             case OP_PUSH: st[sp++] = constVal(in.t1, in.imm, static_cast<uint32_t>(in.a), env.pool); break;
             case OP_ERR: st[sp++] = mkErr(); break;
             case OP_ECOL: st[sp++] = opEcol(env, ec, in.a, in.b, in.mode, constVal(in.t2, in.imm, 0, env.pool)); break;
@@ -514,10 +692,12 @@ static __device__ __noinline__ Val vmEval(const Insn* code, const VmEnv& env, co
             case OP_NEG: st[sp - 1] = opNeg(st[sp - 1]); break;
             case OP_NOT: st[sp - 1] = opNot(st[sp - 1]); break;
             case OP_CAST:
-                if (in.t1 == 1) st[sp - 1] = nsb < kMaxStrCasts ? castToString(st[sp - 1], sbuf[nsb++], env) : mkErr();
+                if (in.t1 == 1) st[sp - 1] = castToString(st[sp - 1], bufOf(in.mode), env);
                 else st[sp - 1] = opCast(st[sp - 1], in.t1, env);
                 break;
-            case OP_ADD: case OP_SUB: case OP_MUL: case OP_DIV: case OP_MOD: case OP_AXOR:
+            case OP_ADD:
+                sp--; st[sp - 1] = opArith(in.op, st[sp - 1], st[sp], env, bufOf(in.mode)); break;
+            case OP_SUB: case OP_MUL: case OP_DIV: case OP_MOD: case OP_AXOR:
                 sp--; st[sp - 1] = opArith(in.op, st[sp - 1], st[sp], env); break;
             case OP_LT: case OP_LE: case OP_GT: case OP_GE: case OP_EQ: case OP_NE: case OP_CONTAINS:
                 sp--; st[sp - 1] = opRel(in.op, st[sp - 1], st[sp]); break;
@@ -525,7 +705,7 @@ static __device__ __noinline__ Val vmEval(const Insn* code, const VmEnv& env, co
                 sp--; st[sp - 1] = opLogic(in.op, st[sp - 1], st[sp]); break;
             case OP_FUNC: {
                 int argc = in.b;
-                Val out = opFunc(in.a, &st[sp - argc], argc, env);
+                Val out = opFunc(in.a, &st[sp - argc], argc, env, bufOf(in.mode));
                 sp -= argc;
                 st[sp++] = out;
                 break;

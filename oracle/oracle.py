@@ -134,6 +134,41 @@ def _s(s: str) -> bytes:
 
 
 # ---------------------------------------------------------------------------- expressions
+
+def go_request(s, pushdown=True, rows=True, digest=False, input=None) -> bytes:
+    """The orc_go request blob of a parsed GoSentence (also fed to the sanitizer driver, tools/san)."""
+    b = struct.pack("<IIi", s.record_from, s.record_to, len(s.vids)) + struct.pack(f"<{len(s.vids)}q", *s.vids)
+    b += struct.pack("<i", len(s.over))
+    for n, a in s.over:
+        b += _s(n) + _s(a)
+    b += struct.pack("<Bi", 1 if s.over_all else 0, s.direction)
+    b += struct.pack("<B", 1 if s.where is not None else 0) + _s(s.where.encode() if s.where is not None else b"")
+    b += struct.pack("<Bi", 1 if s.distinct else 0, len(s.yields))
+    for y in s.yields:
+        b += _s(y.expr.encode()) + _s(y.alias)
+    b += struct.pack("<BB", 1 if pushdown else 0, 2 if digest else (0 if rows else 1))
+    ft = getattr(s, "from_type", 0)
+    b += struct.pack("<B", ft) + _s(getattr(s, "from_var", "")) + _s(getattr(s, "from_col", ""))
+    names = input.names if (ft and input is not None) else []
+    types = input.types if (ft and input is not None) else []
+    rws = input.rows if (ft and input is not None) else []
+    b += struct.pack("<i", len(names))
+    for i, n in enumerate(names):
+        b += _s(n) + struct.pack("<i", types[i] if i < len(types) else 0)
+    b += struct.pack("<q", len(rws))
+    for row in rws:
+        for kind, v in row:
+            if kind == "str":
+                b += struct.pack("<B", 3) + _s(v.encode("utf-8", "surrogateescape"))
+            elif kind in ("float", "double"):
+                b += struct.pack("<Bd", 1, v)
+            elif kind == "bool" or (kind == "empty" and v is not None):
+                b += struct.pack("<BB", 2, 1 if v else 0)
+            else:
+                b += struct.pack("<Bq", 0, int(v))
+    return b
+
+
 def expr_eval(enc: bytes):
     """Evaluate a constant encoded expression. Returns ('ok', value) | ('err', msg) | ('prep', msg)."""
     r = _Rd(_call(lib().orc_expr_eval, enc, len(enc)))
@@ -360,35 +395,7 @@ class Oracle:
     def go(self, space: int, s, pushdown=True, rows=True, digest=False, input=None) -> GoResult:
         """Run a parsed nebula_amd.ngql.GoSentence through the restated GoExecutor. digest=True
         returns the rows as sorted 128-bit digests of their serialized cells (digest_columns())."""
-        b = struct.pack("<IIi", s.record_from, s.record_to, len(s.vids)) + struct.pack(f"<{len(s.vids)}q", *s.vids)
-        b += struct.pack("<i", len(s.over))
-        for n, a in s.over:
-            b += _s(n) + _s(a)
-        b += struct.pack("<Bi", 1 if s.over_all else 0, s.direction)
-        b += struct.pack("<B", 1 if s.where is not None else 0) + _s(s.where.encode() if s.where is not None else b"")
-        b += struct.pack("<Bi", 1 if s.distinct else 0, len(s.yields))
-        for y in s.yields:
-            b += _s(y.expr.encode()) + _s(y.alias)
-        b += struct.pack("<BB", 1 if pushdown else 0, 2 if digest else (0 if rows else 1))
-        ft = getattr(s, "from_type", 0)
-        b += struct.pack("<B", ft) + _s(getattr(s, "from_var", "")) + _s(getattr(s, "from_col", ""))
-        names = input.names if (ft and input is not None) else []
-        types = input.types if (ft and input is not None) else []
-        rws = input.rows if (ft and input is not None) else []
-        b += struct.pack("<i", len(names))
-        for i, n in enumerate(names):
-            b += _s(n) + struct.pack("<i", types[i] if i < len(types) else 0)
-        b += struct.pack("<q", len(rws))
-        for row in rws:
-            for kind, v in row:
-                if kind == "str":
-                    b += struct.pack("<B", 3) + _s(v.encode("utf-8", "surrogateescape"))
-                elif kind in ("float", "double"):
-                    b += struct.pack("<Bd", 1, v)
-                elif kind == "bool" or (kind == "empty" and v is not None):
-                    b += struct.pack("<BB", 2, 1 if v else 0)
-                else:
-                    b += struct.pack("<Bq", 0, int(v))
+        b = go_request(s, pushdown, rows, digest, input)
         r = _Rd(_call(self.L.orc_go, self.h, space, b, len(b)))
         ok = r.get("B") == 1
         err = r.str().decode()

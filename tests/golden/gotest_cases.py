@@ -323,9 +323,7 @@ CASES = [
 ]
 
 # Pipes and variables (GoTest.cpp): `names' is verifyColNames' list when the test checks it.
-# Not transcribed: GoTest.cpp:146 (`A | (B | C)' from Boris Diaw expects 4 rows, while the same
-# nesting at :667 / :688 and the flat pipe at :120 give the 7 rows the PipeExecutor / back-tracker
-# semantics produce; the executor sources show no path to 4 rows), :3095 and :55 (YIELD sentences).
+# Not transcribed: GoTest.cpp:3095 and :55 (YIELD sentences, another executor).
 _SPURS7 = [("T:Spurs",)] * 5 + [("T:Hornets",), ("T:Trail Blazers",)]
 _REF_PIPE = [("Tim Duncan", "Manu Ginobili", "Tim Duncan"), ("Tim Duncan", "Tony Parker", "LaMarcus Aldridge"),
              ("Tim Duncan", "Tony Parker", "Manu Ginobili"), ("Tim Duncan", "Tony Parker", "Tim Duncan"),
@@ -376,6 +374,8 @@ PIPE_CASES = [
                          "YIELD like._dst as id | GO FROM $-.id OVER serve", empty=True),
     dict(line=414, query="GO FROM {P:Nobody} OVER like YIELD like._dst as id | (GO FROM $-.id OVER like "
                          "YIELD like._dst as id | GO FROM $-.id OVER serve)", empty=True),
+    dict(line=141, query="GO FROM {P:Boris Diaw} OVER like YIELD like._dst as id | ( GO FROM $-.id OVER like "
+                         "YIELD like._dst as id | GO FROM $-.id OVER serve )", names=["serve._dst"], rows=_SPURS7),
     dict(line=665, query="GO FROM {P:Boris Diaw} OVER like, serve YIELD like._dst as id | ( GO FROM $-.id OVER "
                          "like YIELD like._dst as id | GO FROM $-.id OVER serve )", rows=_SPURS7),
     dict(line=686, query="GO FROM {P:Boris Diaw} OVER * YIELD like._dst as id | ( GO FROM $-.id OVER like "

@@ -58,3 +58,34 @@ def test_many_shapes_queued(nba):
         r = e.go(ds.space, q)
         assert r.ok and e.jit_note() != "jit: compiling"
         assert fixtures.normalize_cells(r.rows) == ([] if c.get("empty") else fixtures.nba_expected(c["rows"]))
+
+
+@pytest.mark.parametrize("async_", [0, 1])
+def test_capacity_one_keeps_the_query_s_kernels(async_):
+    """jit_cache_capacity 1 with an M TO N query whose WHERE is pushed: the query needs two modules (the
+    final hop with the pushed filter and the earlier record hops without it), so fetching the second
+    evicts the first while the query still holds it. The evicted module is retired, not unloaded, until
+    the next query: rows equal the oracle's, query after query."""
+    ds = fixtures.nba()
+    o = oracle.Oracle()
+    ds.load_oracle(o)
+    with engine.Engine(0) as e:
+        ds.load_engine(e)
+        e.set_flag("jit", 1)
+        e.set_flag("jit_async", async_)
+        e.set_flag("jit_cache_capacity", 1)
+        qs = ["GO 1 TO 3 STEPS FROM {P:Tim Duncan} OVER like WHERE like.likeness > 80 YIELD like._dst, like.likeness",
+              "GO 2 TO 3 STEPS FROM {P:Tony Parker} OVER like WHERE like.likeness >= 90 YIELD like._dst",
+              "GO 1 TO 2 STEPS FROM {P:Tim Duncan}, {P:LeBron James} OVER like, serve WHERE serve.start_year > 2005 "
+              "YIELD serve._dst, like._dst"]
+        for rnd in range(3):
+            for text in qs:
+                s = ngql.parse_go(fixtures.nba_query(text))
+                ref = o.go(ds.space, s)
+                got = e.go(ds.space, s)
+                assert got.ok == ref.ok, (text, got.error, ref.error)
+                assert fixtures.normalize_cells(got.rows) == fixtures.normalize_cells(ref.rows), (rnd, text)
+            if async_:
+                e.set_flag("jit_wait", 1)
+        assert e.get_flag("jit_cached") <= 1
+        assert e.get_flag("jit_evicted") >= 2
