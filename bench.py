@@ -3,7 +3,8 @@ e._rank, e.p0, e.p1` on an RMAT graph (BASELINE.json metric).
 
 Workload by GPU count (one process per GPU, parts hashed to GPUs as part % N, Nebula's pickHosts):
   N = 1  configs[1] (C2): RMAT scale 22, edge factor 16, 100 parts
-  N = 8  configs[2] (C3): RMAT scale 26, edge factor 16, 100 parts, per-hop frontier all-to-all (RCCL)
+  N = 8  configs[2] (C3): RMAT scale 26, edge factor 16, 100 parts, per-hop frontier exchange (RCCL:
+         bitmap all-to-all after a push hop, bitmap all-gather before a pull hop)
   N = 2, 4: scale 22 + log2(N) (weak scaling between the two anchors); --scale overrides.
 
 One step = one GO query through libnebula_gn (seeds on host -> result rows and YIELD columns in HBM),
@@ -115,10 +116,10 @@ def main():
         log(f"[rank 0] libnebula_gn {build['raw']} (sources in tree: {build['tree_sha']}, "
             f"match={build['matches_tree']})")
     t0 = time.time()
-    # every out-edge also stored as its in-edge (-e), as InsertEdgeExecutor writes them;
-    # one shard only: the in-edge slot is what the pull hops read (world > 1 pushes, so the 8-GPU run
-    # keeps the out-edge layout and its host memory)
-    with_in = world == 1 and not args.out_only
+    # every out-edge also stored as its in-edge (-e), as InsertEdgeExecutor writes them,
+    # at every N: the in-edge slot is what the pull hops read (world > 1: against the all-gathered
+    # frontier bitmap), so N = 1 and N = 8 run the same direction-optimizing algorithm
+    with_in = not args.out_only
     rows = datagen.rmat(scale, args.ef, 42, args.parts, with_in=with_in, with_tag=False, rank=rank, world=world,
                         threads=args.threads)
     log(f"[rank {rank}] generated {rows.n} rows of RMAT scale {scale} in {time.time() - t0:.1f}s")
@@ -340,10 +341,13 @@ def cpu_baseline(rows, scale, args, gpu_edges_per_step):
     from nebula_amd import datagen, ngql
     from oracle import oracle
     model, nproc, usable = cpu_info()
-    threads = max(1, min(args.threads, usable))
+    # every core this process may use: the affinity set, capped by the host share the launcher grants
+    # (OMP_NUM_THREADS; 16 per GPU on the MI355X boxes, whose nproc counts the whole machine)
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = max(1, min(usable, share) if share > 0 else usable)
     t0 = time.time()
     o = oracle.Oracle()
-    o.set_flags(threads=threads, max_handlers=threads)
+    o.set_flags(threads=threads, max_handlers=threads, graph_threads=threads)
     o.add_space(datagen.RMAT_SPACE, args.parts)
     for is_edge, sid, name, fields in datagen.rmat_schemas():
         o.add_schema(datagen.RMAT_SPACE, is_edge, sid, name, fields)
@@ -363,6 +367,15 @@ def cpu_baseline(rows, scale, args, gpu_edges_per_step):
             break
         k *= 2
     k, edges, sec = best
+    # the reference's own shape of the same work: graphd's final evaluation on one thread
+    # (processFinalResult), storage on all of them; a quarter of the sample keeps the run short
+    o.set_flags(threads=threads, max_handlers=threads, graph_threads=1)
+    k1 = max(1, k // 4)
+    seeds = datagen.rmat_seeds(scale, k1, args.ef, 42, 42, threads=args.threads)
+    r1 = o.go(datagen.RMAT_SPACE, ngql.parse_go(QUERY.replace("{S}", ", ".join(str(int(v)) for v in seeds))),
+              rows=False)
+    serial = round(sum(r1.hop_scanned) / r1.seconds, 1)
+    log(f"oracle GO, one graphd thread: {k1} seeds, {sum(r1.hop_scanned)} edges, {r1.seconds:.2f}s")
     # storage-only, one thread: GetNeighbors over a sample of vertices, `_dst` + one prop, no filter
     o.set_flags(threads=1, max_handlers=1)
     vids = datagen.rmat_seeds(scale, 50000, args.ef, 42, 4343, threads=args.threads)
@@ -377,17 +390,22 @@ def cpu_baseline(rows, scale, args, gpu_edges_per_step):
         gn["edges"] = resp.total_edges
     o.close()
     return {"value": round(edges / sec, 1), "unit": "edges/s", "cores": threads, "kind": "port",
+            "per_thread": round(edges / sec / threads, 1),
             "sample": f"same graph and query, first {k} seed(s) of the seed sample: {edges} edges traversed "
                       f"({100.0 * edges / max(gpu_edges_per_step, 1):.0f}% of one GPU step) in {sec:.2f}s, "
-                      f"oracle C++ restatement on {threads} threads",
+                      f"oracle C++ restatement on {threads} threads (storage scan and final evaluation alike)",
+            "graphd_one_thread": {"value": serial, "seeds": k1,
+                                  "note": "the reference's shape: storage on all threads, graphd's "
+                                          "processFinalResult on one"},
             "cpu_model": model, "nproc": nproc, "usable_cpus": usable,
             "storage_get_neighbors_1thread": {
                 "edges_per_s_one_prop": gn["one_prop"], "edges_per_s_dst_only": gn["dst_only"],
                 "edges": gn["edges"],
                 "reference_published": "1.51e6 edges/s one prop, 5.28e6 _dst only, 1 thread, Xeon E5-2690 v2 "
                                        "(GetNeighborsBenchmark.cpp:390-403)"},
-            "note": "GO end to end is bounded by graphd's single-threaded processFinalResult (re-decode + "
-                    "WHERE + YIELD per returned edge, GoExecutor.cpp:1082-1335), not by the storage scan"}
+            "note": "value parallelises graphd's final evaluation too (rows kept in order), which the "
+                    "reference runs on one thread (GoExecutor.cpp:1082-1335): a more generous baseline "
+                    "than the reference's own shape (graphd_one_thread)"}
 
 
 if __name__ == "__main__":

@@ -220,6 +220,8 @@ typedef struct {
     const int32_t* tag_row_tag;
     const uint8_t* tag_props;
     const uint64_t* tag_props_off;    /* ntag_rows + 1 */
+    int64_t latency_in_us;            /* ResponseCommon.latency_in_us (BaseProcessor.h:51-60): the call's
+                                       * wall time on the host, entry to result */
 } ngx_gn_result;
 
 int32_t ngx_get_neighbors(ngx_ctx* ctx, const ngx_gn_request* req, ngx_gn_result** out);
@@ -335,6 +337,16 @@ typedef struct {
     double total_ms;
     uint64_t algo_bytes;               /* algorithmic bytes attributed to this kernel class */
 } ngx_kernel_stat;
+/* Service counters, named as the reference's stats::Stats registers them (src/common/stats/Stats.cpp:
+ * "<server>_<module>_qps" / "_error_qps" / "_latency", StorageServiceHandler.h:55 get_bound):
+ * storage_get_bound_qps (requests without failed parts), storage_get_bound_error_qps (the others),
+ * storage_get_bound_latency_us_sum / _count / _max (the latency histogram's inputs, in microseconds).
+ * Values since ngx_open; the array is valid until the next call on the context. */
+typedef struct {
+    const char* name;
+    int64_t value;
+} ngx_stat;
+int32_t ngx_stats(ngx_ctx* ctx, const ngx_stat** out, int32_t* n);
 int32_t ngx_set_profiling(ngx_ctx* ctx, int32_t on);
 int32_t ngx_kernel_stats(ngx_ctx* ctx, const ngx_kernel_stat** out, int32_t* n);
 

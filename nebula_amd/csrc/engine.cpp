@@ -126,6 +126,9 @@ struct ngx_ctx {
     DBuf oFlags, rowCols, rowLen, rowOff, rowBytes;     // GetNeighbors response rows (encode_rows)
     DBuf dkTable, dkKeep, dkPre, dSrc, dDst, dRank, dType;   // YIELD DISTINCT (table, marks, compacted rows)
     std::vector<DBuf> strArena;                         // result string arenas, one per record hop (FinalArgs::strOut)
+    DBuf localBits, pullGather;                         // world > 1 pull: this shard's frontier bitmap, all shards' 
+    struct { int64_t qps = 0, errorQps = 0, latencySum = 0, latencyCount = 0, latencyMax = 0; } gbStats;
+    std::vector<ngx_stat> statList;                     // ngx_stats view
     int64_t maxEdgesPerVertex = INT32_MAX;             // storaged FLAGS_max_edge_returned_per_vertex (GO hops)
     struct ColBuf { DBuf x, len, t; };
     struct PinBuf {                                     // page-locked host staging for result D2H
@@ -555,10 +558,7 @@ struct ColView {
     }
 };
 
-int hostThreads() {
-    unsigned n = std::thread::hardware_concurrency();
-    return static_cast<int>(std::max(1u, std::min(n, 16u)));
-}
+int hostThreads() { return hostThreadBudget(); }
 
 // f(lo, hi, t) over T contiguous row ranges on T threads (T = 0: hostThreads(), small n: one)
 template <typename F>
@@ -588,7 +588,8 @@ struct PairDigest {
     bool operator==(const PairDigest& o) const { return ok && o.ok && n == o.n && h1 == o.h1 && h2 == o.h2; }
 };
 
-PairDigest slotDigest(const HostSlot& s, bool transpose) {
+// gbase: the shard's first global row (dgid values are global rows), so digests of every shard add up
+PairDigest slotDigest(const HostSlot& s, bool transpose, uint64_t gbase = 0) {
     const uint64_t V = s.off.empty() ? 0 : s.off.size() - 1;
     const int T = V < (1u << 16) ? 1 : hostThreads();
     std::vector<PairDigest> part(T);
@@ -598,7 +599,7 @@ PairDigest slotDigest(const HostSlot& s, bool transpose) {
             for (uint64_t e = s.off[r]; e < s.off[r + 1]; e++) {
                 const uint64_t g = s.dgid[e];
                 if (g == kNoRow) { d.ok = false; continue; }
-                const uint64_t a = transpose ? g : r, b = transpose ? r : g;
+                const uint64_t a = transpose ? g : gbase + r, b = transpose ? gbase + r : g;
                 d.h1 += mixPair(a, b, 0x9E3779B97F4A7C15ULL);
                 d.h2 += mixPair(b, a, 0xD1B54A32D192ED03ULL);
                 d.n++;
@@ -618,7 +619,7 @@ PairDigest slotDigest(const HostSlot& s, bool transpose) {
 // over s (a frontier reached by expansion holds the hubs first, so most reached rows hit on their
 // first probe). Which in-neighbours are probed first changes nothing but the probe count: the pull
 // computes set membership.
-void buildPullHead(const HostGraph& g, int32_t s, int32_t m, DeviceGraph& d) {
+void buildPullHead(const HostGraph& g, int32_t s, int32_t m, DeviceGraph& d, const std::vector<uint32_t>* globalDeg = nullptr) {
     const HostSlot& out = g.slots[s];
     const HostSlot& in = g.slots[m];
     const uint64_t V = g.vid.size();
@@ -627,7 +628,11 @@ void buildPullHead(const HostGraph& g, int32_t s, int32_t m, DeviceGraph& d) {
     std::vector<uint8_t> nk(slices, 0);
     const uint64_t windows = (V + kPullWindow - 1) / kPullWindow;
     std::vector<uint64_t> longRows(hostThreads() + 1, 0);
-    auto outDeg = [&](uint32_t u) -> uint64_t { return u < V ? out.off[u + 1] - out.off[u] : 0; };
+    // in-neighbours are global rows: world 1 reads the out-degree here, world > 1 the gathered one
+    auto outDeg = [&](uint32_t u) -> uint64_t {
+        if (globalDeg) return u < globalDeg->size() ? (*globalDeg)[u] : 0;
+        return u < V ? out.off[u + 1] - out.off[u] : 0;
+    };
     parallelRows(windows, [&](uint64_t lo, uint64_t hi, int t) {
         std::vector<std::pair<uint32_t, uint32_t>> rows;        // (head length, row)
         std::vector<uint32_t> nb;
@@ -683,12 +688,67 @@ std::vector<int32_t> findMirrors(const HostGraph& g) {
     return m;
 }
 
-// mirror slots and, for every slot with one, its pull head image (world 1: one shard holds every row)
-void attachMirrors(ngx_ctx* c, const HostGraph& g, DeviceGraph& d) {
-    d.mirror = c->world == 1 ? findMirrors(g) : std::vector<int32_t>(g.slots.size(), -1);
+std::vector<uint8_t> gatherHost(ngx_ctx* c, const void* host, uint64_t bytes);
+template <typename T>
+std::vector<T> gatherRows(ngx_ctx* c, const HostGraph& g, const std::vector<T>& local);
+
+// world > 1: type t's in-edge slots mirror its out-edge slots over the whole graph when every shard
+// holds both slots and the digests of every shard's (src row, dst row) pairs, over global rows, add up
+// to the same multiset both ways. One all-gather of a fixed record per edge type of the schema, so
+// every shard takes the same decision (the pull's collectives run in lockstep).
+std::vector<int32_t> findMirrorsGlobal(ngx_ctx* c, const Space& sp, const HostGraph& g) {
+    std::vector<int32_t> m(g.slots.size(), -1);
+    std::vector<int32_t> types;
+    for (auto& e : sp.edges) types.push_back(e.first);
+    if (types.empty()) return m;
+    struct Rec { uint64_t have, ok, n1, a1, b1, n2, a2, b2; };
+    std::vector<Rec> mine(types.size(), Rec{0, 0, 0, 0, 0, 0, 0, 0});
+    std::vector<std::pair<int32_t, int32_t>> slotOf(types.size(), {-1, -1});
+    for (size_t i = 0; i < types.size(); i++) {
+        for (size_t k = 0; k < g.slots.size(); k++) {
+            if (g.slots[k].etype == types[i]) slotOf[i].first = static_cast<int32_t>(k);
+            if (g.slots[k].etype == -types[i]) slotOf[i].second = static_cast<int32_t>(k);
+        }
+        const auto [so, si] = slotOf[i];
+        if (so < 0 || si < 0 || g.vglobal >= (1ULL << 31)) continue;
+        const PairDigest o = slotDigest(g.slots[so], false, g.gbase), t = slotDigest(g.slots[si], true, g.gbase);
+        mine[i] = Rec{1, o.ok && t.ok ? 1u : 0u, o.n, o.h1, o.h2, t.n, t.h1, t.h2};
+    }
+    const std::vector<uint8_t> all = gatherHost(c, mine.data(), mine.size() * sizeof(Rec));
+    for (size_t i = 0; i < types.size(); i++) {
+        Rec sum{1, 1, 0, 0, 0, 0, 0, 0};
+        for (int w = 0; w < c->world; w++) {
+            Rec r;
+            std::memcpy(&r, all.data() + (static_cast<size_t>(w) * types.size() + i) * sizeof(Rec), sizeof(Rec));
+            sum.have &= r.have; sum.ok &= r.ok;
+            sum.n1 += r.n1; sum.a1 += r.a1; sum.b1 += r.b1; sum.n2 += r.n2; sum.a2 += r.a2; sum.b2 += r.b2;
+        }
+        if (sum.have && sum.ok && sum.n1 == sum.n2 && sum.a1 == sum.a2 && sum.b1 == sum.b2) {
+            m[slotOf[i].first] = slotOf[i].second;
+            m[slotOf[i].second] = slotOf[i].first;
+        }
+    }
+    return m;
+}
+
+// mirror slots and, for every slot with one, its pull head image; world > 1 orders the head by the
+// out-degrees of every shard's rows (gathered once per mirrored slot)
+void attachMirrors(ngx_ctx* c, const Space& sp, const HostGraph& g, DeviceGraph& d) {
+    d.mirror = c->world == 1 ? findMirrors(g) : findMirrorsGlobal(c, sp, g);
     d.pullHead.assign(g.slots.size(), DeviceGraph::PullHead());
-    for (size_t s = 0; s < g.slots.size(); s++)
-        if (d.mirror[s] >= 0) buildPullHead(g, static_cast<int32_t>(s), d.mirror[s], d);
+    for (size_t s = 0; s < g.slots.size(); s++) {
+        if (d.mirror[s] < 0) continue;
+        if (c->world == 1) {
+            buildPullHead(g, static_cast<int32_t>(s), d.mirror[s], d);
+            continue;
+        }
+        const HostSlot& out = g.slots[s];
+        std::vector<uint32_t> deg(g.vid.size());
+        for (size_t r = 0; r < deg.size(); r++)
+            deg[r] = static_cast<uint32_t>(std::min<uint64_t>(out.off[r + 1] - out.off[r], UINT32_MAX));
+        const std::vector<uint32_t> globalDeg = gatherRows(c, g, deg);
+        buildPullHead(g, static_cast<int32_t>(s), d.mirror[s], d, &globalDeg);
+    }
 }
 
 // ColumnValue per calculateExprType (GoExecutor::toThriftResponse, GoExecutor.cpp:775-829); string
@@ -1256,7 +1316,7 @@ int32_t ngx_open_snapshot(ngx_ctx* c, int32_t space, const char* path, char* tag
         }
         if (e.code) return fail(c, e.code, e.msg);
         auto dev = upload(*hg, *sp);
-        attachMirrors(c, *hg, *dev);
+        attachMirrors(c, *sp, *hg, *dev);
         HIP_OK(hipDeviceSynchronize());
         sp->dev = std::move(dev);
         sp->gen = nextGeneration();
@@ -1319,7 +1379,7 @@ int32_t ngx_commit(ngx_ctx* c, int32_t space) {
         if (hg->shardBase.empty()) { hg->shardBase = {0, hg->vid.size()}; hg->vglobal = hg->vid.size(); }
         hg->gbase = hg->shardBase[c->rank];
         sp->dev = upload(*hg, *sp);
-        attachMirrors(c, *hg, *sp->dev);
+        attachMirrors(c, *sp, *hg, *sp->dev);
         sp->gen = nextGeneration();
         sp->host = std::move(hg);
         sp->staged = StagedRows();
@@ -1977,8 +2037,10 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     ensureVisited(c, 2 * vAl);
     uint8_t* const marksA = c->visited.get<uint8_t>(2 * vAl);
     PullArgs pa{};                                              // pull expansion (kernels.h launchPull)
-    bool pullable = c->pullFactor > 0 && c->world == 1 && hs.n >= 1 && hs.n <= kPullMaxSlots && d.V < (1ULL << 32) &&
-                    d.mirror.size() == d.slots.size();
+    // world > 1: every shard pulls its own rows against the all-gathered frontier bitmap; the mirrors
+    // and the decision are global (findMirrorsGlobal, one all-gather per intermediate hop)
+    bool pullable = c->pullFactor > 0 && (c->world == 1 || (d.vglobal < (1ULL << 31) && c->world <= kMaxWorld)) &&
+                    hs.n >= 1 && hs.n <= kPullMaxSlots && d.V < (1ULL << 32) && d.mirror.size() == d.slots.size();
     if (pullable) {
         uint64_t inEdges = 0, longRows = 0, slices = 0;
         pa.n = hs.n;
@@ -2041,6 +2103,12 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     // compaction after it
     if (!lbCompact) pullable = false;
     uint64_t* fbits = pullable ? c->frontierBits.get<uint64_t>(vAl / 64 + 1) : nullptr;
+    // world > 1: the compaction writes this shard's bitmap (local rows), gathered into fbits when a hop
+    // pulls; segWords = the largest shard's words (the all-gather block)
+    uint64_t segWords = 0;
+    for (int q = 0; q + 1 < static_cast<int>(d.shardBase.size()); q++)
+        segWords = std::max<uint64_t>(segWords, (d.shardBase[q + 1] - d.shardBase[q] + 63) / 64);
+    uint64_t* lbits = (pullable && c->world > 1) ? c->localBits.get<uint64_t>(std::max<uint64_t>(segWords, 1)) : fbits;
     bool haveBits = false;
     pa.curBits = fbits;
     // storage-side request of each hop (getStepOutProps): props only on record hops, TTL info always
@@ -2264,12 +2332,41 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         // probed instead of every frontier edge storing a mark); push otherwise, or when a storage mask
         // (TTL / max-edges) decides which edges count
         // dyn: both expansions are enqueued and the device takes the one its E selects (pullMinE)
-        const bool pull = dyn ? pullable : pullable && !mask && E && E * 100 >= static_cast<uint64_t>(c->pullFactor) * d.V;
+        bool pull = dyn ? pullable : pullable && !mask && E && E * 100 >= static_cast<uint64_t>(c->pullFactor) * d.V;
+        if (!dyn && pullable && c->world > 1) {
+            // the hop's edges over every shard, and whether every shard can pull (no storage mask)
+            const uint64_t rec[2] = {E, mask ? 0u : 1u};
+            const std::vector<uint8_t> all = gatherHost(c, rec, sizeof(rec));
+            uint64_t eAll = 0, can = 1;
+            for (int w = 0; w < c->world; w++) {
+                uint64_t r[2];
+                std::memcpy(r, all.data() + w * sizeof(rec), sizeof(rec));
+                eAll += r[0];
+                can &= r[1];
+            }
+            pull = can && eAll && eAll * 100 >= static_cast<uint64_t>(c->pullFactor) * d.vglobal;
+        }
         // the hop's output marks (pull and push alike; the pull reads the frontier from the bitmap)
         uint8_t* const marks = marksA;
         if (pull && !haveBits) {                                // the seed frontier: bitmap from its list
-            HIP_OK(hipMemsetAsync(fbits, 0, (d.V + 63) / 64 * 8, c->stream));
-            if (launchMarkBits(F, nF, fbits, c->stream)) throw Error{NGX_E_DEVICE, "mark bits"};
+            HIP_OK(hipMemsetAsync(lbits, 0, (d.V + 63) / 64 * 8, c->stream));
+            if (launchMarkBits(F, nF, lbits, c->stream)) throw Error{NGX_E_DEVICE, "mark bits"};
+        }
+        if (pull && c->world > 1) {
+            // every shard's frontier bitmap -> one bitmap over global rows
+            uint64_t* seg = c->pullGather.get<uint64_t>(segWords * c->world);
+            c->timed("frontier_allgather", 0, [&] { allGather(c, lbits, seg, segWords * 8); });
+            RepackArgs ra{};
+            ra.seg = seg;
+            ra.segWords = segWords;
+            for (int q = 0; q <= c->world; q++) ra.sb[q] = d.shardBase[q];
+            ra.world = c->world;
+            ra.out = fbits;
+            ra.outWords = (d.vglobal + 63) / 64;
+            if (launchRepackBits(ra, c->stream)) throw Error{NGX_E_DEVICE, "repack bits"};
+            c->lastXchgBytes = segWords * 8 * static_cast<uint64_t>(c->world - 1);
+            c->addBytes("exchange", c->lastXchgBytes);
+            R.hopXchg.push_back(c->lastXchgBytes);
         }
         uint8_t ep = nextEpoch(c);
         if (pull) {
@@ -2290,7 +2387,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                     throw Error{NGX_E_DEVICE, "expand"};
             });
         }
-        if (c->world > 1) {
+        if (c->world > 1 && !pull) {                            // a pull computed every local row already
             c->timed("exchange", 0, [&] { exchangeFrontier(c, d, ep); });
             c->addBytes("exchange", c->lastXchgBytes);
             R.hopXchg.push_back(c->lastXchgBytes);
@@ -2311,8 +2408,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             ca.tileSum = cmpTile;
             ca.waveSum = cmpWave;
             ca.clear32 = pullable ? pa.ctl : nullptr;
-            ca.bits = fbits;
-            haveBits = fbits != nullptr;
+            ca.bits = lbits;
+            haveBits = lbits != nullptr;
             ca.total = dyn ? dynStats + h : counters + 2;
             ca.pub = dyn ? Publish{nullptr, 0} : nextPub(c);
             ca.zero = lbw;
@@ -3257,6 +3354,7 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
 }  // namespace
 
 extern "C" int32_t ngx_get_neighbors(ngx_ctx* c, const ngx_gn_request* q, ngx_gn_result** out) {
+    const auto tIn = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> g(c->mu);
     auto R = std::make_unique<GnResultHolder>();
     int32_t rc;
@@ -3299,6 +3397,27 @@ extern "C" int32_t ngx_get_neighbors(ngx_ctx* c, const ngx_gn_request* q, ngx_gn
         R->r.tag_props = R->tagProps.data();
         R->r.tag_props_off = R->tagPropsOff.data();
     }
+    // onFinished (BaseProcessor.h:51-60): latency_in_us, and the get_bound stats (ok = no failed part)
+    const int64_t us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - tIn).count();
+    R->r.latency_in_us = us;
+    if (rc == NGX_OK && R->failed.empty()) c->gbStats.qps++;
+    else c->gbStats.errorQps++;
+    c->gbStats.latencySum += us;
+    c->gbStats.latencyCount++;
+    c->gbStats.latencyMax = std::max(c->gbStats.latencyMax, us);
     *out = &R.release()->r;
     return rc;
+}
+
+extern "C" int32_t ngx_stats(ngx_ctx* c, const ngx_stat** out, int32_t* n) {
+    if (!c || !out || !n) return NGX_E_BAD_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->statList = {{"storage_get_bound_qps", c->gbStats.qps},
+                   {"storage_get_bound_error_qps", c->gbStats.errorQps},
+                   {"storage_get_bound_latency_us_sum", c->gbStats.latencySum},
+                   {"storage_get_bound_latency_us_count", c->gbStats.latencyCount},
+                   {"storage_get_bound_latency_us_max", c->gbStats.latencyMax}};
+    *out = c->statList.data();
+    *n = static_cast<int32_t>(c->statList.size());
+    return NGX_OK;
 }

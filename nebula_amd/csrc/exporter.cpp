@@ -28,10 +28,7 @@ inline uint64_t be64(const uint8_t* p) {
 template <typename T>
 inline T rd(const uint8_t* p) { T v; std::memcpy(&v, p, sizeof(T)); return v; }
 
-int hwThreads() {
-    unsigned n = std::thread::hardware_concurrency();
-    return static_cast<int>(std::max(1u, std::min(n, 16u)));
-}
+int hwThreads() { return hostThreadBudget(); }
 
 template <typename F>
 void parallelFor(uint64_t n, F&& f) {

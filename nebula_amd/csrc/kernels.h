@@ -190,6 +190,18 @@ int launchMarkRows(const uint32_t* F, uint64_t n, uint8_t* marks, uint8_t ep, hi
 int launchPublishTail(const uint32_t* err, const uint64_t* extra, int nExtra, uint64_t* slot, uint64_t seq, hipStream_t s);
 // bits of a frontier list's rows set in a bitmap (zeroed by the caller)
 int launchMarkBits(const uint32_t* F, uint64_t n, uint64_t* bits, hipStream_t s);
+// world > 1 pull: the all-gathered shard bitmaps (segWords words each, local row order) -> one bitmap
+// over global rows (shard q's rows start at sb[q])
+constexpr int kMaxWorld = 64;
+struct RepackArgs {
+    const uint64_t* seg;
+    uint64_t segWords;
+    uint64_t sb[kMaxWorld + 1];
+    int world;
+    uint64_t* out;
+    uint64_t outWords;
+};
+int launchRepackBits(const RepackArgs& a, hipStream_t s);
 // YIELD DISTINCT on the device (GoExecutor::processFinalResult, GoExecutor.cpp:1298-1305): one row of
 // every group of rows with equal YIELD values is kept. Values are equal when their value types are
 // equal and their bits are, doubles by value (0.0 == -0.0, NaN == NaN: what the reference's

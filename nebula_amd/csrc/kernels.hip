@@ -673,6 +673,31 @@ __global__ void k_mark_bits(const uint32_t* F, uint64_t n, uint64_t* bits) {
     if (i < n && F[i] != kNoRow) atomicOr(reinterpret_cast<unsigned long long*>(bits + (F[i] >> 6)), 1ULL << (F[i] & 63));
 }
 
+// The global frontier bitmap from the all-gathered per-shard ones: shard q's segment (segWords words,
+// bit i = its local row i) lands at global rows [sb[q], sb[q + 1]). Output word w collects the 64
+// global rows [64 w, 64 w + 64) from every shard overlapping them (a funnel shift of two words).
+__global__ void k_repack_bits(RepackArgs a) {
+    const uint64_t w = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (w >= a.outWords) return;
+    const uint64_t g0 = w * 64, g1 = g0 + 64;
+    uint64_t out = 0;
+    for (int q = 0; q < a.world; q++) {
+        const uint64_t lo = a.sb[q] > g0 ? a.sb[q] : g0;
+        const uint64_t hi = a.sb[q + 1] < g1 ? a.sb[q + 1] : g1;
+        if (lo >= hi) continue;
+        const uint64_t* seg = a.seg + static_cast<uint64_t>(q) * a.segWords;
+        // local bits [lo - sb[q], hi - sb[q]) -> output bits [lo - g0, hi - g0)
+        const uint64_t l0 = lo - a.sb[q];
+        const uint64_t wi = l0 >> 6, sh = l0 & 63;
+        uint64_t x = seg[wi] >> sh;
+        if (sh && wi + 1 < a.segWords) x |= seg[wi + 1] << (64 - sh);
+        const uint64_t n = hi - lo;
+        const uint64_t m = n == 64 ? ~0ULL : ((1ULL << n) - 1);
+        out |= (x & m) << (lo - g0);
+    }
+    a.out[w] = out;
+}
+
 __global__ void k_mark_rows(const uint32_t* F, uint64_t n, uint8_t* marks, uint8_t ep) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i < n && F[i] != kNoRow) marks[F[i]] = ep;
@@ -1148,6 +1173,13 @@ int launchPublishTail(const uint32_t* err, const uint64_t* extra, int nExtra, ui
 int launchMarkBits(const uint32_t* F, uint64_t n, uint64_t* bits, hipStream_t s) {
     if (n == 0) return 0;
     hipLaunchKernelGGL(k_mark_bits, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, F, n, bits);
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchRepackBits(const RepackArgs& a, hipStream_t s) {
+    if (a.outWords == 0) return 0;
+    if (a.world < 1 || a.world > kMaxWorld) return static_cast<int>(hipErrorInvalidValue);
+    hipLaunchKernelGGL(k_repack_bits, dim3(static_cast<unsigned>((a.outWords + 255) / 256)), dim3(256), 0, s, a);
     return static_cast<int>(hipGetLastError());
 }
 

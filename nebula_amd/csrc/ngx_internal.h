@@ -3,12 +3,16 @@
 // device mirror descriptors shared with the HIP kernels (kernels.hip).
 #pragma once
 
+#include <sched.h>
+
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/nebula_gn.h"
@@ -129,6 +133,23 @@ struct Space {
     int32_t slotOf(int32_t signedType) const;   // index into host->slots, -1 if none
     int32_t tagSlotOf(int32_t tagId) const;
 };
+
+// host threads for the exporter, the head-image build and result decoding: NGX_HOST_THREADS, else the
+// launcher's per-process share (OMP_NUM_THREADS: 16 per GPU on the MI355X boxes), else every CPU this
+// process may run on (sched_getaffinity)
+inline int hostThreadBudget() {
+    static const int n = [] {
+        for (const char* v : {"NGX_HOST_THREADS", "OMP_NUM_THREADS"}) {
+            const char* s = std::getenv(v);
+            if (s && std::atoi(s) > 0) return std::atoi(s);
+        }
+        cpu_set_t set;
+        if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) return CPU_COUNT(&set);
+        const unsigned h = std::thread::hardware_concurrency();
+        return h ? static_cast<int>(h) : 1;
+    }();
+    return n;
+}
 
 inline int32_t idHash(int64_t vid, int32_t numParts) {        // ID_HASH (src/common/base/Base.h:166-167)
     return static_cast<int32_t>(static_cast<uint64_t>(vid) % static_cast<uint64_t>(numParts) + 1);

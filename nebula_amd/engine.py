@@ -91,7 +91,8 @@ class GnResult(ctypes.Structure):
                 ("vertex_has_tag", P(ctypes.c_uint8)), ("strings", ctypes.c_void_p), ("strings_len", c_u64),
                 ("edge_props", ctypes.c_void_p), ("edge_props_off", P(c_u64)), ("nschemas", c_i32),
                 ("schemas", P(SchemaDefC)), ("ntag_rows", c_u32), ("tag_row_vertex", P(c_u32)),
-                ("tag_row_tag", P(c_i32)), ("tag_props", ctypes.c_void_p), ("tag_props_off", P(c_u64))]
+                ("tag_row_tag", P(c_i32)), ("tag_props", ctypes.c_void_p), ("tag_props_off", P(c_u64)),
+                ("latency_in_us", c_i64)]
 
 
 class GoPlan(ctypes.Structure):
@@ -144,6 +145,10 @@ class GoResultC(ctypes.Structure):
                 ("hop_exchange_bytes", P(c_u64)), ("host_prep_ms", c_dbl), ("host_tail_ms", c_dbl)]
 
 
+class Stat(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("value", c_i64)]
+
+
 class KernelStat(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char_p), ("launches", c_u32), ("total_ms", c_dbl), ("algo_bytes", c_u64)]
 
@@ -166,6 +171,7 @@ SIGNATURES = {
     "ngx_go": (c_i32, [ctypes.c_void_p, P(GoPlan), P(P(GoResultC))]),
     "ngx_go_result_free": (None, [P(GoResultC)]),
     "ngx_set_profiling": (c_i32, [ctypes.c_void_p, c_i32]),
+    "ngx_stats": (c_i32, [ctypes.c_void_p, P(P(Stat)), P(c_i32)]),
     "ngx_kernel_stats": (c_i32, [ctypes.c_void_p, P(P(KernelStat)), P(c_i32)]),
     "ngx_set_flag": (c_i32, [ctypes.c_void_p, ctypes.c_char_p, c_i64]),
     "ngx_get_flag": (c_i32, [ctypes.c_void_p, ctypes.c_char_p, P(c_i64)]),
@@ -301,6 +307,7 @@ class NeighborsResult:
     edge_schema: Optional[dict] = None                 # signed type -> [(name, type)]
     vertex_schema: Optional[dict] = None               # tag id -> [(name, type)]
     tag_rows: Optional[List[Tuple[int, int, bytes]]] = None   # (request vid index, tag id, TagData.data)
+    latency_in_us: int = 0                             # ResponseCommon.latency_in_us
 
 
 def _arr(ptr, n, dtype):
@@ -418,7 +425,7 @@ class Engine:
             if not decode:
                 return NeighborsResult(code=r.code, failed_codes=failed, total_edges=r.nedges, edge_vertex=None,
                                        edge_type=None, edge_dst=None, edge_cells=[], vertex_cells=[],
-                                       vertex_has_tag=None)
+                                       vertex_has_tag=None, latency_in_us=r.latency_in_us)
             strings = ctypes.string_at(r.strings, r.strings_len) if r.strings_len else b""
             nc = r.ncols
             enc = {}
@@ -442,7 +449,8 @@ class Engine:
                 edge_dst=_arr(r.edge_dst, r.nedges, np.int64),
                 edge_cells=_cells(r.edge_cells, r.nedges, nc, strings),
                 vertex_cells=_cells(r.vertex_cells, r.nvertices, nc, strings),
-                vertex_has_tag=_arr(r.vertex_has_tag, r.nvertices * nc, np.uint8), **enc)
+                vertex_has_tag=_arr(r.vertex_has_tag, r.nvertices * nc, np.uint8),
+                latency_in_us=r.latency_in_us, **enc)
         finally:
             self.L.ngx_gn_result_free(out)
 
@@ -623,6 +631,13 @@ class Engine:
     # ---- measurement
     def set_profiling(self, on: bool):
         self._check(self.L.ngx_set_profiling(self.h, 1 if on else 0), "set_profiling")
+
+    def stats(self) -> Dict[str, int]:
+        """Service counters (storage_get_bound_qps / _error_qps / _latency_us_*), as ngx_stats names them."""
+        p = P(Stat)()
+        n = c_i32()
+        self._check(self.L.ngx_stats(self.h, ctypes.byref(p), ctypes.byref(n)), "stats")
+        return {p[i].name.decode(): p[i].value for i in range(n.value)}
 
     def kernel_stats(self) -> Dict[str, Tuple[int, float, int]]:
         p = P(KernelStat)()

@@ -43,13 +43,16 @@ def main():
     rows.free()
     e.commit(datagen.RMAT_SPACE)
     res = []
+    default_pf = e.get_flag("pull_factor")
     for i, q in enumerate(queries):
+        e.set_flag("pull_factor", q.get("pull_factor", default_pf))
+        pulls = e.get_flag("pull_hops")
         r = e.go(datagen.RMAT_SPACE, ngql.parse_go(q["text"]), pushdown=q.get("pushdown", True), columnar=True,
                  rows=False, digest_fn=oracle.digest_columns)
         np.save(f"{out}.{i}.npy", r.digests if r.ok else np.zeros((0, 2), np.uint64))
         res.append({"ok": r.ok, "error": r.error, "col_types": list(r.col_types) if r.ok else [], "nrows": r.nrows,
                     "hop_edges": list(r.hop_edges), "hop_xchg": list(r.hop_xchg),
-                    "jit_failed": e.get_flag("jit_failed")})
+                    "jit_failed": e.get_flag("jit_failed"), "pull_hops": e.get_flag("pull_hops") - pulls})
     e.close()
     with open(out, "w") as f:
         json.dump(res, f)

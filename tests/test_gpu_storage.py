@@ -134,10 +134,19 @@ def test_get_neighbors_part_not_found():
         parts = sorted(byp.items()) + [(101, [7, 8]), (0, [9])]
         cols = [(3, 1, "_dst"), (3, 1, "p0")]
         ref = o.get_neighbors(ds.space, parts, [1], cols)
+        before = e.stats()
         got = e.get_neighbors(ds.space, parts, [1], cols)
+        ok = e.get_neighbors(ds.space, parts[:3], [1], cols)
+        after = e.stats()
     assert sorted(got.failed_codes) == sorted(ref.failed_codes) == [(-14, 0), (-14, 101)]
     assert got.total_edges == ref.total_edges > 0
     assert _edges(got, parts, cols) == _oracle_edges(ref)
+    # onFinished (BaseProcessor.h:51-60): latency_in_us, get_bound qps / error_qps / latency
+    assert got.latency_in_us > 0 and ok.latency_in_us > 0 and not ok.failed_codes
+    d = {k: after[k] - before.get(k, 0) for k in after}
+    assert d["storage_get_bound_qps"] == 1 and d["storage_get_bound_error_qps"] == 1
+    assert d["storage_get_bound_latency_us_count"] == 2
+    assert d["storage_get_bound_latency_us_sum"] == got.latency_in_us + ok.latency_in_us
 
 
 # ----------------------------------------------------------------------------- GO
