@@ -126,6 +126,8 @@ struct ngx_ctx {
     DBuf oFlags, rowCols, rowLen, rowOff, rowBytes;     // GetNeighbors response rows (encode_rows)
     DBuf dkTable, dkKeep, dkPre, dSrc, dDst, dRank, dType;   // YIELD DISTINCT (table, marks, compacted rows)
     std::vector<DBuf> strArena;                         // result string arenas, one per record hop (FinalArgs::strOut)
+    DBuf roots[2], rootBits;                            // multi-root walk: root sets over rows, per-entry bits
+    uint64_t pipeWalks = 0;                             // walks run for FROM $- / $var sentences (flag pipe_walks)
     DBuf localBits, pullGather;                         // world > 1 pull: this shard's frontier bitmap, all shards' 
     struct { int64_t qps = 0, errorQps = 0, latencySum = 0, latencyCount = 0, latencyMax = 0; } gbStats;
     std::vector<ngx_stat> statList;                     // ngx_stats view
@@ -1458,6 +1460,7 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "dyn_hops") *value = c->dynHops ? 1 : 0;
     else if (n == "device_libm") *value = c->deviceLibm ? 1 : 0;
     else if (n == "pull_hops") *value = static_cast<int64_t>(c->pullHops);
+    else if (n == "pipe_walks") *value = static_cast<int64_t>(c->pipeWalks);
     else if (n == "jit_compiled") *value = static_cast<int64_t>(c->jit.compiled);
     else if (n == "jit_hits") *value = static_cast<int64_t>(c->jit.hits);
     else if (n == "jit_cached") *value = static_cast<int64_t>(c->jit.size());
@@ -1869,7 +1872,19 @@ void jitSlotConsts(JitQuery& jq, std::vector<int64_t>& kc, std::vector<uint32_t>
     for (auto& y : jq.Y) slotConsts(y.code);
 }
 
-int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, const InputBind* in = nullptr) {
+// A multi-root walk (runPipe): the sentence from every start at once, each frontier row carrying the
+// bitmask of the starts (roots, at most 64) that reach it — GoExecutor's VertexBackTracker
+// (GoExecutor.h:189-207) — so that every record hop's rows can be attributed to their roots
+// (getRoots, GoExecutor.cpp:1317-1330). World 1, push hops, no storage mask (the caller walks per
+// root otherwise: runGo fails such a walk with NGX_E_UNSUPPORTED before any row).
+struct RootWalk {
+    std::unordered_map<int64_t, uint64_t> bitsOf;              // start vid -> its root bit
+    struct Hop { uint64_t rowBase = 0, rows = 0; std::unordered_map<int64_t, uint64_t> rootsOf; };
+    std::vector<Hop> record;                                   // per record hop: src vid -> roots
+};
+
+int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, const InputBind* in = nullptr,
+              RootWalk* rw = nullptr) {
     c->hmark("in");
     DeviceGraph& d = *sp.dev;
     const int64_t now = p.now_sec > 0 ? p.now_sec : static_cast<int64_t>(std::time(nullptr));   // WallClock
@@ -2039,7 +2054,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     PullArgs pa{};                                              // pull expansion (kernels.h launchPull)
     // world > 1: every shard pulls its own rows against the all-gathered frontier bitmap; the mirrors
     // and the decision are global (findMirrorsGlobal, one all-gather per intermediate hop)
-    bool pullable = c->pullFactor > 0 && (c->world == 1 || (d.vglobal < (1ULL << 31) && c->world <= kMaxWorld)) &&
+    if (rw && c->world != 1) return fail(c, NGX_E_UNSUPPORTED, "multi-root walk at world > 1");
+    bool pullable = !rw && c->pullFactor > 0 && (c->world == 1 || (d.vglobal < (1ULL << 31) && c->world <= kMaxWorld)) &&
                     hs.n >= 1 && hs.n <= kPullMaxSlots && d.V < (1ULL << 32) && d.mirror.size() == d.slots.size();
     if (pullable) {
         uint64_t inEdges = 0, longRows = 0, slices = 0;
@@ -2129,7 +2145,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     for (int s = 0; s < hs.n; s++) {
         if ((ttlMask >> s & 1u) && (hs.eflags[s] != nullptr || ttlCol[s] >= 0)) intermediateChecks = true;
     }
-    const bool dyn = c->dynHops && c->world == 1 && lbCompact && hs.n > 0 && !capped && recordFrom == steps && !pushInvalid &&
+    const bool dyn = !rw && c->dynHops && c->world == 1 && lbCompact && hs.n > 0 && !capped && recordFrom == steps && !pushInvalid &&
                      !intermediateChecks && !svids.empty() && svids.size() <= kSeedFuseMax &&
                      svids.size() * static_cast<uint64_t>(hs.n) <= kSeedFuseMax && d.vindex.slots != nullptr;
     uint64_t* dynStats = dyn ? c->dynStats.get<uint64_t>(steps + 2) : nullptr;
@@ -2171,7 +2187,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         // the fused seed kernel reads the seeds from the mapped page-locked stage; else a device copy
         const int64_t* dv = nullptr;
         const int32_t* dp_ = nullptr;
-        if (!fusedSeed || !stageSeedsMapped(c, sparts, svids, dp_, dv)) {
+        static const bool seedCopy = std::getenv("NGX_SEED_COPY") && std::atoi(std::getenv("NGX_SEED_COPY")) != 0;
+        if (!fusedSeed || seedCopy || !stageSeedsMapped(c, sparts, svids, dp_, dv)) {
             int64_t* cv = reinterpret_cast<int64_t*>(c->seedVid.get<uint8_t>(nF * 12));   // vids, then parts
             int32_t* cp = reinterpret_cast<int32_t*>(cv + nF);
             stageSeeds(c, sparts, svids, cp, cv);
@@ -2200,6 +2217,25 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             c->timed("lookup", nF * 12, [&] {
                 if (launchLookup(dp_, dv, nF, d.vpart, d.vid, d.V, F, c->stream)) throw Error{NGX_E_DEVICE, "lookup"};
             });
+        }
+    }
+    // multi-root walk: root sets over rows, the seed frontier's from the starts' bits
+    uint64_t* rootsCur = nullptr;
+    uint64_t* rootsNext = nullptr;
+    if (rw) {
+        rootsCur = c->roots[0].get<uint64_t>(std::max<uint64_t>(d.V, 1));
+        rootsNext = c->roots[1].get<uint64_t>(std::max<uint64_t>(d.V, 1));
+        HIP_OK(hipMemsetAsync(rootsCur, 0, std::max<uint64_t>(d.V, 1) * 8, c->stream));
+        if (nF) {
+            std::vector<uint64_t> bits(nF, 0);
+            for (uint64_t i = 0; i < nF; i++) {
+                auto it = rw->bitsOf.find(svids[i]);
+                bits[i] = it == rw->bitsOf.end() ? 0 : it->second;
+            }
+            uint64_t* db = c->rootBits.get<uint64_t>(nF);
+            HIP_OK(hipMemcpyAsync(db, bits.data(), nF * 8, hipMemcpyHostToDevice, c->stream));
+            if (launchScatterRoots(F, nF, db, rootsCur, c->stream)) throw Error{NGX_E_DEVICE, "scatter roots"};
+            HIP_OK(hipStreamSynchronize(c->stream));           // `bits` leaves scope
         }
     }
     uint64_t totalRows = 0;
@@ -2322,6 +2358,23 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                 uint64_t nrows = awaitPub(c, rowsPub, a.lbStatus, &finalErrBits, errFlag);
                 haveFinalErrs = true;
                 c->addBytes("final", nrows * (8 * __builtin_popcount(rowMask) + 8 * ky));
+                if (rw) {                                       // the rows' src vids -> their roots
+                    RootWalk::Hop hop;
+                    hop.rowBase = totalRows;
+                    hop.rows = nrows;
+                    std::vector<uint64_t> m(nF);
+                    std::vector<uint32_t> rows(nF);
+                    if (nF) {
+                        uint64_t* dm = c->rootBits.get<uint64_t>(nF);
+                        if (launchGatherRoots(F, nF, rootsCur, dm, c->stream)) throw Error{NGX_E_DEVICE, "gather roots"};
+                        HIP_OK(hipMemcpyAsync(m.data(), dm, nF * 8, hipMemcpyDeviceToHost, c->stream));
+                        HIP_OK(hipMemcpyAsync(rows.data(), F, nF * 4, hipMemcpyDeviceToHost, c->stream));
+                        HIP_OK(hipStreamSynchronize(c->stream));
+                    }
+                    for (uint64_t i = 0; i < nF; i++)
+                        if (rows[i] != kNoRow) hop.rootsOf[sp.host->vid[rows[i]]] |= m[i];
+                    rw->record.push_back(std::move(hop));
+                }
                 totalRows += nrows;
                 if (nStrOut) arenas.back().rows = nrows;
             }
@@ -2380,7 +2433,15 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             });
             if (!dyn) c->pullHops++;
         }
-        if ((!pull || dyn) && E) {
+        if (rw && E) {
+            // multi-root walk: destinations take the union of their sources' roots
+            if (mask) return fail(c, NGX_E_UNSUPPORTED, "multi-root walk over a storage mask (TTL / max-edges cap)");
+            HIP_OK(hipMemsetAsync(rootsNext, 0, std::max<uint64_t>(d.V, 1) * 8, c->stream));
+            c->timed("expand_roots", E * 16, [&] {
+                if (launchExpandRoots(F, nF, hs, rootsCur, rootsNext, marks, ep, c->stream))
+                    throw Error{NGX_E_DEVICE, "expand roots"};
+            });
+        } else if ((!pull || dyn) && E) {
             c->timed("expand", dyn ? 0 : E * 8, [&] {
                 if (launchExpandMark(F, estart, chunkFirst, nEnt, E, hs, marks, ep, pos32, c->stream, mask,
                                      dynTotal, dyn ? pullMinE : ~0ULL))
@@ -2454,6 +2515,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         }
         if (!dyn) R.hopNext.push_back(nF);
         F = Fn;
+        if (rw) std::swap(rootsCur, rootsNext);
         if (!dyn && nF == 0 && c->world == 1) break;            // GO_EXIT: empty frontier
     }
     if (t1) HIP_OK(hipEventRecord(t1, c->stream));
@@ -2836,19 +2898,62 @@ int32_t runPipe(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) 
     if (oneWalk) {
         GoResultHolder S;
         if ((rc = walk(vids.data(), vids.size(), nullptr, S))) return rc;
+        c->pipeWalks++;
         absorb(S, [&](uint64_t r) { return rowsOf[group.at(S.src[r])].size(); });
     } else if (!perRow) {
-        for (size_t g = 0; g < vids.size(); g++) {
-            GoResultHolder S;
-            if ((rc = walk(&vids[g], 1, nullptr, S))) return rc;
-            const uint64_t m = rowsOf[g].size();
-            absorb(S, [&](uint64_t) { return m; });
+        // multi-step, nothing reads the input: one multi-root walk per 64 distinct vids (root sets over
+        // the frontier rows); a row from a src reached by roots R repeats once per input row of every
+        // root in R. A walk the device cannot key by root (world > 1, a storage mask) falls back to a
+        // walk per vid, before any row is kept.
+        bool batched = c->world == 1;
+        std::vector<std::pair<std::unique_ptr<GoResultHolder>, std::unique_ptr<RootWalk>>> walks;
+        for (size_t b0 = 0; batched && b0 < vids.size(); b0 += 64) {
+            const size_t n = std::min<size_t>(64, vids.size() - b0);
+            auto rw = std::make_unique<RootWalk>();
+            for (size_t j = 0; j < n; j++) rw->bitsOf[vids[b0 + j]] = 1ULL << j;
+            auto S = std::make_unique<GoResultHolder>();
+            sub.starts = &vids[b0];
+            sub.nstarts = n;
+            b.row = nullptr;
+            S->tIn = std::chrono::steady_clock::now();
+            S->tLaunch = S->tDone = S->tIn;
+            rc = runGo(c, sp, sub, *S, &b, rw.get());
+            if (rc == NGX_E_UNSUPPORTED) { batched = false; break; }
+            if (rc) return rc;
+            walks.emplace_back(std::move(S), std::move(rw));
+        }
+        if (batched) {
+            c->pipeWalks += walks.size();
+            for (size_t w = 0; w < walks.size(); w++) {
+                GoResultHolder& S = *walks[w].first;
+                const RootWalk& rw = *walks[w].second;
+                const size_t b0 = w * 64;
+                absorb(S, [&](uint64_t r) {
+                    for (const RootWalk::Hop& hop : rw.record) {
+                        if (r < hop.rowBase || r >= hop.rowBase + hop.rows) continue;
+                        auto it = hop.rootsOf.find(S.src[r]);
+                        uint64_t roots = it == hop.rootsOf.end() ? 0 : it->second, k = 0;
+                        for (; roots; roots &= roots - 1) k += rowsOf[b0 + __builtin_ctzll(roots)].size();
+                        return k;
+                    }
+                    return uint64_t(0);
+                });
+            }
+        } else {
+            for (size_t g = 0; g < vids.size(); g++) {
+                GoResultHolder S;
+                if ((rc = walk(&vids[g], 1, nullptr, S))) return rc;
+                c->pipeWalks++;
+                const uint64_t m = rowsOf[g].size();
+                absorb(S, [&](uint64_t) { return m; });
+            }
         }
     } else {
         for (size_t g = 0; g < vids.size(); g++) {
             for (uint64_t r : rowsOf[g]) {
                 GoResultHolder S;
                 if ((rc = walk(&vids[g], 1, p.input_cells + r * nc, S))) return rc;
+                c->pipeWalks++;
                 absorb(S, [](uint64_t) { return uint64_t(1); });
             }
         }

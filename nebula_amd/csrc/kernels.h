@@ -202,6 +202,12 @@ struct RepackArgs {
     uint64_t outWords;
 };
 int launchRepackBits(const RepackArgs& a, hipStream_t s);
+// multi-root walk (pipes): every destination of a frontier row ORs in the row's root set (64-bit
+// masks over rows) and is marked `epoch`; roots[F[i]] |= bits[i]; out[i] = roots[F[i]]
+int launchExpandRoots(const uint32_t* F, uint64_t nF, const HopSlots& hs, const uint64_t* rootsCur, uint64_t* rootsNext,
+                      uint8_t* visited, uint8_t epoch, hipStream_t s);
+int launchScatterRoots(const uint32_t* F, uint64_t n, const uint64_t* bits, uint64_t* roots, hipStream_t s);
+int launchGatherRoots(const uint32_t* F, uint64_t n, const uint64_t* roots, uint64_t* out, hipStream_t s);
 // YIELD DISTINCT on the device (GoExecutor::processFinalResult, GoExecutor.cpp:1298-1305): one row of
 // every group of rows with equal YIELD values is kept. Values are equal when their value types are
 // equal and their bits are, doubles by value (0.0 == -0.0, NaN == NaN: what the reference's

@@ -182,13 +182,18 @@ __global__ void k_lookup(const int32_t* qpart, const int64_t* qvid, uint64_t n, 
     out[i] = (lo < V && vpart[lo] == p && vid[lo] == v) ? static_cast<uint32_t>(lo) : kNoRow;
 }
 
+// linear probing, two slots per round trip: both loads issue before either is compared (most keys
+// resolve in the first pair at the index's load factor)
 __device__ __forceinline__ uint32_t vindexFind(const VIndex& idx, int32_t part, int64_t vid) {
     uint64_t h = vindexHash(part, vid) & idx.mask;
-    for (uint64_t probe = 0; probe <= idx.mask; probe++) {
-        const VIndexSlot& sl = idx.slots[h];
-        if (sl.row == kNoRow) return kNoRow;
-        if (sl.vid == vid && sl.part == part) return sl.row;
-        h = (h + 1) & idx.mask;
+    for (uint64_t probe = 0; probe <= idx.mask; probe += 2) {
+        const VIndexSlot a = idx.slots[h];
+        const VIndexSlot b = idx.slots[(h + 1) & idx.mask];
+        if (a.row == kNoRow) return kNoRow;
+        if (a.vid == vid && a.part == part) return a.row;
+        if (b.row == kNoRow) return kNoRow;
+        if (b.vid == vid && b.part == part) return b.row;
+        h = (h + 2) & idx.mask;
     }
     return kNoRow;
 }
@@ -538,14 +543,15 @@ __device__ __forceinline__ bool probe(const PullArgs& a, bool want, uint32_t g) 
 
 // one slice's first loads: its rows, round count and first KH head rounds (independent loads; rounds
 // past the slice's count hold kNoRow: the image is kPullK rounds deep everywhere)
-constexpr int kPullKH = 4;
+constexpr int kPullKB = 4;                             // head rounds per batch after the first KH
+template <int KH>
 struct PullSlice {
     uint32_t pw;
     int nk;
-    uint32_t u[kPullKH];
+    uint32_t u[KH];
 };
-template <bool ONE>
-__device__ __forceinline__ void pullLoad(const PullArgs& a, uint64_t j, int lane, int& s, uint64_t& js, PullSlice& p) {
+template <bool ONE, int KH>
+__device__ __forceinline__ void pullLoad(const PullArgs& a, uint64_t j, int lane, int& s, uint64_t& js, PullSlice<KH>& p) {
     s = 0;
     if (!ONE) while (j >= a.sliceEnd[s]) s++;
     js = (ONE || s == 0) ? j : j - a.sliceEnd[s - 1];
@@ -553,7 +559,7 @@ __device__ __forceinline__ void pullLoad(const PullArgs& a, uint64_t j, int lane
     p.pw = a.perm[s][js * 64 + lane];
     p.nk = a.nk[s][js];
 #pragma unroll
-    for (int k = 0; k < kPullKH; k++) p.u[k] = hp[k * 64];
+    for (int k = 0; k < KH; k++) p.u[k] = hp[k * 64];
 }
 
 // probes of N consecutive head rounds held in u[off .. off + N), for the lanes still open: every probe
@@ -574,7 +580,7 @@ __device__ __forceinline__ void pullProbe(const PullArgs& a, const uint32_t* u, 
     open = open && ev == 0;
 }
 
-template <bool ONE>
+template <bool ONE, int KH>
 __global__ __launch_bounds__(WG) void k_pull_head(PullArgs a) {
     if (a.dyn != nullptr && (*a.dyn & kDynMask) < a.minE) return;   // a push hop (k_expand_mark takes it)
     const int lane = threadIdx.x & 63;
@@ -584,26 +590,28 @@ __global__ __launch_bounds__(WG) void k_pull_head(PullArgs a) {
     if (j >= total) return;
     int s;
     uint64_t js;
-    PullSlice cur;
-    pullLoad<ONE>(a, j, lane, s, js, cur);
+    PullSlice<KH> cur;
+    pullLoad<ONE, KH>(a, j, lane, s, js, cur);
     while (true) {
         // the next slice's loads go out before this slice's probes (software pipelining over the grid stride)
         const uint64_t jn = j + nw;
         int sn = 0;
         uint64_t jsn = 0;
-        PullSlice nxt;
-        pullLoad<ONE>(a, jn < total ? jn : total - 1, lane, sn, jsn, nxt);   // unconditional: no branch wait
+        PullSlice<KH> nxt;
+        pullLoad<ONE, KH>(a, jn < total ? jn : total - 1, lane, sn, jsn, nxt);   // unconditional: no branch wait
         const uint32_t* hp = a.head[s] + js * (kPullK * 64) + lane;
         // round 0 alone (most reached rows hit there), then the rest of the batch for the lanes still open
         bool hit = probe(a, cur.u[0] != kNoRow, cur.u[0]);
         bool open = cur.pw != kNoRow && !hit && cur.u[0] != kNoRow && cur.nk > 1;
         if (__any(open)) {
-            pullProbe<kPullKH - 1>(a, cur.u + 1, open, hit);           // rounds 1 .. kPullKH - 1
-            uint32_t u[kPullKH];
-            for (int k0 = kPullKH; k0 < cur.nk && __any(open); k0 += kPullKH) {
+            if constexpr (KH > 1) pullProbe<KH - 1>(a, cur.u + 1, open, hit);   // rounds 1 .. KH - 1
+            uint32_t u[kPullKB];
+            for (int k0 = KH; k0 < cur.nk && __any(open); k0 += kPullKB) {
 #pragma unroll
-                for (int k = 0; k < kPullKH; k++) u[k] = hp[(k0 + k) * 64];
-                pullProbe<kPullKH>(a, u, open, hit);
+                // a batch reaching past the image re-probes its last round (kNoRow would end the lane's
+                // search, and a long row's in-list continues past the head)
+                for (int k = 0; k < kPullKB; k++) u[k] = hp[(k0 + k < kPullK ? k0 + k : kPullK - 1) * 64];
+                pullProbe<kPullKB>(a, u, open, hit);
             }
         }
         const uint32_t row = cur.pw & ~kPullLong;
@@ -696,6 +704,41 @@ __global__ void k_repack_bits(RepackArgs a) {
         out |= (x & m) << (lo - g0);
     }
     a.out[w] = out;
+}
+
+// ------------------------------------------------------------------------------ multi-root walk
+// A pipe's sentence from many roots in one walk (engine.cpp runPipe): each frontier row carries the
+// set of roots (bit j = root j of a batch of 64) that reach it at this hop, the reference's
+// VertexBackTracker (GoExecutor.h:189-207) as a bitmask. A wave per frontier entry, lanes striding
+// over its edges: every destination ORs in the source's roots and is marked for the compaction.
+__global__ __launch_bounds__(WG) void k_expand_roots(const uint32_t* F, uint64_t nEnt, HopSlots hs, const uint64_t* rootsCur,
+                                                     unsigned long long* rootsNext, uint8_t* visited, uint8_t epoch) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = static_cast<uint64_t>(gridDim.x) * NW;
+    for (uint64_t w = (static_cast<uint64_t>(blockIdx.x) * WG + threadIdx.x) >> 6; w < nEnt; w += nw) {
+        const uint32_t row = F[w / hs.n];
+        const int s = static_cast<int>(w % hs.n);
+        if (row == kNoRow) continue;
+        const unsigned long long m = rootsCur[row];
+        if (m == 0) continue;
+        const uint64_t b = hs.off[s][row], e = hs.off[s][row + 1];
+        for (uint64_t p = b + lane; p < e; p += 64) {
+            const uint32_t g = hs.dgid[s][p];
+            if (g == kNoRow) continue;
+            atomicOr(rootsNext + g, m);
+            visited[g] = epoch;
+        }
+    }
+}
+
+// roots[F[i]] |= bits[i] (the seed frontier's roots; a vid may repeat) and out[i] = roots of F[i]
+__global__ void k_scatter_roots(const uint32_t* F, uint64_t n, const uint64_t* bits, unsigned long long* roots) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n && F[i] != kNoRow) atomicOr(roots + F[i], static_cast<unsigned long long>(bits[i]));
+}
+__global__ void k_gather_roots(const uint32_t* F, uint64_t n, const uint64_t* roots, uint64_t* out) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = F[i] == kNoRow ? 0 : roots[F[i]];
 }
 
 __global__ void k_mark_rows(const uint32_t* F, uint64_t n, uint8_t* marks, uint8_t ep) {
@@ -1127,12 +1170,22 @@ int launchPull(const PullArgs& a, hipStream_t s) {
     if (a.n < 1 || a.n > kPullMaxSlots || a.V >= (1ULL << 31)) return 1;
     const uint64_t slices = a.sliceEnd[a.n - 1];
     if (slices == 0) return 0;
-    // waves stride over the slices (8 resident workgroups per CU on 256 CUs), each prefetching its next
-    // slice while it probes the current one
-    static const uint64_t maxGrid = getenv("NGX_PULL_GRID") ? std::strtoull(getenv("NGX_PULL_GRID"), nullptr, 10) : kDynGrid;
+    // a wave per slice (measured at C2: 52 vs 56 us for 2048 workgroups striding over the slices, each
+    // prefetching its next slice while it probes the current one); NGX_PULL_GRID caps the grid
+    static const uint64_t maxGrid = getenv("NGX_PULL_GRID") ? std::strtoull(getenv("NGX_PULL_GRID"), nullptr, 10) : ~0u;
     dim3 grid(static_cast<unsigned>(std::min<uint64_t>((slices + NW - 1) / NW, maxGrid)));
-    if (a.n == 1) hipLaunchKernelGGL((k_pull_head<true>), grid, dim3(WG), 0, s, a);
-    else hipLaunchKernelGGL((k_pull_head<false>), grid, dim3(WG), 0, s, a);
+    // head rounds loaded with the slice before its first probe (NGX_PULL_KH: 1, 2 or 4; default 4)
+    static const int kh = getenv("NGX_PULL_KH") ? std::atoi(getenv("NGX_PULL_KH")) : 4;
+    if (kh == 1) {
+        if (a.n == 1) hipLaunchKernelGGL((k_pull_head<true, 1>), grid, dim3(WG), 0, s, a);
+        else hipLaunchKernelGGL((k_pull_head<false, 1>), grid, dim3(WG), 0, s, a);
+    } else if (kh == 2) {
+        if (a.n == 1) hipLaunchKernelGGL((k_pull_head<true, 2>), grid, dim3(WG), 0, s, a);
+        else hipLaunchKernelGGL((k_pull_head<false, 2>), grid, dim3(WG), 0, s, a);
+    } else {
+        if (a.n == 1) hipLaunchKernelGGL((k_pull_head<true, 4>), grid, dim3(WG), 0, s, a);
+        else hipLaunchKernelGGL((k_pull_head<false, 4>), grid, dim3(WG), 0, s, a);
+    }
     // long unresolved in-lists: at most a.segCap segments, 2 workgroups per CU striding over them
     hipLaunchKernelGGL(k_pull_segments, dim3(256), dim3(WG), 0, s, a);
     return static_cast<int>(hipGetLastError());
@@ -1180,6 +1233,29 @@ int launchRepackBits(const RepackArgs& a, hipStream_t s) {
     if (a.outWords == 0) return 0;
     if (a.world < 1 || a.world > kMaxWorld) return static_cast<int>(hipErrorInvalidValue);
     hipLaunchKernelGGL(k_repack_bits, dim3(static_cast<unsigned>((a.outWords + 255) / 256)), dim3(256), 0, s, a);
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchExpandRoots(const uint32_t* F, uint64_t nF, const HopSlots& hs, const uint64_t* rootsCur, uint64_t* rootsNext,
+                      uint8_t* visited, uint8_t epoch, hipStream_t s) {
+    const uint64_t nEnt = nF * static_cast<uint64_t>(hs.n);
+    if (nEnt == 0) return 0;
+    dim3 grid(static_cast<unsigned>(std::min<uint64_t>((nEnt + NW - 1) / NW, kDynGrid)));
+    hipLaunchKernelGGL(k_expand_roots, grid, dim3(WG), 0, s, F, nEnt, hs, rootsCur,
+                       reinterpret_cast<unsigned long long*>(rootsNext), visited, epoch);
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchScatterRoots(const uint32_t* F, uint64_t n, const uint64_t* bits, uint64_t* roots, hipStream_t s) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_scatter_roots, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, F, n, bits,
+                       reinterpret_cast<unsigned long long*>(roots));
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchGatherRoots(const uint32_t* F, uint64_t n, const uint64_t* roots, uint64_t* out, hipStream_t s) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_gather_roots, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, F, n, roots, out);
     return static_cast<int>(hipGetLastError());
 }
 

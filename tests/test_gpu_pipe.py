@@ -115,3 +115,28 @@ def test_pipe_empty_input_keeps_types(rmat):
     # no data: `$-.id' is UNKNOWN (calculateExprType, TraverseExecutor.cpp:150-158); the reference's
     # onEmptyInputs response carries no rows, so the oracle reports no types at all
     assert got.col_types == [0, 2]
+
+
+@pytest.mark.parametrize("q", [
+    "GO 2 STEPS FROM $-.id OVER e WHERE e.p0 < 3 YIELD e._dst, e.p1 % 5",
+    "GO 1 TO 3 STEPS FROM $-.id OVER e REVERSELY WHERE e.p0 < 2 YIELD e._dst, e._src",
+    "GO 3 STEPS FROM $-.id OVER e BIDIRECT YIELD DISTINCT e._dst",
+])
+def test_multi_root_walk_in_batches(rmat, q):
+    """A multi-step sentence that reads nothing of its input walks from 64 distinct input vids at a time
+    (root sets over the frontier rows, GoExecutor's back tracker as bitmasks), not once per vid: the
+    input here has ~300 distinct vids and duplicates, the rows equal the oracle's back-tracker result."""
+    ds, o, e = rmat
+    seeds = ", ".join(str(int(v)) for v in datagen.sample_vids(4242, 1 << ds.scale, 20))
+    first = f"GO FROM {seeds} OVER e YIELD e._dst AS id"
+    full = f"{first} | {q}"
+    ids = {r[0][1] for r in pipeline.run(o, ds.space, first).rows}
+    assert len(ids) > 128
+    before = e.get_flag("pipe_walks")
+    ref = pipeline.run(o, ds.space, full)
+    got = pipeline.run(e, ds.space, full)
+    walks = e.get_flag("pipe_walks") - before
+    assert ref.ok and got.ok, (got.error, ref.error)
+    assert sorted(fixtures.normalize_cells(got.rows), key=repr) == sorted(fixtures.normalize_cells(ref.rows), key=repr)
+    assert len(got.rows) > 0
+    assert walks == (len(ids) + 63) // 64
