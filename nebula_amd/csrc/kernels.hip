@@ -580,7 +580,9 @@ __device__ __forceinline__ void pullProbe(const PullArgs& a, const uint32_t* u, 
     open = open && ev == 0;
 }
 
-template <bool ONE, int KH>
+// PREF: waves stride over the slices, loading the next slice before probing this one; !PREF: the grid
+// has a wave per slice (no stride, no prefetch of a slice nobody probes)
+template <bool ONE, int KH, bool PREF>
 __global__ __launch_bounds__(WG) void k_pull_head(PullArgs a) {
     if (a.dyn != nullptr && (*a.dyn & kDynMask) < a.minE) return;   // a push hop (k_expand_mark takes it)
     const int lane = threadIdx.x & 63;
@@ -598,7 +600,7 @@ __global__ __launch_bounds__(WG) void k_pull_head(PullArgs a) {
         int sn = 0;
         uint64_t jsn = 0;
         PullSlice<KH> nxt;
-        pullLoad<ONE, KH>(a, jn < total ? jn : total - 1, lane, sn, jsn, nxt);   // unconditional: no branch wait
+        if constexpr (PREF) pullLoad<ONE, KH>(a, jn < total ? jn : total - 1, lane, sn, jsn, nxt);   // unconditional
         const uint32_t* hp = a.head[s] + js * (kPullK * 64) + lane;
         // round 0 alone (most reached rows hit there), then the rest of the batch for the lanes still open
         bool hit = probe(a, cur.u[0] != kNoRow, cur.u[0]);
@@ -631,7 +633,7 @@ __global__ __launch_bounds__(WG) void k_pull_head(PullArgs a) {
                 else atomicOr(a.err + 3, 1u);
             }
         }
-        if (jn >= total) break;
+        if (!PREF || jn >= total) break;
         j = jn; s = sn; js = jsn; cur = nxt;
     }
 }
@@ -1175,18 +1177,19 @@ int launchPull(const PullArgs& a, hipStream_t s) {
     // prefetching its next slice while it probes the current one); NGX_PULL_GRID caps the grid
     static const uint64_t maxGrid = getenv("NGX_PULL_GRID") ? std::strtoull(getenv("NGX_PULL_GRID"), nullptr, 10) : ~0u;
     dim3 grid(static_cast<unsigned>(std::min<uint64_t>((slices + NW - 1) / NW, maxGrid)));
-    // head rounds loaded with the slice before its first probe (NGX_PULL_KH: 1, 2 or 4; default 4)
-    static const int kh = getenv("NGX_PULL_KH") ? std::atoi(getenv("NGX_PULL_KH")) : 4;
-    if (kh == 1) {
-        if (a.n == 1) hipLaunchKernelGGL((k_pull_head<true, 1>), grid, dim3(WG), 0, s, a);
-        else hipLaunchKernelGGL((k_pull_head<false, 1>), grid, dim3(WG), 0, s, a);
-    } else if (kh == 2) {
-        if (a.n == 1) hipLaunchKernelGGL((k_pull_head<true, 2>), grid, dim3(WG), 0, s, a);
-        else hipLaunchKernelGGL((k_pull_head<false, 2>), grid, dim3(WG), 0, s, a);
-    } else {
-        if (a.n == 1) hipLaunchKernelGGL((k_pull_head<true, 4>), grid, dim3(WG), 0, s, a);
-        else hipLaunchKernelGGL((k_pull_head<false, 4>), grid, dim3(WG), 0, s, a);
-    }
+    // head rounds loaded with the slice before its first probe (NGX_PULL_KH: 1, 2 or 4; default 2:
+    // 48.1 us at C2 against 49.9 for 4 and 50.9 for 1, and half the head bytes of 4)
+    static const int kh = getenv("NGX_PULL_KH") ? std::atoi(getenv("NGX_PULL_KH")) : 2;
+    const bool pref = static_cast<uint64_t>(grid.x) * NW < slices;
+#define NGX_PULL(KH) do { \
+        if (pref) { if (a.n == 1) hipLaunchKernelGGL((k_pull_head<true, KH, true>), grid, dim3(WG), 0, s, a); \
+                    else hipLaunchKernelGGL((k_pull_head<false, KH, true>), grid, dim3(WG), 0, s, a); } \
+        else { if (a.n == 1) hipLaunchKernelGGL((k_pull_head<true, KH, false>), grid, dim3(WG), 0, s, a); \
+               else hipLaunchKernelGGL((k_pull_head<false, KH, false>), grid, dim3(WG), 0, s, a); } } while (0)
+    if (kh == 1) NGX_PULL(1);
+    else if (kh == 2) NGX_PULL(2);
+    else NGX_PULL(4);
+#undef NGX_PULL
     // long unresolved in-lists: at most a.segCap segments, 2 workgroups per CU striding over them
     hipLaunchKernelGGL(k_pull_segments, dim3(256), dim3(WG), 0, s, a);
     return static_cast<int>(hipGetLastError());
