@@ -127,6 +127,8 @@ struct ngx_ctx {
     DBuf dkTable, dkKeep, dkPre, dSrc, dDst, dRank, dType;   // YIELD DISTINCT (table, marks, compacted rows)
     std::vector<DBuf> strArena;                         // result string arenas, one per record hop (FinalArgs::strOut)
     DBuf roots[2], rootBits;                            // multi-root walk: root sets over rows, per-entry bits
+    DBuf pwF, pwIn, pwEst, pwCf;                        // ... reading $-: (row, input row) entries, their estart / heads
+    DBuf inX, inLen, inT, inStr, inDesc;                // ... the pipe's input table
     uint64_t pipeWalks = 0;                             // walks run for FROM $- / $var sentences (flag pipe_walks)
     DBuf localBits, pullGather;                         // world > 1 pull: this shard's frontier bitmap, all shards' 
     struct { int64_t qps = 0, errorQps = 0, latencySum = 0, latencyCount = 0, latencyMax = 0; } gbStats;
@@ -1879,6 +1881,13 @@ void jitSlotConsts(JitQuery& jq, std::vector<int64_t>& kc, std::vector<uint32_t>
 // root otherwise: runGo fails such a walk with NGX_E_UNSUPPORTED before any row).
 struct RootWalk {
     std::unordered_map<int64_t, uint64_t> bitsOf;              // start vid -> its root bit
+    // WHERE / YIELD read $-.x: every record hop's entries are (frontier row, input row) pairs, one per
+    // input row of each root reaching the row, and the programs read the row's columns (OP_INPUT)
+    bool perRow = false;
+    const std::vector<std::vector<uint32_t>>* rowsOfBit = nullptr;   // root bit -> its input rows
+    const DInputCol* input = nullptr;                          // the input table on the device
+    uint64_t inStrDev = 0, inStrBytes = 0;                     // its string pool (device) ...
+    const char* inStrHost = nullptr;                           // ... and the same bytes on the host
     struct Hop { uint64_t rowBase = 0, rows = 0; std::unordered_map<int64_t, uint64_t> rootsOf; };
     std::vector<Hop> record;                                   // per record hop: src vid -> roots
 };
@@ -1901,6 +1910,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     GraphdCtx gctx;
     gctx.sp = &sp;
     gctx.deviceLibm = c->deviceLibm;
+    if (rw && rw->perRow && in) gctx.inputCols = &in->colIdx;
     gctx.aliasType = gp.aliasType;
     gctx.direction = p.direction;
     gctx.nEdgeTypes = gp.edgeTypes.size();
@@ -1998,6 +2008,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         jq.yKey = yAlias;
         jq.dstReplica = dstReplica;
         jq.rowMask = rowMask;
+        jq.input = rw && rw->perRow;
         jitSlotConsts(jq, jitKc, jitKl);
         std::string jerr;
         // kernels cached by query shape: the source is generated only on a miss
@@ -2316,8 +2327,49 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             for (size_t k = 0; k < jitKc.size(); k++) { a.kc[k] = jitKc[k]; a.kl[k] = jitKl[k]; }
             // a masked hop (max-edges cap) runs on the interpreter kernel: the generated ones skip the mask
             const JitKernels* kj = mask ? nullptr : (isFinal ? jk.get() : jkNoP.get());
+            uint64_t Ef = E;                                    // edges the final launch evaluates
+            uint64_t gridf = chunks;
+            a.fin = nullptr;
+            if (rw && rw->perRow) {
+                // the hop's entries as (frontier row, input row) pairs: a frontier row once per input row
+                // of every root that reaches it, the input row travelling with the entry (FinalArgs::fin)
+                if (mask) return fail(c, NGX_E_UNSUPPORTED, "multi-root walk over a storage mask (TTL / max-edges cap)");
+                std::vector<uint64_t> m(nF);
+                std::vector<uint32_t> rows(nF);
+                uint64_t* dm = c->rootBits.get<uint64_t>(std::max<uint64_t>(nF, 1));
+                if (launchGatherRoots(F, nF, rootsCur, dm, c->stream)) throw Error{NGX_E_DEVICE, "gather roots"};
+                HIP_OK(hipMemcpyAsync(m.data(), dm, nF * 8, hipMemcpyDeviceToHost, c->stream));
+                HIP_OK(hipMemcpyAsync(rows.data(), F, nF * 4, hipMemcpyDeviceToHost, c->stream));
+                HIP_OK(hipStreamSynchronize(c->stream));
+                std::vector<uint32_t> f2, in2;
+                for (uint64_t i = 0; i < nF; i++) {
+                    if (rows[i] == kNoRow) continue;
+                    for (uint64_t r = m[i]; r; r &= r - 1) {
+                        for (uint32_t ir : (*rw->rowsOfBit)[__builtin_ctzll(r)]) { f2.push_back(rows[i]); in2.push_back(ir); }
+                    }
+                }
+                const uint64_t n2 = f2.size(), nEnt2 = n2 * static_cast<uint64_t>(hs.n);
+                uint32_t* dF2 = c->pwF.get<uint32_t>(std::max<uint64_t>(n2, 1));
+                uint32_t* dIn2 = c->pwIn.get<uint32_t>(std::max<uint64_t>(n2, 1));
+                uint64_t* est2 = c->pwEst.get<uint64_t>(nEnt2 + 1);
+                uint64_t* tiles2 = c->tileSums.get<uint64_t>((std::max<uint64_t>(nEnt2, 1) + kTile - 1) / kTile + 1);
+                HIP_OK(hipMemcpyAsync(dF2, f2.data(), n2 * 4, hipMemcpyHostToDevice, c->stream));
+                HIP_OK(hipMemcpyAsync(dIn2, in2.data(), n2 * 4, hipMemcpyHostToDevice, c->stream));
+                Ef = 0;
+                if (nEnt2) {
+                    Publish pub = nextPub(c);
+                    if (launchDegreeScan(dF2, nEnt2, hs, est2, tiles2, c->stream, pub)) throw Error{NGX_E_DEVICE, "degree scan"};
+                    Ef = awaitPub(c, pub, est2 + nEnt2);
+                }
+                gridf = (Ef + kChunk - 1) / kChunk;
+                uint64_t* cf2 = c->pwCf.get<uint64_t>(std::max<uint64_t>(gridf, 1));
+                if (launchChunkFirst(est2, nEnt2, cf2, c->stream, lb, kDoneOff + 1)) throw Error{NGX_E_DEVICE, "chunk first"};
+                HIP_OK(hipStreamSynchronize(c->stream));       // f2 / in2 leave scope
+                a.F = dF2; a.fin = dIn2; a.estart = est2; a.chunkFirst = cf2; a.nEnt = nEnt2; a.E = Ef;
+                a.env.input = rw->input;
+            }
             // outputs sized for every edge passing (rows are written in the same launch)
-            uint64_t cap = totalRows + E;
+            uint64_t cap = totalRows + Ef;
             growKeep(c, c->oSrc, cap * 8, totalRows * 8);
             growKeep(c, c->oDst, cap * 8, totalRows * 8);
             growKeep(c, c->oRank, cap * 8, totalRows * 8);
@@ -2340,12 +2392,13 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             a.strOutMask = strOutMask;
             if (nStrOut) {
                 if (c->strArena.size() <= arenas.size()) c->strArena.resize(arenas.size() + 1);
-                a.strOut = c->strArena[arenas.size()].get<char>(E * nStrOut * static_cast<uint64_t>(kStrBuildBytes));
+                a.strOut = c->strArena[arenas.size()].get<char>(std::max<uint64_t>(Ef, 1) * nStrOut * static_cast<uint64_t>(kStrBuildBytes));
                 arenas.push_back(Arena{a.strOut, 0});
             }
             // dyn: chunks of the upper bound E; the workgroups past the real chunks return at once
-            const unsigned grid = static_cast<unsigned>(chunks);
-            c->timed("final", dyn ? 0 : E * (16 + kfBytes), [&] {
+            const unsigned grid = static_cast<unsigned>(gridf);
+            c->timed("final", dyn ? 0 : Ef * (16 + kfBytes), [&] {
+                if (grid == 0) return;
                 if (kj) {
                     void* args[] = {&a};
                     HIP_OK(hipModuleLaunchKernel(kj->final, grid, 1, 1, 256, 1, 1, 0, c->stream, args, nullptr));
@@ -2358,7 +2411,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                 uint64_t nrows = awaitPub(c, rowsPub, a.lbStatus, &finalErrBits, errFlag);
                 haveFinalErrs = true;
                 c->addBytes("final", nrows * (8 * __builtin_popcount(rowMask) + 8 * ky));
-                if (rw) {                                       // the rows' src vids -> their roots
+                if (rw && !rw->perRow) {                        // the rows' src vids -> their roots
                     RootWalk::Hop hop;
                     hop.rowBase = totalRows;
                     hop.rows = nrows;
@@ -2720,6 +2773,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         builtRanges.push_back(StrMap::Range{reinterpret_cast<uint64_t>(ar.dev), bytes, R.built.back().data()});
     }
     if (!builtRanges.empty()) HIP_OK(hipStreamSynchronize(c->stream));
+    if (rw && rw->perRow && rw->inStrBytes)                      // YIELD $-.s: strings of the input table
+        builtRanges.push_back(StrMap::Range{rw->inStrDev, rw->inStrBytes, rw->inStrHost});
     StrMap sm{&d, reinterpret_cast<uint64_t>(dp.pool), &R.strings, &builtRanges};
     uint64_t nOut = n;
     R.r.nrows = nOut;
@@ -2949,12 +3004,98 @@ int32_t runPipe(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) 
             }
         }
     } else {
-        for (size_t g = 0; g < vids.size(); g++) {
-            for (uint64_t r : rowsOf[g]) {
-                GoResultHolder S;
-                if ((rc = walk(&vids[g], 1, p.input_cells + r * nc, S))) return rc;
-                c->pipeWalks++;
-                absorb(S, [](uint64_t) { return uint64_t(1); });
+        // WHERE / YIELD read $-.x: one multi-root walk per 64 distinct vids, the input table on the
+        // device and every record hop's entries keyed by (frontier row, input row) (RootWalk::perRow);
+        // a walk per input row, values bound as constants, where the device cannot key a walk by root
+        bool batched = c->world == 1;
+        for (uint64_t i = 0; batched && i < p.input_nrows * static_cast<uint64_t>(nc); i++) {
+            const int32_t k = p.input_cells[i].kind;
+            batched = k == NGX_CELL_BOOL || k == NGX_CELL_INT || k == NGX_CELL_ID || k == NGX_CELL_TIMESTAMP ||
+                      k == NGX_CELL_FLOAT || k == NGX_CELL_DOUBLE || k == NGX_CELL_STR;
+        }
+        std::vector<std::pair<std::unique_ptr<GoResultHolder>, std::unique_ptr<RootWalk>>> walks;
+        std::vector<std::vector<std::vector<uint32_t>>> rowsOfBit;
+        const DInputCol* inputDev = nullptr;
+        uint64_t inStrBytes = 0;
+        if (batched) {
+            // the input table: per column value bits / lengths / VM types, strings in one device pool
+            const uint64_t n = p.input_nrows;
+            uint64_t strBytes = 0;
+            for (uint64_t i = 0; i < n * static_cast<uint64_t>(nc); i++)
+                if (p.input_cells[i].kind == NGX_CELL_STR)
+                    strBytes = std::max<uint64_t>(strBytes, p.input_cells[i].v.str_off + static_cast<uint64_t>(p.input_cells[i].str_len));
+            inStrBytes = strBytes;
+            char* dStr = c->inStr.get<char>(std::max<uint64_t>(strBytes, 1));
+            int64_t* dX = c->inX.get<int64_t>(n * nc);
+            uint32_t* dLen = c->inLen.get<uint32_t>(n * nc);
+            uint8_t* dT = c->inT.get<uint8_t>(n * nc);
+            std::vector<int64_t> hx(n * nc);
+            std::vector<uint32_t> hl(n * nc, 0);
+            std::vector<uint8_t> ht(n * nc);
+            std::vector<DInputCol> desc(nc);
+            for (int32_t col = 0; col < nc; col++) {
+                desc[col] = DInputCol{dX + col * n, dLen + col * n, dT + col * n};
+                for (uint64_t r = 0; r < n; r++) {
+                    const ngx_cell& v = p.input_cells[r * nc + col];
+                    const uint64_t at = col * n + r;
+                    switch (v.kind) {
+                        case NGX_CELL_BOOL: ht[at] = V_BOOL; hx[at] = v.v.i != 0; break;
+                        case NGX_CELL_FLOAT: case NGX_CELL_DOUBLE: ht[at] = V_DBL; std::memcpy(&hx[at], &v.v.d, 8); break;
+                        case NGX_CELL_STR:
+                            ht[at] = V_STR; hl[at] = static_cast<uint32_t>(v.str_len);
+                            hx[at] = reinterpret_cast<int64_t>(dStr + v.v.str_off);
+                            break;
+                        default: ht[at] = V_INT; hx[at] = v.v.i; break;
+                    }
+                }
+            }
+            DInputCol* dDesc = c->inDesc.get<DInputCol>(std::max<int32_t>(nc, 1));
+            if (strBytes) HIP_OK(hipMemcpyAsync(dStr, p.input_strings, strBytes, hipMemcpyHostToDevice, c->stream));
+            HIP_OK(hipMemcpyAsync(dX, hx.data(), hx.size() * 8, hipMemcpyHostToDevice, c->stream));
+            HIP_OK(hipMemcpyAsync(dLen, hl.data(), hl.size() * 4, hipMemcpyHostToDevice, c->stream));
+            HIP_OK(hipMemcpyAsync(dT, ht.data(), ht.size(), hipMemcpyHostToDevice, c->stream));
+            HIP_OK(hipMemcpyAsync(dDesc, desc.data(), nc * sizeof(DInputCol), hipMemcpyHostToDevice, c->stream));
+            HIP_OK(hipStreamSynchronize(c->stream));
+            inputDev = dDesc;
+            rowsOfBit.resize((vids.size() + 63) / 64);
+        }
+        for (size_t b0 = 0; batched && b0 < vids.size(); b0 += 64) {
+            const size_t n = std::min<size_t>(64, vids.size() - b0);
+            auto& rob = rowsOfBit[b0 / 64];
+            rob.resize(n);
+            auto rwk = std::make_unique<RootWalk>();
+            for (size_t j = 0; j < n; j++) {
+                rwk->bitsOf[vids[b0 + j]] = 1ULL << j;
+                for (uint64_t r : rowsOf[b0 + j]) rob[j].push_back(static_cast<uint32_t>(r));
+            }
+            rwk->perRow = true;
+            rwk->rowsOfBit = &rob;
+            rwk->input = inputDev;
+            rwk->inStrDev = reinterpret_cast<uint64_t>(c->inStr.p);
+            rwk->inStrBytes = inStrBytes;
+            rwk->inStrHost = p.input_strings;
+            auto S = std::make_unique<GoResultHolder>();
+            sub.starts = &vids[b0];
+            sub.nstarts = n;
+            b.row = nullptr;
+            S->tIn = std::chrono::steady_clock::now();
+            S->tLaunch = S->tDone = S->tIn;
+            rc = runGo(c, sp, sub, *S, &b, rwk.get());
+            if (rc == NGX_E_UNSUPPORTED) { batched = false; break; }
+            if (rc) return rc;
+            walks.emplace_back(std::move(S), std::move(rwk));
+        }
+        if (batched) {
+            c->pipeWalks += walks.size();
+            for (auto& w : walks) absorb(*w.first, [](uint64_t) { return uint64_t(1); });
+        } else {
+            for (size_t g = 0; g < vids.size(); g++) {
+                for (uint64_t r : rowsOf[g]) {
+                    GoResultHolder S;
+                    if ((rc = walk(&vids[g], 1, p.input_cells + r * nc, S))) return rc;
+                    c->pipeWalks++;
+                    absorb(S, [](uint64_t) { return uint64_t(1); });
+                }
             }
         }
     }

@@ -574,6 +574,16 @@ int32_t compileGraphd(const ExprNode& root, GraphdCtx& ctx, Program& out, std::s
                 else { out.usesDstTag = true; em.emit(OP_DSTTAG, col, tslot, 0, dvt, 1, dbits); }
                 return NGX_OK;
             }
+            case K_INPUT_PROP: case K_VAR_PROP: {
+                if (ctx.inputCols == nullptr) {
+                    err = "$- / $var inputs are outside the GO fast path";
+                    return NGX_E_UNSUPPORTED;
+                }
+                auto it = ctx.inputCols->find(n.prop);          // InterimResult::getColumnWithRow
+                if (it == ctx.inputCols->end()) { err = "Prop `" + n.prop + "' not found"; return NGX_E_QUERY; }
+                em.emit(OP_INPUT, it->second);
+                return NGX_OK;
+            }
             default:
                 err = "$- / $var inputs are outside the GO fast path";
                 return NGX_E_UNSUPPORTED;

@@ -78,6 +78,8 @@ struct GraphdCtx {
     // final-hop response schema per signed type: prop name -> type
     std::map<int32_t, std::map<std::string, int32_t>> respSchema;
     bool deviceLibm = false;                     // flag device_libm: inexact libm of row values allowed
+    // $-.x / $var.x read from the pipe's input table (OP_INPUT: column index); null: outside the fast path
+    const std::map<std::string, int32_t>* inputCols = nullptr;
 };
 
 // Compile. Returns NGX_OK, NGX_E_INVALID_FILTER (storage checkExp failure), NGX_E_UNSUPPORTED, or

@@ -891,6 +891,9 @@ struct VmEv {
 
 template <bool ONE, bool FIDX>
 __global__ __launch_bounds__(WG) void k_final(FinalArgs a) { finalBody<VmEv, ONE, FIDX, FIDX>(a); }
+// a GO whose frontier entries carry input rows (FinalArgs::fin: multi-root pipe walks reading $-)
+template <bool ONE>
+__global__ __launch_bounds__(WG) void k_final_in(FinalArgs a) { finalBody<VmEv, ONE, true, false>(a); }
 
 // ------------------------------------------------------------------------------ max_edge_returned_per_vertex
 // Storage outcome of every hop edge (bad row / TTL / pushed filter; the interpreter evaluates the
@@ -1158,7 +1161,10 @@ int finalOccupancy(const FinalArgs& a) {
 int launchFinal(const FinalArgs& a, hipStream_t s, unsigned g) {
     if (a.E == 0) return 0;
     dim3 grid(g ? g : static_cast<unsigned>((a.E + CE - 1) / CE));
-    if (a.oEntry != nullptr) {
+    if (a.fin != nullptr) {
+        if (a.hs.n == 1) hipLaunchKernelGGL((k_final_in<true>), grid, dim3(WG), 0, s, a);
+        else hipLaunchKernelGGL((k_final_in<false>), grid, dim3(WG), 0, s, a);
+    } else if (a.oEntry != nullptr) {
         if (a.hs.n == 1) hipLaunchKernelGGL((k_final<true, true>), grid, dim3(WG), 0, s, a);
         else hipLaunchKernelGGL((k_final<false, true>), grid, dim3(WG), 0, s, a);
     } else {

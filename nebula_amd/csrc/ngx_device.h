@@ -17,6 +17,14 @@ constexpr int kStrBuildBytes = 64;          // longest string a builder (lower, 
 constexpr int kMaxStrBuilds = 4;            // builder buffers per program (exprc.cpp refuses more)
 constexpr uint8_t kNoBuf = 0xFF;            // Insn::mode of an OP_ADD / OP_FUNC / OP_CAST without a buffer
 
+// a column of a pipe's input table on the device (the InterimResult rows a $- / $var sentence reads):
+// value bits (string: device pointer), string lengths, VM value types per row
+struct DInputCol {
+    const int64_t* x;
+    const uint32_t* len;
+    const uint8_t* t;
+};
+
 // per-edge flags (HostSlot::eflags)
 enum : uint8_t {
     EF_EMPTY_VALUE = 1,    // the KV value was empty: no RowReader, filter not evaluated (.inl:520)
@@ -82,6 +90,7 @@ enum Op : uint8_t {
     OP_LT, OP_LE, OP_GT, OP_GE, OP_EQ, OP_NE, OP_CONTAINS,
     OP_AND, OP_OR, OP_LXOR,
     OP_FUNC,           // a = function id, b = argc, mode = builder buffer (kNoBuf: none)
+    OP_INPUT,          // $-.x / $var.x of the edge's input row (multi-root pipe walks): a = input column
 };
 
 enum Func : int32_t {

@@ -32,6 +32,7 @@ struct EdgeCtx {
     uint32_t srow;      // local row of the source vertex
     uint32_t drow;      // global row of the destination (kNoRow: no vertex row on any shard)
     int64_t src, dst, rank;
+    uint32_t in;        // input row of the edge's frontier entry (multi-root pipe walks; 0 otherwise)
 };
 
 struct VmEnv {
@@ -43,6 +44,7 @@ struct VmEnv {
     int64_t now;               // WallClock::fastNowInSec of the request (TTL)
     const DTag* dtags;         // $$ props: tag tables over GLOBAL rows (world 1: the shard's own tables;
     const DCol* dcols;         // world > 1: replicas of every shard's rows, built on first use)
+    const DInputCol* input;    // the pipe's input columns (OP_INPUT), nullptr when none
 };
 
 // Loads through the global address space. Column pointers come from device-side tables (DCol, DTag),
@@ -669,6 +671,12 @@ __device__ __forceinline__ Val opFunc(int32_t fid, const Val* args, int argc, co
     }
 }
 
+// $-.x / $var.x: the value of input column `col` in the edge's input row
+__device__ __forceinline__ Val opInput(const VmEnv& env, const EdgeCtx& ec, int32_t col) {
+    const DInputCol& c = env.input[col];
+    return Val{gld<int64_t>(c.x, ec.in), gld<uint32_t>(c.len, ec.in), gld<uint8_t>(c.t, ec.in)};
+}
+
 // ------------------------------------------------------------------------------ interpreter
 static __device__ __noinline__ Val vmEval(const Insn* code, const VmEnv& env, const EdgeCtx& ec, char* sout = nullptr) {
     Val st[kMaxStack];
@@ -684,6 +692,7 @@ static __device__ __noinline__ Val vmEval(const Insn* code, const VmEnv& env, co
             case OP_ECOL: st[sp++] = opEcol(env, ec, in.a, in.b, in.mode, constVal(in.t2, in.imm, 0, env.pool)); break;
             case OP_EKEY: st[sp++] = opEkey(ec, in.a, in.b, in.mode, constVal(in.t2, in.imm, 0, env.pool)); break;
             case OP_EDST: st[sp++] = opEdst(ec, in.b); break;
+            case OP_INPUT: st[sp++] = opInput(env, ec, in.a); break;
             case OP_SRCTAG: case OP_DSTTAG:
                 st[sp++] = opTag(env, in.op == OP_SRCTAG ? ec.srow : ec.drow, in.a, in.b, in.mode,
                                  constVal(in.t2, in.imm, 0, env.pool), in.op == OP_DSTTAG);

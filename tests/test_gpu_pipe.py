@@ -121,14 +121,19 @@ def test_pipe_empty_input_keeps_types(rmat):
     "GO 2 STEPS FROM $-.id OVER e WHERE e.p0 < 3 YIELD e._dst, e.p1 % 5",
     "GO 1 TO 3 STEPS FROM $-.id OVER e REVERSELY WHERE e.p0 < 2 YIELD e._dst, e._src",
     "GO 3 STEPS FROM $-.id OVER e BIDIRECT YIELD DISTINCT e._dst",
+    # reading the input: (frontier row, input row) entries, $-.x from the device input table
+    "GO 2 STEPS FROM $-.id OVER e WHERE e.p0 < $-.w / 20 YIELD $-.w, $-.nm, e._dst, e.p0 + $-.w",
+    "GO FROM $-.id OVER e WHERE $-.w > 90 || e.p0 == 3 YIELD DISTINCT $-.nm, e.p0 % 4",
+    "GO 1 TO 2 STEPS FROM $-.id OVER e REVERSELY WHERE e.p0 < 2 YIELD upper($-.nm) + \"/\" + (string)$-.w, e._dst",
 ])
 def test_multi_root_walk_in_batches(rmat, q):
-    """A multi-step sentence that reads nothing of its input walks from 64 distinct input vids at a time
-    (root sets over the frontier rows, GoExecutor's back tracker as bitmasks), not once per vid: the
-    input here has ~300 distinct vids and duplicates, the rows equal the oracle's back-tracker result."""
+    """A sentence from an input walks from 64 distinct input vids at a time (root sets over the frontier
+    rows, GoExecutor's back tracker as bitmasks), not once per vid or per input row: the input here has
+    179 distinct vids (3 walks), 234 rows and duplicates; the rows equal the oracle's back-tracker result.
+    Sentences that read $-.x evaluate it per (frontier row, input row) entry on the device."""
     ds, o, e = rmat
     seeds = ", ".join(str(int(v)) for v in datagen.sample_vids(4242, 1 << ds.scale, 20))
-    first = f"GO FROM {seeds} OVER e YIELD e._dst AS id"
+    first = f"GO FROM {seeds} OVER e YIELD e._dst AS id, e.p0 AS w, $$.vt.name AS nm"
     full = f"{first} | {q}"
     ids = {r[0][1] for r in pipeline.run(o, ds.space, first).rows}
     assert len(ids) > 128
