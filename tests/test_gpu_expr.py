@@ -211,6 +211,7 @@ STRING_YIELDS = [
     "substr(e.s, 2, 3)", "substr(e.s, -3, 2)", "substr(e.s, e.a, 2)", "e.s + \"!\"", "\"<\" + upper(e.s) + \">\"",
     "(string)e.a", "(string)e.a + e.s", "trim(lower(e.s))", "length(rpad(e.s, 20, \"xyz\"))",
     "lower($^.t.name) + \"/\" + upper($$.t.name)", "(string)(e.a > 0)", "hash(lower(e.s))",
+    "(string)(e.a * 1.0)", "(string)floor(e.b)", "(string)(e.a * 0.0)", "(string)(e.a * 1e14)",
 ]
 
 
@@ -274,7 +275,8 @@ def test_strings_longer_than_a_builder_buffer_are_refused(env):
     ds, o, e = env
     for q in ("GO FROM 5 OVER e YIELD upper(e.s)", "GO FROM 5 OVER e YIELD e.s + e.s",
               "GO FROM 5 OVER e WHERE lower(e.s) != \"\" YIELD e._dst",
-              "GO FROM 6 OVER e YIELD (double)e.s"):         # 1.79e308: strtod's big-number rounding
+              "GO FROM 6 OVER e YIELD (double)e.s",          # 1.79e308: strtod's big-number rounding
+              "GO FROM 3 OVER e YIELD (string)e.b"):         # a non-integral double: shortest round trip
         with pytest.raises(engine.EngineError) as x:
             e.go(ds.space, ngql.parse_go(q))
         assert x.value.code == engine.E_UNSUPPORTED, q
