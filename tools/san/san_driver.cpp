@@ -200,6 +200,11 @@ void compileBoth(const ExprNode& n, const Space& sp) {
     Program q;
     (void)compileGraphd(n, gc, q, err);
     for (const Insn& in : q.code) (void)in;
+    // the pipe form: $-.x / $var.x read from an input table (OP_INPUT)
+    static const std::map<std::string, int32_t> inputCols = {{"a", 0}, {"b", 1}, {"id", 2}};
+    gc.inputCols = &inputCols;
+    Program q2;
+    (void)compileGraphd(n, gc, q2, err);
     (void)exprType(n, sp);
 }
 
