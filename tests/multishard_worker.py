@@ -9,6 +9,7 @@ its rows as sorted 128-bit digests (oracle.digest_columns, the test checker) in 
 parent merges them as graphd merges storage responses.
 
 Usage: python tests/multishard_worker.py RANK WORLD PORT OUT.json SCALE QUERIES.json [jit|vm] [full|plain]
+       [snap:DIR | snapmix:DIR]
 (full: in-edges + tag `vt`, the multi-shard parity graph; plain: the bench / C2 layout)
 """
 import datetime
@@ -33,15 +34,51 @@ def main():
     from oracle import oracle
 
     queries = json.load(open(qfile))
-    rows = datagen.rmat(scale, 16, 42, 100, full, full, rank=rank, world=world, threads=4)
-    e = engine.Engine(0, rank, world, exchange=engine.dist_exchange())
-    e.set_flag("jit", 1 if mode == "jit" else 0)
-    e.add_space(datagen.RMAT_SPACE, 100)
-    for is_edge, sid, name, fields in datagen.rmat_schemas(full):
-        e.add_schema(datagen.RMAT_SPACE, is_edge, sid, name, fields)
-    e.load_kv(datagen.RMAT_SPACE, *rows.arrays())
-    rows.free()
-    e.commit(datagen.RMAT_SPACE)
+    snap = sys.argv[9] if len(sys.argv) > 9 else ""
+
+    def fresh():
+        x = engine.Engine(0, rank, world, exchange=engine.dist_exchange())
+        x.set_flag("jit", 1 if mode == "jit" else 0)
+        x.add_space(datagen.RMAT_SPACE, 100)
+        for is_edge, sid, name, fields in datagen.rmat_schemas(full):
+            x.add_schema(datagen.RMAT_SPACE, is_edge, sid, name, fields)
+        return x
+
+    def committed(seed):
+        x = fresh()
+        rows = datagen.rmat(scale, 16, seed, 100, full, full, rank=rank, world=world, threads=4)
+        x.load_kv(datagen.RMAT_SPACE, *rows.arrays())
+        rows.free()
+        x.commit(datagen.RMAT_SPACE)
+        return x
+
+    e = committed(42)
+    if snap:
+        # snap:DIR  every shard saves its snapshot, and a fresh context per shard opens it (collective:
+        #           the shards check they hold snapshots of one commit); the queries run on those
+        # snapmix:DIR  shard 1 opens a snapshot of another commit: every shard's open must fail
+        kind, d = snap.split(":", 1)
+        e.save_snapshot(datagen.RMAT_SPACE, os.path.join(d, f"a{rank}.snap"), "a")
+        e.close()
+        if kind == "snapmix":
+            other = committed(43)
+            other.save_snapshot(datagen.RMAT_SPACE, os.path.join(d, f"b{rank}.snap"), "b")
+            other.close()
+        e = fresh()
+        path = os.path.join(d, f"{'b' if kind == 'snapmix' and rank == 1 else 'a'}{rank}.snap")
+        try:
+            e.open_snapshot(datagen.RMAT_SPACE, path)
+            opened = ""
+        except engine.EngineError as x:
+            opened = str(x)
+        if kind == "snapmix":
+            with open(out, "w") as f:
+                json.dump({"open_error": opened}, f)
+            e.close()
+            dist.barrier()
+            dist.destroy_process_group()
+            return
+        assert not opened, opened
     res = []
     default_pf = e.get_flag("pull_factor")
     for i, q in enumerate(queries):

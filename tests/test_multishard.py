@@ -115,7 +115,7 @@ MS_QUERIES = [
 ]
 
 
-def _run_shards(tmp_path, world, scale, queries, mode="jit", layout="full", timeout=400):
+def _run_shards(tmp_path, world, scale, queries, mode="jit", layout="full", timeout=400, snap=""):
     """Start `world` worker processes (all on device 0, host exchange) and collect their results."""
     qfile = tmp_path / "q.json"
     qfile.write_text(json.dumps(queries))
@@ -123,7 +123,8 @@ def _run_shards(tmp_path, world, scale, queries, mode="jit", layout="full", time
     env = dict(os.environ, PYTHONPATH=ROOT)
     procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "multishard_worker.py"), str(r),
                                str(world), str(port), str(tmp_path / f"r{r}.json"), str(scale), str(qfile), mode,
-                               layout], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                               layout] + ([snap] if snap else []), env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT)
              for r in range(world)]
     logs = []
     for p in procs:
@@ -137,6 +138,8 @@ def _run_shards(tmp_path, world, scale, queries, mode="jit", layout="full", time
     for p, lg in zip(procs, logs):
         assert p.returncode == 0, lg
     shards = [json.load(open(tmp_path / f"r{r}.json")) for r in range(world)]
+    if snap.startswith("snapmix"):
+        return shards, None
     digests = [[np.load(tmp_path / f"r{r}.json.{i}.npy") for r in range(world)] for i in range(len(queries))]
     return shards, digests
 
@@ -244,3 +247,32 @@ def test_exchange_failure_fails_the_query():
         assert ei.value.code == engine.E_DEVICE and "exchange" in str(ei.value)
     finally:
         e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_multishard_snapshot_files(tmp_path):
+    """World 2: every shard saves its committed snapshot and a fresh context opens it (ngx_open_snapshot
+    is collective at world > 1: the shards compare the commit-set digest in their headers); the queries
+    on the reopened shards equal the oracle's. A shard that opens a snapshot of another commit makes
+    every shard's open fail, instead of mismatched shard bases and exchange counts."""
+    from nebula_amd import datagen
+    from oracle import oracle
+    from tests import fixtures
+
+    ds = fixtures.RmatDataset(11, with_in=True, with_tag=True)
+    o = oracle.Oracle()
+    o.set_flags(threads=8)
+    ds.load_oracle(o)
+    queries = []
+    for i, (text, push) in enumerate(MS_QUERIES[:4]):
+        seeds = datagen.sample_vids(700 + i, 1 << 11, 30)
+        queries.append({"text": text.replace("{S}", ", ".join(str(int(v)) for v in seeds)), "pushdown": push})
+    snapdir = tmp_path / "snaps"
+    snapdir.mkdir()
+    shards, digests = _run_shards(tmp_path, 2, 11, queries, snap=f"snap:{snapdir}")
+    _check_merged(o, ds.space, queries, shards, digests)
+    mixdir = tmp_path / "mix"
+    mixdir.mkdir()
+    res, _ = _run_shards(tmp_path, 2, 11, queries, snap=f"snapmix:{mixdir}")
+    assert all(r["open_error"] for r in res), res
