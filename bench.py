@@ -129,13 +129,15 @@ def main():
         eng.add_schema(datagen.RMAT_SPACE, is_edge, sid, name, fields)
     t0 = time.time()
     eng.load_kv(datagen.RMAT_SPACE, *rows.arrays())
+    # the library staged its own copy: the generator's rows go before the export doubles the footprint
+    # (C3: ~20 GB of rows per rank), unless the CPU baseline reads them
+    keep_rows = rank == 0 and world == 1 and args.cpu_budget > 0
+    if not keep_rows:
+        rows.free()
     eng.commit(datagen.RMAT_SPACE)
     info = eng.info(datagen.RMAT_SPACE)
     log(f"[rank {rank}] snapshot: {info.vertices} vertices, {info.edges} edges, "
         f"{info.device_bytes / 2**30:.2f} GiB in HBM, load+commit {time.time() - t0:.1f}s")
-    keep_rows = rank == 0 and world == 1 and args.cpu_budget > 0
-    if not keep_rows:
-        rows.free()
 
     def sentence(step, k):
         seeds = datagen.rmat_seeds(scale, k, args.ef, 42, 42 + step, threads=args.threads)

@@ -580,6 +580,45 @@ __device__ __forceinline__ void pullProbe(const PullArgs& a, const uint32_t* u, 
     open = open && ev == 0;
 }
 
+// One slice's search: true for a lane whose row has an in-neighbour in the frontier among its head
+// rounds (round 0 alone first: most reached rows hit there; then batches for the lanes still open).
+// A lane left open on a long row reserves the segments of its in-list past the head (one atomic per
+// wave) for the segment pass.
+template <int KH>
+__device__ __forceinline__ bool pullSliceHit(const PullArgs& a, const PullSlice<KH>& cur, int s, uint64_t js, int lane,
+                                             uint32_t& row) {
+    const uint32_t* hp = a.head[s] + js * (kPullK * 64) + lane;
+    bool hit = probe(a, cur.u[0] != kNoRow, cur.u[0]);
+    bool open = cur.pw != kNoRow && !hit && cur.u[0] != kNoRow && cur.nk > 1;
+    if (__any(open)) {
+        if constexpr (KH > 1) pullProbe<KH - 1>(a, cur.u + 1, open, hit);   // rounds 1 .. KH - 1
+        uint32_t u[kPullKB];
+        for (int k0 = KH; k0 < cur.nk && __any(open); k0 += kPullKB) {
+            // a batch reaching past the image re-probes its last round (kNoRow would end the lane's
+            // search, and a long row's in-list continues past the head)
+#pragma unroll
+            for (int k = 0; k < kPullKB; k++) u[k] = hp[(k0 + k < kPullK ? k0 + k : kPullK - 1) * 64];
+            pullProbe<kPullKB>(a, u, open, hit);
+        }
+    }
+    row = cur.pw & ~kPullLong;
+    const bool more = open && cur.pw != kNoRow && (cur.pw & kPullLong) != 0;
+    uint32_t nseg = 0;
+    if (more) nseg = static_cast<uint32_t>((a.ioff[s][row + 1] - a.ioff[s][row] + kPullSeg - 1) / kPullSeg);
+    if (__any(nseg != 0)) {
+        const uint64_t incl = waveInclScan(nseg, lane);
+        uint32_t base = 0;
+        if (lane == 63) base = atomicAdd(&a.ctl[0], static_cast<uint32_t>(incl));
+        base = __shfl(base, 63, 64);
+        uint64_t at = base + incl - nseg;
+        for (uint32_t k = 0; k < nseg; k++, at++) {
+            if (at < a.segCap) a.seg[at] = pullSegWord(row, s, k);
+            else atomicOr(a.err + 3, 1u);
+        }
+    }
+    return hit && cur.pw != kNoRow;
+}
+
 // PREF: waves stride over the slices, loading the next slice before probing this one; !PREF: the grid
 // has a wave per slice (no stride, no prefetch of a slice nobody probes)
 template <bool ONE, int KH, bool PREF>
@@ -595,47 +634,44 @@ __global__ __launch_bounds__(WG) void k_pull_head(PullArgs a) {
     PullSlice<KH> cur;
     pullLoad<ONE, KH>(a, j, lane, s, js, cur);
     while (true) {
-        // the next slice's loads go out before this slice's probes (software pipelining over the grid stride)
         const uint64_t jn = j + nw;
         int sn = 0;
         uint64_t jsn = 0;
         PullSlice<KH> nxt;
         if constexpr (PREF) pullLoad<ONE, KH>(a, jn < total ? jn : total - 1, lane, sn, jsn, nxt);   // unconditional
-        const uint32_t* hp = a.head[s] + js * (kPullK * 64) + lane;
-        // round 0 alone (most reached rows hit there), then the rest of the batch for the lanes still open
-        bool hit = probe(a, cur.u[0] != kNoRow, cur.u[0]);
-        bool open = cur.pw != kNoRow && !hit && cur.u[0] != kNoRow && cur.nk > 1;
-        if (__any(open)) {
-            if constexpr (KH > 1) pullProbe<KH - 1>(a, cur.u + 1, open, hit);   // rounds 1 .. KH - 1
-            uint32_t u[kPullKB];
-            for (int k0 = KH; k0 < cur.nk && __any(open); k0 += kPullKB) {
-#pragma unroll
-                // a batch reaching past the image re-probes its last round (kNoRow would end the lane's
-                // search, and a long row's in-list continues past the head)
-                for (int k = 0; k < kPullKB; k++) u[k] = hp[(k0 + k < kPullK ? k0 + k : kPullK - 1) * 64];
-                pullProbe<kPullKB>(a, u, open, hit);
-            }
-        }
-        const uint32_t row = cur.pw & ~kPullLong;
-        if (hit) a.out[row] = a.ep;
-        // an open lane of a long row: its in-list continues past the head
-        const bool more = open && cur.pw != kNoRow && (cur.pw & kPullLong) != 0;
-        uint32_t nseg = 0;
-        if (more) nseg = static_cast<uint32_t>((a.ioff[s][row + 1] - a.ioff[s][row] + kPullSeg - 1) / kPullSeg);
-        if (__any(nseg != 0)) {
-            const uint64_t incl = waveInclScan(nseg, lane);
-            uint32_t base = 0;
-            if (lane == 63) base = atomicAdd(&a.ctl[0], static_cast<uint32_t>(incl));
-            base = __shfl(base, 63, 64);
-            uint64_t at = base + incl - nseg;
-            for (uint32_t k = 0; k < nseg; k++, at++) {
-                if (at < a.segCap) a.seg[at] = pullSegWord(row, s, k);
-                else atomicOr(a.err + 3, 1u);
-            }
-        }
+        uint32_t row;
+        if (pullSliceHit<KH>(a, cur, s, js, lane, row)) a.out[row] = a.ep;
         if (!PREF || jn >= total) break;
         j = jn; s = sn; js = jsn; cur = nxt;
     }
+}
+
+// One slot: a 1024-thread workgroup per 2048-row window (32 slices, 2 per wave); the window's marks
+// gather in LDS and leave as one contiguous 2 KiB write (0 for the rows not reached: marks are
+// compared with the hop's epoch), instead of a byte store per reached row scattered over the window.
+template <int KH>
+__global__ __launch_bounds__(1024) void k_pull_win(PullArgs a) {
+    if (a.dyn != nullptr && (*a.dyn & kDynMask) < a.minE) return;
+    __shared__ uint8_t win[kPullWindow];
+    const uint64_t r0 = static_cast<uint64_t>(blockIdx.x) * kPullWindow;
+    for (int i = threadIdx.x; i < static_cast<int>(kPullWindow); i += 1024) win[i] = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t total = a.sliceEnd[0];
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+        const uint64_t j = static_cast<uint64_t>(blockIdx.x) * (kPullWindow / 64) + wid * 2 + t;
+        if (j >= total) break;
+        int s;
+        uint64_t js;
+        PullSlice<KH> cur;
+        pullLoad<true, KH>(a, j, lane, s, js, cur);
+        uint32_t row;
+        if (pullSliceHit<KH>(a, cur, s, js, lane, row)) win[row - r0] = 1;
+    }
+    __syncthreads();
+    const uint64_t n = a.V - r0 < kPullWindow ? a.V - r0 : kPullWindow;
+    for (uint64_t i = threadIdx.x; i < n; i += 1024) a.out[r0 + i] = win[i] ? a.ep : 0;
 }
 
 // Segment pass (the next launch on the stream, so every segment word is visible): a workgroup per
@@ -1192,7 +1228,14 @@ int launchPull(const PullArgs& a, hipStream_t s) {
                     else hipLaunchKernelGGL((k_pull_head<false, KH, true>), grid, dim3(WG), 0, s, a); } \
         else { if (a.n == 1) hipLaunchKernelGGL((k_pull_head<true, KH, false>), grid, dim3(WG), 0, s, a); \
                else hipLaunchKernelGGL((k_pull_head<false, KH, false>), grid, dim3(WG), 0, s, a); } } while (0)
-    if (kh == 1) NGX_PULL(1);
+    // NGX_PULL_WIN=1 (one slot): a workgroup per 2048-row window writing its marks in one piece
+    static const bool winMarks = getenv("NGX_PULL_WIN") && std::atoi(getenv("NGX_PULL_WIN")) != 0;
+    if (winMarks && a.n == 1) {
+        const dim3 wgrid(static_cast<unsigned>((slices + kPullWindow / 64 - 1) / (kPullWindow / 64)));
+        if (kh == 1) hipLaunchKernelGGL((k_pull_win<1>), wgrid, dim3(1024), 0, s, a);
+        else if (kh == 2) hipLaunchKernelGGL((k_pull_win<2>), wgrid, dim3(1024), 0, s, a);
+        else hipLaunchKernelGGL((k_pull_win<4>), wgrid, dim3(1024), 0, s, a);
+    } else if (kh == 1) NGX_PULL(1);
     else if (kh == 2) NGX_PULL(2);
     else NGX_PULL(4);
 #undef NGX_PULL
