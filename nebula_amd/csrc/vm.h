@@ -15,6 +15,7 @@
 #endif
 
 #include "ngx_device.h"
+#include "dtoa.h"
 
 namespace ngx {
 
@@ -416,11 +417,9 @@ __device__ __forceinline__ Val opCast(Val v, uint8_t t1, const VmEnv& env) {
 }
 
 // (string) cast, Expression::toString (Expressions.h:334-348), into the cast's builder buffer.
-// int64 prints as folly::to<std::string> (decimal, '-' sign), bool as "true" / "false". A double prints
-// in double-conversion's SHORTEST form (orc_expr.cpp toString): NaN, [-]Infinity, [-]0, and a double
-// holding an integer below 2^53 exactly — its shortest digits are the integer's own (a string with
-// fewer significant digits is another integer, another double), printed without an exponent since it
-// has at most 16 digits; other doubles need the shortest round-trip search: host only.
+// int64 prints as folly::to<std::string> (decimal, '-' sign), bool as "true" / "false", a double in
+// double-conversion's SHORTEST form (dtoa.h: exact shortest round-trip digits, formatted as
+// orc_expr.cpp toString does).
 __device__ __forceinline__ Val castToString(Val v, char* buf, const VmEnv& env) {
     if (v.t == V_ERR || v.t == V_STR) return v;
     if (buf == nullptr) return hostOnly(env);
@@ -428,23 +427,9 @@ __device__ __forceinline__ Val castToString(Val v, char* buf, const VmEnv& env) 
     if (v.t == V_BOOL) {
         const char* w = v.x ? "true" : "false";
         for (; w[n]; n++) buf[n] = w[n];
-    } else if (v.t == V_INT || v.t == V_DBL) {
-        bool neg = v.x < 0;
+    } else if (v.t == V_INT) {
+        const bool neg = v.x < 0;
         uint64_t u = neg ? 0ULL - static_cast<uint64_t>(v.x) : static_cast<uint64_t>(v.x);
-        if (v.t == V_DBL) {
-            const double d = dblOf(v);
-            const char* w = nullptr;
-            if (d != d) w = "NaN";
-            else if (d == __builtin_inf()) w = "Infinity";
-            else if (d == -__builtin_inf()) w = "-Infinity";
-            if (w) {
-                for (; w[n]; n++) buf[n] = w[n];
-                return mkStr(buf, n);
-            }
-            const double a = fabs(d);
-            if (!(a < 9007199254740992.0) || a != floor(a)) return hostOnly(env);
-            u = static_cast<uint64_t>(a);                 // neg: the sign bit (-0.0 prints "-0")
-        }
         uint32_t digits = 1;
         for (uint64_t t = u; t >= 10; t /= 10) digits++;
         if (neg) buf[n++] = '-';
@@ -453,6 +438,8 @@ __device__ __forceinline__ Val castToString(Val v, char* buf, const VmEnv& env) 
             u /= 10;
         }
         n += digits;
+    } else if (v.t == V_DBL) {
+        n = static_cast<uint32_t>(dtoa::format(dblOf(v), buf));     // at most 25 bytes
     } else {
         return hostOnly(env);
     }
