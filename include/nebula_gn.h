@@ -77,7 +77,7 @@ typedef int32_t (*ngx_exchange_fn)(void* user, int32_t op, const void* send, voi
 typedef struct {
     int32_t device;               /* HIP device ordinal */
     int32_t rank;                 /* this shard (GPU) 0..world-1 */
-    int32_t world;                /* shards on the node; part p lives on shard p % world */
+    int32_t world;                /* shards on the node (1..64); part p lives on shard p % world */
     const void* nccl_unique_id;   /* 128-byte ncclUniqueId when world > 1 and no host exchange */
     ngx_exchange_fn exchange;     /* optional: host collective instead of RCCL (may be NULL) */
     void* exchange_user;

@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <random>
 #include <cstdio>
 #include <cstdlib>
 #include <ctime>
@@ -1139,7 +1140,7 @@ int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
     c->device = cfg->device;
     c->rank = cfg->rank;
     c->world = cfg->world < 1 ? 1 : cfg->world;
-    if (c->rank < 0 || c->rank >= c->world || c->device < 0) return NGX_E_BAD_ARGUMENT;
+    if (c->rank < 0 || c->rank >= c->world || c->device < 0 || c->world > kMaxWorld) return NGX_E_BAD_ARGUMENT;
     if (const char* j = std::getenv("NGX_JIT")) c->jitOn = std::string(j) != "0";
     if (const char* t = std::getenv("NGX_RCCL_TIMEOUT_MS")) c->rcclTimeoutMs = std::max<int64_t>(1, std::atoll(t));
     int n = 0;
@@ -1350,17 +1351,22 @@ int32_t ngx_commit(ngx_ctx* c, int32_t space) {
         std::vector<std::vector<std::pair<int32_t, int64_t>>> tables(c->world);
         std::vector<std::pair<int32_t, int64_t>> mine(hg->vid.size());
         for (size_t i = 0; i < mine.size(); i++) mine[i] = {hg->vpart[i], hg->vid[i]};
+        std::vector<uint64_t> nonces(c->world);
+        const uint64_t nonce = std::random_device{}() ^ (static_cast<uint64_t>(std::random_device{}()) << 32) ^
+                               static_cast<uint64_t>(std::chrono::steady_clock::now().time_since_epoch().count());
         if (c->world == 1) {
             tables[0] = mine;
+            nonces[0] = nonce;
         } else {
-            // allgather counts, then the (part, vid) tables, through RCCL
-            uint64_t* dcnt = c->misc.get<uint64_t>(c->world * 2);
-            uint64_t myCount = mine.size();
-            HIP_OK(hipMemcpyAsync(dcnt + c->world, &myCount, 8, hipMemcpyHostToDevice, c->stream));
-            allGather(c, dcnt + c->world, dcnt, 8);
-            std::vector<uint64_t> counts(c->world);
-            HIP_OK(hipMemcpyAsync(counts.data(), dcnt, 8 * c->world, hipMemcpyDeviceToHost, c->stream));
+            // allgather (count, commit nonce) pairs, then the (part, vid) tables, through RCCL
+            uint64_t* dcnt = c->misc.get<uint64_t>(c->world * 2 + 2);
+            uint64_t myCount[2] = {mine.size(), nonce};
+            HIP_OK(hipMemcpyAsync(dcnt + 2 * c->world, myCount, 16, hipMemcpyHostToDevice, c->stream));
+            allGather(c, dcnt + 2 * c->world, dcnt, 16);
+            std::vector<uint64_t> cn(2 * c->world), counts(c->world);
+            HIP_OK(hipMemcpyAsync(cn.data(), dcnt, 16 * c->world, hipMemcpyDeviceToHost, c->stream));
             HIP_OK(hipStreamSynchronize(c->stream));
+            for (int w = 0; w < c->world; w++) { counts[w] = cn[2 * w]; nonces[w] = cn[2 * w + 1]; }
             uint64_t maxc = *std::max_element(counts.begin(), counts.end());
             std::vector<int64_t> packed(maxc * 2, 0);
             for (size_t i = 0; i < mine.size(); i++) { packed[2 * i] = mine[i].first; packed[2 * i + 1] = mine[i].second; }
@@ -1379,7 +1385,7 @@ int32_t ngx_commit(ngx_ctx* c, int32_t space) {
             }
         }
         resolveDstRows(*sp, *hg, tables, c->world);
-        hg->commitDigest = tablesDigest(tables);
+        hg->commitDigest = tablesDigest(tables, nonces);
         if (hg->shardBase.empty()) { hg->shardBase = {0, hg->vid.size()}; hg->vglobal = hg->vid.size(); }
         hg->gbase = hg->shardBase[c->rank];
         sp->dev = upload(*hg, *sp);
@@ -1653,11 +1659,15 @@ void exchangeFrontier(ngx_ctx* c, const DeviceGraph& d, uint8_t epoch) {
     uint64_t* recv = c->recvBits.get<uint64_t>(std::max<uint64_t>(maxWords * W, 1));
     uint64_t myRows = sb[c->rank + 1] - sb[c->rank];
     uint64_t myWords = (myRows + 63) / 64;
-    for (int q = 0; q < W; q++) {
-        if (q == c->rank) continue;
-        uint64_t n = sb[q + 1] - sb[q];
-        if (launchPack(c->visited.get<uint8_t>(d.vglobal), epoch, sb[q], n, send + q * maxWords, c->stream)) throw Error{NGX_E_DEVICE, "pack"};
-    }
+    ExchangeArgs xa{};
+    xa.visited = c->visited.get<uint8_t>(d.vglobal);
+    xa.epoch = epoch;
+    for (int q = 0; q <= W; q++) xa.sb[q] = sb[q];
+    xa.world = W;
+    xa.rank = c->rank;
+    xa.words = maxWords;
+    xa.bits = send;
+    if (launchPackPeers(xa, c->stream)) throw Error{NGX_E_DEVICE, "pack"};
     c->lastXchgBytes = 0;
     for (int q = 0; q < W; q++) if (q != c->rank) c->lastXchgBytes += (sb[q + 1] - sb[q] + 63) / 64 * 8;
     if (c->xchg) {
@@ -1673,11 +1683,8 @@ void exchangeFrontier(ngx_ctx* c, const DeviceGraph& d, uint8_t epoch) {
         NCCL_OK(ncclGroupEnd());
         rcclWait(c, "frontier all-to-all");
     }
-    for (int q = 0; q < W; q++) {
-        if (q == c->rank) continue;
-        if (launchMerge(recv + q * maxWords, myRows, c->visited.get<uint8_t>(d.vglobal), sb[c->rank], epoch, c->stream))
-            throw Error{NGX_E_DEVICE, "merge"};
-    }
+    xa.bits = recv;
+    if (launchMergePeers(xa, c->stream)) throw Error{NGX_E_DEVICE, "merge"};
 }
 
 // grow a device buffer to `bytes`, keeping its first `keep` bytes

@@ -252,8 +252,18 @@ struct CopyBatch {
 };
 int launchCopyBatch(const CopyBatch& b, hipStream_t s);
 int launchVertexCells(const VertexCellArgs& a, hipStream_t s);
-int launchPack(const uint8_t* visited, uint8_t epoch, uint64_t lo, uint64_t n, uint64_t* bits, hipStream_t s);
-int launchMerge(const uint64_t* bits, uint64_t n, uint8_t* visited, uint64_t lo, uint8_t epoch, hipStream_t s);
+// frontier exchange, one launch each side: pack every peer q's marked rows into bits + q * words;
+// merge ORs the world - 1 received bitmaps (bits + q * words, over this shard's rows) into the marks
+struct ExchangeArgs {
+    uint8_t* visited;
+    uint8_t epoch;
+    uint64_t sb[kMaxWorld + 1];                      // shard q's rows are [sb[q], sb[q + 1])
+    int world, rank;
+    uint64_t words;                                  // bitmap stride per peer
+    uint64_t* bits;
+};
+int launchPackPeers(const ExchangeArgs& a, hipStream_t s);
+int launchMergePeers(const ExchangeArgs& a, hipStream_t s);
 
 
 }  // namespace ngx

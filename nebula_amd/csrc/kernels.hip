@@ -1053,17 +1053,25 @@ struct WriteArr {
 // ------------------------------------------------------------------------------ multi-GPU exchange
 // pack this shard's marks for peer q's rows into a bitmap: one row byte per lane (coalesced), the
 // wave's ballot is the 64-bit word of its 64 rows; merge received bitmaps into visited
-__global__ __launch_bounds__(256) void k_pack(const uint8_t* visited, uint8_t epoch, uint64_t lo, uint64_t n, uint64_t* bits) {
-    uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    bool mark = i < n && visited[lo + i] == epoch;
-    uint64_t word = __ballot(mark);
-    if ((threadIdx.x & 63) == 0 && i < n) bits[i >> 6] = word;
+// grid.y = peer; a wave's ballot is one bitmap word (the whole block leaves together for q == rank)
+__global__ __launch_bounds__(256) void k_pack(const ExchangeArgs a) {
+    const int q = blockIdx.y;
+    if (q == a.rank) return;
+    const uint64_t lo = a.sb[q], n = a.sb[q + 1] - lo;
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const bool mark = i < n && a.visited[lo + i] == a.epoch;
+    const uint64_t word = __ballot(mark);
+    if ((threadIdx.x & 63) == 0 && i < n) a.bits[q * a.words + (i >> 6)] = word;
 }
-__global__ void k_merge(const uint64_t* bits, uint64_t nwords, uint8_t* visited, uint64_t lo, uint64_t n, uint8_t epoch) {
-    uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+// one thread per own row: the OR over the peers' words (each a wave-wide broadcast load), one store
+__global__ __launch_bounds__(256) void k_merge(const ExchangeArgs a) {
+    const uint64_t lo = a.sb[a.rank], n = a.sb[a.rank + 1] - lo;
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    if ((bits[i >> 6] >> (i & 63)) & 1) visited[lo + i] = epoch;
-    (void)nwords;
+    uint64_t any = 0;
+    for (int q = 0; q < a.world; q++)
+        if (q != a.rank) any |= a.bits[q * a.words + (i >> 6)];
+    if ((any >> (i & 63)) & 1) a.visited[lo + i] = a.epoch;
 }
 
 // ------------------------------------------------------------------------------ launchers
@@ -1318,15 +1326,19 @@ int launchVertexCells(const VertexCellArgs& a, hipStream_t s) {
     return static_cast<int>(hipGetLastError());
 }
 
-int launchPack(const uint8_t* visited, uint8_t epoch, uint64_t lo, uint64_t n, uint64_t* bits, hipStream_t s) {
-    if (n == 0) return 0;
-    hipLaunchKernelGGL(k_pack, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, visited, epoch, lo, n, bits);
+int launchPackPeers(const ExchangeArgs& a, hipStream_t s) {
+    uint64_t maxRows = 0;
+    for (int q = 0; q < a.world; q++)
+        if (q != a.rank) maxRows = std::max(maxRows, a.sb[q + 1] - a.sb[q]);
+    if (maxRows == 0 || a.world < 2 || a.world > kMaxWorld) return 0;
+    hipLaunchKernelGGL(k_pack, dim3(static_cast<unsigned>((maxRows + 255) / 256), a.world), dim3(256), 0, s, a);
     return static_cast<int>(hipGetLastError());
 }
 
-int launchMerge(const uint64_t* bits, uint64_t n, uint8_t* visited, uint64_t lo, uint8_t epoch, hipStream_t s) {
-    if (n == 0) return 0;
-    hipLaunchKernelGGL(k_merge, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, bits, (n + 63) / 64, visited, lo, n, epoch);
+int launchMergePeers(const ExchangeArgs& a, hipStream_t s) {
+    const uint64_t n = a.sb[a.rank + 1] - a.sb[a.rank];
+    if (n == 0 || a.world < 2 || a.world > kMaxWorld) return 0;
+    hipLaunchKernelGGL(k_merge, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, a);
     return static_cast<int>(hipGetLastError());
 }
 

@@ -161,7 +161,10 @@ Error exportSnapshot(Space& sp, int32_t rank, int32_t world, HostGraph& out);
 uint64_t schemaDigest(const Space& sp);
 // digest of the vertex tables of every shard, in rank order: equal on all ranks of one commit (the
 // global rows dgid / shardBase encode), different for tables of different commits
-uint64_t tablesDigest(const std::vector<std::vector<std::pair<int32_t, int64_t>>>& tables);
+// the commit's identity: every shard's vertex table plus one random nonce per shard drawn at that
+// commit (two commits of identical data are still different commits)
+uint64_t tablesDigest(const std::vector<std::vector<std::pair<int32_t, int64_t>>>& tables,
+                      const std::vector<uint64_t>& nonces);
 Error writeSnapshotFile(const Space& sp, const HostGraph& g, int32_t rank, int32_t world, const std::string& path,
                         const std::string& tag);
 Error readSnapshotFile(const Space& sp, const std::string& path, int32_t rank, int32_t world, HostGraph& out,

@@ -282,13 +282,15 @@ uint64_t schemaDigest(const Space& sp) {
     return h.done();
 }
 
-uint64_t tablesDigest(const std::vector<std::vector<std::pair<int32_t, int64_t>>>& tables) {
+uint64_t tablesDigest(const std::vector<std::vector<std::pair<int32_t, int64_t>>>& tables,
+                      const std::vector<uint64_t>& nonces) {
     StreamHash h;
     for (auto& t : tables) {
         uint64_t n = t.size();
         h.add(&n, 8);
         for (auto& pv : t) { h.add(&pv.first, 4); h.add(&pv.second, 8); }
     }
+    for (uint64_t x : nonces) h.add(&x, 8);
     return h.done();
 }
 

@@ -137,7 +137,7 @@ std::vector<HostGraph> exportWorld(const ngd_rows& r, int32_t world) {
         addSchemas(sp);
         resolveDstRows(sp, gs[w], tables, world);
         gs[w].gbase = gs[w].shardBase[w];                    // as ngx_commit places the shard
-        gs[w].commitDigest = tablesDigest(tables);
+        gs[w].commitDigest = tablesDigest(tables, std::vector<uint64_t>(tables.size(), 7));
     }
     return gs;
 }
