@@ -128,6 +128,7 @@ struct ngx_ctx {
     DBuf dkTable, dkKeep, dkPre, dSrc, dDst, dRank, dType;   // YIELD DISTINCT (table, marks, compacted rows)
     std::vector<DBuf> strArena;                         // result string arenas, one per record hop (FinalArgs::strOut)
     DBuf roots[2], rootBits;                            // multi-root walk: root sets over rows, per-entry bits
+    DBuf rootSend, rootRecv;                            // world > 1: root sets of peer rows, both ways
     DBuf pwF, pwIn, pwEst, pwCf;                        // ... reading $-: (row, input row) entries, their estart / heads
     DBuf inX, inLen, inT, inStr, inDesc;                // ... the pipe's input table
     uint64_t pipeWalks = 0;                             // walks run for FROM $- / $var sentences (flag pipe_walks)
@@ -1687,6 +1688,43 @@ void exchangeFrontier(ngx_ctx* c, const DeviceGraph& d, uint8_t epoch) {
     if (launchMergePeers(xa, c->stream)) throw Error{NGX_E_DEVICE, "merge"};
 }
 
+// multi-root walk at world > 1: the expansion OR-ed root sets into next[] over global rows; every
+// shard sends peer q the sets of q's rows (next + sb[q], dense) and ORs what it receives into its own
+// rows: out[i] = next[gbase + i] | the peers' sets of row i. Dense like the frontier bitmaps, 8 B per
+// peer row: root walks serve pipes, whose frontiers are small next to a full GO's.
+void exchangeRoots(ngx_ctx* c, const DeviceGraph& d, const uint64_t* next, uint64_t* out) {
+    const int W = c->world;
+    const auto& sb = d.shardBase;
+    uint64_t maxRows = 1;
+    for (int q = 0; q < W; q++) maxRows = std::max<uint64_t>(maxRows, sb[q + 1] - sb[q]);
+    const uint64_t myRows = sb[c->rank + 1] - sb[c->rank];
+    uint64_t* recv = c->rootRecv.get<uint64_t>(maxRows * W);
+    uint64_t sent = 0;
+    for (int q = 0; q < W; q++) if (q != c->rank) sent += (sb[q + 1] - sb[q]) * 8;
+    c->lastXchgBytes += sent;
+    if (c->xchg) {
+        uint64_t* send = c->rootSend.get<uint64_t>(maxRows * W);      // equal blocks for the host collective
+        for (int q = 0; q < W; q++) {
+            const uint64_t nq = sb[q + 1] - sb[q];
+            if (q != c->rank && nq)
+                HIP_OK(hipMemcpyAsync(send + q * maxRows, next + sb[q], nq * 8, hipMemcpyDeviceToDevice, c->stream));
+        }
+        hostExchange(c, NGX_XCHG_ALLTOALL, send, recv, maxRows * 8);
+    } else {
+        NCCL_OK(ncclGroupStart());
+        for (int q = 0; q < W; q++) {
+            if (q == c->rank) continue;
+            const uint64_t nq = sb[q + 1] - sb[q];
+            if (nq) NCCL_OK(ncclSend(next + sb[q], nq * 8, ncclUint8, q, c->comm, c->stream));
+            if (myRows) NCCL_OK(ncclRecv(recv + q * maxRows, myRows * 8, ncclUint8, q, c->comm, c->stream));
+        }
+        NCCL_OK(ncclGroupEnd());
+        rcclWait(c, "root set all-to-all");
+    }
+    if (launchMergeRoots(next + d.gbase, recv, maxRows, myRows, W, c->rank, out, c->stream))
+        throw Error{NGX_E_DEVICE, "merge roots"};
+}
+
 // grow a device buffer to `bytes`, keeping its first `keep` bytes
 void growKeep(ngx_ctx* c, DBuf& b, size_t bytes, size_t keep) {
     bytes = std::max<size_t>(bytes, 64);
@@ -2072,7 +2110,6 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     PullArgs pa{};                                              // pull expansion (kernels.h launchPull)
     // world > 1: every shard pulls its own rows against the all-gathered frontier bitmap; the mirrors
     // and the decision are global (findMirrorsGlobal, one all-gather per intermediate hop)
-    if (rw && c->world != 1) return fail(c, NGX_E_UNSUPPORTED, "multi-root walk at world > 1");
     bool pullable = !rw && c->pullFactor > 0 && (c->world == 1 || (d.vglobal < (1ULL << 31) && c->world <= kMaxWorld)) &&
                     hs.n >= 1 && hs.n <= kPullMaxSlots && d.V < (1ULL << 32) && d.mirror.size() == d.slots.size();
     if (pullable) {
@@ -2163,6 +2200,22 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     for (int s = 0; s < hs.n; s++) {
         if ((ttlMask >> s & 1u) && (hs.eflags[s] != nullptr || ttlCol[s] >= 0)) intermediateChecks = true;
     }
+    if (rw && c->world > 1) {
+        // a root walk cannot run over a storage mask (below); at world > 1 the shards agree on that
+        // before the first exchange, so all of them fall back together (a shard's rows decide whether
+        // its slots carry flags)
+        bool maskPossible = capped;
+        const uint32_t checked = ttlMask | (recordFrom < steps ? recordPropsMask : 0u);
+        for (int s = 0; s < hs.n; s++)
+            if ((checked >> s & 1u) && (hs.eflags[s] != nullptr || ttlCol[s] >= 0)) maskPossible = true;
+        const uint64_t mine = maskPossible ? 1 : 0;
+        const std::vector<uint8_t> all = gatherHost(c, &mine, sizeof(mine));
+        for (int w = 0; w < c->world; w++) {
+            uint64_t x;
+            std::memcpy(&x, all.data() + w * sizeof(x), sizeof(x));
+            if (x) return fail(c, NGX_E_UNSUPPORTED, "multi-root walk over a storage mask (TTL / max-edges cap)");
+        }
+    }
     const bool dyn = !rw && c->dynHops && c->world == 1 && lbCompact && hs.n > 0 && !capped && recordFrom == steps && !pushInvalid &&
                      !intermediateChecks && !svids.empty() && svids.size() <= kSeedFuseMax &&
                      svids.size() * static_cast<uint64_t>(hs.n) <= kSeedFuseMax && d.vindex.slots != nullptr;
@@ -2241,8 +2294,9 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     uint64_t* rootsCur = nullptr;
     uint64_t* rootsNext = nullptr;
     if (rw) {
+        // cur: this shard's rows; next: global rows (world > 1: peers' rows exchanged after each hop)
         rootsCur = c->roots[0].get<uint64_t>(std::max<uint64_t>(d.V, 1));
-        rootsNext = c->roots[1].get<uint64_t>(std::max<uint64_t>(d.V, 1));
+        rootsNext = c->roots[1].get<uint64_t>(std::max<uint64_t>(d.vglobal, 1));
         HIP_OK(hipMemsetAsync(rootsCur, 0, std::max<uint64_t>(d.V, 1) * 8, c->stream));
         if (nF) {
             std::vector<uint64_t> bits(nF, 0);
@@ -2496,7 +2550,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         if (rw && E) {
             // multi-root walk: destinations take the union of their sources' roots
             if (mask) return fail(c, NGX_E_UNSUPPORTED, "multi-root walk over a storage mask (TTL / max-edges cap)");
-            HIP_OK(hipMemsetAsync(rootsNext, 0, std::max<uint64_t>(d.V, 1) * 8, c->stream));
+            HIP_OK(hipMemsetAsync(rootsNext, 0, std::max<uint64_t>(d.vglobal, 1) * 8, c->stream));
             c->timed("expand_roots", E * 16, [&] {
                 if (launchExpandRoots(F, nF, hs, rootsCur, rootsNext, marks, ep, c->stream))
                     throw Error{NGX_E_DEVICE, "expand roots"};
@@ -2509,7 +2563,13 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             });
         }
         if (c->world > 1 && !pull) {                            // a pull computed every local row already
-            c->timed("exchange", 0, [&] { exchangeFrontier(c, d, ep); });
+            c->timed("exchange", 0, [&] {
+                exchangeFrontier(c, d, ep);
+                if (rw) {                                       // E == 0: no expansion wrote next[]
+                    if (!E) HIP_OK(hipMemsetAsync(rootsNext, 0, std::max<uint64_t>(d.vglobal, 1) * 8, c->stream));
+                    exchangeRoots(c, d, rootsNext, rootsCur);   // cur is dead after the expansion
+                }
+            });
             c->addBytes("exchange", c->lastXchgBytes);
             R.hopXchg.push_back(c->lastXchgBytes);
         }
@@ -2575,7 +2635,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         }
         if (!dyn) R.hopNext.push_back(nF);
         F = Fn;
-        if (rw) std::swap(rootsCur, rootsNext);
+        if (rw && c->world == 1) std::swap(rootsCur, rootsNext);
         if (!dyn && nF == 0 && c->world == 1) break;            // GO_EXIT: empty frontier
     }
     if (t1) HIP_OK(hipEventRecord(t1, c->stream));
@@ -2965,9 +3025,9 @@ int32_t runPipe(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) 
     } else if (!perRow) {
         // multi-step, nothing reads the input: one multi-root walk per 64 distinct vids (root sets over
         // the frontier rows); a row from a src reached by roots R repeats once per input row of every
-        // root in R. A walk the device cannot key by root (world > 1, a storage mask) falls back to a
-        // walk per vid, before any row is kept.
-        bool batched = c->world == 1;
+        // root in R. A walk the device cannot key by root (a storage mask; at world > 1 decided by all
+        // shards together) falls back to a walk per vid, before any row is kept.
+        bool batched = true;
         std::vector<std::pair<std::unique_ptr<GoResultHolder>, std::unique_ptr<RootWalk>>> walks;
         for (size_t b0 = 0; batched && b0 < vids.size(); b0 += 64) {
             const size_t n = std::min<size_t>(64, vids.size() - b0);
@@ -3014,7 +3074,7 @@ int32_t runPipe(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) 
         // WHERE / YIELD read $-.x: one multi-root walk per 64 distinct vids, the input table on the
         // device and every record hop's entries keyed by (frontier row, input row) (RootWalk::perRow);
         // a walk per input row, values bound as constants, where the device cannot key a walk by root
-        bool batched = c->world == 1;
+        bool batched = true;
         for (uint64_t i = 0; batched && i < p.input_nrows * static_cast<uint64_t>(nc); i++) {
             const int32_t k = p.input_cells[i].kind;
             batched = k == NGX_CELL_BOOL || k == NGX_CELL_INT || k == NGX_CELL_ID || k == NGX_CELL_TIMESTAMP ||

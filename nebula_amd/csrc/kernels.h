@@ -208,6 +208,10 @@ int launchExpandRoots(const uint32_t* F, uint64_t nF, const HopSlots& hs, const 
                       uint8_t* visited, uint8_t epoch, hipStream_t s);
 int launchScatterRoots(const uint32_t* F, uint64_t n, const uint64_t* bits, uint64_t* roots, hipStream_t s);
 int launchGatherRoots(const uint32_t* F, uint64_t n, const uint64_t* roots, uint64_t* out, hipStream_t s);
+// world > 1 multi-root walk: out[i] = own[i] | recv[q * stride + i] over the peers q != rank (the root
+// sets the peers' expansions gave this shard's rows), i < n
+int launchMergeRoots(const uint64_t* own, const uint64_t* recv, uint64_t stride, uint64_t n, int world, int rank,
+                     uint64_t* out, hipStream_t s);
 // YIELD DISTINCT on the device (GoExecutor::processFinalResult, GoExecutor.cpp:1298-1305): one row of
 // every group of rows with equal YIELD values is kept. Values are equal when their value types are
 // equal and their bits are, doubles by value (0.0 == -0.0, NaN == NaN: what the reference's

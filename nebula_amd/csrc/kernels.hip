@@ -779,6 +779,16 @@ __global__ void k_gather_roots(const uint32_t* F, uint64_t n, const uint64_t* ro
     if (i < n) out[i] = F[i] == kNoRow ? 0 : roots[F[i]];
 }
 
+__global__ void k_merge_roots(const uint64_t* own, const uint64_t* recv, uint64_t stride, uint64_t n, int world, int rank,
+                              uint64_t* out) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t m = own[i];
+    for (int q = 0; q < world; q++)
+        if (q != rank) m |= recv[q * stride + i];
+    out[i] = m;
+}
+
 __global__ void k_mark_rows(const uint32_t* F, uint64_t n, uint8_t* marks, uint8_t ep) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i < n && F[i] != kNoRow) marks[F[i]] = ep;
@@ -1317,6 +1327,14 @@ int launchScatterRoots(const uint32_t* F, uint64_t n, const uint64_t* bits, uint
 int launchGatherRoots(const uint32_t* F, uint64_t n, const uint64_t* roots, uint64_t* out, hipStream_t s) {
     if (n == 0) return 0;
     hipLaunchKernelGGL(k_gather_roots, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, F, n, roots, out);
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchMergeRoots(const uint64_t* own, const uint64_t* recv, uint64_t stride, uint64_t n, int world, int rank,
+                     uint64_t* out, hipStream_t s) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_merge_roots, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, own, recv, stride, n,
+                       world, rank, out);
     return static_cast<int>(hipGetLastError());
 }
 

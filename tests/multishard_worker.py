@@ -16,6 +16,7 @@ import datetime
 import json
 import os
 import sys
+import types
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -30,7 +31,7 @@ def main():
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
                             timeout=datetime.timedelta(seconds=300))
-    from nebula_amd import datagen, engine, ngql
+    from nebula_amd import datagen, engine, ngql, pipeline
     from oracle import oracle
 
     queries = json.load(open(qfile))
@@ -81,7 +82,37 @@ def main():
         assert not opened, opened
     res = []
     default_pf = e.get_flag("pull_factor")
+
+    class Sharded:
+        """graphd over the shards: every shard runs the sentence on the whole input (multi-root walks
+        exchange root sets per hop), the responses are concatenated in rank order (GoExecutor merges
+        storage responses, GoExecutor.cpp:580-606) and DISTINCT applies to the merged rows."""
+
+        def go(self, space, s, **kw):
+            r = e.go(space, s, **kw)
+            mine = (r.ok, r.error, list(r.col_types) if r.ok else [], [tuple(x) for x in r.rows] if r.ok else [])
+            parts = [None] * world
+            dist.all_gather_object(parts, mine)
+            bad = [p for p in parts if not p[0]]
+            rows = [x for p in parts for x in p[3]]
+            if s.distinct:
+                seen, uniq = set(), []
+                for x in rows:
+                    if x not in seen:
+                        seen.add(x)
+                        uniq.append(x)
+                rows = uniq
+            return types.SimpleNamespace(ok=not bad, error=bad[0][1] if bad else "", rows=rows,
+                                         col_types=next((p[2] for p in parts if p[3]), parts[0][2]))
+
     for i, q in enumerate(queries):
+        if q.get("pipe"):
+            walks = e.get_flag("pipe_walks")
+            o = pipeline.run(Sharded(), datagen.RMAT_SPACE, q["text"])
+            np.save(f"{out}.{i}.npy", np.zeros((0, 2), np.uint64))
+            res.append({"ok": o.ok, "error": o.error, "rows": [list(map(list, x)) for x in o.rows],
+                        "pipe_walks": e.get_flag("pipe_walks") - walks})
+            continue
         e.set_flag("pull_factor", q.get("pull_factor", default_pf))
         pulls = e.get_flag("pull_hops")
         r = e.go(datagen.RMAT_SPACE, ngql.parse_go(q["text"]), pushdown=q.get("pushdown", True), columnar=True,

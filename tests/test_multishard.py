@@ -276,3 +276,48 @@ def test_multishard_snapshot_files(tmp_path):
     mixdir.mkdir()
     res, _ = _run_shards(tmp_path, 2, 11, queries, snap=f"snapmix:{mixdir}")
     assert all(r["open_error"] for r in res), res
+
+
+PIPE_FIRST = "GO FROM {S} OVER e YIELD e._dst AS id, e.p0 AS w, $$.vt.name AS nm"
+MS_PIPES = [
+    "{F} | GO FROM $-.id OVER e YIELD e._dst, e.p1",
+    "{F} | GO 2 STEPS FROM $-.id OVER e WHERE e.p0 > 40 YIELD e._dst, e.p0",
+    "{F} | GO 2 STEPS FROM $-.id OVER e WHERE e.p0 > $-.w YIELD $-.nm, e._dst, $-.w + e.p0",
+    "{F} | GO 1 TO 2 STEPS FROM $-.id OVER e REVERSELY YIELD $-.id, e._dst",
+    "$a = {F}; GO 2 STEPS FROM $a.id OVER e WHERE $a.w < 30 YIELD $a.w, e._dst, e.p1",
+    "{F} | GO 2 STEPS FROM $-.id OVER e YIELD DISTINCT e._dst",
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 3])
+def test_multishard_pipes(tmp_path, world):
+    """Pipes at world > 1: every shard walks the whole input (64 distinct vids per walk, root sets over
+    global rows, the peers' sets exchanged after each hop with the frontier marks) and graphd's merge
+    of the shard responses feeds the next sentence; the rows equal the oracle's single-process
+    pipeline, and the walks are batched (not one per vid)."""
+    from nebula_amd import datagen, pipeline
+    from oracle import oracle
+    from tests import fixtures
+
+    ds = fixtures.RmatDataset(11, with_in=True, with_tag=True)
+    o = oracle.Oracle()
+    o.set_flags(threads=8)
+    ds.load_oracle(o)
+    seeds = ", ".join(str(int(v)) for v in datagen.sample_vids(4242, 1 << 11, 20))
+    first = PIPE_FIRST.replace("{S}", seeds)
+    ids = {r[0][1] for r in pipeline.run(o, ds.space, first).rows}
+    assert len(ids) > 64
+    queries = [{"text": t.replace("{F}", first), "pipe": True} for t in MS_PIPES]
+    shards, _ = _run_shards(tmp_path, world, 11, queries)
+    for i, q in enumerate(queries):
+        ref = pipeline.run(o, ds.space, q["text"])
+        assert ref.ok, ref.error
+        for s in shards:
+            got = s[i]
+            assert got["ok"], (q["text"], got["error"])
+            assert fixtures.normalize_cells(got["rows"]) == fixtures.normalize_cells(ref.rows), q["text"]
+            if "STEPS" in q["text"]:
+                assert got["pipe_walks"] == (len(ids) + 63) // 64, q["text"]
+        assert len(shards[0][i]["rows"]) > 0, q["text"]
