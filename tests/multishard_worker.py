@@ -16,6 +16,7 @@ import datetime
 import json
 import os
 import sys
+import time
 import types
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -53,7 +54,9 @@ def main():
         x.commit(datagen.RMAT_SPACE)
         return x
 
+    t0 = time.time()
     e = committed(42)
+    print(f"[rank {rank}] committed in {(time.time() - t0) * 1e3:.0f} ms", file=sys.stderr, flush=True)
     if snap:
         # snap:DIR  every shard saves its snapshot, and a fresh context per shard opens it (collective:
         #           the shards check they hold snapshots of one commit); the queries run on those
@@ -108,7 +111,9 @@ def main():
     for i, q in enumerate(queries):
         if q.get("pipe"):
             walks = e.get_flag("pipe_walks")
+            t0 = time.time()
             o = pipeline.run(Sharded(), datagen.RMAT_SPACE, q["text"])
+            print(f"[rank {rank}] pipe {i}: {(time.time() - t0) * 1e3:.0f} ms", file=sys.stderr, flush=True)
             np.save(f"{out}.{i}.npy", np.zeros((0, 2), np.uint64))
             res.append({"ok": o.ok, "error": o.error, "rows": [list(map(list, x)) for x in o.rows],
                         "pipe_walks": e.get_flag("pipe_walks") - walks})

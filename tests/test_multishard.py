@@ -16,6 +16,7 @@ import os
 import socket
 import subprocess
 import sys
+import time
 
 import numpy as np
 import pytest
@@ -127,6 +128,7 @@ def _run_shards(tmp_path, world, scale, queries, mode="jit", layout="full", time
                               stderr=subprocess.STDOUT)
              for r in range(world)]
     logs = []
+    t0 = time.time()
     for p in procs:
         try:
             out, _ = p.communicate(timeout=timeout)
@@ -137,6 +139,7 @@ def _run_shards(tmp_path, world, scale, queries, mode="jit", layout="full", time
         logs.append(out.decode(errors="replace")[-3000:])
     for p, lg in zip(procs, logs):
         assert p.returncode == 0, lg
+    print(f"shards done in {time.time() - t0:.1f} s; rank 0 log tail:\n{logs[0][-1500:]}")
     shards = [json.load(open(tmp_path / f"r{r}.json")) for r in range(world)]
     if snap.startswith("snapmix"):
         return shards, None
@@ -279,12 +282,12 @@ def test_multishard_snapshot_files(tmp_path):
 
 
 PIPE_FIRST = "GO FROM {S} OVER e YIELD e._dst AS id, e.p0 AS w, $$.vt.name AS nm"
-MS_PIPES = [
+MS_PIPES = [                  # selective filters: the multiplied rows stay ~10^4-10^5 (fast to compare)
     "{F} | GO FROM $-.id OVER e YIELD e._dst, e.p1",
-    "{F} | GO 2 STEPS FROM $-.id OVER e WHERE e.p0 > 40 YIELD e._dst, e.p0",
-    "{F} | GO 2 STEPS FROM $-.id OVER e WHERE e.p0 > $-.w YIELD $-.nm, e._dst, $-.w + e.p0",
-    "{F} | GO 1 TO 2 STEPS FROM $-.id OVER e REVERSELY YIELD $-.id, e._dst",
-    "$a = {F}; GO 2 STEPS FROM $a.id OVER e WHERE $a.w < 30 YIELD $a.w, e._dst, e.p1",
+    "{F} | GO 2 STEPS FROM $-.id OVER e WHERE e.p0 > 95 YIELD e._dst, e.p0",
+    "{F} | GO 2 STEPS FROM $-.id OVER e WHERE e.p0 > $-.w + 90 YIELD $-.nm, e._dst, $-.w + e.p0",
+    "{F} | GO 1 TO 2 STEPS FROM $-.id OVER e REVERSELY WHERE e.p0 < 3 YIELD $-.id, e._dst",
+    "$a = {F}; GO 2 STEPS FROM $a.id OVER e WHERE $a.w < 5 && e.p0 < 20 YIELD $a.w, e._dst, e.p1",
     "{F} | GO 2 STEPS FROM $-.id OVER e YIELD DISTINCT e._dst",
 ]
 
