@@ -53,6 +53,9 @@ def parse():
     p.add_argument("--yield-only", action="store_true",
                    help="timed step writes only the YIELD columns (no src row array): measured 428 vs 433 us "
                         "per final hop, the src stores hide under the loads")
+    p.add_argument("--no-compact", action="store_true",
+                   help="timed step writes every result value at 8 bytes (default: compact_results, integer "
+                        "arrays at the widths of the stored columns they copy)")
     p.add_argument("--host-exchange", action="store_true",
                    help="rehearsal of the N > 1 path on one GPU: every rank on device 0, frontier exchange "
                         "through the host collective (gloo) instead of RCCL")
@@ -151,7 +154,8 @@ def main():
         key = (id(s), on_device, columnar)
         if key not in prepared:
             prepared[key] = eng.prepare_go(datagen.RMAT_SPACE, s, on_device=on_device, columnar=columnar,
-                                           yield_only=on_device and args.yield_only)
+                                           yield_only=on_device and args.yield_only,
+                                           compact=on_device and not args.no_compact)
         r = eng.go(datagen.RMAT_SPACE, prepared[key], rows=rows_, arrays=False)
         if not r.ok:
             raise RuntimeError(r.error)
@@ -163,7 +167,7 @@ def main():
 
     for s_ in plans:                                        # encoded before the timed region
         prepared[(id(s_), True, False)] = eng.prepare_go(datagen.RMAT_SPACE, s_, on_device=True,
-                                                         yield_only=args.yield_only)
+                                                         yield_only=args.yield_only, compact=not args.no_compact)
     for i in range(args.warmup):
         step(plans[i])
     log(f"[rank {rank}] warmup done")

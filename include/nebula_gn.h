@@ -270,6 +270,13 @@ typedef struct {
      * (dev_src / dev_dst / dev_rank NULL otherwise). The reference's response holds the YIELD
      * columns alone (GoExecutor::toThriftResponse); the row arrays are this library's extra. */
     int32_t yield_only;
+    /* result_on_device without DISTINCT: 1 = compact integer results. The row arrays and every YIELD
+     * column that copies one stored integer column (INT / TIMESTAMP / VID, of the only OVER type, present
+     * in every row) are written at the width that column is stored at in HBM (1, 2 or 4 bytes, signed
+     * two's complement; the src array at the width that holds every vid of the shard), so each value
+     * keeps all its bits in fewer bytes. The widths come back in dev_key_w / dev_col_w. The reference's
+     * own response carries integers as RowWriter varints (src/dataman/RowWriter.cpp), not at 8 bytes. */
+    int32_t compact_results;
 } ngx_go_plan;
 
 /* One YIELD column of a device-resident result (result_on_device), columnar in HBM, nrows entries:
@@ -320,6 +327,10 @@ typedef struct {
     const uint64_t* hop_exchange_bytes;/* world > 1: frontier bytes this shard sent per hop (0 otherwise) */
     double host_prep_ms;               /* host time from the call to the first launch (plan, programs) */
     double host_tail_ms;               /* host time after the device finished (results, checks) */
+    /* result_on_device: bytes per element of dev_src / dev_dst / dev_rank and of each dev_cols[c].x
+     * (8 unless plan.compact_results; then 1, 2, 4 or 8, signed integers below 8) */
+    int32_t dev_key_w[3];
+    const int32_t* dev_col_w;          /* ncols entries */
 } ngx_go_result;
 
 int32_t ngx_go(ngx_ctx* ctx, const ngx_go_plan* plan, ngx_go_result** out);

@@ -40,6 +40,7 @@ struct DeviceGraph {
     std::vector<uint64_t> shardBase;
     int32_t* vpart = nullptr;
     int64_t* vid = nullptr;
+    int32_t vidW = 8;                                   // narrowest signed width holding every vid of vid[]
     VIndex vindex{nullptr, 0};                          // (part, vid) -> row hash index (seed lookup)
     std::vector<DSlot> slots;
     std::vector<int32_t> mirror;                        // per slot: the slot holding its exact transpose, or -1
@@ -308,6 +309,16 @@ const void* uploadNarrow(DeviceGraph& d, const std::vector<int64_t>& v, uint64_t
     return d.upload(v.data(), n);
 }
 
+// narrowest signed width (1, 2, 4 or 8 bytes) that holds every value of v[0 .. n)
+int32_t narrowWidth(const int64_t* v, uint64_t n) {
+    int64_t lo = 0, hi = 0;
+    for (uint64_t i = 0; i < n; i++) { lo = std::min(lo, v[i]); hi = std::max(hi, v[i]); }
+    if (lo >= INT8_MIN && hi <= INT8_MAX) return 1;
+    if (lo >= INT16_MIN && hi <= INT16_MAX) return 2;
+    if (lo >= INT32_MIN && hi <= INT32_MAX) return 4;
+    return 8;
+}
+
 void uploadColumns(DeviceGraph& d, std::vector<HostColumn>& hc, uint64_t n) {
     for (auto& c : hc) {
         DCol dc{};
@@ -353,6 +364,7 @@ std::unique_ptr<DeviceGraph> upload(HostGraph& g, const Space& sp) {
     d->shardBase = g.shardBase;
     d->vpart = d->upload(g.vpart.data(), d->V);
     d->vid = d->upload(g.vid.data(), d->V);
+    d->vidW = narrowWidth(g.vid.data(), d->V);
     {
         uint64_t cap = 1024;
         while (cap < 2 * d->V) cap <<= 1;
@@ -907,6 +919,7 @@ struct GoResultHolder {
     // host_columnar: the row arrays live in the context's page-locked staging
     const int64_t *rowSrcView = nullptr, *rowDstView = nullptr, *rowRankView = nullptr;
     const int32_t* rowTypeView = nullptr;
+    std::vector<int32_t> devColW;                               // result_on_device: bytes per dev_cols[c].x
 };
 struct GnResultHolder {
     ngx_gn_result r{};
@@ -1764,9 +1777,10 @@ std::vector<int32_t> keyAliases(const Programs& progs, const std::vector<int32_t
 // size the result columns for `cap` rows (keeping `keep`) and upload their descriptors; aliased
 // key columns (keyAliases) point at oSrc/oDst/oRank, which must already be sized
 void prepareCols(ngx_ctx* c, FinalArgs& a, const std::vector<ColSpec>& spec, uint64_t cap, uint64_t keep,
-                 const std::vector<int32_t>& alias = {}) {
+                 const std::vector<int32_t>& alias = {}, const std::vector<int32_t>* widths = nullptr) {
     if (c->oCols.size() < spec.size()) c->oCols.resize(spec.size());
-    c->oColView.assign(spec.size(), OutCol{nullptr, nullptr, nullptr});
+    c->oColView.assign(spec.size(), OutCol{nullptr, nullptr, nullptr, 8, 0});
+    for (size_t y = 0; widths && y < spec.size() && y < widths->size(); y++) c->oColView[y].w = (*widths)[y];
     for (size_t y = 0; y < spec.size(); y++) {
         auto& cb = c->oCols[y];
         if (y < alias.size() && alias[y] >= 0) {
@@ -2041,6 +2055,32 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         rowMask = 0;
         for (int32_t al : yAlias) if (al >= 0) rowMask |= 1 << al;
     }
+    // compact results (plan.compact_results): the row arrays at the width of the stored key columns
+    // (src: of the shard's vid table), and a YIELD column that copies one stored integer column of the
+    // only OVER type, present in every row, at that column's width; every other column at 8 bytes
+    const bool compact = p.compact_results && p.result_on_device && !p.distinct && rw == nullptr;
+    int32_t outW[3] = {8, 8, 8};
+    std::vector<int32_t> yW(progs.yOff.size(), 8);
+    if (compact) {
+        outW[0] = d.vidW;
+        outW[1] = outW[2] = 1;
+        for (int s = 0; s < hs.n; s++) {
+            outW[1] = std::max<int32_t>(outW[1], hs.dstW[s]);
+            outW[2] = std::max<int32_t>(outW[2], hs.rankW[s]);
+        }
+        for (size_t y = 0; y < progs.yOff.size() && hs.n == 1; y++) {
+            const Insn* code = progs.code.data() + progs.yOff[y];
+            const int32_t ct = y < gp.colTypes.size() ? gp.colTypes[y] : T_UNKNOWN;
+            if (y < yAlias.size() && yAlias[y] >= 0) { yW[y] = outW[yAlias[y]]; continue; }
+            if (code[0].op != OP_ECOL || code[1].op != OP_END || code[0].b != std::abs(hs.etype[0])) continue;
+            if (!(ct == T_INT || ct == T_VID || ct == T_TIMESTAMP)) continue;
+            const HostSlot& hsl = sp.host->slots[hs.slotIdx[0]];
+            if (code[0].a < 0 || code[0].a >= static_cast<int32_t>(hsl.cols.size())) continue;
+            const auto& col = hsl.cols[code[0].a];
+            if (!col.allValid || !(col.type == T_INT || col.type == T_VID || col.type == T_TIMESTAMP)) continue;
+            if (col.width == 1 || col.width == 2 || col.width == 4) yW[y] = col.width;
+        }
+    }
     // per-query straight-line kernels (jit.cpp); the interpreter kernels otherwise
     std::shared_ptr<const JitKernels> jk, jkNoP;             // jkNoP: record hops before the last (no pushdown)
     std::vector<int64_t> jitKc;                              // their literal table (FinalArgs::kc/kl)
@@ -2053,6 +2093,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         jq.yKey = yAlias;
         jq.dstReplica = dstReplica;
         jq.rowMask = rowMask;
+        for (int k = 0; k < 3; k++) jq.outW[k] = outW[k];
+        if (compact) jq.yW = yW;
         jq.input = rw && rw->perRow;
         jitSlotConsts(jq, jitKc, jitKl);
         std::string jerr;
@@ -2080,12 +2122,44 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             return n + r.srcTag.size() + r.dstTag.size();
         };
         ky = count(yr);
-        // 8 logical bytes per edge for each filter edge prop (§8d), whatever width it is stored at
+        // 8 logical bytes per edge for each filter edge prop (§8d), whatever width it is stored at;
+        // compact results count every integer column at its stored width (the bytes this layout reads)
+        auto storedWidth = [&](const std::string& alias, const std::string& prop) -> uint64_t {
+            auto at = gp.aliasType.find(alias);
+            const SchemaSet* es = at == gp.aliasType.end() ? nullptr : sp.edge(at->second);
+            const int32_t col = es ? es->latest().index(prop) : -1;
+            int32_t w = 0;
+            for (int s = 0; col >= 0 && s < hs.n; s++) {
+                if (std::abs(hs.etype[s]) != at->second) continue;
+                const auto& cols = sp.host->slots[hs.slotIdx[s]].cols;
+                const int32_t t = col < static_cast<int32_t>(cols.size()) ? cols[col].type : T_UNKNOWN;
+                w = std::max<int32_t>(w, (t == T_INT || t == T_VID || t == T_TIMESTAMP) ? cols[col].width
+                                         : t == T_BOOL ? 1 : 8);
+            }
+            return w > 0 ? static_cast<uint64_t>(w) : 8u;
+        };
         for (auto& ap : wr.alias) {
             if (ap.second == "_src" || ap.second == "_dst" || ap.second == "_rank" || ap.second == "_type") continue;
-            kfBytes += 8;
+            kfBytes += compact ? storedWidth(ap.first, ap.second) : 8;
         }
         kfBytes += 8 * (wr.srcTag.size() + wr.dstTag.size());
+    }
+    // per scanned edge: dst + rank (8 B each in §8d; compact: their stored widths) + the filter props
+    const uint64_t keyReadBytes = compact ? static_cast<uint64_t>(outW[1] + outW[2]) : 16u;
+    // bytes written per passing edge: the row arrays and the k_y yielded props, 8 B each (§8d); compact
+    // results count each at the width it is written at
+    uint64_t rowBytes = 0;
+    for (int k = 0; k < 3; k++) rowBytes += (rowMask >> k & 1) ? (compact ? outW[k] : 8) : 0;
+    if (compact) {
+        uint64_t stored = 0, storedBytes = 0;
+        for (size_t y = 0; y < yW.size(); y++) {
+            if (y < yAlias.size() && yAlias[y] >= 0) continue;
+            stored++;
+            storedBytes += yW[y];
+        }
+        rowBytes += storedBytes + 8 * (ky > stored ? ky - stored : 0);
+    } else {
+        rowBytes += 8 * ky;
     }
 
     // ---- seeds (starts_), routed by ID_HASH; duplicates kept unless DISTINCT (:123-129)
@@ -2435,8 +2509,11 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             growKeep(c, c->oDst, cap * 8, totalRows * 8);
             growKeep(c, c->oRank, cap * 8, totalRows * 8);
             growKeep(c, c->oType, cap * 4, totalRows * 4);
-            prepareCols(c, a, colSpec, cap, totalRows, yAlias);
+            prepareCols(c, a, colSpec, cap, totalRows, yAlias, compact ? &yW : nullptr);
             a.oBase = totalRows;
+            a.oSrcW = static_cast<int8_t>(outW[0]);
+            a.oDstW = static_cast<int8_t>(outW[1]);
+            a.oRankW = static_cast<int8_t>(outW[2]);
             a.oSrc = (rowMask & 1) ? static_cast<int64_t*>(c->oSrc.p) : nullptr;
             a.oDst = (rowMask & 2) ? static_cast<int64_t*>(c->oDst.p) : nullptr;
             a.oRank = (rowMask & 4) ? static_cast<int64_t*>(c->oRank.p) : nullptr;
@@ -2458,7 +2535,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             }
             // dyn: chunks of the upper bound E; the workgroups past the real chunks return at once
             const unsigned grid = static_cast<unsigned>(gridf);
-            c->timed("final", dyn ? 0 : Ef * (16 + kfBytes), [&] {
+            c->timed("final", dyn ? 0 : Ef * (keyReadBytes + kfBytes), [&] {
                 if (grid == 0) return;
                 if (kj) {
                     void* args[] = {&a};
@@ -2471,7 +2548,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                 // GO: rows reserved by atomicAdd, and the query's error bits so far (final_kernels.h)
                 uint64_t nrows = awaitPub(c, rowsPub, a.lbStatus, &finalErrBits, errFlag);
                 haveFinalErrs = true;
-                c->addBytes("final", nrows * (8 * __builtin_popcount(rowMask) + 8 * ky));
+                c->addBytes("final", nrows * rowBytes);
                 if (rw && !rw->perRow) {                        // the rows' src vids -> their roots
                     RootWalk::Hop hop;
                     hop.rowBase = totalRows;
@@ -2681,7 +2758,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                             pullable && e >= pullMinE ? d.V * 9 * static_cast<uint64_t>(hs.n) : e * 8);
                 c->addBytes("compact_degrees", (st[h] >> kFdShift) * (8 + 24 * static_cast<uint64_t>(hs.n)));
             } else {
-                c->addBytes("final", e * (16 + kfBytes) + rows * (8 * __builtin_popcount(rowMask) + 8 * ky));
+                c->addBytes("final", e * (keyReadBytes + kfBytes) + rows * rowBytes);
             }
         }
         totalRows = rows;
@@ -2795,6 +2872,10 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                                                have ? c->oColView[y].t : nullptr});
         }
         R.r.dev_cols = R.devCols.data();
+        R.devColW.assign(nY, 8);
+        for (int k = 0; k < 3; k++) R.r.dev_key_w[k] = compact ? outW[k] : 8;
+        for (int32_t y = 0; compact && y < nY; y++) R.devColW[y] = yW[y];
+        R.r.dev_col_w = R.devColW.data();
         return NGX_OK;
     }
     // ---- results to the host: every array in one batch of D2H copies into page-locked staging

@@ -53,6 +53,8 @@ struct JitQuery {
     bool input = false;             // GO over frontier entries that carry input rows (OP_INPUT, FinalArgs::fin)
     std::vector<int32_t> ySlot;     // per column: 0 any edge, else the signed type whose edges it reads
                                     // (others get an empty cell); INT32_MIN: never an edge column
+    int32_t outW[3] = {8, 8, 8};    // bytes per row of the src / dst / rank arrays (compact results)
+    std::vector<int32_t> yW;        // bytes per value of each stored column (empty or 8: int64 bits)
 };
 
 class JitCache {

@@ -33,6 +33,8 @@ struct OutCol {
     int64_t* x;                         // value bits: int, double bits, bool 0/1, string device pointer
     uint32_t* len;                      // string lengths; nullptr when the column holds no strings
     uint8_t* t;                         // V_* (0xFF none) per row; nullptr when every row has the column's static type
+    int32_t w;                          // bytes per x element: 1, 2 or 4 (compact integer results, signed), else 8
+    int32_t pad;
 };
 
 constexpr int kJitConsts = 24;          // PUSH literals a generated kernel reads from its arguments
@@ -66,9 +68,10 @@ struct FinalArgs {
     const int32_t* yColType;            // calculateExprType per column (0 UNKNOWN: any value type), may be null
     uint32_t wIsP;                      // WHERE == pushed filter: W is implied by P where P was evaluated
     uint64_t oBase;                     // first output row of this launch (earlier record hops before it)
-    int64_t* oSrc;
+    int64_t* oSrc;                      // row arrays at oSrcW / oDstW / oRankW bytes per row (1, 2, 4; else 8)
     int64_t* oDst;
     int64_t* oRank;
+    int8_t oSrcW, oDstW, oRankW;
     int32_t* oType;
     uint32_t* oEntry;                   // frontier index of each row (GetNeighbors), may be null
     uint8_t* oFlags;                    // EF_* flags of each row's edge (GetNeighbors row encoding), may be null

@@ -909,6 +909,7 @@ struct VmEv {
     static constexpr bool kEflags = true, kTtl = true; // per-edge flags / TTL read when the slot has them
     static constexpr int kEtype = 0;                  // edge type read per slot
     static constexpr int kRowMask = 7;                // row arrays: written where FinalArgs::o* is set
+    static constexpr int kOutSrcW = 0, kOutDstW = 0, kOutRankW = 0;   // row array widths from FinalArgs
     static __device__ __forceinline__ void YV(const FinalArgs&, const EdgeCtx&, Val*) {}
     static __device__ __forceinline__ void YS(const FinalArgs&, const Val*, uint64_t, uint32_t&) {}
     static __device__ __forceinline__ bool hasP(const FinalArgs& a) { return a.P != nullptr; }
@@ -928,7 +929,7 @@ struct VmEv {
                 if (v.t == V_ERR) errs |= 1u;
                 else if (a.yColType != nullptr && !cellTypeOk(a.yColType[y], v.t)) errs |= 4u;
             }
-            gst<int64_t>(oc.x, o, v.x);
+            storeW(oc.x, oc.w, o, v.x);
             if (oc.len) gst<uint32_t>(oc.len, o, v.len);
             if (oc.t) gst<uint8_t>(oc.t, o, v.t);
         }

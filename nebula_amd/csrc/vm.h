@@ -87,6 +87,26 @@ __device__ __forceinline__ int64_t loadWT(const void* p, int32_t w, uint64_t i) 
     else return loadW(p, w, i);
 }
 
+// element i of an integer result array at width w (1, 2 or 4 bytes, two's complement; else 8): compact
+// device results (ngx_go_plan::compact_results) hold each integer column at the width of the stored
+// column it copies, so the store keeps every bit of the value
+__device__ __forceinline__ void storeW(void* p, int32_t w, uint64_t i, int64_t v) {
+    switch (w) {
+        case 1: gst<int8_t>(p, i, static_cast<int8_t>(v)); break;
+        case 2: gst<int16_t>(p, i, static_cast<int16_t>(v)); break;
+        case 4: gst<int32_t>(p, i, static_cast<int32_t>(v)); break;
+        default: gst<int64_t>(p, i, v); break;
+    }
+}
+template <int W>                        // width known at compile time (generated kernels); 0: runtime w
+__device__ __forceinline__ void storeWT(void* p, int32_t w, uint64_t i, int64_t v) {
+    if constexpr (W == 1) gst<int8_t>(p, i, static_cast<int8_t>(v));
+    else if constexpr (W == 2) gst<int16_t>(p, i, static_cast<int16_t>(v));
+    else if constexpr (W == 4) gst<int32_t>(p, i, static_cast<int32_t>(v));
+    else if constexpr (W == 8) gst<int64_t>(p, i, v);
+    else storeW(p, w, i, v);
+}
+
 __device__ __forceinline__ Val mkInt(int64_t v) { return Val{v, 0, V_INT}; }
 __device__ __forceinline__ Val mkBool(bool v) { return Val{v ? 1 : 0, 0, V_BOOL}; }
 __device__ __forceinline__ Val mkDbl(double d) { return Val{__double_as_longlong(d), 0, V_DBL}; }

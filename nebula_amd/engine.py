@@ -105,7 +105,7 @@ class GoPlan(ctypes.Structure):
                 ("host_columnar", c_i32), ("input_vid_col", ctypes.c_char_p), ("input_var", ctypes.c_char_p),
                 ("input_ncols", c_i32), ("input_names", P(ctypes.c_char_p)), ("input_types", P(c_i32)),
                 ("input_nrows", c_u64), ("input_cells", P(Cell)), ("input_strings", ctypes.c_char_p),
-                ("yield_only", c_i32)]
+                ("yield_only", c_i32), ("compact_results", c_i32)]
 
 
 _CELL_KIND = {"empty": 0, "bool": 1, "int": 2, "id": 3, "float": 4, "double": 5, "str": 6, "timestamp": 21}
@@ -142,7 +142,8 @@ class GoResultC(ctypes.Structure):
                 ("device_ms", c_dbl), ("dev_src", ctypes.c_void_p), ("dev_dst", ctypes.c_void_p),
                 ("dev_rank", ctypes.c_void_p), ("dev_type", ctypes.c_void_p), ("dev_cols", ctypes.c_void_p),
                 ("dev_type_const", ctypes.c_int32), ("host_cols", ctypes.c_void_p),
-                ("hop_exchange_bytes", P(c_u64)), ("host_prep_ms", c_dbl), ("host_tail_ms", c_dbl)]
+                ("hop_exchange_bytes", P(c_u64)), ("host_prep_ms", c_dbl), ("host_tail_ms", c_dbl),
+                ("dev_key_w", c_i32 * 3), ("dev_col_w", P(c_i32))]
 
 
 class Stat(ctypes.Structure):
@@ -286,6 +287,8 @@ class GoResult:
     nrows: int = 0
     # on_device + fetch: the HBM result copied back as arrays (x, len or None, type or None) per column
     dev_cols: List[tuple] = field(default_factory=list)
+    # on_device: ([src, dst, rank] widths, per-column widths) in bytes; 8 unless compact
+    dev_widths: Optional[tuple] = None
     digests: object = None               # columnar + digest_fn: whatever digest_fn returned
     host_prep_ms: float = 0.0            # library host time before the first launch / after the device
     host_tail_ms: float = 0.0
@@ -458,7 +461,7 @@ class Engine:
     def go(self, space: int, s: Union[str, ngql.GoSentence], pushdown: bool = True, now_sec: int = 0,
            raise_on_error: bool = False, rows: bool = True, on_device: bool = False, fetch: bool = False,
            columnar: bool = False, digest_fn=None, arrays: bool = True, input=None,
-           yield_only: bool = False) -> GoResult:
+           yield_only: bool = False, compact: bool = False) -> GoResult:
         """Run one GO. rows=False skips decoding cells into Python tuples; on_device=True leaves the
         result rows in HBM (GoResult.nrows and the statistics only); with fetch=True the HBM arrays
         (src/dst/rank/type and the columnar YIELD columns) are copied back into the result.
@@ -467,7 +470,9 @@ class Engine:
         digest_fn(col_types, nrows, x_ptrs, len_ptrs, type_ptrs) is called on the host columns
         before the result is freed (tests: large-result comparison). FROM $-.col / $var.col reads
         `input' (a nebula_amd.pipeline.Interim; None: no input, no rows). yield_only (with on_device):
-        only the YIELD columns are materialised; src / dst / rank arrays only where a column aliases them."""
+        only the YIELD columns are materialised; src / dst / rank arrays only where a column aliases them.
+        compact (with on_device): integer result arrays at the widths of the stored columns they copy
+        (ngx_go_plan.compact_results); fetch widens them back to int64 (GoResult.dev_widths keeps them)."""
         if isinstance(s, PreparedGo):                       # its own pushdown / result-placement flags
             plan, keep = s.plan, s
             on_device, columnar = bool(plan.result_on_device), bool(plan.host_columnar)
@@ -475,7 +480,7 @@ class Engine:
             if isinstance(s, str):
                 s = ngql.parse_go(s)
             keep = self.prepare_go(space, s, pushdown=pushdown, now_sec=now_sec, on_device=on_device,
-                                   columnar=columnar, yield_only=yield_only, input=input)
+                                   columnar=columnar, yield_only=yield_only, input=input, compact=compact)
             plan = keep.plan
         out = P(GoResultC)()
         rc = self.L.ngx_go(self.h, ctypes.byref(plan), ctypes.byref(out))
@@ -494,16 +499,20 @@ class Engine:
                                hop_next=[r.hop_next[i] for i in range(r.nhops)],
                                hop_xchg=[r.hop_exchange_bytes[i] for i in range(r.nhops)] if r.hop_exchange_bytes else [],
                                device_ms=r.device_ms)
+                if rc == 0 and r.dev_col_w:
+                    res.dev_widths = ([r.dev_key_w[k] for k in range(3)], [r.dev_col_w[c] for c in range(r.ncols)])
                 if fetch and rc == 0:
-                    res.src = self._d2h(r.dev_src, n, np.int64) if r.dev_src else None
-                    res.dst = self._d2h(r.dev_dst, n, np.int64) if r.dev_dst else None
-                    res.rank = self._d2h(r.dev_rank, n, np.int64) if r.dev_rank else None
+                    kw = res.dev_widths[0] if res.dev_widths else [8, 8, 8]
+                    cw = res.dev_widths[1] if res.dev_widths else [8] * r.ncols
+                    res.src = self._d2h_int(r.dev_src, n, kw[0]) if r.dev_src else None
+                    res.dst = self._d2h_int(r.dev_dst, n, kw[1]) if r.dev_dst else None
+                    res.rank = self._d2h_int(r.dev_rank, n, kw[2]) if r.dev_rank else None
                     res.etype = (self._d2h(r.dev_type, n, np.int32) if r.dev_type
                                  else np.full(n, r.dev_type_const, np.int32))   # one OVER type: no column
                     cols = ctypes.cast(r.dev_cols, P(DevColumn)) if r.dev_cols else None
                     for c in range(r.ncols):
                         dc = cols[c]
-                        res.dev_cols.append((self._d2h(dc.x, n, np.int64),
+                        res.dev_cols.append((self._d2h_int(dc.x, n, cw[c]),
                                              self._d2h(dc.len, n, np.uint32) if dc.len else None,
                                              self._d2h(dc.type, n, np.uint8) if dc.type else None))
                 return res
@@ -528,7 +537,7 @@ class Engine:
             self.L.ngx_go_result_free(out)
 
     def prepare_go(self, space: int, s, pushdown: bool = True, now_sec: int = 0, on_device: bool = False,
-                   columnar: bool = False, yield_only: bool = False, input=None) -> PreparedGo:
+                   columnar: bool = False, yield_only: bool = False, input=None, compact: bool = False) -> PreparedGo:
         """Encode a GO sentence (expressions in Expression::encode bytes, vids as int64) into the C plan
         once; go() accepts the result in place of the sentence (the bench's timed loop)."""
         if isinstance(s, str):
@@ -545,6 +554,7 @@ class Engine:
                       len(yb), yarr, ylen, 1 if s.distinct else 0, 1 if pushdown else 0, now_sec,
                       1 if on_device else 0, 1 if columnar else 0)
         plan.yield_only = 1 if yield_only else 0
+        plan.compact_results = 1 if compact else 0
         keep = [starts, names, aliases, where, yb, yarr, ylen]
         if s.from_type:
             from .pipeline import Interim
@@ -615,6 +625,11 @@ class Engine:
         if n and ptr:
             self._check(self.L.ngx_device_to_host(self.h, out.ctypes.data, ptr, out.nbytes), "device_to_host")
         return out
+
+    def _d2h_int(self, ptr, n, width):
+        """A device array of n signed integers at `width` bytes each, widened to int64."""
+        dt = {1: np.int8, 2: np.int16, 4: np.int32}.get(int(width), np.int64)
+        return self._d2h(ptr, n, dt).astype(np.int64, copy=False)
 
     # ---- flags
     def set_flag(self, name: str, value: int):

@@ -113,6 +113,17 @@ def test_c2_bench_step_vs_oracle(c2):
         e.set_flag("jit", 1)
     # factor 1 pulls every intermediate hop with E >= V / 100 (hop 2 here; hop 1 scans ~1 % of V)
     assert pulls[(1, 1)] >= 1 and pulls[(0, 1)] == 0 and pulls[(default, 1)] >= 1
+    # the bench's own result placement: rows in HBM with compact integer arrays (compact_results),
+    # fetched and widened, digest for digest equal to the oracle's rows
+    got = e.go(ds.space, s, on_device=True, fetch=True, compact=True)
+    assert got.ok and got.hop_edges == ref.hop_scanned
+    key_w, col_w = got.dev_widths
+    assert key_w == [4, 4, 1] and col_w == [4, 1, 1, 8]      # src / dst vids < 2^31, rank 0, p0 < 100
+    cols = [np.ascontiguousarray(x) for x, _, _ in got.dev_cols]
+    assert all(ln is None and t is None for _, ln, t in got.dev_cols)
+    digests = oracle.digest_columns(got.col_types, got.nrows, [c.ctypes.data for c in cols], [None] * 4, [None] * 4)
+    assert got.nrows == ref.nrows and np.array_equal(digests, ref.digests)
+    del cols, got
 
 
 @pytest.mark.timeout(600)
