@@ -179,6 +179,7 @@ def main():
     dev_ms = 0.0
     hop_edges = None
     hop_xchg = None
+    result_rows_last = 0
     prep_ms = tail_ms = 0.0
     for i in range(args.steps):
         r = step(plans[args.warmup + i])
@@ -188,6 +189,7 @@ def main():
         tail_ms += r.host_tail_ms
         hop_edges = r.hop_edges
         hop_xchg = r.hop_xchg
+        result_rows_last = r.nrows
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t_start
@@ -268,7 +270,8 @@ def main():
         if os.path.exists(args.traffic) and world == 1 and scale == 22 and not args.yield_only:
             try:
                 tj = json.load(open(args.traffic))
-                if tj.get("kernel_class") == name:
+                # and on the same result layout (compact_results changes the final hop's writes)
+                if tj.get("kernel_class") == name and bool(tj.get("compact", False)) == (not args.no_compact):
                     traffic = tj.get("bytes_per_launch")
             except Exception:
                 traffic = None
@@ -280,6 +283,14 @@ def main():
                 # the HBM bytes the PMC counters measured per launch over this launch time: the kernel's
                 # real memory throughput (frac above credits the algorithmic bytes)
                 "frac_counter": round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 4) if traffic and avg_s > 0 else None}
+        if name == "final" and hop_edges and avg_s > 0:
+            # SURVEY.md §8d's figure with every field at 8 bytes: 24 B per scanned edge (dst, rank, the
+            # filter prop) + 40 B per result row (src, dst, rank, p0, p1), per launch of the last step
+            b8 = 24 * hop_edges[-1] + 40 * (result_rows_last or 0)
+            roof["algo_bytes_8d_per_launch"] = b8
+            roof["frac_8d"] = round(b8 / avg_s / 1e9 / HBM_PEAK_GBS, 4)
+            roof["bytes_model"] = ("8-byte fields (§8d)" if args.no_compact else
+                                   "§8d per-unit figure at the stored / written widths (compact_results)")
     all_ms = sum(v[1] for v in hbm.values())
     all_bytes = sum(v[2] for v in hbm.values())
 
