@@ -2068,10 +2068,12 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             outW[1] = std::max<int32_t>(outW[1], hs.dstW[s]);
             outW[2] = std::max<int32_t>(outW[2], hs.rankW[s]);
         }
-        for (size_t y = 0; y < progs.yOff.size() && hs.n == 1; y++) {
+        for (size_t y = 0; y < progs.yOff.size(); y++) {
             const Insn* code = progs.code.data() + progs.yOff[y];
             const int32_t ct = y < gp.colTypes.size() ? gp.colTypes[y] : T_UNKNOWN;
+            // an aliased key column is the row array itself, at its width, whatever the slots
             if (y < yAlias.size() && yAlias[y] >= 0) { yW[y] = outW[yAlias[y]]; continue; }
+            if (hs.n != 1) continue;
             if (code[0].op != OP_ECOL || code[1].op != OP_END || code[0].b != std::abs(hs.etype[0])) continue;
             if (!(ct == T_INT || ct == T_VID || ct == T_TIMESTAMP)) continue;
             const HostSlot& hsl = sp.host->slots[hs.slotIdx[0]];

@@ -627,7 +627,12 @@ __global__ __launch_bounds__(WG) void k_pull_head(PullArgs a) {
     const int lane = threadIdx.x & 63;
     const uint64_t nw = static_cast<uint64_t>(gridDim.x) * NW;
     const uint64_t total = a.sliceEnd[ONE ? 0 : a.n - 1];
-    uint64_t j = (static_cast<uint64_t>(blockIdx.x) * WG + threadIdx.x) >> 6;
+    // workgroups are dispatched to the 8 XCDs round robin (b % 8): logical workgroup (b % 8) * (G / 8) +
+    // b / 8 keeps consecutive logical workgroups — the 32 slices of a 2048-row window, whose mark bytes
+    // share 16 cache lines — on one XCD, so each line is dirtied in one L2 and written back whole
+    // instead of partially from up to 8 L2s
+    const uint64_t b = a.xcdRemap ? (blockIdx.x % 8u) * (gridDim.x / 8u) + blockIdx.x / 8u : blockIdx.x;
+    uint64_t j = (b * WG + threadIdx.x) >> 6;
     if (j >= total) return;
     int s;
     uint64_t js;
@@ -1238,15 +1243,23 @@ int launchPull(const PullArgs& a, hipStream_t s) {
     // prefetching its next slice while it probes the current one); NGX_PULL_GRID caps the grid
     static const uint64_t maxGrid = getenv("NGX_PULL_GRID") ? std::strtoull(getenv("NGX_PULL_GRID"), nullptr, 10) : ~0u;
     dim3 grid(static_cast<unsigned>(std::min<uint64_t>((slices + NW - 1) / NW, maxGrid)));
+    // NGX_PULL_XCD=0: workgroups in dispatch order (no XCD-aware remap of the slices)
+    static const bool xcd = !(getenv("NGX_PULL_XCD") && std::atoi(getenv("NGX_PULL_XCD")) == 0);
     // head rounds loaded with the slice before its first probe (NGX_PULL_KH: 1, 2 or 4; default 2:
     // 48.1 us at C2 against 49.9 for 4 and 50.9 for 1, and half the head bytes of 4)
     static const int kh = getenv("NGX_PULL_KH") ? std::atoi(getenv("NGX_PULL_KH")) : 2;
     const bool pref = static_cast<uint64_t>(grid.x) * NW < slices;
+    PullArgs ax = a;
+    ax.xcdRemap = 0;
+    if (xcd && !pref) {                                 // grid padded to a multiple of 8 (extra waves exit)
+        grid.x = (grid.x + 7u) & ~7u;
+        ax.xcdRemap = 1;
+    }
 #define NGX_PULL(KH) do { \
-        if (pref) { if (a.n == 1) hipLaunchKernelGGL((k_pull_head<true, KH, true>), grid, dim3(WG), 0, s, a); \
-                    else hipLaunchKernelGGL((k_pull_head<false, KH, true>), grid, dim3(WG), 0, s, a); } \
-        else { if (a.n == 1) hipLaunchKernelGGL((k_pull_head<true, KH, false>), grid, dim3(WG), 0, s, a); \
-               else hipLaunchKernelGGL((k_pull_head<false, KH, false>), grid, dim3(WG), 0, s, a); } } while (0)
+        if (pref) { if (a.n == 1) hipLaunchKernelGGL((k_pull_head<true, KH, true>), grid, dim3(WG), 0, s, ax); \
+                    else hipLaunchKernelGGL((k_pull_head<false, KH, true>), grid, dim3(WG), 0, s, ax); } \
+        else { if (a.n == 1) hipLaunchKernelGGL((k_pull_head<true, KH, false>), grid, dim3(WG), 0, s, ax); \
+               else hipLaunchKernelGGL((k_pull_head<false, KH, false>), grid, dim3(WG), 0, s, ax); } } while (0)
     // NGX_PULL_WIN=1 (one slot): a workgroup per 2048-row window writing its marks in one piece
     static const bool winMarks = getenv("NGX_PULL_WIN") && std::atoi(getenv("NGX_PULL_WIN")) != 0;
     if (winMarks && a.n == 1) {
