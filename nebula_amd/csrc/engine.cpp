@@ -125,6 +125,7 @@ struct ngx_ctx {
     DBuf cmpStatus[2];                                  // compaction tile / wave totals (kernels.h CompactArgs)
     DBuf frontierBits;                                  // the pull's frontier bitmap over global rows
     DBuf oSrc, oDst, oRank, oType, oEntry, progBuf, sendBits, recvBits, vcells, misc, oColDesc, edgeMask;
+    DBuf chunkRows;                                     // two-pass final hop: rows per chunk -> offsets
     DBuf oFlags, rowCols, rowLen, rowOff, rowBytes;     // GetNeighbors response rows (encode_rows)
     DBuf dkTable, dkKeep, dkPre, dSrc, dDst, dRank, dType;   // YIELD DISTINCT (table, marks, compacted rows)
     std::vector<DBuf> strArena;                         // result string arenas, one per record hop (FinalArgs::strOut)
@@ -203,7 +204,7 @@ struct ngx_ctx {
         if (stream) (void)hipStreamSynchronize(stream);
         spaces.clear();
         for (DBuf* b : {&visited, &F0, &F1, &estart, &tileSums, &counters, &lbStatus, &seedPart, &seedVid, &oSrc,
-                        &oDst, &oRank, &oType, &oEntry, &chunkFirst, &oColDesc, &progBuf, &sendBits, &recvBits,
+                        &oDst, &oRank, &oType, &oEntry, &chunkFirst, &oColDesc, &progBuf, &sendBits, &recvBits, &chunkRows,
                         &vcells, &misc, &edgeMask, &cmpStatus[0], &cmpStatus[1], &frontierBits, &oFlags, &rowCols, &rowLen,
                         &rowOff, &rowBytes, &pullSeg, &pullCtl, &dkTable, &dkKeep, &dkPre, &dSrc, &dDst, &dRank,
                         &dType, &dynStats}) b->release();
@@ -2537,6 +2538,20 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             }
             // dyn: chunks of the upper bound E; the workgroups past the real chunks return at once
             const unsigned grid = static_cast<unsigned>(gridf);
+            // two passes (generated kernels, host-driven hops): count each chunk's rows, scan the counts,
+            // then the write pass reads its chunk's first row instead of one atomicAdd per chunk on a
+            // single counter, which serialises at the memory side (~12 ns per chunk, tools/mb_atomic.hip).
+            // NGX_FINAL_2PASS=0 keeps the one-pass atomic reservation
+            static const bool twoPass = !(std::getenv("NGX_FINAL_2PASS") && std::atoi(std::getenv("NGX_FINAL_2PASS")) == 0);
+            a.chunkRows = nullptr;
+            if (twoPass && kj && kj->count && !dyn && grid) {
+                a.chunkRows = c->chunkRows.get<uint64_t>(static_cast<uint64_t>(grid) + 1);
+                c->timed("final_count", Ef * kfBytes, [&] {
+                    void* args[] = {&a};
+                    HIP_OK(hipModuleLaunchKernel(kj->count, grid, 1, 1, 256, 1, 1, 0, c->stream, args, nullptr));
+                    if (launchScanInPlace(a.chunkRows, grid, c->stream)) throw Error{NGX_E_DEVICE, "final count scan"};
+                });
+            }
             c->timed("final", dyn ? 0 : Ef * (keyReadBytes + kfBytes), [&] {
                 if (grid == 0) return;
                 if (kj) {

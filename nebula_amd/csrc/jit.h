@@ -24,6 +24,7 @@ namespace ngx {
 struct JitKernels {
     hipModule_t mod = nullptr;
     hipFunction_t final = nullptr;      // the fused final-hop kernel (final_kernels.h finalBody)
+    hipFunction_t count = nullptr;      // GO: its count pass (finalBody COUNT, FinalArgs::chunkRows)
 };
 
 // one compiled program segment of a query: code[off ...] up to OP_END

@@ -91,6 +91,11 @@ struct FinalArgs {
                                         // for the strings YIELD columns build; nullptr when none does
     uint32_t nStrOut;                   // columns that build strings (bits of strOutMask, y < 32)
     uint32_t strOutMask;
+    // GO final hop in two passes (generated kernels): the count pass writes each chunk's passing rows to
+    // chunkRows[chunk]; scanned in place (exclusive, [nChunks] = rows), the write pass reads its chunk's
+    // first row there instead of reserving it with an atomicAdd on one counter (~12 ns each, serialised
+    // at the memory side: 31 K chunks = 380 us at C2, tools/mb_atomic.hip). nullptr: one pass, atomicAdd
+    uint64_t* chunkRows;
 };
 
 // the row's slot of the result string arena for the j-th column that builds strings

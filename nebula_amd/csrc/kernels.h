@@ -133,6 +133,8 @@ struct RowEncArgs {
 int launchEncodeRows(const RowEncArgs& a, bool write, hipStream_t s);
 // out[0 .. n) = exclusive prefix of in, out[n] = total (3-phase scan, tileSums as launchDegreeScan)
 int launchScanU64(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tileSums, hipStream_t s);
+// v[0 .. n) -> exclusive prefix in place, v[n] = total (one 1024-thread workgroup: n up to ~1e6)
+int launchScanInPlace(uint64_t* v, uint64_t n, hipStream_t s);
 
 // final hop, one pass (interpreter kernel): a.lbStatus zeroed, ceil(E / kChunk) + 1 words; outputs
 // sized for a.oBase + a.E rows. a.oEntry set (GetNeighbors): rows in edge order, rows written = the

@@ -1202,6 +1202,11 @@ int launchEncodeRows(const RowEncArgs& a, bool write, hipStream_t s) {
     return static_cast<int>(hipGetLastError());
 }
 
+int launchScanInPlace(uint64_t* v, uint64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, s, v, n, v + n, nullptr, 0, Publish{nullptr, 0});
+    return static_cast<int>(hipGetLastError());
+}
+
 int launchScanU64(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tileSums, hipStream_t s) {
     return scan3(ArrIn{in}, n, WriteArr{out}, tileSums, out + n, s);
 }

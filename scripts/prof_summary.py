@@ -84,7 +84,7 @@ def main():
             d = dom[0]
             traffic["kernel_class"] = args.kernel_class
             # the result layout the profiled bench ran with (bench.py uses the bytes only for the same one)
-            traffic["compact"] = bool(bench and (bench.get("roofline") or {}).get("bytes_model", "").startswith("§8d per-unit"))
+            traffic["compact"] = bool(bench and ((bench.get("roofline") or {}).get("stored_width") or {}).get("compact_results"))
             traffic["kernel_name"] = d["kernel"]
             if d["fetch_bytes_x2"] is not None and d["write_bytes"] is not None:
                 traffic["bytes_per_launch"] = d["fetch_bytes_x2"] + d["write_bytes"]
