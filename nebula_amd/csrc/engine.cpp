@@ -2538,11 +2538,12 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             }
             // dyn: chunks of the upper bound E; the workgroups past the real chunks return at once
             const unsigned grid = static_cast<unsigned>(gridf);
-            // two passes (generated kernels, host-driven hops): count each chunk's rows, scan the counts,
-            // then the write pass reads its chunk's first row instead of one atomicAdd per chunk on a
-            // single counter, which serialises at the memory side (~12 ns per chunk, tools/mb_atomic.hip).
-            // NGX_FINAL_2PASS=0 keeps the one-pass atomic reservation
-            static const bool twoPass = !(std::getenv("NGX_FINAL_2PASS") && std::atoi(std::getenv("NGX_FINAL_2PASS")) == 0);
+            // NGX_FINAL_2PASS=1 (measured slower, off): count each chunk's rows, scan the counts, then the
+            // write pass reads its chunk's first row instead of one atomicAdd per chunk on a single counter
+            // (same-address atomics serialise at ~12 ns each, tools/mb_atomic.hip: 31 K chunks = 380 us
+            // alone). At C2 the write pass drops 424 -> 400 us, but the count pass costs 144 us: the chunk
+            // map (a chain of dependent loads per workgroup) dominates it, not the filter's bytes
+            static const bool twoPass = std::getenv("NGX_FINAL_2PASS") && std::atoi(std::getenv("NGX_FINAL_2PASS")) != 0;
             a.chunkRows = nullptr;
             if (twoPass && kj && kj->count && !dyn && grid) {
                 a.chunkRows = c->chunkRows.get<uint64_t>(static_cast<uint64_t>(grid) + 1);
