@@ -2098,6 +2098,9 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         jq.rowMask = rowMask;
         for (int k = 0; k < 3; k++) jq.outW[k] = outW[k];
         if (compact) jq.yW = yW;
+        // NGX_FINAL_WG=512: 512-thread workgroups of 2 CE edges (half the per-chunk reservations)
+        static const int finalWg = std::getenv("NGX_FINAL_WG") ? std::atoi(std::getenv("NGX_FINAL_WG")) : 256;
+        jq.threads = finalWg == 512 ? 512 : 256;
         jq.input = rw && rw->perRow;
         jitSlotConsts(jq, jitKc, jitKl);
         std::string jerr;
@@ -2537,7 +2540,9 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                 arenas.push_back(Arena{a.strOut, 0});
             }
             // dyn: chunks of the upper bound E; the workgroups past the real chunks return at once
-            const unsigned grid = static_cast<unsigned>(gridf);
+            // a 512-thread generated kernel covers two CE chunks per workgroup (dyn: an upper bound anyway)
+            const unsigned nt = kj ? static_cast<unsigned>(kj->threads) : 256u;
+            const unsigned grid = static_cast<unsigned>(nt == 512 && !dyn ? (Ef + 2 * kChunk - 1) / (2 * kChunk) : gridf);
             // NGX_FINAL_2PASS=1 (measured slower, off): count each chunk's rows, scan the counts, then the
             // write pass reads its chunk's first row instead of one atomicAdd per chunk on a single counter
             // (same-address atomics serialise at ~12 ns each, tools/mb_atomic.hip: 31 K chunks = 380 us
@@ -2549,7 +2554,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                 a.chunkRows = c->chunkRows.get<uint64_t>(static_cast<uint64_t>(grid) + 1);
                 c->timed("final_count", Ef * kfBytes, [&] {
                     void* args[] = {&a};
-                    HIP_OK(hipModuleLaunchKernel(kj->count, grid, 1, 1, 256, 1, 1, 0, c->stream, args, nullptr));
+                    HIP_OK(hipModuleLaunchKernel(kj->count, grid, 1, 1, nt, 1, 1, 0, c->stream, args, nullptr));
                     if (launchScanInPlace(a.chunkRows, grid, c->stream)) throw Error{NGX_E_DEVICE, "final count scan"};
                 });
             }
@@ -2557,7 +2562,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                 if (grid == 0) return;
                 if (kj) {
                     void* args[] = {&a};
-                    HIP_OK(hipModuleLaunchKernel(kj->final, grid, 1, 1, 256, 1, 1, 0, c->stream, args, nullptr));
+                    HIP_OK(hipModuleLaunchKernel(kj->final, grid, 1, 1, nt, 1, 1, 0, c->stream, args, nullptr));
                 } else if (launchFinal(a, c->stream, grid)) {
                     throw Error{NGX_E_DEVICE, "final"};
                 }

@@ -915,6 +915,7 @@ struct VmEv {
     static constexpr int kEtype = 0;                  // edge type read per slot
     static constexpr int kRowMask = 7;                // row arrays: written where FinalArgs::o* is set
     static constexpr int kOutSrcW = 0, kOutDstW = 0, kOutRankW = 0;   // row array widths from FinalArgs
+    static constexpr int kThreads = WG;               // 256 threads, CE edges per workgroup
     static __device__ __forceinline__ void YV(const FinalArgs&, const EdgeCtx&, Val*) {}
     static __device__ __forceinline__ void YS(const FinalArgs&, const Val*, uint64_t, uint32_t&) {}
     static __device__ __forceinline__ bool hasP(const FinalArgs& a) { return a.P != nullptr; }
