@@ -16,6 +16,8 @@
  *   ngx_load_kv / ngx_commit    the part -> CSR snapshot export: KVStore::prefix over a part
  *                               (src/kvstore/KVStore.h:108-111, NebulaStore.cpp:451-464) as dumped by
  *                               DumpEdgesTool (src/tools/dump-edges/DumpEdgesTool.cpp:17-50)
+ *   ngx_load_csr                a bulk-built shard (spark-sstfile-generator + ingest's role: offline
+ *                               tabular data -> the store, src/tools/spark-sstfile-generator)
  *   ngx_load_snapshot_rows      a part's raft snapshot stream: SnapshotManagerImpl::accessAllRowsInSnapshot
  *                               rows (src/kvstore/SnapshotManagerImpl.cpp:15-53) as Part::commitSnapshot
  *                               applies them (src/kvstore/Part.cpp:319-344), encodeKV records
@@ -119,6 +121,34 @@ int32_t ngx_commit(ngx_ctx* ctx, int32_t space);
  * vertex / edge data (system, uuid keys) are skipped at commit; rows of parts this shard does not own
  * are dropped. NGX_E_BAD_ARGUMENT (nothing staged) if the last record is truncated. */
 int32_t ngx_load_snapshot_rows(ngx_ctx* ctx, int32_t space, const uint8_t* rows, uint64_t len);
+
+/* Columnar bulk load of this shard's edges, in place of KV rows: the snapshot an offline bulk tool
+ * builds from tabular data (the role of the reference's spark-sstfile-generator + ingest,
+ * src/tools/spark-sstfile-generator, src/storage/admin), in the form ngx_commit's export would give
+ * the same edges' KV rows. The next ngx_commit uses it and drops any staged rows; the commit is
+ * collective as usual. Checked, NGX_E_BAD_ARGUMENT otherwise: the vertex table is sorted by (part, vid)
+ * without duplicates, part = ID_HASH(vid) and part % world == rank; offsets start at 0 and never
+ * decrease; within a vertex row the edges are in RocksDB key order (rank LE bytes, then dst LE bytes)
+ * with no (rank, dst) twice (one version per edge); slots have distinct signed types with a schema.
+ * Columns are the latest schema's fields in order (STRING: NGX_E_UNSUPPORTED, load KV rows). Tags
+ * of the space get no rows. */
+typedef struct {
+    int32_t etype;                /* signed edge type (-t: in-edges of t, stored under the dst's part) */
+    const uint64_t* off;          /* nvertices + 1: the edges of vertex row r are [off[r], off[r + 1]) */
+    const int64_t* dst;           /* off[nvertices] destination vids */
+    const int64_t* rank;          /* NULL: rank 0 for every edge */
+    int32_t ncols;
+    const int64_t* const* cols;   /* per field: INT / TIMESTAMP / VID values, FLOAT / DOUBLE as double
+                                   * bits, BOOL 0 / 1 */
+} ngx_csr_slot;
+typedef struct {
+    uint64_t nvertices;
+    const int32_t* vpart;
+    const int64_t* vid;
+    int32_t nslots;
+    const ngx_csr_slot* slots;
+} ngx_csr_shard;
+int32_t ngx_load_csr(ngx_ctx* ctx, int32_t space, const ngx_csr_shard* shard);
 
 /* Device snapshot file of the committed shard (CSR, destination rows, prop and tag columns), so a
  * restart skips the KV decode. `tag` (<= 63 bytes) names the checkpoint. ngx_open_snapshot needs the
@@ -281,7 +311,8 @@ typedef struct {
 
 /* One YIELD column of a device-resident result (result_on_device), columnar in HBM, nrows entries:
  *   x     value bits per row: int, double bits, bool 0/1, or a device pointer to string bytes
- *         (into the snapshot or the query's constant pool)
+ *         (into the snapshot, the query's constant pool or the result string arena of the strings a
+ *         YIELD column builds)
  *   len   string byte lengths; NULL when the column holds no strings (its static type is not STRING
  *         and not UNKNOWN)
  *   type  per-row value type (1 int, 2 double, 3 bool, 4 string); NULL when every row has the
@@ -311,7 +342,9 @@ typedef struct {
     const uint64_t* hop_edges;         /* edges scanned per hop (TEPS numerator) */
     const uint64_t* hop_next;          /* unique next-frontier vertices per hop (this shard) */
     double device_ms;                  /* HIP-event time from the first kernel to the last result write */
-    /* result_on_device: HBM arrays valid until the next call on the context (nrows entries) */
+    /* result_on_device: HBM arrays valid until the next call on the context (nrows entries). Their
+     * last writes are ordered on the context's stream: ngx_device_to_host and every later call on the
+     * context see them complete; a reader on another stream or process calls ngx_synchronize first. */
     const int64_t* dev_src;
     const int64_t* dev_dst;
     const int64_t* dev_rank;
@@ -339,6 +372,8 @@ void ngx_go_result_free(ngx_go_result* r);
 /* Copy `bytes` from device memory of this context (e.g. a result_on_device array) to host memory,
  * ordered after the context's work. */
 int32_t ngx_device_to_host(ngx_ctx* ctx, void* dst, const void* src, uint64_t bytes);
+/* Wait until all work issued on the context has completed (result_on_device arrays fully written). */
+int32_t ngx_synchronize(ngx_ctx* ctx);
 
 /* ---------------------------------------------------------------- measurement hooks */
 /* Per-kernel device times of the last ngx_go (HIP events on the engine stream), for bench.py. */
@@ -382,6 +417,10 @@ int32_t ngx_kernel_stats(ngx_ctx* ctx, const ngx_kernel_stat** out, int32_t* n);
  *   "max_edge_returned_per_vertex"  storaged's flag for the storage requests of every GO hop: at most
  *          this many edges emitted per (vertex, edge type) in key order, counted after the storage
  *          checks and the pushed filter (QueryBaseProcessor.inl:501-505); <= 0: unlimited (default).
+ *   "enable_reservoir_sampling"  storaged's FLAGS_enable_reservoir_sampling (default 0). With 1, storage
+ *          keeps a random sample of each vertex's edges (QueryBoundProcessor::processEdgeSampling,
+ *          QueryBoundProcessor.cpp:83-164): ngx_get_neighbors and ngx_go return NGX_E_UNSUPPORTED before
+ *          any work, so the caller runs the reference's CPU path (set it alike on every rank).
  *   "rccl_timeout_ms"     deadline of every RCCL collective (default 120000; env NGX_RCCL_TIMEOUT_MS).
  *          On a timeout or an asynchronous RCCL error the communicator is aborted, the call returns
  *          NGX_E_DEVICE and every later call on the context fails (the caller exits).

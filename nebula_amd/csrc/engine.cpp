@@ -125,7 +125,10 @@ struct ngx_ctx {
     DBuf cmpStatus[2];                                  // compaction tile / wave totals (kernels.h CompactArgs)
     DBuf frontierBits;                                  // the pull's frontier bitmap over global rows
     DBuf oSrc, oDst, oRank, oType, oEntry, progBuf, sendBits, recvBits, vcells, misc, oColDesc, edgeMask;
-    DBuf chunkRows;                                     // two-pass final hop: rows per chunk -> offsets
+    DBuf resvTab, resvCtl;                              // GO final hop: block tables, counters (kargs.h resv*)
+    uint64_t resvTabWords = 0;
+    uint32_t resvSeq = 0, resvLastG = 0, resvLastStride = 0, resvParity = 0;
+    const uint64_t* resvRows = nullptr;                 // the last GO final launch's row count (device word)
     DBuf oFlags, rowCols, rowLen, rowOff, rowBytes;     // GetNeighbors response rows (encode_rows)
     DBuf dkTable, dkKeep, dkPre, dSrc, dDst, dRank, dType;   // YIELD DISTINCT (table, marks, compacted rows)
     std::vector<DBuf> strArena;                         // result string arenas, one per record hop (FinalArgs::strOut)
@@ -180,6 +183,7 @@ struct ngx_ctx {
     // 680 vs 656 us, profiles/r02_dyn_*); kept as an option ("dyn_hops", NGX_DYN_HOPS=1)
     bool dynHops = false;
     bool deviceLibm = false;                            // inexact libm of row values on the device (exprc.cpp)
+    bool reservoirSampling = false;                     // storaged FLAGS_enable_reservoir_sampling: refused
     DBuf dynStats;                                      // per hop: packed (|F|, E) written by seed / compaction
     int cus = 256;                                      // compute units of the device
     // RCCL watchdog: collective work must finish within this; else the communicator is aborted
@@ -204,7 +208,7 @@ struct ngx_ctx {
         if (stream) (void)hipStreamSynchronize(stream);
         spaces.clear();
         for (DBuf* b : {&visited, &F0, &F1, &estart, &tileSums, &counters, &lbStatus, &seedPart, &seedVid, &oSrc,
-                        &oDst, &oRank, &oType, &oEntry, &chunkFirst, &oColDesc, &progBuf, &sendBits, &recvBits, &chunkRows,
+                        &oDst, &oRank, &oType, &oEntry, &chunkFirst, &oColDesc, &progBuf, &sendBits, &recvBits, &resvTab, &resvCtl,
                         &vcells, &misc, &edgeMask, &cmpStatus[0], &cmpStatus[1], &frontierBits, &oFlags, &rowCols, &rowLen,
                         &rowOff, &rowBytes, &pullSeg, &pullCtl, &dkTable, &dkKeep, &dkPre, &dSrc, &dDst, &dRank,
                         &dType, &dynStats}) b->release();
@@ -1352,16 +1356,34 @@ int32_t ngx_open_snapshot(ngx_ctx* c, int32_t space, const char* path, char* tag
     }
 }
 
+int32_t ngx_load_csr(ngx_ctx* c, int32_t space, const ngx_csr_shard* shard) {
+    if (!c || !shard) return NGX_E_BAD_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    Space* sp = findSpace(c, space);
+    if (!sp) return fail(c, NGX_E_SPACE_NOT_FOUND, "space not found");
+    auto hg = std::make_unique<HostGraph>();
+    Error e = loadCsrShard(*sp, c->rank, c->world, *shard, *hg);
+    if (e.code != NGX_OK) return fail(c, e.code, e.msg);
+    sp->loaded = std::move(hg);
+    sp->staged = StagedRows();
+    return NGX_OK;
+}
+
 int32_t ngx_commit(ngx_ctx* c, int32_t space) {
     std::lock_guard<std::mutex> g(c->mu);
     Space* sp = findSpace(c, space);
     if (!sp) return fail(c, NGX_E_SPACE_NOT_FOUND, "space not found");
     try {
         HIP_OK(hipSetDevice(c->device));
-        auto hg = std::make_unique<HostGraph>();
-        if (sp->staged.voff.empty()) sp->staged.voff.push_back(0);
-        Error e = exportSnapshot(*sp, c->rank, c->world, *hg);
-        if (e.code != NGX_OK) return fail(c, e.code, e.msg);
+        std::unique_ptr<HostGraph> hg;
+        if (sp->loaded) {                                        // ngx_load_csr: the shard is built
+            hg = std::move(sp->loaded);
+        } else {
+            hg = std::make_unique<HostGraph>();
+            if (sp->staged.voff.empty()) sp->staged.voff.push_back(0);
+            Error e = exportSnapshot(*sp, c->rank, c->world, *hg);
+            if (e.code != NGX_OK) return fail(c, e.code, e.msg);
+        }
         // vertex tables of every shard -> destination rows
         std::vector<std::vector<std::pair<int32_t, int64_t>>> tables(c->world);
         std::vector<std::pair<int32_t, int64_t>> mine(hg->vid.size());
@@ -1441,6 +1463,18 @@ int32_t ngx_device_to_host(ngx_ctx* c, void* dst, const void* src, uint64_t byte
     return NGX_OK;
 }
 
+int32_t ngx_synchronize(ngx_ctx* c) {
+    if (!c) return NGX_E_BAD_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    try {
+        HIP_OK(hipSetDevice(c->device));
+        HIP_OK(hipStreamSynchronize(c->stream));
+    } catch (const Error& e) {
+        return fail(c, e.code, e.msg);
+    }
+    return NGX_OK;
+}
+
 int32_t ngx_set_profiling(ngx_ctx* c, int32_t on) {
     std::lock_guard<std::mutex> g(c->mu);
     c->prof = on != 0;
@@ -1468,6 +1502,7 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
     if (n == "jit_async") { c->jit.async = value != 0; c->jit.device = c->device; return NGX_OK; }
     if (n == "dyn_hops") { c->dynHops = value != 0; return NGX_OK; }
     if (n == "device_libm") { c->deviceLibm = value != 0; return NGX_OK; }
+    if (n == "enable_reservoir_sampling") { c->reservoirSampling = value != 0; return NGX_OK; }
     if (n == "jit_wait") { c->jit.drain(); return NGX_OK; }
     return fail(c, NGX_E_BAD_ARGUMENT, "unknown flag " + n);
 }
@@ -1482,6 +1517,7 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "jit_async") *value = c->jit.async ? 1 : 0;
     else if (n == "dyn_hops") *value = c->dynHops ? 1 : 0;
     else if (n == "device_libm") *value = c->deviceLibm ? 1 : 0;
+    else if (n == "enable_reservoir_sampling") *value = c->reservoirSampling ? 1 : 0;
     else if (n == "pull_hops") *value = static_cast<int64_t>(c->pullHops);
     else if (n == "pipe_walks") *value = static_cast<int64_t>(c->pipeWalks);
     else if (n == "jit_compiled") *value = static_cast<int64_t>(c->jit.compiled);
@@ -1755,7 +1791,42 @@ void growKeep(ngx_ctx* c, DBuf& b, size_t bytes, size_t keep) {
 // the final kernel's look-back words: ticket / row counter, one status per chunk, the done counter
 // (chunks + 2 words); zeroed by the hop's k_chunk_first launch
 uint64_t lookBackWords(uint64_t chunks) { return chunks + 2; }
+constexpr uint64_t kStrArenaMax = uint64_t(8) << 30;   // bytes of one record hop's result string arena
 uint64_t* lookBack(ngx_ctx* c, uint64_t chunks) { return c->lbStatus.get<uint64_t>(lookBackWords(chunks)); }
+// the GO final hop's block tables (kargs.h kResv*): entries carry the launch's tag, so the table is
+// cleared only when it is (re)allocated
+// reservation geometry (kargs.h resv*) and the counters, cleared once here and then by every k_final_close
+void resvGeometry(ngx_ctx* c, FinalArgs& a) {
+    static const uint32_t G = std::getenv("NGX_RESV_G") ? std::atoi(std::getenv("NGX_RESV_G")) : 8;
+    static const uint32_t sh = std::getenv("NGX_RESV_SHIFT") ? std::atoi(std::getenv("NGX_RESV_SHIFT")) : 16;
+    static const uint32_t st = std::getenv("NGX_RESV_STRIDE") ? std::atoi(std::getenv("NGX_RESV_STRIDE")) : 32;
+    a.resvG = std::min<uint32_t>(std::max<uint32_t>(G, 1), kResvMaxGroups);
+    a.resvShift = std::max<uint32_t>(sh, 12);                  // a block holds a 512-thread chunk's rows
+    a.resvStride = std::max<uint32_t>(st, 1);
+    // two sets of counters: a launch uses one and its k_final_close clears the other for the next
+    const uint64_t words = (a.resvG + 2) * static_cast<uint64_t>(a.resvStride);
+    if (c->resvCtl.cap < 2 * words * 8 || c->resvCtl.p == nullptr || c->resvLastG != a.resvG ||
+        c->resvLastStride != a.resvStride) {
+        c->resvCtl.get<uint64_t>(2 * words);
+        HIP_OK(hipMemsetAsync(c->resvCtl.p, 0, c->resvCtl.cap, c->stream));
+        c->resvParity = 0;
+    }
+    uint64_t* base = static_cast<uint64_t*>(c->resvCtl.p);
+    a.resvCtl = base + c->resvParity * words;
+    a.resvNext = base + (1 - c->resvParity) * words;
+    c->resvParity ^= 1;
+    c->resvLastG = a.resvG;
+    c->resvLastStride = a.resvStride;
+    c->resvRows = a.resvCtl + (a.resvG + 1) * static_cast<uint64_t>(a.resvStride);
+}
+uint64_t* resvTable(ngx_ctx* c, uint64_t words) {
+    if (c->resvTabWords < words || c->resvTab.p == nullptr) {
+        c->resvTab.get<uint64_t>(words);
+        HIP_OK(hipMemsetAsync(c->resvTab.p, 0, c->resvTab.cap, c->stream));
+        c->resvTabWords = c->resvTab.cap / 8;
+    }
+    return static_cast<uint64_t*>(c->resvTab.p);
+}
 
 // YIELD columns that are exactly an edge key prop of every edge the hop expands (`e._dst`,
 // `e._src`, `e._rank` of the only OVER type, typed INT/VID): their cells equal the oSrc/oDst/oRank
@@ -1951,6 +2022,13 @@ struct RootWalk {
     struct Hop { uint64_t rowBase = 0, rows = 0; std::unordered_map<int64_t, uint64_t> rootsOf; };
     std::vector<Hop> record;                                   // per record hop: src vid -> roots
 };
+
+// FLAGS_enable_reservoir_sampling: storage keeps a random sample of each vertex's edges
+// (QueryBoundProcessor::processEdgeSampling, QueryBoundProcessor.cpp:83-164, chosen at :213; the cap
+// stops applying in collectEdgeProps, QueryBaseProcessor.inl:502). A random sample has no bit-exact
+// device counterpart, so requests under the flag go to the reference's CPU path.
+const char* const kSamplingRefused =
+    "enable_reservoir_sampling: edges are sampled at random by the CPU path (QueryBoundProcessor::processEdgeSampling)";
 
 int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, const InputBind* in = nullptr,
               RootWalk* rw = nullptr) {
@@ -2240,7 +2318,6 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     const bool lbCompact = fuseDeg && d.V < kCompactLbMaxV;
     const uint64_t cfCap = slotEdges / kChunk + 2;
     c->chunkFirst.get<uint64_t>(cfCap);
-    uint64_t* lbw = lookBack(c, std::max<uint64_t>(cfCap, kDoneOff));   // GO final words: [0] rows, [kDoneOff] done
     // compaction tile / wave totals (kernels.h CompactArgs)
     uint64_t* cmpTile = nullptr;
     uint64_t* cmpWave = nullptr;
@@ -2357,7 +2434,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             const uint64_t cf0 = (slotEdges * mult + kChunk - 1) / kChunk + 1;
             uint64_t* cf = c->chunkFirst.get<uint64_t>(std::max(cf0, cfCap));
             c->timed("seed", nF * 12 + nEnt0 * 24, [&] {
-                if (launchSeedFrontierCf(dp_, dv, nF, d.vindex, hs, F, est0, pub, cf, std::max(cf0, cfCap), lbw, 2, errFlag,
+                if (launchSeedFrontierCf(dp_, dv, nF, d.vindex, hs, F, est0, pub, cf, std::max(cf0, cfCap), nullptr, 0, errFlag,
                                          c->stream, dynStats, counters))
                     throw Error{NGX_E_DEVICE, "seed"};
             });
@@ -2421,10 +2498,9 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         const uint64_t* dynTotal = dyn ? dynStats + (h - 1) : nullptr;   // this hop's (|F|, E), device side
         uint64_t chunks = (E + kChunk - 1) / kChunk;
         uint64_t* chunkFirst = c->chunkFirst.get<uint64_t>(std::max<uint64_t>(chunks, 1));
-        uint64_t* lb = (isRecord && E) ? lbw : nullptr;        // GO final: [0] rows reserved, [kDoneOff] chunks done
         if (E && !haveHeads) {
             c->timed("chunk_first", nEnt * 16, [&] {
-                if (launchChunkFirst(estart, nEnt, chunkFirst, c->stream, lb, lb ? kDoneOff + 1 : 0))
+                if (launchChunkFirst(estart, nEnt, chunkFirst, c->stream, nullptr, 0))
                     throw Error{NGX_E_DEVICE, "chunk first"};
             });
         }
@@ -2504,13 +2580,15 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                 }
                 gridf = (Ef + kChunk - 1) / kChunk;
                 uint64_t* cf2 = c->pwCf.get<uint64_t>(std::max<uint64_t>(gridf, 1));
-                if (launchChunkFirst(est2, nEnt2, cf2, c->stream, lb, kDoneOff + 1)) throw Error{NGX_E_DEVICE, "chunk first"};
+                if (launchChunkFirst(est2, nEnt2, cf2, c->stream, nullptr, 0)) throw Error{NGX_E_DEVICE, "chunk first"};
                 HIP_OK(hipStreamSynchronize(c->stream));       // f2 / in2 leave scope
                 a.F = dF2; a.fin = dIn2; a.estart = est2; a.chunkFirst = cf2; a.nEnt = nEnt2; a.E = Ef;
                 a.env.input = rw->input;
             }
-            // outputs sized for every edge passing (rows are written in the same launch)
-            uint64_t cap = totalRows + Ef;
+            // outputs sized for every edge passing (rows are written in the same launch), plus the groups'
+            // partly filled last blocks (kargs.h resv*)
+            resvGeometry(c, a);
+            uint64_t cap = totalRows + Ef + resvSlack(a);
             growKeep(c, c->oSrc, cap * 8, totalRows * 8);
             growKeep(c, c->oDst, cap * 8, totalRows * 8);
             growKeep(c, c->oRank, cap * 8, totalRows * 8);
@@ -2525,9 +2603,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             a.oRank = (rowMask & 4) ? static_cast<int64_t*>(c->oRank.p) : nullptr;
             a.oType = constType ? nullptr : static_cast<int32_t*>(c->oType.p);
             a.oEntry = nullptr;
-            a.lbStatus = lb;
-            a.done = reinterpret_cast<uint32_t*>(lb + kDoneOff);
-            Publish rowsPub = dyn ? Publish{nullptr, 0} : nextPub(c);   // the last chunk publishes the row count
+            a.lbStatus = nullptr;
+            Publish rowsPub = dyn ? Publish{nullptr, 0} : nextPub(c);   // k_final_close publishes the row count
             a.rowsPub = rowsPub.slot;
             a.rowsSeq = rowsPub.seq;
             a.dynTotal = dynTotal;
@@ -2535,29 +2612,25 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             a.nStrOut = nStrOut;
             a.strOutMask = strOutMask;
             if (nStrOut) {
+                // one 64-byte slot per (edge, building column): past kStrArenaMax the caller's CPU path
+                // runs the query instead of a device allocation failure
+                const uint64_t arenaBytes = (Ef + resvSlack(a)) * nStrOut * static_cast<uint64_t>(kStrBuildBytes);
+                if (arenaBytes > kStrArenaMax)
+                    return fail(c, NGX_E_UNSUPPORTED, "built strings of " + std::to_string(Ef) + " edges exceed the device string arena");
                 if (c->strArena.size() <= arenas.size()) c->strArena.resize(arenas.size() + 1);
-                a.strOut = c->strArena[arenas.size()].get<char>(std::max<uint64_t>(Ef, 1) * nStrOut * static_cast<uint64_t>(kStrBuildBytes));
+                a.strOut = c->strArena[arenas.size()].get<char>((Ef + resvSlack(a)) * nStrOut * static_cast<uint64_t>(kStrBuildBytes));
                 arenas.push_back(Arena{a.strOut, 0});
             }
             // dyn: chunks of the upper bound E; the workgroups past the real chunks return at once
             // a 512-thread generated kernel covers two CE chunks per workgroup (dyn: an upper bound anyway)
             const unsigned nt = kj ? static_cast<unsigned>(kj->threads) : 256u;
             const unsigned grid = static_cast<unsigned>(nt == 512 && !dyn ? (Ef + 2 * kChunk - 1) / (2 * kChunk) : gridf);
-            // NGX_FINAL_2PASS=1 (measured slower, off): count each chunk's rows, scan the counts, then the
-            // write pass reads its chunk's first row instead of one atomicAdd per chunk on a single counter
-            // (same-address atomics serialise at ~12 ns each, tools/mb_atomic.hip: 31 K chunks = 380 us
-            // alone). At C2 the write pass drops 424 -> 400 us, but the count pass costs 144 us: the chunk
-            // map (a chain of dependent loads per workgroup) dominates it, not the filter's bytes
-            static const bool twoPass = std::getenv("NGX_FINAL_2PASS") && std::atoi(std::getenv("NGX_FINAL_2PASS")) != 0;
-            a.chunkRows = nullptr;
-            if (twoPass && kj && kj->count && !dyn && grid) {
-                a.chunkRows = c->chunkRows.get<uint64_t>(static_cast<uint64_t>(grid) + 1);
-                c->timed("final_count", Ef * kfBytes, [&] {
-                    void* args[] = {&a};
-                    HIP_OK(hipModuleLaunchKernel(kj->count, grid, 1, 1, nt, 1, 1, 0, c->stream, args, nullptr));
-                    if (launchScanInPlace(a.chunkRows, grid, c->stream)) throw Error{NGX_E_DEVICE, "final count scan"};
-                });
-            }
+            // each group's block table: virtual rows of the group's chunks / block, + 1 partial block
+            const uint64_t perGroup = (grid + a.resvG - 1) / a.resvG * static_cast<uint64_t>(nt) * (kChunk / 256);
+            a.resvTB = static_cast<uint32_t>(((perGroup + (1ULL << a.resvShift) - 1) >> a.resvShift) + 1);
+            a.resvTab = resvTable(c, static_cast<uint64_t>(a.resvTB) * a.resvG);
+            if (++c->resvSeq == 0) c->resvSeq = 1;
+            a.resvSeq = c->resvSeq;
             c->timed("final", dyn ? 0 : Ef * (keyReadBytes + kfBytes), [&] {
                 if (grid == 0) return;
                 if (kj) {
@@ -2567,9 +2640,13 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                     throw Error{NGX_E_DEVICE, "final"};
                 }
             });
+            // the holes of the groups' last blocks closed, the row count published (also for grid 0)
+            c->timed("final_close", 0, [&] {
+                if (launchFinalClose(a, c->stream)) throw Error{NGX_E_DEVICE, "final close"};
+            });
             if (!dyn) {
-                // GO: rows reserved by atomicAdd, and the query's error bits so far (final_kernels.h)
-                uint64_t nrows = awaitPub(c, rowsPub, a.lbStatus, &finalErrBits, errFlag);
+                // GO: the row count and the query's error bits so far, published by k_final_close
+                uint64_t nrows = awaitPub(c, rowsPub, c->resvRows, &finalErrBits, errFlag);
                 haveFinalErrs = true;
                 c->addBytes("final", nrows * rowBytes);
                 if (rw && !rw->perRow) {                        // the rows' src vids -> their roots
@@ -2693,8 +2770,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             haveBits = lbits != nullptr;
             ca.total = dyn ? dynStats + h : counters + 2;
             ca.pub = dyn ? Publish{nullptr, 0} : nextPub(c);
-            ca.zero = lbw;
-            ca.nzero = 2;
+            ca.zero = nullptr;
+            ca.nzero = 0;
             ca.err = errFlag;
             ca.epoch = ep;
             c->timed("compact_degrees", 0, [&] {
@@ -2745,7 +2822,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     const int nExtra = dyn ? static_cast<int>(steps) + 1 : 0;
     bool tailOk = false;
     if (dyn) {                                                   // the row count next to the hop totals
-        HIP_OK(hipMemcpyAsync(dynStats + steps, lbw, 8, hipMemcpyDeviceToDevice, c->stream));
+        if (c->resvRows) HIP_OK(hipMemcpyAsync(dynStats + steps, c->resvRows, 8, hipMemcpyDeviceToDevice, c->stream));
+        else HIP_OK(hipMemsetAsync(dynStats + steps, 0, 8, c->stream));
     }
     if (!dyn && haveFinalErrs) {                                 // the last final kernel published them
         tail[0] = finalErrBits;
@@ -3287,6 +3365,7 @@ extern "C" int32_t ngx_go(ngx_ctx* c, const ngx_go_plan* p, ngx_go_result** out)
         HIP_OK(hipSetDevice(c->device));
         Space* sp = findSpace(c, p->space);
         if (!sp || !sp->dev) rc = fail(c, NGX_E_NOT_LOADED, "space not committed");
+        else if (c->reservoirSampling) rc = fail(c, NGX_E_UNSUPPORTED, kSamplingRefused);
         else if (p->input_vid_col) rc = runPipe(c, *sp, *p, *R);
         else rc = runGo(c, *sp, *p, *R);
     } catch (const Error& e) {
@@ -3779,6 +3858,7 @@ extern "C" int32_t ngx_get_neighbors(ngx_ctx* c, const ngx_gn_request* q, ngx_gn
         HIP_OK(hipSetDevice(c->device));
         Space* sp = findSpace(c, q->space);
         if (!sp || !sp->dev) rc = fail(c, NGX_E_NOT_LOADED, "space not committed");
+        else if (c->reservoirSampling) rc = fail(c, NGX_E_UNSUPPORTED, kSamplingRefused);
         else rc = runGetNeighbors(c, *sp, *q, *R);
     } catch (const Error& e) {
         rc = fail(c, e.code, e.msg);

@@ -506,6 +506,98 @@ Error exportSnapshot(Space& sp, int32_t rank, int32_t world, HostGraph& g) {
     return Error{NGX_OK, ""};
 }
 
+// Columnar bulk load (ngx_load_csr): the caller's CSR becomes the shard snapshot exportSnapshot would
+// build from the same edges' KV rows. Everything the exporter guarantees is checked instead of built:
+// the vertex table sorted by (part, vid) with part = ID_HASH(vid) owned by this shard, CSR offsets,
+// every row's adjacency strictly in RocksDB key order (rank LE bytes, then dst LE bytes: no two versions
+// of one edge), one slot per signed type with a schema whose latest version has no STRING field.
+Error loadCsrShard(const Space& sp, int32_t rank, int32_t world, const ngx_csr_shard& in, HostGraph& g) {
+    const uint64_t V = in.nvertices;
+    if ((V && (!in.vpart || !in.vid)) || in.nslots < 0 || (in.nslots && !in.slots))
+        return Error{NGX_E_BAD_ARGUMENT, "csr: missing arrays"};
+    std::atomic<bool> bad{false};
+    parallelFor(V, [&](uint64_t lo, uint64_t hi) {
+        for (uint64_t i = lo; i < hi && !bad; i++) {
+            const int32_t p = in.vpart[i];
+            if (sp.numParts > 0 && (p != idHash(in.vid[i], sp.numParts) || (world > 1 && p % world != rank))) bad = true;
+            if (i && (in.vpart[i - 1] > p || (in.vpart[i - 1] == p && in.vid[i - 1] >= in.vid[i]))) bad = true;
+        }
+    });
+    if (bad) return Error{NGX_E_BAD_ARGUMENT, "csr: vertex table not sorted by (part, vid), duplicated, or of parts this shard does not own"};
+    g.vpart.assign(in.vpart, in.vpart + V);
+    g.vid.assign(in.vid, in.vid + V);
+    std::vector<const ngx_csr_slot*> order;
+    for (int32_t k = 0; k < in.nslots; k++) order.push_back(&in.slots[k]);
+    std::sort(order.begin(), order.end(), [](const ngx_csr_slot* a, const ngx_csr_slot* b) { return a->etype < b->etype; });
+    for (size_t k = 0; k < order.size(); k++) {
+        const ngx_csr_slot& cs = *order[k];
+        if (cs.etype == 0 || (k && order[k - 1]->etype == cs.etype)) return Error{NGX_E_BAD_ARGUMENT, "csr: slot types must be distinct and nonzero"};
+        const SchemaSet* ss = sp.edge(std::abs(cs.etype));
+        if (!ss) return Error{NGX_E_EDGE_NOT_FOUND, "csr: no schema for edge type " + std::to_string(cs.etype)};
+        const SchemaDef& latest = ss->latest();
+        if (cs.ncols != static_cast<int32_t>(latest.fields.size()) || (cs.ncols && !cs.cols))
+            return Error{NGX_E_BAD_ARGUMENT, "csr: columns must be the latest schema's fields"};
+        for (auto& f : latest.fields)
+            if (f.type == T_STRING) return Error{NGX_E_UNSUPPORTED, "csr: STRING columns are loaded from KV rows"};
+        if (!cs.off || cs.off[0] != 0) return Error{NGX_E_BAD_ARGUMENT, "csr: offsets must start at 0"};
+        const uint64_t ne = cs.off[V];
+        if (ne && !cs.dst) return Error{NGX_E_BAD_ARGUMENT, "csr: missing dst"};
+        parallelFor(V, [&](uint64_t lo, uint64_t hi) {
+            for (uint64_t r = lo; r < hi && !bad; r++) {
+                if (cs.off[r] > cs.off[r + 1]) { bad = true; break; }
+                for (uint64_t e = cs.off[r] + 1; e < cs.off[r + 1]; e++) {
+                    const uint64_t ra = cs.rank ? __builtin_bswap64(static_cast<uint64_t>(cs.rank[e - 1])) : 0;
+                    const uint64_t rb = cs.rank ? __builtin_bswap64(static_cast<uint64_t>(cs.rank[e])) : 0;
+                    const uint64_t da = __builtin_bswap64(static_cast<uint64_t>(cs.dst[e - 1]));
+                    const uint64_t db = __builtin_bswap64(static_cast<uint64_t>(cs.dst[e]));
+                    if (ra > rb || (ra == rb && da >= db)) { bad = true; break; }
+                }
+            }
+        });
+        if (bad) return Error{NGX_E_BAD_ARGUMENT, "csr: offsets not monotone or a row's edges not in key order (rank, dst LE bytes)"};
+        g.slots.emplace_back();
+        HostSlot& hs = g.slots.back();
+        hs.etype = cs.etype;
+        hs.off.assign(cs.off, cs.off + V + 1);
+        hs.dst.assign(cs.dst, cs.dst + ne);
+        if (cs.rank) hs.rank.assign(cs.rank, cs.rank + ne);
+        else hs.rank.assign(ne, 0);
+        hs.dgid.assign(ne, kNoRow);
+        hs.cols.resize(latest.fields.size());
+        for (size_t c = 0; c < hs.cols.size(); c++) {
+            HostColumn& col = hs.cols[c];
+            col.type = latest.fields[c].type;
+            const int64_t* x = cs.cols[c];
+            if (ne && !x) return Error{NGX_E_BAD_ARGUMENT, "csr: missing column " + latest.fields[c].name};
+            switch (col.type) {
+                case T_INT: case T_TIMESTAMP: case T_VID: col.i64.assign(x, x + ne); break;
+                case T_FLOAT: case T_DOUBLE:
+                    col.f64.resize(ne);
+                    if (ne) std::memcpy(col.f64.data(), x, ne * 8);
+                    break;
+                case T_BOOL:
+                    col.b.resize(ne);
+                    for (uint64_t e = 0; e < ne; e++) col.b[e] = x[e] != 0;
+                    break;
+                default: break;
+            }
+        }
+        g.edges += ne;
+    }
+    // tags of the space: no rows (ngx_load_csr carries edges only)
+    for (auto& kv : sp.tags) {
+        g.tags.emplace_back();
+        HostTag& t = g.tags.back();
+        t.tag = kv.first;
+        initColumns(t.cols, kv.second.latest(), V);
+        t.present.assign(V, 0);
+        std::vector<std::vector<std::string>> none(t.cols.size());
+        for (size_t c = 0; c < t.cols.size(); c++) if (t.cols[c].type == T_STRING) none[c].resize(V);
+        packStrings(t.cols, none);
+    }
+    return Error{NGX_OK, ""};
+}
+
 void resolveDstRows(const Space& sp, HostGraph& g,
                     const std::vector<std::vector<std::pair<int32_t, int64_t>>>& shardTables, int32_t world) {
     if (sp.numParts <= 0) return;                    // test-only layouts: no ID_HASH routing

@@ -24,7 +24,6 @@ namespace ngx {
 struct JitKernels {
     hipModule_t mod = nullptr;
     hipFunction_t final = nullptr;      // the fused final-hop kernel (final_kernels.h finalBody)
-    hipFunction_t count = nullptr;      // GO: its count pass (finalBody COUNT, FinalArgs::chunkRows)
     int threads = 256;                  // workgroup size of both (JitQuery::threads)
 };
 

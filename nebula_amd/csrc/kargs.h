@@ -58,7 +58,7 @@ struct FinalArgs {
     int32_t ttlCol[kMaxSlots];          // TTL column of hop slot s (INT / TIMESTAMP / VID), -1 if none
     int64_t ttlDur[kMaxSlots];
     int64_t now;
-    uint64_t* lbStatus;                 // [0] chunk ticket, [1 + c] look-back status of chunk c (zeroed per launch)
+    uint64_t* lbStatus;                 // GetNeighbors: [0] chunk ticket, [1 + c] look-back status of chunk c
     uint32_t* err;                      // [0] graphd evaluation error, [1] host-only construct, [2] YIELD type
                                         // mismatch, [3] look-back spin limit (device fault)
     int32_t nY;
@@ -77,9 +77,16 @@ struct FinalArgs {
     uint8_t* oFlags;                    // EF_* flags of each row's edge (GetNeighbors row encoding), may be null
     const OutCol* oCols;                // nY columns (device array; columns >= kInlineCols read it)
     OutCol oColsIn[kInlineCols];        // the first columns' descriptors, by value (no upload)
-    uint64_t* rowsPub;                  // host-mapped [rows, seq] published by the last chunk (GO), or null
+    uint64_t* rowsPub;                  // host-mapped [rows, seq, error bits] published by k_final_close (GO), or null
     uint64_t rowsSeq;
-    uint32_t* done;                     // chunks finished (zeroed with lbStatus), for rowsPub
+    uint64_t* resvTab;                  // GO: per group, the physical block of each virtual row block (resv*)
+    uint64_t* resvCtl;                  // GO: this launch's reservation counters (below)
+    uint64_t* resvNext;                 // GO: the next launch's (cleared by k_final_close)
+    uint32_t resvTB;                    // blocks per group in resvTab
+    uint32_t resvSeq;                   // tag of this launch's resvTab entries (never 0; no clearing)
+    uint32_t resvG;                     // groups (<= kResvMaxGroups)
+    uint32_t resvShift;                 // log2 of the block's rows (block >= rows of one chunk)
+    uint32_t resvStride;                // words between two counters of resvCtl
     const uint8_t* mask;                // per hop edge: storage emitted it (max_edge_returned_per_vertex
                                         // path); when set, replaces the storage checks. nullptr: none
     int64_t kc[kJitConsts];             // generated kernels: literal bits (string: pool offset)
@@ -91,12 +98,10 @@ struct FinalArgs {
                                         // for the strings YIELD columns build; nullptr when none does
     uint32_t nStrOut;                   // columns that build strings (bits of strOutMask, y < 32)
     uint32_t strOutMask;
-    // GO final hop in two passes (generated kernels): the count pass writes each chunk's passing rows to
-    // chunkRows[chunk]; scanned in place (exclusive, [nChunks] = rows), the write pass reads its chunk's
-    // first row there instead of reserving it with an atomicAdd on one counter (~12 ns each, serialised
-    // at the memory side: 31 K chunks = 380 us at C2, tools/mb_atomic.hip). nullptr: one pass, atomicAdd
-    uint64_t* chunkRows;
 };
+
+// rows a GO final launch may leave past its row count before k_final_close (outputs are sized for them)
+__host__ __device__ inline uint64_t resvSlack(const FinalArgs& a) { return static_cast<uint64_t>(a.resvG) << a.resvShift; }
 
 // the row's slot of the result string arena for the j-th column that builds strings
 __device__ __forceinline__ char* strSlot(const FinalArgs& a, uint64_t o, uint32_t j) {
@@ -119,5 +124,21 @@ struct VertexCellArgs {
 
 constexpr uint64_t kTile = 4096;        // items per scan tile
 constexpr uint64_t kChunk = 2048;       // edges per edge-balanced workgroup (expansion, final hop)
+
+// GO final hop: where a chunk's passing rows go. One counter per group of chunks (chunk % resvG:
+// dispatch puts consecutive workgroups on different XCDs, so with 8 groups a group is one XCD's
+// chunks) hands out virtual rows; each group's virtual rows live in blocks of 2^resvShift physical
+// rows taken from one global counter (one atomic per block). Same-address atomics serialise at the
+// memory side (~12 ns each, tools/mb_atomic.hip): one counter for every chunk made C2's 31 K chunks a
+// 380 us chain. The last block of each group is partly empty: k_final_close moves the rows that lie
+// past the row count into those holes (at most resvG blocks of rows), publishes the count and the
+// query's error bits, and clears the counters for the next launch.
+// Words of FinalArgs::resvCtl, one of two sets used by alternate launches (stride resvStride words;
+// cleared at allocation, then k_final_close of each launch clears the other set, resvNext):
+//   [0] physical rows handed out (a multiple of the block)
+//   [(1 + g) * stride] virtual rows of group g
+//   [(1 + G) * stride] the row count (written by k_final_close)
+constexpr uint64_t kDoneOff = 1024;
+constexpr uint32_t kResvMaxGroups = 64;
 
 }  // namespace ngx

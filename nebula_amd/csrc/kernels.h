@@ -98,10 +98,8 @@ struct CompactArgs {
 };
 constexpr uint64_t kCompactLbMaxV = 1ULL << (62 - kFdShift);
 constexpr uint64_t kCompactTile = 4096;     // rows per compaction tile (256 threads x 16 rows)
-// GO final kernel words: [0] rows reserved (one atomicAdd per chunk), [kDoneOff] chunks finished. Kept
-// 8 KiB apart: two per-chunk atomics on one cache line serialize at the memory side (+300 us/launch).
-// The seed / compaction kernels clear zero[k * kDoneOff] for k < nzero.
-constexpr uint64_t kDoneOff = 1024;
+// GO final kernel words: kargs.h (kResv*, kDoneOff). The seed / compaction kernels clear zero[k * kDoneOff]
+// for k < nzero.
 int launchCompactLb(const CompactArgs& a, hipStream_t s);
 // seed hop variant that also writes chunkFirst (cfCap entries) and clears zero[0 .. nzero)
 int launchSeedFrontierCf(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, const HopSlots& hs,
@@ -136,10 +134,15 @@ int launchScanU64(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tileS
 // v[0 .. n) -> exclusive prefix in place, v[n] = total (one 1024-thread workgroup: n up to ~1e6)
 int launchScanInPlace(uint64_t* v, uint64_t n, hipStream_t s);
 
-// final hop, one pass (interpreter kernel): a.lbStatus zeroed, ceil(E / kChunk) + 1 words; outputs
-// sized for a.oBase + a.E rows. a.oEntry set (GetNeighbors): rows in edge order, rows written = the
-// inclusive status of the last chunk; else (GO) chunks in completion order, rows written = lbStatus[0]
+// final hop, one pass (interpreter kernel). a.oEntry set (GetNeighbors): a.lbStatus zeroed, ceil(E /
+// kChunk) + 1 words; outputs sized for a.oBase + a.E rows; rows in edge order, rows written = the
+// inclusive status of the last chunk. Else (GO): the kResv words of a.lbStatus zeroed, outputs sized for
+// a.oBase + a.E + resvSlack() rows, chunks' rows in per-group blocks; launchFinalClose must follow.
 int launchFinal(const FinalArgs& a, hipStream_t s, unsigned grid = 0);   // grid 0: one workgroup per chunk of a.E
+// GO final hop, after the final kernel (generated or interpreter) on the same stream: the rows past the
+// row count moved into the holes of the groups' last blocks, then rows = lbStatus[0] and the row count
+// and the query's error bits (bit k = a.err[k] != 0) published to a.rowsPub when set
+int launchFinalClose(const FinalArgs& a, hipStream_t s);
 // resident workgroups per CU of the interpreter final kernel launchFinal would run for `a`
 int finalOccupancy(const FinalArgs& a);
 

@@ -905,7 +905,6 @@ __global__ __launch_bounds__(256) void k_copy_batch(CopyBatch b) {
 // ------------------------------------------------------------------------------ final hop (interpreter)
 struct VmEv {
     static constexpr int kEager = -1;                 // YIELD evaluated in the write pass
-    static constexpr bool kEagerSkip = false;
     static constexpr bool kPos32 = false;             // 64-bit CSR positions in the chunk map
     static constexpr bool kMask = true;               // reads FinalArgs::mask when set
     static constexpr int kDstW = 0, kRankW = 0;       // key column widths read per slot
@@ -947,6 +946,129 @@ __global__ __launch_bounds__(WG) void k_final(FinalArgs a) { finalBody<VmEv, ONE
 // a GO whose frontier entries carry input rows (FinalArgs::fin: multi-root pipe walks reading $-)
 template <bool ONE>
 __global__ __launch_bounds__(WG) void k_final_in(FinalArgs a) { finalBody<VmEv, ONE, true, false>(a); }
+
+// ------------------------------------------------------------------------------ GO final hop: close
+// After the final kernel (kargs.h resv*): every group's last block is partly empty, so physical rows
+// [0, P) hold R rows with at most resvG holes. The i-th occupied row at or past R moves to the i-th
+// hole below R (as many of one as of the other; a thread per moved row), then [0, R) is dense.
+// Workgroup 0 publishes R and the error bits to host-mapped memory at once (the final kernel has
+// ended, so every error atomic of it has landed), keeps R in the control words and clears the other
+// set of counters for the next launch: no count of finished workgroups (another same-address stream).
+// The moves complete in the stream's order, before any later work on the context's stream.
+__device__ __forceinline__ void moveW(void* p, int32_t w, uint64_t from, uint64_t to) {
+    switch (w) {
+        case 1: gst<uint8_t>(p, to, gld<uint8_t>(p, from)); break;
+        case 2: gst<uint16_t>(p, to, gld<uint16_t>(p, from)); break;
+        case 4: gst<uint32_t>(p, to, gld<uint32_t>(p, from)); break;
+        default: gst<uint64_t>(p, to, gld<uint64_t>(p, from)); break;
+    }
+}
+
+__global__ __launch_bounds__(WG) void k_final_close(FinalArgs a) {
+    __shared__ uint64_t hLo[kResvMaxGroups], hHi[kResvMaxGroups], gV[kResvMaxGroups];
+    __shared__ uint64_t sR, sP, sM;
+    __shared__ int sNh;
+    const uint64_t B = 1ULL << a.resvShift, st = a.resvStride;
+    const uint32_t G = a.resvG;
+    // every group's count and last block at once (one load round trip, not G dependent ones)
+    if (threadIdx.x < G) {
+        const uint32_t g = threadIdx.x;
+        const uint64_t v = lbLoad(a.resvCtl + (1 + g) * st);
+        gV[g] = v;
+        hLo[g] = hHi[g] = 0;
+        if (v & (B - 1)) {
+            const uint64_t k = v >> a.resvShift;
+            const uint64_t e = k < a.resvTB ? lbLoad(a.resvTab + static_cast<uint64_t>(g) * a.resvTB + k) : 0;
+            if ((e >> 32) != a.resvSeq) {
+                atomicOr(a.err + 3, 1u);                    // every reserved block is published: cannot happen
+            } else {
+                hLo[g] = ((e & 0xFFFFFFFFULL) << a.resvShift) + (v & (B - 1));
+                hHi[g] = ((e & 0xFFFFFFFFULL) + 1) << a.resvShift;
+            }
+        }
+    }
+    if (threadIdx.x == WG - 1) sP = lbLoad(a.resvCtl);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t R = 0;
+        int nh = 0;
+        for (uint32_t g = 0; g < G; g++) {                  // holes sorted by position (insertion sort)
+            R += gV[g];
+            if (hHi[g] == 0) continue;
+            const uint64_t lo = hLo[g], hi = hHi[g];
+            int j = nh++;
+            while (j > 0 && hLo[j - 1] > lo) { hLo[j] = hLo[j - 1]; hHi[j] = hHi[j - 1]; j--; }
+            hLo[j] = lo;
+            hHi[j] = hi;
+        }
+        uint64_t M = 0;
+        for (int j = 0; j < nh; j++) M += hLo[j] < R ? (hHi[j] < R ? hHi[j] : R) - hLo[j] : 0;
+        sR = R;
+        sM = M;
+        sNh = nh;
+        if (blockIdx.x == 0) {
+            lbStore(a.resvCtl + (1 + G) * st, R);           // the row count (device copy; dyn hops read it)
+            for (uint32_t g = 0; g <= G; g++) lbStore(a.resvNext + g * st, 0);   // the next launch's counters
+            if (a.rowsPub != nullptr) {
+                uint64_t bits = 0;
+                for (int k = 0; k < 4; k++)
+                    bits |= static_cast<uint64_t>(__hip_atomic_load(a.err + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) << k;
+                __hip_atomic_store(a.rowsPub, R, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(a.rowsPub + 2, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(a.rowsPub + 1, a.rowsSeq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
+    __syncthreads();
+    const uint64_t R = sR, P = sP, M = sM;
+    const int nh = sNh;
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * WG + threadIdx.x;
+    if (i >= M) return;
+    uint64_t to = ~0ULL, acc = 0;                           // the i-th hole below R
+    for (int j = 0; j < nh && hLo[j] < R; j++) {
+        const uint64_t len = (hHi[j] < R ? hHi[j] : R) - hLo[j];
+        if (i < acc + len) { to = hLo[j] + (i - acc); break; }
+        acc += len;
+    }
+    uint64_t from = ~0ULL, cur = R, left = i;               // the i-th occupied row in [R, P)
+    for (int j = 0; j <= nh; j++) {
+        if (j < nh && hHi[j] <= R) continue;
+        const uint64_t segEnd = j < nh ? hLo[j] : P;
+        if (segEnd > cur) {
+            if (left < segEnd - cur) { from = cur + left; break; }
+            left -= segEnd - cur;
+        }
+        if (j < nh && hHi[j] > cur) cur = hHi[j];
+    }
+    if (to == ~0ULL || from == ~0ULL) { atomicOr(a.err + 3, 1u); return; }
+    from += a.oBase;
+    to += a.oBase;
+    if (a.oSrc) moveW(a.oSrc, a.oSrcW, from, to);
+    if (a.oDst) moveW(a.oDst, a.oDstW, from, to);
+    if (a.oRank) moveW(a.oRank, a.oRankW, from, to);
+    if (a.oType) moveW(a.oType, 4, from, to);
+    if (a.oEntry) moveW(a.oEntry, 4, from, to);
+    if (a.oFlags) moveW(a.oFlags, 1, from, to);
+    // strings the row's YIELD columns built live in its slots of the result string arena: they move
+    // with the row, and a value pointing into them is rebased
+    const uint64_t slotBytes = static_cast<uint64_t>(a.nStrOut) * kStrBuildBytes;
+    char* const sFrom = a.strOut ? strSlot(a, from, 0) : nullptr;
+    char* const sTo = a.strOut ? strSlot(a, to, 0) : nullptr;
+    for (uint64_t b = 0; sFrom && b < slotBytes; b += 8) gst<uint64_t>(sTo, b / 8, gld<uint64_t>(sFrom, b / 8));
+    for (int y = 0; y < a.nY; y++) {
+        const OutCol& oc = outCol(a, y);
+        // a key column aliased to a row array moved with it
+        if (oc.x && oc.x != a.oSrc && oc.x != a.oDst && oc.x != a.oRank) {
+            int64_t x = oc.w == 8 ? gld<int64_t>(oc.x, from) : loadW(oc.x, oc.w, from);
+            const uint64_t ux = static_cast<uint64_t>(x);
+            if (oc.len && sFrom && ux >= reinterpret_cast<uint64_t>(sFrom) && ux < reinterpret_cast<uint64_t>(sFrom) + slotBytes)
+                x = static_cast<int64_t>(ux - reinterpret_cast<uint64_t>(sFrom) + reinterpret_cast<uint64_t>(sTo));
+            storeW(oc.x, oc.w, to, x);
+        }
+        if (oc.len) moveW(oc.len, 4, from, to);
+        if (oc.t) moveW(oc.t, 1, from, to);
+    }
+}
 
 // ------------------------------------------------------------------------------ max_edge_returned_per_vertex
 // Storage outcome of every hop edge (bad row / TTL / pushed filter; the interpreter evaluates the
@@ -1237,6 +1359,12 @@ int launchFinal(const FinalArgs& a, hipStream_t s, unsigned g) {
         if (a.hs.n == 1) hipLaunchKernelGGL((k_final<true, false>), grid, dim3(WG), 0, s, a);
         else hipLaunchKernelGGL((k_final<false, false>), grid, dim3(WG), 0, s, a);
     }
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchFinalClose(const FinalArgs& a, hipStream_t s) {
+    const unsigned grid = static_cast<unsigned>((resvSlack(a) + WG - 1) / WG);   // a thread per row that may move
+    hipLaunchKernelGGL(k_final_close, dim3(grid), dim3(WG), 0, s, a);
     return static_cast<int>(hipGetLastError());
 }
 

@@ -120,6 +120,7 @@ struct Space {
     std::map<std::string, int32_t> tagByName, edgeByName;
     std::vector<std::string> edgeOrder;
     StagedRows staged;
+    std::unique_ptr<HostGraph> loaded;  // ngx_load_csr: the next commit's shard (instead of the staged rows)
     std::unique_ptr<HostGraph> host;
     std::unique_ptr<DeviceGraph> dev;
     const SchemaSet* edge(int32_t absType) const {
@@ -157,6 +158,8 @@ inline int32_t idHash(int64_t vid, int32_t numParts) {        // ID_HASH (src/co
 
 // exporter.cpp: build the shard snapshot from staged rows
 Error exportSnapshot(Space& sp, int32_t rank, int32_t world, HostGraph& out);
+// exporter.cpp: the same snapshot from a caller's CSR (ngx_load_csr), validated
+Error loadCsrShard(const Space& sp, int32_t rank, int32_t world, const ngx_csr_shard& in, HostGraph& out);
 // snapshot.cpp: device snapshot files of a committed shard
 uint64_t schemaDigest(const Space& sp);
 // digest of the vertex tables of every shard, in rank order: equal on all ranks of one commit (the

@@ -27,6 +27,12 @@ class _Rows(ctypes.Structure):
                 ("vals", ctypes.c_void_p), ("val_off", ctypes.c_void_p)]
 
 
+class _Csr(ctypes.Structure):
+    _fields_ = [("nv", ctypes.c_uint64), ("vpart", ctypes.c_void_p), ("vid", ctypes.c_void_p), ("nslots", ctypes.c_int32),
+                ("etype", ctypes.c_int32 * 2), ("ne", ctypes.c_uint64 * 2), ("off", ctypes.c_void_p * 2),
+                ("dst", ctypes.c_void_p * 2), ("p0", ctypes.c_void_p * 2), ("p1", ctypes.c_void_p * 2)]
+
+
 _lib = None
 
 
@@ -48,6 +54,10 @@ def lib():
         L.ngd_sample_vids.argtypes = [u64, u64, u64, ctypes.c_void_p]
         L.ngd_rmat_seeds.argtypes = [i32, i32, dbl, dbl, dbl, u64, u64, u64, i32, ctypes.c_void_p]
         L.ngd_rmat_seeds.restype = i32
+        C_ = ctypes.POINTER(_Csr)
+        L.ngd_rmat_csr.argtypes = [i32, i32, dbl, dbl, dbl, u64, i32, i32, i32, i32, i32, i32, C_]
+        L.ngd_rmat_csr.restype = i32
+        L.ngd_csr_free.argtypes = [C_]
         _lib = L
     return _lib
 
@@ -92,6 +102,62 @@ def rmat(scale: int, ef: int = 16, seed: int = 42, num_parts: int = 100, with_in
     if rc:
         raise ValueError("bad rmat parameters")
     return r
+
+
+class Csr:
+    """One shard of the RMAT graph as CSR arrays (ngd_rmat_csr): `vpart`/`vid` (the vertex table sorted by
+    (part, vid)) and per slot `slots[s] = (etype, off, dst, [p0, p1])` as zero-copy numpy views; the
+    input of Engine.load_csr (ngx_load_csr)."""
+
+    def __init__(self):
+        self.c = _Csr()
+
+    def _view(self, ptr, n, ct, dt):
+        return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ct)), shape=(max(n, 1),))[:n].view(dt)
+
+    @property
+    def nv(self) -> int:
+        return self.c.nv
+
+    @property
+    def vpart(self):
+        return self._view(self.c.vpart, self.c.nv, ctypes.c_int32, np.int32)
+
+    @property
+    def vid(self):
+        return self._view(self.c.vid, self.c.nv, ctypes.c_int64, np.int64)
+
+    @property
+    def slots(self):
+        out = []
+        for s in range(self.c.nslots):
+            ne = self.c.ne[s]
+            out.append((self.c.etype[s], self._view(self.c.off[s], self.c.nv + 1, ctypes.c_uint64, np.uint64),
+                        self._view(self.c.dst[s], ne, ctypes.c_int64, np.int64),
+                        [self._view(self.c.p0[s], ne, ctypes.c_int64, np.int64),
+                         self._view(self.c.p1[s], ne, ctypes.c_int64, np.int64)]))
+        return out
+
+    def free(self):
+        if self.c.vid:
+            lib().ngd_csr_free(ctypes.byref(self.c))
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def rmat_csr(scale: int, ef: int = 16, seed: int = 42, num_parts: int = 100, with_in: bool = False,
+             rank: int = 0, world: int = 1, threads: int = 0, abc=GRAPH500) -> Csr:
+    """The graph of rmat() (same edges, props; no tags) as this shard's CSR, without KV rows."""
+    c = Csr()
+    rc = lib().ngd_rmat_csr(scale, ef, abc[0], abc[1], abc[2], seed, num_parts, RMAT_EDGE, int(with_in), rank, world,
+                            _threads(threads), ctypes.byref(c.c))
+    if rc:
+        raise ValueError("bad rmat_csr parameters")
+    return c
 
 
 def powerlaw(n: int, ef: int = 8, alpha: float = 2.0, nsuper: int = 4, superdeg: int = 1_000_000, seed: int = 42,

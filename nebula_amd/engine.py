@@ -134,6 +134,16 @@ def _input_arrays(inp):
     return names, types, cells, bytes(strings) + b"\0", nc, nr
 
 
+class CsrSlotC(ctypes.Structure):
+    _fields_ = [("etype", c_i32), ("off", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("rank", ctypes.c_void_p),
+                ("ncols", c_i32), ("cols", ctypes.c_void_p)]
+
+
+class CsrShardC(ctypes.Structure):
+    _fields_ = [("nvertices", c_u64), ("vpart", ctypes.c_void_p), ("vid", ctypes.c_void_p), ("nslots", c_i32),
+                ("slots", P(CsrSlotC))]
+
+
 class GoResultC(ctypes.Structure):
     _fields_ = [("code", c_i32), ("ncols", c_i32), ("col_types", P(c_i32)), ("nrows", c_u64), ("cells", P(Cell)),
                 ("row_src", P(c_i64)), ("row_dst", P(c_i64)), ("row_rank", P(c_i64)), ("row_type", P(c_i32)),
@@ -165,6 +175,7 @@ SIGNATURES = {
     "ngx_add_schema": (c_i32, [ctypes.c_void_p, c_i32, c_i32, c_i32, ctypes.c_char_p, c_i64, c_i32,
                                P(ctypes.c_char_p), P(c_i32), ctypes.c_char_p, c_i64]),
     "ngx_load_kv": (c_i32, [ctypes.c_void_p, c_i32, P(KVBatchC)]),
+    "ngx_load_csr": (c_i32, [ctypes.c_void_p, c_i32, P(CsrShardC)]),
     "ngx_commit": (c_i32, [ctypes.c_void_p, c_i32]),
     "ngx_graph_info_get": (c_i32, [ctypes.c_void_p, c_i32, P(GraphInfo)]),
     "ngx_get_neighbors": (c_i32, [ctypes.c_void_p, P(GnRequest), P(P(GnResult))]),
@@ -172,6 +183,7 @@ SIGNATURES = {
     "ngx_go": (c_i32, [ctypes.c_void_p, P(GoPlan), P(P(GoResultC))]),
     "ngx_go_result_free": (None, [P(GoResultC)]),
     "ngx_set_profiling": (c_i32, [ctypes.c_void_p, c_i32]),
+    "ngx_synchronize": (c_i32, [ctypes.c_void_p]),
     "ngx_stats": (c_i32, [ctypes.c_void_p, P(P(Stat)), P(c_i32)]),
     "ngx_kernel_stats": (c_i32, [ctypes.c_void_p, P(P(KernelStat)), P(c_i32)]),
     "ngx_set_flag": (c_i32, [ctypes.c_void_p, ctypes.c_char_p, c_i64]),
@@ -376,6 +388,25 @@ class Engine:
         koff, voff = np.ascontiguousarray(koff, dtype=np.uint64), np.ascontiguousarray(voff, dtype=np.uint64)
         b = KVBatchC(len(koff) - 1, keys.ctypes.data, koff.ctypes.data, vals.ctypes.data, voff.ctypes.data)
         self._check(self.L.ngx_load_kv(self.h, space, ctypes.byref(b)), "load_kv")
+
+    def load_csr(self, space: int, vpart, vid, slots):
+        """ngx_load_csr: this shard's vertex table (sorted by (part, vid)) and per slot (etype, off, dst,
+        [column arrays of the latest schema's fields]) as int64 / uint64 arrays (datagen.Csr.slots)."""
+        vpart = np.ascontiguousarray(vpart, dtype=np.int32)
+        vid = np.ascontiguousarray(vid, dtype=np.int64)
+        keep = [vpart, vid]
+        cs = (CsrSlotC * max(1, len(slots)))()
+        for k, (etype, off, dst, cols) in enumerate(slots):
+            off = np.ascontiguousarray(off, dtype=np.uint64)
+            dst = np.ascontiguousarray(dst, dtype=np.int64)
+            cols = [np.ascontiguousarray(c, dtype=np.int64) for c in cols]
+            ptrs = (ctypes.c_void_p * max(1, len(cols)))(*[c.ctypes.data for c in cols])
+            keep += [off, dst, cols, ptrs]
+            cs[k] = CsrSlotC(int(etype), off.ctypes.data, dst.ctypes.data, None, len(cols),
+                             ctypes.cast(ptrs, ctypes.c_void_p))
+        sh = CsrShardC(len(vid), vpart.ctypes.data, vid.ctypes.data, len(slots), cs)
+        self._check(self.L.ngx_load_csr(self.h, space, ctypes.byref(sh)), "load_csr")
+        del keep
 
     def load_batch(self, space: int, batch):
         self.load_kv(space, *batch.arrays())
