@@ -88,6 +88,38 @@ def main():
             traffic["kernel_name"] = d["kernel"]
             if d["fetch_bytes_x2"] is not None and d["write_bytes"] is not None:
                 traffic["bytes_per_launch"] = d["fetch_bytes_x2"] + d["write_bytes"]
+    # SQ pass (profile.sh SQPASS=1): per-launch wave counters; WAVE_CYCLES / WAIT_* / ACTIVE_INST count
+    # quad-cycles (MI355X_MICROARCH.md), WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES
+    sqf = os.path.join(src, "sq", "run_counter_collection.csv")
+    if os.path.exists(sqf):
+        acc = collections.defaultdict(lambda: collections.defaultdict(list))
+        for r in csv.DictReader(open(sqf)):
+            acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        sq = {}
+        for k, d in acc.items():
+            per = {c: sum(v) / len(v) for c, v in d.items()}
+            wc = per.get("SQ_WAVE_CYCLES") or 0.0
+            if wc:
+                per["frac_wait_any"] = per.get("SQ_WAIT_ANY", 0.0) / wc
+                per["frac_wait_inst_any"] = per.get("SQ_WAIT_INST_ANY", 0.0) / wc
+                per["frac_active_inst_any"] = per.get("SQ_ACTIVE_INST_ANY", 0.0) / wc
+            durs = trace.get(k)
+            if wc and durs:
+                # average resident waves = wave cycles (4 per quad-cycle) / kernel cycles at 2.4 GHz
+                per["avg_resident_waves_at_2p4ghz"] = 4 * wc / (sum(durs) / len(durs) * 2.4)
+            sq[k] = per
+        traffic["sq_per_launch"] = sq
+        with open(os.path.join(dst, f"{args.tag}_summary.md"), "a") as f:
+            f.write("\nSQ counters per launch (separate --pmc pass; quad-cycle units):\n\n")
+            f.write("| kernel | waves | wave quad-cycles | wait_any | wait_inst_any | active_inst_any | VMEM rd / wr instr | resident waves @2.4 GHz |\n")
+            f.write("|---|---|---|---|---|---|---|---|\n")
+            for k, per in sorted(sq.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0)):
+                if not per.get("SQ_WAVE_CYCLES"):
+                    continue
+                f.write(f"| `{k[:60]}` | {per.get('SQ_WAVES', 0):.0f} | {per['SQ_WAVE_CYCLES']:.4g} | "
+                        f"{per['frac_wait_any']:.2f} | {per['frac_wait_inst_any']:.2f} | {per['frac_active_inst_any']:.2f} | "
+                        f"{per.get('SQ_INSTS_VMEM_RD', 0):.3g} / {per.get('SQ_INSTS_VMEM_WR', 0):.3g} | "
+                        f"{per.get('avg_resident_waves_at_2p4ghz', 0):.0f} |\n")
     json.dump(traffic, open(os.path.join(dst, f"{args.tag}_traffic.json"), "w"), indent=1)
     if "bytes_per_launch" in traffic:        # the file bench.py reads by default
         json.dump(traffic, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
