@@ -384,71 +384,69 @@ void sortUnique(std::vector<uint64_t>& v) {
 
 inline uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
-}  // namespace
+struct RmatParams {
+    int32_t scale;
+    uint64_t E, seed, np;
+    uint32_t a, ab, abc;
+    int32_t numParts;
+    bool withIn;
+    RmatParams(int32_t scale_, int32_t ef, double A, double B, double C, uint64_t seed_, int32_t numParts_, bool withIn_)
+        : scale(scale_), E(static_cast<uint64_t>(ef) << scale_), seed(seed_), np(static_cast<uint64_t>(numParts_)),
+          a(static_cast<uint32_t>(A * 65536)), ab(static_cast<uint32_t>((A + B) * 65536)),
+          abc(static_cast<uint32_t>((A + B + C) * 65536)), numParts(numParts_), withIn(withIn_) {}
+};
 
-extern "C" {
-
-int32_t ngd_rmat_csr(int32_t scale, int32_t ef, double A, double B, double C, uint64_t seed, int32_t num_parts,
-                     int32_t etype, int32_t with_in, int32_t rank, int32_t world, int32_t threads, ngd_csr* out) {
-    if (scale < 1 || scale > 31 || ef < 1 || num_parts < 1 || num_parts > 4096 || etype <= 0 || !out) return -1;
-    std::memset(out, 0, sizeof(*out));
-    const int T = threads < 1 ? 1 : threads;
-    const int NS = with_in ? 2 : 1;
-    const uint32_t a = static_cast<uint32_t>(A * 65536), ab = static_cast<uint32_t>((A + B) * 65536),
-                   abc = static_cast<uint32_t>((A + B + C) * 65536);
-    const uint64_t E = static_cast<uint64_t>(ef) << scale;
-    const uint64_t np = static_cast<uint64_t>(num_parts);
-    std::vector<uint8_t> mine(num_parts + 1, 0);                 // the parts this shard owns
-    for (int32_t p = 1; p <= num_parts; p++) mine[p] = world <= 1 || p % world == rank;
-    // keys (vid << 32 | bswap32(other)) per (thread, slot, part): the order of (vid, dst LE bytes)
-    const size_t NB = static_cast<size_t>(NS) * (num_parts + 1);
-    const bool trace = std::getenv("NGD_TRACE") != nullptr;
-    auto t0 = std::chrono::steady_clock::now();
-    auto lap = [&](const char* what) {
-        if (!trace) return;
+struct Lap {
+    bool on = std::getenv("NGD_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    void operator()(const char* what) {
+        if (!on) return;
         auto t1 = std::chrono::steady_clock::now();
         std::fprintf(stderr, "[ngd_rmat_csr] %s %.2fs\n", what, std::chrono::duration<double>(t1 - t0).count());
         t0 = t1;
-    };
-    std::vector<std::vector<std::vector<uint64_t>>> loc(T, std::vector<std::vector<uint64_t>>(NB));
-    {
-        std::vector<std::thread> th;
-        for (int t = 0; t < T; t++) {
-            th.emplace_back([&, t] {
-                auto& L = loc[t];
-                for (uint64_t i = E * t / T; i < E * (t + 1) / T; i++) {
-                    uint64_t su, du;
-                    rmatEdge(seed, i, scale, a, ab, abc, su, du);
-                    const uint64_t src = scramble(su, scale, seed), dst = scramble(du, scale, seed);
-                    const uint32_t ps = static_cast<uint32_t>(src % np) + 1, pd = static_cast<uint32_t>(dst % np) + 1;
-                    if (mine[ps]) L[ps].push_back(src << 32 | bswap32(static_cast<uint32_t>(dst)));
-                    if (with_in && mine[pd]) L[(num_parts + 1) + pd].push_back(dst << 32 | bswap32(static_cast<uint32_t>(src)));
-                }
-            });
-        }
-        for (auto& x : th) x.join();
     }
-    lap("sample");
-    // per (slot, part): gather, sort, unique (threads take buckets from a counter)
-    std::vector<std::vector<uint64_t>> bk(NB);
+};
+
+// samples [lo, hi) of the RMAT stream on T threads; every edge becomes an out-key under its src and
+// (withIn) an in-key under its dst: keys (vid << 32 | bswap32(other)), the order of (vid, the other
+// end's LE bytes) = RocksDB's within one (part, vid, type) prefix at rank 0. bucketOf(slot, part)
+// picks the output vector (or -1: not kept); returns per-thread vectors, nb of them per thread.
+template <typename BucketOf>
+std::vector<std::vector<std::vector<uint64_t>>> sampleKeys(const RmatParams& P, uint64_t lo, uint64_t hi, int T, size_t nb,
+                                                            BucketOf bucketOf) {
+    std::vector<std::vector<std::vector<uint64_t>>> loc(T, std::vector<std::vector<uint64_t>>(nb));
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++) {
+        th.emplace_back([&, t] {
+            auto& L = loc[t];
+            for (uint64_t i = lo + (hi - lo) * t / T; i < lo + (hi - lo) * (t + 1) / T; i++) {
+                uint64_t su, du;
+                rmatEdge(P.seed, i, P.scale, P.a, P.ab, P.abc, su, du);
+                const uint64_t src = scramble(su, P.scale, P.seed), dst = scramble(du, P.scale, P.seed);
+                const uint32_t ps = static_cast<uint32_t>(src % P.np) + 1, pd = static_cast<uint32_t>(dst % P.np) + 1;
+                const int64_t bo = bucketOf(0, ps);
+                if (bo >= 0) L[bo].push_back(src << 32 | bswap32(static_cast<uint32_t>(dst)));
+                if (P.withIn) {
+                    const int64_t bi = bucketOf(1, pd);
+                    if (bi >= 0) L[bi].push_back(dst << 32 | bswap32(static_cast<uint32_t>(src)));
+                }
+            }
+        });
+    }
+    for (auto& x : th) x.join();
+    return loc;
+}
+
+// the shard's CSR from its keys per (slot, part) bucket (bk[slot * (numParts + 1) + part], unsorted;
+// consumed): sorted and deduplicated per bucket, vertex table = union of the key vids per part
+void buildCsr(const RmatParams& P, int32_t etype, int T, std::vector<std::vector<uint64_t>>& bk, ngd_csr* out, Lap& lap) {
+    const int NS = P.withIn ? 2 : 1;
+    const int32_t num_parts = P.numParts;
+    const size_t NB = static_cast<size_t>(NS) * (num_parts + 1);
     {
         std::atomic<size_t> next{0};
         std::vector<std::thread> th;
-        for (int t = 0; t < T; t++) {
-            th.emplace_back([&] {
-                for (size_t b; (b = next.fetch_add(1)) < NB;) {
-                    size_t n = 0;
-                    for (int u = 0; u < T; u++) n += loc[u][b].size();
-                    if (!n) continue;
-                    bk[b].reserve(n);
-                    for (int u = 0; u < T; u++) {
-                        bk[b].insert(bk[b].end(), loc[u][b].begin(), loc[u][b].end());
-                        std::vector<uint64_t>().swap(loc[u][b]);
-                    }
-                    sortUnique(bk[b]);
-                }
-            });
-        }
+        for (int t = 0; t < T; t++) th.emplace_back([&] { for (size_t b; (b = next.fetch_add(1)) < NB;) sortUnique(bk[b]); });
         for (auto& x : th) x.join();
     }
     lap("sort");
@@ -490,7 +488,6 @@ int32_t ngd_rmat_csr(int32_t scale, int32_t ef, double A, double B, double C, ui
         out->dst[s] = static_cast<int64_t*>(std::malloc(std::max<uint64_t>(ne, 1) * 8));
         out->p0[s] = static_cast<int64_t*>(std::malloc(std::max<uint64_t>(ne, 1) * 8));
         out->p1[s] = static_cast<int64_t*>(std::malloc(std::max<uint64_t>(ne, 1) * 8));
-        // edge bases of each part, then the parts in parallel
         std::vector<uint64_t> ebase(num_parts + 2, 0);
         for (int32_t p = 1; p <= num_parts; p++) ebase[p + 1] = ebase[p] + bk[static_cast<size_t>(s) * (num_parts + 1) + p].size();
         std::atomic<int32_t> next{1};
@@ -509,7 +506,7 @@ int32_t ngd_rmat_csr(int32_t scale, int32_t ef, double A, double B, double C, ui
                             const int64_t o = static_cast<int64_t>(bswap32(static_cast<uint32_t>(K[j])));
                             out->dst[s][e] = o;
                             const int64_t os = s == 0 ? v : o, od = s == 0 ? o : v;   // the edge as generated
-                            const uint64_t h = mix64((static_cast<uint64_t>(os) << 20) ^ static_cast<uint64_t>(od) ^ seed);
+                            const uint64_t h = mix64((static_cast<uint64_t>(os) << 20) ^ static_cast<uint64_t>(od) ^ P.seed);
                             out->p0[s][e] = static_cast<int64_t>(h % 100);
                             out->p1[s][e] = static_cast<int64_t>(mix64(h ^ 0x70f1));
                         }
@@ -522,6 +519,117 @@ int32_t ngd_rmat_csr(int32_t scale, int32_t ef, double A, double B, double C, ui
         out->off[s][nv] = ne;
     }
     lap("csr");
+}
+
+std::string shardFile(const char* prefix, int32_t producer, int32_t consumer, int s) {
+    return std::string(prefix) + "." + std::to_string(producer) + "." + std::to_string(consumer) + "." + std::to_string(s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t ngd_rmat_csr(int32_t scale, int32_t ef, double A, double B, double C, uint64_t seed, int32_t num_parts,
+                     int32_t etype, int32_t with_in, int32_t rank, int32_t world, int32_t threads, ngd_csr* out) {
+    if (scale < 1 || scale > 31 || ef < 1 || num_parts < 1 || num_parts > 4096 || etype <= 0 || !out) return -1;
+    std::memset(out, 0, sizeof(*out));
+    const int T = threads < 1 ? 1 : threads;
+    const RmatParams P(scale, ef, A, B, C, seed, num_parts, with_in != 0);
+    const int NS = with_in ? 2 : 1;
+    const size_t NB = static_cast<size_t>(NS) * (num_parts + 1);
+    std::vector<uint8_t> mine(num_parts + 1, 0);                 // the parts this shard owns
+    for (int32_t p = 1; p <= num_parts; p++) mine[p] = world <= 1 || p % world == rank;
+    Lap lap;
+    auto loc = sampleKeys(P, 0, P.E, T, NB, [&](int s, uint32_t p) -> int64_t {
+        return mine[p] ? static_cast<int64_t>(s) * (num_parts + 1) + p : -1;
+    });
+    lap("sample");
+    std::vector<std::vector<uint64_t>> bk(NB);
+    for (size_t b = 0; b < NB; b++) {
+        size_t n = 0;
+        for (int u = 0; u < T; u++) n += loc[u][b].size();
+        bk[b].reserve(n);
+        for (int u = 0; u < T; u++) {
+            bk[b].insert(bk[b].end(), loc[u][b].begin(), loc[u][b].end());
+            std::vector<uint64_t>().swap(loc[u][b]);
+        }
+    }
+    buildCsr(P, etype, T, bk, out, lap);
+    return 0;
+}
+
+// The same shard built by `world` processes that split the sampling: producer q samples its 1/producers
+// of the edge stream and writes the keys of every consumer shard r (the owner of the key's part) to
+// "<prefix>.<q>.<r>.<slot>" (raw u64); once every producer has written, each shard reads its files
+// (ngd_rmat_csr_build, which removes them) and builds exactly what ngd_rmat_csr would.
+int32_t ngd_rmat_csr_sample(int32_t scale, int32_t ef, double A, double B, double C, uint64_t seed, int32_t num_parts,
+                            int32_t with_in, int32_t world, int32_t producer, int32_t producers, int32_t threads,
+                            const char* prefix) {
+    if (scale < 1 || scale > 31 || ef < 1 || num_parts < 1 || num_parts > 4096 || world < 1 || producers < 1 ||
+        producer < 0 || producer >= producers || !prefix)
+        return -1;
+    const int T = threads < 1 ? 1 : threads;
+    const RmatParams P(scale, ef, A, B, C, seed, num_parts, with_in != 0);
+    const int NS = with_in ? 2 : 1;
+    const size_t NB = static_cast<size_t>(world) * NS;
+    Lap lap;
+    const uint64_t lo = P.E * producer / producers, hi = P.E * (producer + 1) / producers;
+    auto loc = sampleKeys(P, lo, hi, T, NB, [&](int s, uint32_t p) -> int64_t {
+        return static_cast<int64_t>(world > 1 ? p % world : 0) * NS + s;
+    });
+    lap("sample");
+    for (int32_t r = 0; r < world; r++) {
+        for (int s = 0; s < NS; s++) {
+            const std::string path = shardFile(prefix, producer, r, s);
+            FILE* f = std::fopen(path.c_str(), "wb");
+            if (!f) return -2;
+            bool ok = true;
+            for (int u = 0; u < T && ok; u++) {
+                auto& v = loc[u][static_cast<size_t>(r) * NS + s];
+                ok = v.empty() || std::fwrite(v.data(), 8, v.size(), f) == v.size();
+                std::vector<uint64_t>().swap(v);
+            }
+            if (std::fclose(f) != 0 || !ok) return -2;
+        }
+    }
+    lap("write");
+    return 0;
+}
+
+int32_t ngd_rmat_csr_build(int32_t scale, uint64_t seed, int32_t num_parts, int32_t etype, int32_t with_in, int32_t rank,
+                           int32_t world, int32_t producers, int32_t threads, const char* prefix, ngd_csr* out) {
+    if (scale < 1 || scale > 31 || num_parts < 1 || num_parts > 4096 || etype <= 0 || !out || !prefix) return -1;
+    std::memset(out, 0, sizeof(*out));
+    const int T = threads < 1 ? 1 : threads;
+    const RmatParams P(scale, 16, 0, 0, 0, seed, num_parts, with_in != 0);
+    const int NS = with_in ? 2 : 1;
+    Lap lap;
+    std::vector<std::vector<uint64_t>> bk(static_cast<size_t>(NS) * (num_parts + 1));
+    for (int s = 0; s < NS; s++) {
+        // every producer's keys for this shard and slot, bucketed by part
+        std::vector<uint64_t> all;
+        for (int32_t q = 0; q < producers; q++) {
+            const std::string path = shardFile(prefix, q, rank, s);
+            FILE* f = std::fopen(path.c_str(), "rb");
+            if (!f) return -2;
+            std::fseek(f, 0, SEEK_END);
+            const long bytes = std::ftell(f);
+            std::fseek(f, 0, SEEK_SET);
+            const size_t n = bytes > 0 ? static_cast<size_t>(bytes) / 8 : 0;
+            const size_t at = all.size();
+            all.resize(at + n);
+            const bool ok = n == 0 || std::fread(all.data() + at, 8, n, f) == n;
+            std::fclose(f);
+            std::remove(path.c_str());
+            if (!ok) return -2;
+        }
+        std::vector<uint64_t> cnt(num_parts + 2, 0);
+        for (uint64_t k : all) cnt[(k >> 32) % P.np + 1]++;
+        for (int32_t p = 1; p <= num_parts; p++) bk[static_cast<size_t>(s) * (num_parts + 1) + p].reserve(cnt[p]);
+        for (uint64_t k : all) bk[static_cast<size_t>(s) * (num_parts + 1) + ((k >> 32) % P.np + 1)].push_back(k);
+    }
+    lap("read");
+    buildCsr(P, etype, T, bk, out, lap);
     return 0;
 }
 

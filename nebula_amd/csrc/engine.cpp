@@ -658,7 +658,7 @@ void buildPullHead(const HostGraph& g, int32_t s, int32_t m, DeviceGraph& d, con
     };
     parallelRows(windows, [&](uint64_t lo, uint64_t hi, int t) {
         std::vector<std::pair<uint32_t, uint32_t>> rows;        // (head length, row)
-        std::vector<uint32_t> nb;
+        std::vector<uint64_t> nb;
         for (uint64_t w = lo; w < hi; w++) {
             const uint64_t r0 = w * kPullWindow, r1 = std::min<uint64_t>(V, r0 + kPullWindow);
             rows.clear();
@@ -671,14 +671,18 @@ void buildPullHead(const HostGraph& g, int32_t s, int32_t m, DeviceGraph& d, con
                 const uint64_t at = r0 + i, slice = at / 64, lane = at % 64;
                 const uint32_t r = rows[i].second;
                 const uint64_t deg = in.off[r + 1] - in.off[r];
-                nb.assign(in.dgid.begin() + in.off[r], in.dgid.begin() + in.off[r + 1]);
-                nb.erase(std::remove(nb.begin(), nb.end(), kNoRow), nb.end());
+                // (out-degree, row) of every in-neighbour, read once each (the comparator of a sort over
+                // rows would re-read the degrees at random on every comparison)
+                nb.clear();
+                for (uint64_t e = in.off[r]; e < in.off[r + 1]; e++) {
+                    const uint32_t u = in.dgid[e];
+                    if (u == kNoRow) continue;
+                    nb.push_back(std::min<uint64_t>(outDeg(u), UINT32_MAX) << 32 | (~static_cast<uint64_t>(u) & 0xFFFFFFFFULL));
+                }
                 const size_t keep = std::min<size_t>(nb.size(), kPullK);
-                std::partial_sort(nb.begin(), nb.begin() + keep, nb.end(), [&](uint32_t a, uint32_t b) {
-                    const uint64_t da = outDeg(a), db = outDeg(b);
-                    return da != db ? da > db : a < b;
-                });
-                for (size_t k = 0; k < keep; k++) head[(slice * kPullK + k) * 64 + lane] = nb[k];
+                // largest degree first, then the smaller row: the largest (degree, ~row) keys
+                std::partial_sort(nb.begin(), nb.begin() + keep, nb.end(), std::greater<uint64_t>());
+                for (size_t k = 0; k < keep; k++) head[(slice * kPullK + k) * 64 + lane] = static_cast<uint32_t>(~nb[k]);
                 const bool isLong = deg > static_cast<uint64_t>(kPullK);
                 perm[at] = r | (isLong ? kPullLong : 0u);
                 longRows[t] += isLong;
@@ -1375,6 +1379,14 @@ int32_t ngx_commit(ngx_ctx* c, int32_t space) {
     if (!sp) return fail(c, NGX_E_SPACE_NOT_FOUND, "space not found");
     try {
         HIP_OK(hipSetDevice(c->device));
+        // NGX_HOST_TRACE=1: the commit's phases on stderr (export, tables, destinations, upload, mirrors)
+        auto tc = std::chrono::steady_clock::now();
+        auto phase = [&](const char* what) {
+            if (!c->htrace) return;
+            const auto now = std::chrono::steady_clock::now();
+            std::fprintf(stderr, "[ngx commit r%d] %s %.2f s\n", c->rank, what, std::chrono::duration<double>(now - tc).count());
+            tc = now;
+        };
         std::unique_ptr<HostGraph> hg;
         if (sp->loaded) {                                        // ngx_load_csr: the shard is built
             hg = std::move(sp->loaded);
@@ -1384,6 +1396,7 @@ int32_t ngx_commit(ngx_ctx* c, int32_t space) {
             Error e = exportSnapshot(*sp, c->rank, c->world, *hg);
             if (e.code != NGX_OK) return fail(c, e.code, e.msg);
         }
+        phase("export");
         // vertex tables of every shard -> destination rows
         std::vector<std::vector<std::pair<int32_t, int64_t>>> tables(c->world);
         std::vector<std::pair<int32_t, int64_t>> mine(hg->vid.size());
@@ -1421,12 +1434,16 @@ int32_t ngx_commit(ngx_ctx* c, int32_t space) {
                 }
             }
         }
+        phase("vertex tables");
         resolveDstRows(*sp, *hg, tables, c->world);
         hg->commitDigest = tablesDigest(tables, nonces);
         if (hg->shardBase.empty()) { hg->shardBase = {0, hg->vid.size()}; hg->vglobal = hg->vid.size(); }
         hg->gbase = hg->shardBase[c->rank];
+        phase("destination rows");
         sp->dev = upload(*hg, *sp);
+        phase("upload");
         attachMirrors(c, *sp, *hg, *sp->dev);
+        phase("mirrors + pull heads");
         sp->gen = nextGeneration();
         sp->host = std::move(hg);
         sp->staged = StagedRows();

@@ -598,24 +598,55 @@ Error loadCsrShard(const Space& sp, int32_t rank, int32_t world, const ngx_csr_s
     return Error{NGX_OK, ""};
 }
 
+// Destination rows: the global row of (ID_HASH(dst), dst) in its owner's vertex table. One open-address
+// hash of every shard's rows (only (part, vid) with part = ID_HASH(vid) can be found, as a lookup of
+// (ID_HASH(dst), dst) in the owner's table would), probed for the edges in blocks with the slots'
+// cache lines prefetched: a per-edge binary search over a 3 M-row table cost ~1 us of cache misses
+// (C3: 254 M edges per shard, 60 s on 2 threads), a prefetched probe ~30 ns.
 void resolveDstRows(const Space& sp, HostGraph& g,
                     const std::vector<std::vector<std::pair<int32_t, int64_t>>>& shardTables, int32_t world) {
     if (sp.numParts <= 0) return;                    // test-only layouts: no ID_HASH routing
     g.shardBase.assign(world + 1, 0);
     for (int32_t w = 0; w < world; w++) g.shardBase[w + 1] = g.shardBase[w] + shardTables[w].size();
     g.vglobal = g.shardBase[world];
+    uint64_t cap = 16;
+    while (cap < 2 * g.vglobal) cap <<= 1;
+    const uint64_t mask = cap - 1;
+    std::vector<int64_t> key(cap);
+    std::vector<uint32_t> row(cap, kNoRow);
+    auto slotOf = [mask](int64_t v) {
+        uint64_t z = static_cast<uint64_t>(v) + 0x9E3779B97F4A7C15ULL;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        return (z ^ (z >> 31)) & mask;
+    };
+    for (int32_t w = 0; w < world; w++) {
+        const auto& tab = shardTables[w];
+        for (uint64_t i = 0; i < tab.size(); i++) {
+            if (tab[i].first != idHash(tab[i].second, sp.numParts)) continue;
+            uint64_t h = slotOf(tab[i].second);
+            while (row[h] != kNoRow && key[h] != tab[i].second) h = (h + 1) & mask;
+            if (row[h] != kNoRow) continue;          // (part, vid) appears once per table: cannot happen
+            key[h] = tab[i].second;
+            row[h] = static_cast<uint32_t>(g.shardBase[w] + i);
+        }
+    }
     for (auto& s : g.slots) {
         parallelFor(s.dst.size(), [&](uint64_t lo, uint64_t hi) {
-            for (uint64_t e = lo; e < hi; e++) {
-                int64_t d = s.dst[e];
-                int32_t part = idHash(d, sp.numParts);
-                int32_t owner = part % world;
-                auto& tab = shardTables[owner];
-                auto it = std::lower_bound(tab.begin(), tab.end(), std::make_pair(part, d));
-                if (it != tab.end() && it->first == part && it->second == d) {
-                    s.dgid[e] = static_cast<uint32_t>(g.shardBase[owner] + (it - tab.begin()));
-                } else {
-                    s.dgid[e] = kNoRow;                 // the destination has no edges or tags here
+            constexpr uint64_t kBlock = 32;
+            uint64_t hs[kBlock];
+            for (uint64_t b = lo; b < hi; b += kBlock) {
+                const uint64_t n = std::min<uint64_t>(kBlock, hi - b);
+                for (uint64_t k = 0; k < n; k++) {
+                    hs[k] = slotOf(s.dst[b + k]);
+                    __builtin_prefetch(&key[hs[k]]);
+                    __builtin_prefetch(&row[hs[k]]);
+                }
+                for (uint64_t k = 0; k < n; k++) {
+                    const int64_t d = s.dst[b + k];
+                    uint64_t h = hs[k];
+                    while (row[h] != kNoRow && key[h] != d) h = (h + 1) & mask;
+                    s.dgid[b + k] = row[h];           // kNoRow: the destination has no edges or tags here
                 }
             }
         });

@@ -58,6 +58,10 @@ def lib():
         L.ngd_rmat_csr.argtypes = [i32, i32, dbl, dbl, dbl, u64, i32, i32, i32, i32, i32, i32, C_]
         L.ngd_rmat_csr.restype = i32
         L.ngd_csr_free.argtypes = [C_]
+        L.ngd_rmat_csr_sample.argtypes = [i32, i32, dbl, dbl, dbl, u64, i32, i32, i32, i32, i32, i32, ctypes.c_char_p]
+        L.ngd_rmat_csr_sample.restype = i32
+        L.ngd_rmat_csr_build.argtypes = [i32, u64, i32, i32, i32, i32, i32, i32, i32, ctypes.c_char_p, C_]
+        L.ngd_rmat_csr_build.restype = i32
         _lib = L
     return _lib
 
@@ -157,6 +161,27 @@ def rmat_csr(scale: int, ef: int = 16, seed: int = 42, num_parts: int = 100, wit
                             _threads(threads), ctypes.byref(c.c))
     if rc:
         raise ValueError("bad rmat_csr parameters")
+    return c
+
+
+def rmat_csr_sample(scale: int, prefix: str, producer: int, producers: int, world: int, ef: int = 16, seed: int = 42,
+                    num_parts: int = 100, with_in: bool = False, threads: int = 0, abc=GRAPH500):
+    """Producer `producer` of `producers` samples its share of the rmat() edge stream and writes every
+    shard's keys to files under `prefix` (then all producers meet; then rmat_csr_build per shard)."""
+    rc = lib().ngd_rmat_csr_sample(scale, ef, abc[0], abc[1], abc[2], seed, num_parts, int(with_in), world, producer,
+                                   producers, _threads(threads), prefix.encode())
+    if rc:
+        raise ValueError(f"rmat_csr_sample failed ({rc})")
+
+
+def rmat_csr_build(scale: int, prefix: str, rank: int, world: int, producers: int, seed: int = 42,
+                   num_parts: int = 100, with_in: bool = False, threads: int = 0) -> Csr:
+    """This shard's CSR from every producer's files (removed as read): equal to rmat_csr(…, rank, world)."""
+    c = Csr()
+    rc = lib().ngd_rmat_csr_build(scale, seed, num_parts, RMAT_EDGE, int(with_in), rank, world, producers,
+                                  _threads(threads), prefix.encode(), ctypes.byref(c.c))
+    if rc:
+        raise ValueError(f"rmat_csr_build failed ({rc})")
     return c
 
 

@@ -8,9 +8,10 @@ one GPU. Per query the rank writes its status, per-hop scanned edges and exchang
 its rows as sorted 128-bit digests (oracle.digest_columns, the test checker) in a .npy file; the
 parent merges them as graphd merges storage responses.
 
-Usage: python tests/multishard_worker.py RANK WORLD PORT OUT.json SCALE QUERIES.json [jit|vm] [full|plain]
+Usage: python tests/multishard_worker.py RANK WORLD PORT OUT.json SCALE QUERIES.json [jit|vm] [full|plain|csr]
        [snap:DIR | snapmix:DIR]
-(full: in-edges + tag `vt`, the multi-shard parity graph; plain: the bench / C2 layout)
+(full: in-edges + tag `vt`, the multi-shard parity graph; plain: out-edges only; csr: in-edges, no tag,
+bulk-loaded with ngx_load_csr from datagen.rmat_csr instead of KV rows)
 """
 import datetime
 import json
@@ -27,7 +28,9 @@ def main():
     rank, world, port = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
     out, scale, qfile = sys.argv[4], int(sys.argv[5]), sys.argv[6]
     mode = sys.argv[7] if len(sys.argv) > 7 else "jit"
-    full = (sys.argv[8] if len(sys.argv) > 8 else "full") == "full"
+    layout = sys.argv[8] if len(sys.argv) > 8 else "full"
+    full = layout == "full"
+    csr = layout == "csr"
     import numpy as np
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
@@ -48,9 +51,14 @@ def main():
 
     def committed(seed):
         x = fresh()
-        rows = datagen.rmat(scale, 16, seed, 100, full, full, rank=rank, world=world, threads=4)
-        x.load_kv(datagen.RMAT_SPACE, *rows.arrays())
-        rows.free()
+        if csr:                                          # in-edges, no tags, bulk-loaded (ngx_load_csr)
+            c = datagen.rmat_csr(scale, 16, seed, 100, True, rank=rank, world=world, threads=4)
+            x.load_csr(datagen.RMAT_SPACE, c.vpart, c.vid, c.slots)
+            c.free()
+        else:
+            rows = datagen.rmat(scale, 16, seed, 100, full, full, rank=rank, world=world, threads=4)
+            x.load_kv(datagen.RMAT_SPACE, *rows.arrays())
+            rows.free()
         x.commit(datagen.RMAT_SPACE)
         return x
 

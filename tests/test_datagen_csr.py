@@ -71,3 +71,21 @@ def test_rmat_csr_equals_kv_rows(rank, world, with_in):
         assert np.array_equal(dst, edst)
         assert np.array_equal(p0, ep0) and np.array_equal(p1, ep1)
     c.free()
+
+
+def test_rmat_csr_split_sampling_equals_one_process(tmp_path):
+    """The C3 test's split generation: 3 producers sample a third each and write every shard's keys;
+    each of 3 shards builds from the files exactly the shard ngd_rmat_csr builds alone."""
+    world = 3
+    prefix = str(tmp_path / "k")
+    for q in range(world):
+        datagen.rmat_csr_sample(11, prefix, q, world, world, num_parts=10, with_in=True, threads=2)
+    for r in range(world):
+        a = datagen.rmat_csr_build(11, prefix, r, world, world, num_parts=10, with_in=True, threads=2)
+        b = datagen.rmat_csr(11, 16, 42, 10, True, rank=r, world=world, threads=2)
+        assert a.nv == b.nv and np.array_equal(a.vid, b.vid) and np.array_equal(a.vpart, b.vpart)
+        for sa, sb in zip(a.slots, b.slots):
+            assert sa[0] == sb[0]
+            assert np.array_equal(sa[1], sb[1]) and np.array_equal(sa[2], sb[2])
+            assert all(np.array_equal(x, y) for x, y in zip(sa[3], sb[3]))
+    assert not list(tmp_path.iterdir())                  # the builders removed every file

@@ -1,0 +1,105 @@
+"""BASELINE C3 at its size: RMAT scale 26 (1.07 G generated edges, every one stored as out-edge and as
+in-edge: 2.1 G CSR edges over the shards), 100 parts over 8 shards by part % 8, `GO 3 STEPS FROM <1000
+vids> OVER e WHERE …`, with the layout `bench.py --gpus 8` uses. The 8 shards run as child processes on
+device 0 (tests/c3_rehearsal_worker.py) with the per-hop frontier exchange over the host collective
+(gloo) in place of RCCL, so push hops exchange bitmaps all-to-all and pull hops run at world 8 over
+the all-gathered frontier bitmap (k_repack_bits). Reference placement: CreateSpaceProcessor.cpp:107-120
+(pickHosts), StorageClient.h:260-290; per-hop frontier: GoExecutor.cpp:675-718.
+
+No oracle holds 2.1 G edges, so the worker checks properties that hold at any size (its docstring):
+per-hop scan sums == a host BFS over the generator's out-edges, unfiltered rows == last-hop edges,
+`p0 < 50` / `p0 >= 50` partition them, the same pull decisions on every rank, and at least one pull.
+The shards are bulk-loaded (ngx_load_csr): tests/test_multishard.py checks at world 8 that this load
+and the KV-row export give the oracle's rows.
+"""
+import json
+import os
+import shutil
+import socket
+import subprocess
+import sys
+import tempfile
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORLD, SCALE = 8, 26
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def run_c3(outdir, world=WORLD, scale=SCALE, layout="in", pull_factor=-1, timeout=700, threads=2):
+    """Start the ranks, wait, and return (summary, checks)."""
+    os.makedirs(outdir, exist_ok=True)
+    port = _free_port()
+    # the ranks' key files (one sampling pass split over the ranks): tmpfs when there is one
+    base = "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else outdir
+    keys = tempfile.mkdtemp(prefix="ngx_c3_", dir=base)
+    env = dict(os.environ, PYTHONPATH=ROOT, NGX_HOST_THREADS=str(threads), OMP_NUM_THREADS=str(threads),
+               NGX_C3_KEYS=keys)
+    logs = [open(os.path.join(outdir, f"r{r}.log"), "w") for r in range(world)]
+    procs = [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "c3_rehearsal_worker.py"), str(r),
+                               str(world), str(port), os.path.join(outdir, f"r{r}.json"), str(scale), layout,
+                               str(pull_factor)], env=env, stdout=logs[r], stderr=subprocess.STDOUT)
+             for r in range(world)]
+    t0 = time.time()
+    try:
+        for p in procs:
+            p.wait(timeout=max(1.0, timeout - (time.time() - t0)))
+    except subprocess.TimeoutExpired:
+        for p in procs:
+            p.kill()
+        for p in procs:
+            p.wait()
+        raise
+    finally:
+        for f in logs:
+            f.close()
+        shutil.rmtree(keys, ignore_errors=True)
+    wall = time.time() - t0
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, open(os.path.join(outdir, f"r{r}.log")).read()[-3000:]
+    rs = [json.load(open(os.path.join(outdir, f"r{r}.json"))) for r in range(world)]
+    summ = {"world": world, "scale": scale, "layout": layout, "wall_s": round(wall, 1),
+            "vertices": sum(r["vertices"] for r in rs), "edges": sum(r["edges"] for r in rs),
+            "device_gib": round(sum(r["device_gib"] for r in rs), 2),
+            "gen_s_max": round(max(r["gen_s"] for r in rs), 1), "commit_s_max": round(max(r["commit_s"] for r in rs), 1),
+            "bfs_s_max": round(max(r["bfs_s"] for r in rs), 1)}
+    for name in ("lt", "ge", "all"):
+        assert all(r[name]["ok"] for r in rs), [r[name]["error"] for r in rs]
+        hops = [sum(r[name]["hop_edges"][h] for r in rs) for h in range(len(rs[0][name]["hop_edges"]))]
+        summ[name] = {"nrows": sum(r[name]["nrows"] for r in rs), "hop_edges": hops,
+                      "hop_xchg_rank0": rs[0][name]["hop_xchg"],
+                      "pull_hops": [r[name]["pull_hops"] for r in rs],
+                      "ms_max": round(max(r[name]["ms"] for r in rs), 1)}
+    bfs = [sum(r["bfs_hop_edges"][h] for r in rs) for h in range(3)]
+    summ["host_bfs_hop_edges"] = bfs
+    checks = {
+        "hop_edges == host BFS": all(summ[n]["hop_edges"] == bfs for n in ("lt", "ge", "all")),
+        "all rows == last-hop edges": summ["all"]["nrows"] == bfs[2],
+        "p0<50 + p0>=50 == all": summ["lt"]["nrows"] + summ["ge"]["nrows"] == summ["all"]["nrows"],
+        "both sides non-empty": summ["lt"]["nrows"] > 0 and summ["ge"]["nrows"] > 0,
+        "same pull decisions on every rank": all(len(set(summ[n]["pull_hops"])) == 1 for n in ("lt", "ge", "all")),
+        "a hop pulled at world > 1": layout != "in" or all(summ[n]["pull_hops"][0] >= 1 for n in ("lt", "ge", "all")),
+    }
+    summ["checks"] = checks
+    with open(os.path.join(outdir, "summary.json"), "w") as f:
+        json.dump(summ, f, indent=1)
+    return summ, checks
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_c3_at_size(tmp_path):
+    out = os.path.join(ROOT, "gpurun_out", "c3") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else str(tmp_path)
+    summ, checks = run_c3(out)
+    print(json.dumps(summ, indent=1))
+    assert summ["edges"] > 2_000_000_000
+    assert all(checks.values()), checks

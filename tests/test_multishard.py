@@ -202,6 +202,34 @@ def test_multishard_go_matches_oracle(tmp_path, world, scale):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_multishard_csr_load_matches_oracle(tmp_path):
+    """World 8 with every shard bulk-loaded through ngx_load_csr (datagen.rmat_csr: the C3 at-size test's
+    input path) against the single-process oracle loaded from the same graph's KV rows: the columnar
+    load and the KV export give the same shards, and pull at world 8 runs over them."""
+    from nebula_amd import datagen
+    from oracle import oracle
+    from tests import fixtures
+
+    scale = 14
+    ds = fixtures.RmatDataset(scale, with_in=True, with_tag=False)
+    o = oracle.Oracle()
+    o.set_flags(threads=8)
+    ds.load_oracle(o)
+    queries = []
+    for i, text in enumerate(["GO 3 STEPS FROM {S} OVER e WHERE e.p0 < 50 YIELD e._dst, e._rank, e.p0, e.p1",
+                              "GO 2 STEPS FROM {S} OVER e REVERSELY YIELD e._dst, e.p1",
+                              "GO 1 TO 3 STEPS FROM {S} OVER e BIDIRECT WHERE e.p1 > 0 YIELD e._dst"]):
+        seeds = datagen.sample_vids(900 + i, 1 << scale, 20)
+        queries.append({"text": text.replace("{S}", ", ".join(str(int(v)) for v in seeds)), "pushdown": True})
+    pulled = [dict(q, pull_factor=1) for q in queries]
+    shards, digests = _run_shards(tmp_path, 8, scale, queries + pulled, layout="csr")
+    _check_merged(o, ds.space, queries + pulled, shards, digests)
+    n = len(queries)
+    assert sum(r["pull_hops"] for r in shards[0][n:]) >= 2
+
+
+@pytest.mark.gpu
 @pytest.mark.timeout(900)
 def test_c3_rehearsal_world8_scale22(tmp_path, rmat22):
     """The C3 code path (8 shards, 100 parts, per-hop frontier exchange) on the C2 graph: the bench query
