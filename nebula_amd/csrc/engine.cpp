@@ -9,6 +9,7 @@
 // per-hop frontier is exchanged as bitmaps over RCCL (ncclSend/ncclRecv all-to-all).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <atomic>
@@ -104,6 +105,16 @@ struct Timer {
     hipEvent_t a = nullptr, b = nullptr;
 };
 
+// ROCTX range on the host timeline of rocprofv3 (--marker-trace): a query, each hop, each kernel class
+// launch (the reference's FLAGS_trace_go step log, GoExecutor.cpp:559-569). Without a
+// tool attached a push / pop is a check of a registration flag.
+struct RoctxRange {
+    explicit RoctxRange(const char* name) { roctxRangePushA(name); }
+    ~RoctxRange() { roctxRangePop(); }
+    RoctxRange(const RoctxRange&) = delete;
+    RoctxRange& operator=(const RoctxRange&) = delete;
+};
+
 }  // namespace
 
 struct ngx_ctx {
@@ -184,6 +195,8 @@ struct ngx_ctx {
     bool dynHops = false;
     bool deviceLibm = false;                            // inexact libm of row values on the device (exprc.cpp)
     bool reservoirSampling = false;                     // storaged FLAGS_enable_reservoir_sampling: refused
+    bool narrowColumns = true;                          // integer columns at their narrowest width (at commit)
+    bool traceGo = false;                               // graphd FLAGS_trace_go: per-step log on stderr
     DBuf dynStats;                                      // per hop: packed (|F|, E) written by seed / compaction
     int cus = 256;                                      // compute units of the device
     // RCCL watchdog: collective work must finish within this; else the communicator is aborted
@@ -250,6 +263,7 @@ struct ngx_ctx {
     // bracket a launch group with events when profiling
     template <typename F>
     void timed(const char* name, uint64_t algoBytes, F&& f) {
+        RoctxRange range(name);                        // a ROCTX range per kernel class launch (rocprofv3 --marker-trace)
         if (htrace) hmark(std::string("L:") + name);
         if (!prof) { f(); if (htrace) hmark(std::string("l:") + name); return; }
         int k = statIndex(name);
@@ -298,13 +312,11 @@ const void* uploadAs(DeviceGraph& d, const std::vector<int64_t>& v, uint64_t n) 
     for (uint64_t i = 0; i < n; i++) t[i] = static_cast<T>(v[i]);
     return d.upload(t.data(), n);
 }
-const void* uploadNarrow(DeviceGraph& d, const std::vector<int64_t>& v, uint64_t n, int32_t& width) {
-    // Default on (NGX_NARROW=0 keeps 8 bytes): fewer HBM bytes per scanned edge. A strided-load
+const void* uploadNarrow(DeviceGraph& d, const std::vector<int64_t>& v, uint64_t n, int32_t& width, bool narrow) {
+    // Default on (flag "narrow_columns" 0 keeps 8 bytes): fewer HBM bytes per scanned edge. A strided-load
     // microbenchmark of the final hop's access pattern (tools/mb_final.hip) runs 607 -> 468 us with dst
     // int32, rank / filter column int8 (profiles/r02_mb_final.txt).
-    const char* env = std::getenv("NGX_NARROW");
-    const bool on = env == nullptr || env[0] != '0';
-    if (!on) { width = 8; return d.upload(v.data(), n); }
+    if (!narrow) { width = 8; return d.upload(v.data(), n); }
     int64_t lo = 0, hi = 0;
     for (uint64_t i = 0; i < n; i++) { lo = std::min(lo, v[i]); hi = std::max(hi, v[i]); }
     if (lo >= INT8_MIN && hi <= INT8_MAX) { width = 1; return uploadAs<int8_t>(d, v, n); }
@@ -324,12 +336,12 @@ int32_t narrowWidth(const int64_t* v, uint64_t n) {
     return 8;
 }
 
-void uploadColumns(DeviceGraph& d, std::vector<HostColumn>& hc, uint64_t n) {
+void uploadColumns(DeviceGraph& d, std::vector<HostColumn>& hc, uint64_t n, bool narrow) {
     for (auto& c : hc) {
         DCol dc{};
         dc.type = c.type;
         switch (c.type) {
-            case T_INT: case T_TIMESTAMP: case T_VID: dc.data = uploadNarrow(d, c.i64, n, dc.width); break;
+            case T_INT: case T_TIMESTAMP: case T_VID: dc.data = uploadNarrow(d, c.i64, n, dc.width, narrow); break;
             case T_FLOAT: case T_DOUBLE: dc.data = d.upload(c.f64.data(), n); break;
             case T_BOOL: dc.data = d.upload(c.b.data(), n); break;
             case T_STRING: {
@@ -387,12 +399,12 @@ std::unique_ptr<DeviceGraph> upload(HostGraph& g, const Space& sp) {
         ds.colBase = static_cast<int32_t>(d->cols.size());
         ds.ncols = static_cast<int32_t>(s.cols.size());
         ds.off = d->upload(s.off.data(), s.off.size());
-        ds.dst = uploadNarrow(*d, s.dst, s.dst.size(), ds.dstW);
+        ds.dst = uploadNarrow(*d, s.dst, s.dst.size(), ds.dstW, sp.narrow);
         ds.dgid = d->upload(s.dgid.data(), s.dgid.size());
-        ds.rank = uploadNarrow(*d, s.rank, s.rank.size(), ds.rankW);
+        ds.rank = uploadNarrow(*d, s.rank, s.rank.size(), ds.rankW, sp.narrow);
         ds.hasFlags = s.anyFlags ? 1 : 0;
         ds.eflags = s.anyFlags ? d->upload(s.eflags.data(), s.eflags.size()) : nullptr;
-        uploadColumns(*d, s.cols, s.dst.size());
+        uploadColumns(*d, s.cols, s.dst.size(), sp.narrow);
         d->slots.push_back(ds);
     }
     for (auto& t : g.tags) {
@@ -402,7 +414,7 @@ std::unique_ptr<DeviceGraph> upload(HostGraph& g, const Space& sp) {
         dt.ncols = static_cast<int32_t>(t.cols.size());
         dt.present = d->upload(t.present.data(), t.present.size());
         if (!ttlInfo(sp.tag(t.tag), dt.ttlCol, dt.ttlDur)) dt.ttlCol = -1;
-        uploadColumns(*d, t.cols, d->V);
+        uploadColumns(*d, t.cols, d->V, sp.narrow);
         d->tags.push_back(dt);
     }
     d->dslots = d->upload(d->slots.data(), d->slots.size());
@@ -1171,7 +1183,6 @@ int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
     if (hipSetDevice(c->device) != hipSuccess) return NGX_E_DEVICE;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return NGX_E_DEVICE;
     if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->cus < 1) c->cus = 256;
-    if (const char* dh = std::getenv("NGX_DYN_HOPS")) c->dynHops = std::string(dh) != "0";
     if (const char* ht = std::getenv("NGX_HOST_TRACE")) c->htrace = std::string(ht) == "1";
     if (hipHostMalloc(reinterpret_cast<void**>(&c->pin), ngx_ctx::kPinBytes, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
         std::memset(c->pin, 0, ngx_ctx::kPinBytes);
@@ -1343,6 +1354,7 @@ int32_t ngx_open_snapshot(ngx_ctx* c, int32_t space, const char* path, char* tag
             }
         }
         if (e.code) return fail(c, e.code, e.msg);
+        sp->narrow = c->narrowColumns;
         auto dev = upload(*hg, *sp);
         attachMirrors(c, *sp, *hg, *dev);
         HIP_OK(hipDeviceSynchronize());
@@ -1440,6 +1452,7 @@ int32_t ngx_commit(ngx_ctx* c, int32_t space) {
         if (hg->shardBase.empty()) { hg->shardBase = {0, hg->vid.size()}; hg->vglobal = hg->vid.size(); }
         hg->gbase = hg->shardBase[c->rank];
         phase("destination rows");
+        sp->narrow = c->narrowColumns;
         sp->dev = upload(*hg, *sp);
         phase("upload");
         attachMirrors(c, *sp, *hg, *sp->dev);
@@ -1520,6 +1533,8 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
     if (n == "dyn_hops") { c->dynHops = value != 0; return NGX_OK; }
     if (n == "device_libm") { c->deviceLibm = value != 0; return NGX_OK; }
     if (n == "enable_reservoir_sampling") { c->reservoirSampling = value != 0; return NGX_OK; }
+    if (n == "narrow_columns") { c->narrowColumns = value != 0; return NGX_OK; }
+    if (n == "trace_go") { c->traceGo = value != 0; return NGX_OK; }
     if (n == "jit_wait") { c->jit.drain(); return NGX_OK; }
     return fail(c, NGX_E_BAD_ARGUMENT, "unknown flag " + n);
 }
@@ -1535,6 +1550,8 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "dyn_hops") *value = c->dynHops ? 1 : 0;
     else if (n == "device_libm") *value = c->deviceLibm ? 1 : 0;
     else if (n == "enable_reservoir_sampling") *value = c->reservoirSampling ? 1 : 0;
+    else if (n == "narrow_columns") *value = c->narrowColumns ? 1 : 0;
+    else if (n == "trace_go") *value = c->traceGo ? 1 : 0;
     else if (n == "pull_hops") *value = static_cast<int64_t>(c->pullHops);
     else if (n == "pipe_walks") *value = static_cast<int64_t>(c->pipeWalks);
     else if (n == "jit_compiled") *value = static_cast<int64_t>(c->jit.compiled);
@@ -1812,14 +1829,14 @@ constexpr uint64_t kStrArenaMax = uint64_t(8) << 30;   // bytes of one record ho
 uint64_t* lookBack(ngx_ctx* c, uint64_t chunks) { return c->lbStatus.get<uint64_t>(lookBackWords(chunks)); }
 // the GO final hop's block tables (kargs.h kResv*): entries carry the launch's tag, so the table is
 // cleared only when it is (re)allocated
-// reservation geometry (kargs.h resv*) and the counters, cleared once here and then by every k_final_close
+// reservation geometry (kargs.h resv*) and the counters, cleared once here and then by every k_final_close.
+// Measured at C2 (final hop / close, us): 8 groups x 8 K-row blocks 765 / 34 (chunks wait on block
+// allocations), 8 x 32 K 346 / 15, 8 x 64 K 325 / 15, 8 x 128 K 320 / 18, 16 x 32 K 326 / 24, 32 x 8 K
+// 347 / 83, 64 x 4 K 339 / 193 (the close kernel moves up to G blocks of rows)
 void resvGeometry(ngx_ctx* c, FinalArgs& a) {
-    static const uint32_t G = std::getenv("NGX_RESV_G") ? std::atoi(std::getenv("NGX_RESV_G")) : 8;
-    static const uint32_t sh = std::getenv("NGX_RESV_SHIFT") ? std::atoi(std::getenv("NGX_RESV_SHIFT")) : 16;
-    static const uint32_t st = std::getenv("NGX_RESV_STRIDE") ? std::atoi(std::getenv("NGX_RESV_STRIDE")) : 32;
-    a.resvG = std::min<uint32_t>(std::max<uint32_t>(G, 1), kResvMaxGroups);
-    a.resvShift = std::max<uint32_t>(sh, 12);                  // a block holds a 512-thread chunk's rows
-    a.resvStride = std::max<uint32_t>(st, 1);
+    a.resvG = kResvGroups;
+    a.resvShift = kResvShift;
+    a.resvStride = 32;                                          // counters 256 B apart
     // two sets of counters: a launch uses one and its k_final_close clears the other for the next
     const uint64_t words = (a.resvG + 2) * static_cast<uint64_t>(a.resvStride);
     if (c->resvCtl.cap < 2 * words * 8 || c->resvCtl.p == nullptr || c->resvLastG != a.resvG ||
@@ -1897,18 +1914,13 @@ void prepareCols(ngx_ctx* c, FinalArgs& a, const std::vector<ColSpec>& spec, uin
 // copy kernel storing into the mapped staging: each DMA copy costs ~8 us of latency, which made a
 // GetNeighbors response's dozen arrays take 166 us (tools/gn_trace.py). Large batches use the DMA
 // engine (57 GB/s vs 55 GB/s for the kernel, tools/mb_d2h.hip, and the CUs stay free);
-// NGX_D2H=kernel / dma forces one.
 struct HostArr { const void* dev; size_t bytes; char* host; };
 void stageArrays(ngx_ctx* c, std::vector<HostArr>& arrs) {
     constexpr size_t kKernelCopyMax = size_t(32) << 20;
     size_t total = 0;
     for (auto& a : arrs) total += (a.bytes + 63) & ~size_t(63);
     char* stage = c->hostStage.get(std::max<size_t>(total, 64));
-    static const int mode = [] {
-        const char* e = std::getenv("NGX_D2H");
-        return e && std::string(e) == "kernel" ? 1 : e && std::string(e) == "dma" ? 2 : 0;
-    }();
-    const bool useKernel = mode == 1 || (mode == 0 && total <= kKernelCopyMax);
+    const bool useKernel = total <= kKernelCopyMax;
     char* stageDev = nullptr;
     if (useKernel && hipHostGetDevicePointer(reinterpret_cast<void**>(&stageDev), c->hostStage.p, 0) != hipSuccess)
         stageDev = nullptr;
@@ -2050,6 +2062,7 @@ const char* const kSamplingRefused =
 int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, const InputBind* in = nullptr,
               RootWalk* rw = nullptr) {
     c->hmark("in");
+    RoctxRange queryRange("ngx_go");
     DeviceGraph& d = *sp.dev;
     const int64_t now = p.now_sec > 0 ? p.now_sec : static_cast<int64_t>(std::time(nullptr));   // WallClock
     GoPlan gp;
@@ -2193,9 +2206,6 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         jq.rowMask = rowMask;
         for (int k = 0; k < 3; k++) jq.outW[k] = outW[k];
         if (compact) jq.yW = yW;
-        // NGX_FINAL_WG=512: 512-thread workgroups of 2 CE edges (half the per-chunk reservations)
-        static const int finalWg = std::getenv("NGX_FINAL_WG") ? std::atoi(std::getenv("NGX_FINAL_WG")) : 256;
-        jq.threads = finalWg == 512 ? 512 : 256;
         jq.input = rw && rw->perRow;
         jitSlotConsts(jq, jitKc, jitKl);
         std::string jerr;
@@ -2432,8 +2442,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         // the fused seed kernel reads the seeds from the mapped page-locked stage; else a device copy
         const int64_t* dv = nullptr;
         const int32_t* dp_ = nullptr;
-        static const bool seedCopy = std::getenv("NGX_SEED_COPY") && std::atoi(std::getenv("NGX_SEED_COPY")) != 0;
-        if (!fusedSeed || seedCopy || !stageSeedsMapped(c, sparts, svids, dp_, dv)) {
+        if (!fusedSeed || !stageSeedsMapped(c, sparts, svids, dp_, dv)) {
             int64_t* cv = reinterpret_cast<int64_t*>(c->seedVid.get<uint8_t>(nF * 12));   // vids, then parts
             int32_t* cp = reinterpret_cast<int32_t*>(cv + nF);
             stageSeeds(c, sparts, svids, cp, cv);
@@ -2490,7 +2499,11 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     std::vector<ColSpec> colSpec;
     for (int32_t ct : gp.colTypes) colSpec.push_back(ColSpec{ct == T_UNKNOWN || ct == T_STRING, ct == T_UNKNOWN});
 
+    std::vector<std::chrono::steady_clock::time_point> hopT;   // trace_go: host time at each hop's start
     for (uint32_t h = 1; h <= steps; h++) {
+        const std::string hopName = "ngx_go hop " + std::to_string(h);
+        RoctxRange hopRange(hopName.c_str());
+        if (c->traceGo) hopT.push_back(std::chrono::steady_clock::now());
         bool isRecord = h >= recordFrom;
         bool isFinal = h == steps;
         uint64_t nEnt = nF * static_cast<uint64_t>(hs.n);
@@ -2640,10 +2653,10 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             }
             // dyn: chunks of the upper bound E; the workgroups past the real chunks return at once
             // a 512-thread generated kernel covers two CE chunks per workgroup (dyn: an upper bound anyway)
-            const unsigned nt = kj ? static_cast<unsigned>(kj->threads) : 256u;
-            const unsigned grid = static_cast<unsigned>(nt == 512 && !dyn ? (Ef + 2 * kChunk - 1) / (2 * kChunk) : gridf);
+            const unsigned nt = 256u;
+            const unsigned grid = static_cast<unsigned>(gridf);
             // each group's block table: virtual rows of the group's chunks / block, + 1 partial block
-            const uint64_t perGroup = (grid + a.resvG - 1) / a.resvG * static_cast<uint64_t>(nt) * (kChunk / 256);
+            const uint64_t perGroup = (grid + a.resvG - 1) / a.resvG * kChunk;
             a.resvTB = static_cast<uint32_t>(((perGroup + (1ULL << a.resvShift) - 1) >> a.resvShift) + 1);
             a.resvTab = resvTable(c, static_cast<uint64_t>(a.resvTB) * a.resvG);
             if (++c->resvSeq == 0) c->resvSeq = 1;
@@ -2890,10 +2903,26 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     c->collectTimings();
     R.r.device_ms = ms;
     R.tDone = std::chrono::steady_clock::now();
+    if (c->traceGo) {
+        // GoExecutor's FLAGS_trace_go log (GoExecutor.cpp:559-569, 748-751, 834-836), one line per step of
+        // this shard: its frontier, scanned edges, the next frontier and the host time from the step's
+        // start to the next one's (or to the result)
+        hopT.push_back(R.tDone);
+        for (size_t h = 0; h + 1 < hopT.size() && h < R.hopEdges.size(); h++) {
+            std::fprintf(stderr, "[ngx trace_go r%d] Step:%zu finished, total request vertices %llu, scanned edges %llu, "
+                         "next frontier %llu, time cost %.0fus\n", c->rank, h + 1,
+                         static_cast<unsigned long long>(h < R.hopFrontier.size() ? R.hopFrontier[h] : 0),
+                         static_cast<unsigned long long>(R.hopEdges[h]),
+                         static_cast<unsigned long long>(h < R.hopNext.size() ? R.hopNext[h] : 0),
+                         std::chrono::duration<double, std::micro>(hopT[h + 1] - hopT[h]).count());
+        }
+        std::fprintf(stderr, "[ngx trace_go r%d] Total rows:%llu, total time %.0fus\n", c->rank,
+                     static_cast<unsigned long long>(totalRows), std::chrono::duration<double, std::micro>(R.tDone - R.tIn).count());
+    }
     c->hmark("done");
     c->hflush();
     const uint64_t flags = tail[0];
-    if (flags & 8u) return fail(c, NGX_E_DEVICE, "final-hop look-back did not complete (device fault)");
+    if (flags & 8u) return fail(c, NGX_E_DEVICE, "final-hop row reservation did not complete (device fault)");
     if (flags & 2u) return fail(c, NGX_E_UNSUPPORTED, "an expression needs a host-only construct (string building or parsing)");
     if (flags & 1u) return fail(c, NGX_E_QUERY, "an expression of WHERE / YIELD failed to evaluate");
     if (flags & 4u) return fail(c, NGX_E_QUERY, "YIELD value does not match its column type (boost::get)");

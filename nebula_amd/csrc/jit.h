@@ -24,7 +24,6 @@ namespace ngx {
 struct JitKernels {
     hipModule_t mod = nullptr;
     hipFunction_t final = nullptr;      // the fused final-hop kernel (final_kernels.h finalBody)
-    int threads = 256;                  // workgroup size of both (JitQuery::threads)
 };
 
 // one compiled program segment of a query: code[off ...] up to OP_END
@@ -56,7 +55,6 @@ struct JitQuery {
                                     // (others get an empty cell); INT32_MIN: never an edge column
     int32_t outW[3] = {8, 8, 8};    // bytes per row of the src / dst / rank arrays (compact results)
     std::vector<int32_t> yW;        // bytes per value of each stored column (empty or 8: int64 bits)
-    int32_t threads = 256;          // final-hop workgroup: 256 (CE edges) or 512 (2 CE edges; GO only)
 };
 
 class JitCache {

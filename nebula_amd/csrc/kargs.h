@@ -125,7 +125,7 @@ struct VertexCellArgs {
 constexpr uint64_t kTile = 4096;        // items per scan tile
 constexpr uint64_t kChunk = 2048;       // edges per edge-balanced workgroup (expansion, final hop)
 
-// GO final hop: where a chunk's passing rows go. One counter per group of chunks (chunk % resvG:
+// GO final hop: where a chunk's passing rows go (engine.cpp resvGeometry). One counter per group of chunks (chunk % resvG:
 // dispatch puts consecutive workgroups on different XCDs, so with 8 groups a group is one XCD's
 // chunks) hands out virtual rows; each group's virtual rows live in blocks of 2^resvShift physical
 // rows taken from one global counter (one atomic per block). Same-address atomics serialise at the
@@ -140,5 +140,7 @@ constexpr uint64_t kChunk = 2048;       // edges per edge-balanced workgroup (ex
 //   [(1 + G) * stride] the row count (written by k_final_close)
 constexpr uint64_t kDoneOff = 1024;
 constexpr uint32_t kResvMaxGroups = 64;
+constexpr uint32_t kResvGroups = 8;                   // a group per XCD
+constexpr uint32_t kResvShift = 16;                   // 64 K rows per block
 
 }  // namespace ngx

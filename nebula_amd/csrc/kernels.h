@@ -186,8 +186,6 @@ struct PullArgs {
     uint8_t curEp, ep;
     const uint64_t* dyn;                   // device-driven hop: packed totals; the row pass does nothing when
     uint64_t minE;                         // the hop's E < minE (the push expansion takes it)
-    uint32_t xcdRemap;                     // k_pull_head (a wave per slice): workgroup -> slices so that the
-                                           // 8 workgroups of a 2048-row window run on one XCD (grid % 8 == 0)
 };
 // worst-case queue words: (rows with in-degree > kPullK) * n + in-edges / kPullSeg + 1
 int launchPull(const PullArgs& a, hipStream_t s);

@@ -304,7 +304,7 @@ __global__ void k_chunk_first(const uint64_t* estart, uint64_t nEnt, uint64_t* c
 template <bool ONE, bool P32, bool MASK>
 __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst,
                                                     uint64_t nEnt, uint64_t E, HopSlots hs, uint8_t* visited,
-                                                    uint8_t epoch, const uint8_t* mask, int mode, const uint64_t* dyn,
+                                                    uint8_t epoch, const uint8_t* mask, const uint64_t* dyn,
                                                     uint64_t pullMinE) {
     __shared__ ChunkMap<ONE, false, P32> m;
     // direct-mapped LDS filter of the rows this workgroup already marked: a repeated destination
@@ -334,15 +334,8 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
             int s = ONE ? 0 : m.slot[q];
             uint64_t pos = P32 ? static_cast<uint64_t>(static_cast<uint32_t>(base + p) + static_cast<uint32_t>(m.pb[q]))
                                : static_cast<uint64_t>(static_cast<int64_t>(base + p) + static_cast<int64_t>(m.pb[q]));
-            g[k] = (mode & 1) ? __builtin_nontemporal_load(hs.dgid[s] + pos) : hs.dgid[s][pos];
+            g[k] = hs.dgid[s][pos];
         }
-    }
-    if (mode & 2) {                                      // already marked: no store
-        uint8_t cur[CITEMS];
-#pragma unroll
-        for (int k = 0; k < CITEMS; k++) cur[k] = g[k] == kNoRow ? epoch : visited[g[k]];
-#pragma unroll
-        for (int k = 0; k < CITEMS; k++) if (cur[k] == epoch) g[k] = kNoRow;
     }
 #pragma unroll
     for (int k = 0; k < CITEMS; k++) {
@@ -619,64 +612,29 @@ __device__ __forceinline__ bool pullSliceHit(const PullArgs& a, const PullSlice<
     return hit && cur.pw != kNoRow;
 }
 
-// PREF: waves stride over the slices, loading the next slice before probing this one; !PREF: the grid
-// has a wave per slice (no stride, no prefetch of a slice nobody probes)
-template <bool ONE, int KH, bool PREF>
+// A wave per slice of the head image (the grid covers the slices: r03 measured a grid of 2048
+// workgroups striding over the slices and loading the next one before probing the current 56 vs 52 us,
+// and one LDS-gathered mark write per 2048-row window 45 vs 33 us); KH = 2 head rounds loaded with the
+// slice before its first probe (48 us at C2 against 50 for 4 and 51 for 1).
+constexpr int kPullKH = 2;
+template <bool ONE>
 __global__ __launch_bounds__(WG) void k_pull_head(PullArgs a) {
     if (a.dyn != nullptr && (*a.dyn & kDynMask) < a.minE) return;   // a push hop (k_expand_mark takes it)
     const int lane = threadIdx.x & 63;
-    const uint64_t nw = static_cast<uint64_t>(gridDim.x) * NW;
     const uint64_t total = a.sliceEnd[ONE ? 0 : a.n - 1];
     // workgroups are dispatched to the 8 XCDs round robin (b % 8): logical workgroup (b % 8) * (G / 8) +
     // b / 8 keeps consecutive logical workgroups — the 32 slices of a 2048-row window, whose mark bytes
     // share 16 cache lines — on one XCD, so each line is dirtied in one L2 and written back whole
-    // instead of partially from up to 8 L2s
-    const uint64_t b = a.xcdRemap ? (blockIdx.x % 8u) * (gridDim.x / 8u) + blockIdx.x / 8u : blockIdx.x;
-    uint64_t j = (b * WG + threadIdx.x) >> 6;
+    // instead of partially from up to 8 L2s (33 vs 44 us at C2)
+    const uint64_t b = (blockIdx.x % 8u) * (gridDim.x / 8u) + blockIdx.x / 8u;
+    const uint64_t j = (b * WG + threadIdx.x) >> 6;
     if (j >= total) return;
     int s;
     uint64_t js;
-    PullSlice<KH> cur;
-    pullLoad<ONE, KH>(a, j, lane, s, js, cur);
-    while (true) {
-        const uint64_t jn = j + nw;
-        int sn = 0;
-        uint64_t jsn = 0;
-        PullSlice<KH> nxt;
-        if constexpr (PREF) pullLoad<ONE, KH>(a, jn < total ? jn : total - 1, lane, sn, jsn, nxt);   // unconditional
-        uint32_t row;
-        if (pullSliceHit<KH>(a, cur, s, js, lane, row)) a.out[row] = a.ep;
-        if (!PREF || jn >= total) break;
-        j = jn; s = sn; js = jsn; cur = nxt;
-    }
-}
-
-// One slot: a 1024-thread workgroup per 2048-row window (32 slices, 2 per wave); the window's marks
-// gather in LDS and leave as one contiguous 2 KiB write (0 for the rows not reached: marks are
-// compared with the hop's epoch), instead of a byte store per reached row scattered over the window.
-template <int KH>
-__global__ __launch_bounds__(1024) void k_pull_win(PullArgs a) {
-    if (a.dyn != nullptr && (*a.dyn & kDynMask) < a.minE) return;
-    __shared__ uint8_t win[kPullWindow];
-    const uint64_t r0 = static_cast<uint64_t>(blockIdx.x) * kPullWindow;
-    for (int i = threadIdx.x; i < static_cast<int>(kPullWindow); i += 1024) win[i] = 0;
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint64_t total = a.sliceEnd[0];
-#pragma unroll
-    for (int t = 0; t < 2; t++) {
-        const uint64_t j = static_cast<uint64_t>(blockIdx.x) * (kPullWindow / 64) + wid * 2 + t;
-        if (j >= total) break;
-        int s;
-        uint64_t js;
-        PullSlice<KH> cur;
-        pullLoad<true, KH>(a, j, lane, s, js, cur);
-        uint32_t row;
-        if (pullSliceHit<KH>(a, cur, s, js, lane, row)) win[row - r0] = 1;
-    }
-    __syncthreads();
-    const uint64_t n = a.V - r0 < kPullWindow ? a.V - r0 : kPullWindow;
-    for (uint64_t i = threadIdx.x; i < n; i += 1024) a.out[r0 + i] = win[i] ? a.ep : 0;
+    PullSlice<kPullKH> cur;
+    pullLoad<ONE, kPullKH>(a, j, lane, s, js, cur);
+    uint32_t row;
+    if (pullSliceHit<kPullKH>(a, cur, s, js, lane, row)) a.out[row] = a.ep;
 }
 
 // Segment pass (the next launch on the stream, so every segment word is visible): a workgroup per
@@ -914,7 +872,6 @@ struct VmEv {
     static constexpr int kEtype = 0;                  // edge type read per slot
     static constexpr int kRowMask = 7;                // row arrays: written where FinalArgs::o* is set
     static constexpr int kOutSrcW = 0, kOutDstW = 0, kOutRankW = 0;   // row array widths from FinalArgs
-    static constexpr int kThreads = WG;               // 256 threads, CE edges per workgroup
     static __device__ __forceinline__ void YV(const FinalArgs&, const EdgeCtx&, Val*) {}
     static __device__ __forceinline__ void YS(const FinalArgs&, const Val*, uint64_t, uint32_t&) {}
     static __device__ __forceinline__ bool hasP(const FinalArgs& a) { return a.P != nullptr; }
@@ -1265,9 +1222,8 @@ int launchExpandMark(const uint32_t* F, const uint64_t* estart, const uint64_t* 
     if (E == 0) return 0;
     // dyn: E is an upper bound here; the grid strides (kDynGrid workgroups at most)
     dim3 grid(static_cast<unsigned>(std::min<uint64_t>((E + CE - 1) / CE, dyn ? kDynGrid : ~0u)));
-    static const int mode = getenv("NGX_EXPAND_MODE") ? atoi(getenv("NGX_EXPAND_MODE")) : 0;
 #define NGX_EXPAND(ONE, P32, MASK) hipLaunchKernelGGL((k_expand_mark<ONE, P32, MASK>), grid, dim3(WG), 0, s, F, estart, \
-                                                    chunkFirst, nEnt, E, hs, visited, epoch, mask, mode, dyn, pullMinE)
+                                                    chunkFirst, nEnt, E, hs, visited, epoch, mask, dyn, pullMinE)
     if (mask) {
         if (hs.n == 1) NGX_EXPAND(true, false, true);
         else NGX_EXPAND(false, false, true);
@@ -1373,38 +1329,10 @@ int launchPull(const PullArgs& a, hipStream_t s) {
     if (a.n < 1 || a.n > kPullMaxSlots || a.V >= (1ULL << 31)) return 1;
     const uint64_t slices = a.sliceEnd[a.n - 1];
     if (slices == 0) return 0;
-    // a wave per slice (measured at C2: 52 vs 56 us for 2048 workgroups striding over the slices, each
-    // prefetching its next slice while it probes the current one); NGX_PULL_GRID caps the grid
-    static const uint64_t maxGrid = getenv("NGX_PULL_GRID") ? std::strtoull(getenv("NGX_PULL_GRID"), nullptr, 10) : ~0u;
-    dim3 grid(static_cast<unsigned>(std::min<uint64_t>((slices + NW - 1) / NW, maxGrid)));
-    // NGX_PULL_XCD=0: workgroups in dispatch order (no XCD-aware remap of the slices)
-    static const bool xcd = !(getenv("NGX_PULL_XCD") && std::atoi(getenv("NGX_PULL_XCD")) == 0);
-    // head rounds loaded with the slice before its first probe (NGX_PULL_KH: 1, 2 or 4; default 2:
-    // 48.1 us at C2 against 49.9 for 4 and 50.9 for 1, and half the head bytes of 4)
-    static const int kh = getenv("NGX_PULL_KH") ? std::atoi(getenv("NGX_PULL_KH")) : 2;
-    const bool pref = static_cast<uint64_t>(grid.x) * NW < slices;
-    PullArgs ax = a;
-    ax.xcdRemap = 0;
-    if (xcd && !pref) {                                 // grid padded to a multiple of 8 (extra waves exit)
-        grid.x = (grid.x + 7u) & ~7u;
-        ax.xcdRemap = 1;
-    }
-#define NGX_PULL(KH) do { \
-        if (pref) { if (a.n == 1) hipLaunchKernelGGL((k_pull_head<true, KH, true>), grid, dim3(WG), 0, s, ax); \
-                    else hipLaunchKernelGGL((k_pull_head<false, KH, true>), grid, dim3(WG), 0, s, ax); } \
-        else { if (a.n == 1) hipLaunchKernelGGL((k_pull_head<true, KH, false>), grid, dim3(WG), 0, s, ax); \
-               else hipLaunchKernelGGL((k_pull_head<false, KH, false>), grid, dim3(WG), 0, s, ax); } } while (0)
-    // NGX_PULL_WIN=1 (one slot): a workgroup per 2048-row window writing its marks in one piece
-    static const bool winMarks = getenv("NGX_PULL_WIN") && std::atoi(getenv("NGX_PULL_WIN")) != 0;
-    if (winMarks && a.n == 1) {
-        const dim3 wgrid(static_cast<unsigned>((slices + kPullWindow / 64 - 1) / (kPullWindow / 64)));
-        if (kh == 1) hipLaunchKernelGGL((k_pull_win<1>), wgrid, dim3(1024), 0, s, a);
-        else if (kh == 2) hipLaunchKernelGGL((k_pull_win<2>), wgrid, dim3(1024), 0, s, a);
-        else hipLaunchKernelGGL((k_pull_win<4>), wgrid, dim3(1024), 0, s, a);
-    } else if (kh == 1) NGX_PULL(1);
-    else if (kh == 2) NGX_PULL(2);
-    else NGX_PULL(4);
-#undef NGX_PULL
+    // a wave per slice; the grid padded to a multiple of 8 for the XCD-aware slice mapping (extra waves exit)
+    dim3 grid(static_cast<unsigned>(((slices + NW - 1) / NW + 7) & ~static_cast<uint64_t>(7)));
+    if (a.n == 1) hipLaunchKernelGGL((k_pull_head<true>), grid, dim3(WG), 0, s, a);
+    else hipLaunchKernelGGL((k_pull_head<false>), grid, dim3(WG), 0, s, a);
     // long unresolved in-lists: at most a.segCap segments, 2 workgroups per CU striding over them
     hipLaunchKernelGGL(k_pull_segments, dim3(256), dim3(WG), 0, s, a);
     return static_cast<int>(hipGetLastError());

@@ -121,6 +121,7 @@ struct Space {
     std::vector<std::string> edgeOrder;
     StagedRows staged;
     std::unique_ptr<HostGraph> loaded;  // ngx_load_csr: the next commit's shard (instead of the staged rows)
+    bool narrow = true;                 // device integer columns at their narrowest width (flag narrow_columns)
     std::unique_ptr<HostGraph> host;
     std::unique_ptr<DeviceGraph> dev;
     const SchemaSet* edge(int32_t absType) const {

@@ -53,20 +53,12 @@ struct VmEnv {
 // traffic: every wait on them also waits on lgkmcnt).
 template <typename T>
 __device__ __forceinline__ T gld(const void* p, uint64_t i) {
-#ifdef NGX_NT_LOAD                                   // generated kernels, NGX_JIT_NT bit 1
-    return __builtin_nontemporal_load(((const __attribute__((address_space(1))) T*)p) + i);
-#else
     return ((const __attribute__((address_space(1))) T*)p)[i];
-#endif
 }
 
 template <typename T>
 __device__ __forceinline__ void gst(void* p, uint64_t i, T v) {
-#ifdef NGX_NT_STORE                                  // generated kernels, NGX_JIT_NT bit 0
-    __builtin_nontemporal_store(v, ((__attribute__((address_space(1))) T*)p) + i);
-#else
     ((__attribute__((address_space(1))) T*)p)[i] = v;
-#endif
 }
 
 // element i of an integer array stored at its narrowest signed width w (1, 2, 4 or 8 bytes)

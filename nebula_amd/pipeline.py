@@ -160,6 +160,38 @@ class Pipeline:
             return Outcome(False, r.error, names)
         return Outcome(True, "", names, list(r.col_types), list(r.rows))
 
+    def _yield_constant(self, text: str) -> Outcome:
+        """A YIELD sentence with no input (YieldExecutor::executeConstant, YieldExecutor.cpp:343-379):
+        one row of its constant expressions (integer literals, hash(...), their negation, and string /
+        bool / double literals), typed as Collector::getSchema types the values; it is the left side
+        of `YIELD <vid> AS id | GO FROM $-.id ...` (GoTest.cpp:3083-3088)."""
+        p = ngql.Parser(text)
+        p.expect("kw", "YIELD")
+        names, row = [], []
+        while True:
+            e = p.expression()
+            alias = p.label() if p.accept("kw", "AS") else ""
+            try:
+                v = ngql.eval_const(e)
+            except ValueError:
+                if not isinstance(e, ngql.Prim):
+                    raise PipelineError("only constant YIELD sentences run in this path: " + text[:40])
+                v = e.value
+            names.append(alias or e.to_string())
+            if isinstance(v, bool):
+                row.append(("bool", v))
+            elif isinstance(v, int):
+                row.append(("int", v))
+            elif isinstance(v, float):
+                row.append(("double", v))
+            else:
+                row.append(("str", v))
+            if not p.accept("op", ","):
+                break
+        p.expect("eof")
+        types = [_KIND_TYPE[k] for k, _ in row]
+        return Outcome(True, "", names, types, [tuple(row)])
+
     def _piped(self, text: str, inp: Optional[Interim]) -> Outcome:
         parts = _split(text, "|")
         cur = inp
@@ -168,6 +200,8 @@ class Pipeline:
             body = _unwrap(part)
             if len(_split(body, "|")) > 1:
                 out = self._piped(body, cur)                      # ( set_sentence ) as a traverse sentence
+            elif body.upper().startswith("YIELD") and cur is None:
+                out = self._yield_constant(body)
             else:
                 if not body.upper().startswith("GO"):
                     raise PipelineError("only GO sentences run in this path: " + body[:40])

@@ -14,7 +14,7 @@ out=gpurun_out/prof/$tag
 mkdir -p "$out"
 args="--steps 10 --warmup 3 --cpu-budget 0 $*"
 echo "[profile] trace: bench.py $args"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run -f csv -- \
+timeout -k 10 300 rocprofv3 --kernel-trace --marker-trace --stats -d "$out/trace" -o run -f csv -- \
     python3 bench.py $args > "$out/bench_trace.json" 2> "$out/bench_trace.err" || { echo "trace pass failed"; tail -20 "$out/bench_trace.err"; exit 1; }
 regex='ngx_jit|k_expand|k_final|k_tile|k_compact|k_lookup|k_chunk|k_pull|k_seed|k_copy'
 echo "[profile] pmc FETCH_SIZE"

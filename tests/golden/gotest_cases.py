@@ -4,7 +4,8 @@ NBA fixture (tests/golden/nba.json). Data only: queries and expected rows.
 Placeholders: {P:<name>} / {T:<name>} in a query are replaced by the player / team vid
 (std::hash<std::string>(name), TraverseTestBase.h:122-126); "P:<name>" / "T:<name>" in an
 expected row stand for that vid. Rows are compared sorted, as verifyResult does
-(src/graph/test/TestBase.h:188-233). "empty": the response had no rows.
+(src/graph/test/TestBase.h:188-233). "empty": the response had no rows. "ok_only": the reference only
+asserts that the query succeeds (its rows are then compared with the oracle's).
 """
 
 RK = ("T:Mavericks",), ("T:Kings",), ("T:Bulls",)
@@ -29,6 +30,11 @@ MTON_STAR_PROPS = [("T:Thunders", 0, 2008, 0, ""), (0, "P:Paul George", 0, 90, "
                    ("T:Thunders", 0, 2017, 0, ""), (0, "P:Russell Westbrook", 0, 95, "Russell Westbrook"),
                    ("T:Thunders", 0, 2009, 0, ""), ("T:Rockets", 0, 2012, 0, ""),
                    (0, "P:Russell Westbrook", 0, 80, "Russell Westbrook")]
+
+# NStepQueryHangAndOOM (GoTest.cpp:3069-3107): GO 1 TO 3 STEPS FROM Tim Duncan OVER like, 11 rows
+NSTEP_HANG = [("P:" + n,) for n in (
+    "Tony Parker", "Manu Ginobili", "Tim Duncan", "Tim Duncan", "LaMarcus Aldridge", "Manu Ginobili",
+    "Tony Parker", "Manu Ginobili", "Tim Duncan", "Tim Duncan", "Tony Parker")]
 
 CASES = [
     # OneStepOutBound (GoTest.cpp:35-168)
@@ -320,10 +326,12 @@ CASES = [
                (0, "P:Kobe Bryant", 0), (0, "P:Marc Gasol", 0)]),
     dict(line=648, query="GO FROM {P:LaMarcus Aldridge} OVER * YIELD $$.team.name, $$.player.name",
          rows=[("Trail Blazers", ""), ("", "Tim Duncan"), ("", "Tony Parker"), ("Spurs", "")]),
+    # NStepQueryHangAndOOM (:3069-3107)
+    dict(line=3086, query="GO 1 TO 3 STEPS FROM {P:Tim Duncan} OVER like YIELD like._dst as dst", rows=NSTEP_HANG),
+    dict(line=3103, query="GO 1 TO 40 STEPS FROM {P:Tim Duncan} OVER like YIELD like._dst as dst", ok_only=True),
 ]
 
 # Pipes and variables (GoTest.cpp): `names' is verifyColNames' list when the test checks it.
-# Not transcribed: GoTest.cpp:3095 and :55 (YIELD sentences, another executor).
 _SPURS7 = [("T:Spurs",)] * 5 + [("T:Hornets",), ("T:Trail Blazers",)]
 _REF_PIPE = [("Tim Duncan", "Manu Ginobili", "Tim Duncan"), ("Tim Duncan", "Tony Parker", "LaMarcus Aldridge"),
              ("Tim Duncan", "Tony Parker", "Manu Ginobili"), ("Tim Duncan", "Tony Parker", "Tim Duncan"),
@@ -356,6 +364,9 @@ _OVERLAP = [(_TP, x, a, b) for x in (_TD, _MG, _LA)
 _TMG = "P:Tracy McGrady"
 
 PIPE_CASES = [
+    # OneStepOutBound (:55-69): a constant YIELD sentence feeding GO FROM $-.vid
+    dict(line=55, query="YIELD {P:Tim Duncan} as vid | GO FROM $-.vid OVER serve", names=["serve._dst"],
+         rows=[("T:Spurs",)]),
     dict(line=118, query="GO FROM {P:Boris Diaw} OVER like YIELD like._dst as id | GO FROM $-.id OVER like "
                          "YIELD like._dst as id | GO FROM $-.id OVER serve", names=["serve._dst"], rows=_SPURS7),
     dict(line=176, query="$var = GO FROM {P:Tracy McGrady} OVER like YIELD like._dst as id; "
@@ -439,4 +450,7 @@ PIPE_CASES = [
                           "FROM $-.src OVER like YIELD $-.src, $-.dst, like._src, like._dst", rows=_OVERLAP),
     dict(line=3057, query="$a = GO FROM {P:Tony Parker} OVER like YIELD like._src as src, like._dst as dst; GO 2 "
                           "STEPS FROM $a.src OVER like YIELD $a.src, $a.dst, like._src, like._dst", rows=_OVERLAP),
+    # NStepQueryHangAndOOM (:3069-3107): the constant YIELD sentence feeding the M TO N walk
+    dict(line=3094, query="YIELD {P:Tim Duncan} as id | GO 1 TO 3 STEPS FROM $-.id OVER like YIELD like._dst as dst",
+         names=["dst"], rows=NSTEP_HANG),
 ]

@@ -72,3 +72,23 @@ def test_reservoir_sampling_refuses_get_neighbors(qb):
         e.set_flag("enable_reservoir_sampling", 0)
     got, ref = e.get_neighbors(0, parts, [101], cols), o.get_neighbors(0, parts, [101], cols)
     assert got.failed_codes == [] and got.total_edges == ref.total_edges > 0
+
+
+def test_trace_go_logs_every_step(nba, capfd):
+    """graphd's FLAGS_trace_go (GoExecutor.cpp:559-569, 834-836): with trace_go set the library logs one
+    line per step (frontier, scanned edges, next frontier, time) and the total row count on stderr."""
+    ds, o, e = nba
+    s = ngql.parse_go(fixtures.nba_query("GO 3 STEPS FROM {P:Tim Duncan} OVER like YIELD like._dst"))
+    e.set_flag("trace_go", 1)
+    try:
+        got = e.go(ds.space, s)
+    finally:
+        e.set_flag("trace_go", 0)
+    err = capfd.readouterr().err
+    steps = [ln for ln in err.splitlines() if "trace_go" in ln and "Step:" in ln]
+    assert [ln.split("Step:")[1].split()[0] for ln in steps] == ["1", "2", "3"]
+    assert f"Total rows:{len(got.rows)}" in err
+    for ln, edges in zip(steps, got.hop_edges):
+        assert f"scanned edges {edges}," in ln
+    e.go(ds.space, s)
+    assert "trace_go" not in capfd.readouterr().err

@@ -173,6 +173,9 @@ def test_pull_gotest_nba(nba, case):
     e.set_flag("pull_factor", 1)
     r = e.go(ds.space, ngql.parse_go(q))
     got = fixtures.normalize_cells(r.rows)
+    if case.get("ok_only"):                  # compared with the oracle by _run
+        assert r.ok
+        return
     assert got == ([] if case.get("empty") else fixtures.nba_expected(case["rows"]))
 
 

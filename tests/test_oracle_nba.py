@@ -27,6 +27,8 @@ def test_gotest_known_answers(nba, case, pushdown):
         assert not r.ok
         return
     assert r.ok, r.error
+    if case.get("ok_only"):                # NStepQueryHangAndOOM: the 40-step walk must succeed
+        return
     got = fixtures.normalize_cells(r.rows)
     if case.get("empty"):
         assert got == []
