@@ -380,7 +380,9 @@ def cpu_baseline(rows, scale, args, gpu_edges_per_step):
     threads = max(1, min(usable, share) if share > 0 else usable)
     t0 = time.time()
     o = oracle.Oracle()
-    o.set_flags(threads=threads, max_handlers=threads, graph_threads=threads)
+    # 4 buckets per thread (max_handlers_per_req): the reader pool balances RMAT's hub-heavy vertices
+    # (genBuckets cuts the request's vertex list into equal counts, not equal edges)
+    o.set_flags(threads=threads, max_handlers=4 * threads, graph_threads=threads)
     o.add_space(datagen.RMAT_SPACE, args.parts)
     for is_edge, sid, name, fields in datagen.rmat_schemas():
         o.add_schema(datagen.RMAT_SPACE, is_edge, sid, name, fields)
@@ -402,7 +404,7 @@ def cpu_baseline(rows, scale, args, gpu_edges_per_step):
     k, edges, sec = best
     # the reference's own shape of the same work: graphd's final evaluation on one thread
     # (processFinalResult), storage on all of them; a quarter of the sample keeps the run short
-    o.set_flags(threads=threads, max_handlers=threads, graph_threads=1)
+    o.set_flags(threads=threads, max_handlers=4 * threads, graph_threads=1)
     k1 = max(1, k // 4)
     seeds = datagen.rmat_seeds(scale, k1, args.ef, 42, 42, threads=args.threads)
     r1 = o.go(datagen.RMAT_SPACE, ngql.parse_go(QUERY.replace("{S}", ", ".join(str(int(v)) for v in seeds))),
@@ -431,6 +433,8 @@ def cpu_baseline(rows, scale, args, gpu_edges_per_step):
                                   "note": "the reference's shape: storage on all threads, graphd's "
                                           "processFinalResult on one"},
             "cpu_model": model, "nproc": nproc, "usable_cpus": usable,
+            "threads_note": "cores = the process's CPU share (OMP_NUM_THREADS, 16 per GPU on these boxes; nproc counts "
+                            "the whole machine), capped by its affinity set",
             "storage_get_neighbors_1thread": {
                 "edges_per_s_one_prop": gn["one_prop"], "edges_per_s_dst_only": gn["dst_only"],
                 "edges": gn["edges"],

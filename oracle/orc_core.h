@@ -240,16 +240,22 @@ class RowReader {
     }
     // Returns nullptr where the reference returns an empty RowReader (or LOG(FATAL)s on a bad
     // header in the constructor, RowReader.cpp:199-212 — treated here as "no reader").
-    static std::unique_ptr<RowReader> make(const std::string& row, SchemaPtr schema) {
+    // the schema is borrowed: its owner (the schema registry, a response's schema map) outlives the reader;
+    // any shared_ptr to a Schema is taken by reference (no reference-count traffic per row)
+    template <class P, class = decltype(std::declval<const P&>().get())>
+    static std::unique_ptr<RowReader> make(const std::string& row, const P& schema) {
+        return make(row, static_cast<const Schema*>(schema.get()));
+    }
+    static std::unique_ptr<RowReader> make(const std::string& row, const Schema* schema) {
         if (!schema) return nullptr;
         std::unique_ptr<RowReader> r(new RowReader());
-        r->schema_ = std::move(schema);
+        r->schema_ = schema;
         r->row_ = &row;
         if (!r->processHeader(row)) return nullptr;
         return r;
     }
 
-    const Schema* getSchema() const { return schema_.get(); }
+    const Schema* getSchema() const { return schema_; }
     int32_t numFields() const { return static_cast<int32_t>(schema_->getNumFields()); }
 
     ResultType getBool(int64_t index, bool& v) const {
@@ -384,7 +390,7 @@ class RowReader {
 
  private:
     RowReader() = default;
-    SchemaPtr schema_;
+    const Schema* schema_ = nullptr;
     const std::string* row_ = nullptr;
     const uint8_t* data_ = nullptr;
     size_t size_ = 0;
@@ -493,9 +499,17 @@ class RowReader {
 // -------------------------------------------------------------------------------------
 class RowWriter {
  public:
-    explicit RowWriter(SchemaPtr schema = nullptr) : schema_(std::move(schema)) {
-        if (!schema_) { own_ = std::make_shared<Schema>(); schema_ = own_; }
+    // the schema is borrowed (see RowReader::make); without one the writer owns the schema it grows
+    explicit RowWriter(const Schema* schema = nullptr) : schema_(schema) {
+        if (!schema_) { own_ = std::make_shared<Schema>(); schema_ = own_.get(); }
     }
+    template <class P, class = decltype(std::declval<const P&>().get())>
+    explicit RowWriter(const P& schema) : RowWriter(static_cast<const Schema*>(schema.get())) {}
+    RowWriter(const RowWriter& o) : schema_(o.own_ ? nullptr : o.schema_), own_(o.own_ ? std::make_shared<Schema>(*o.own_) : nullptr),
+                                    cord_(o.cord_), colNum_(o.colNum_), blockOffsets_(o.blockOffsets_) {
+        if (own_) schema_ = own_.get();
+    }
+    RowWriter& operator=(const RowWriter&) = delete;
     const Schema& schema() const { return *schema_; }
 
     RowWriter& operator<<(bool v) {
@@ -578,7 +592,7 @@ class RowWriter {
     }
 
  private:
-    SchemaPtr schema_;
+    const Schema* schema_;
     std::shared_ptr<Schema> own_;       // set when writing without a schema (SchemaWriter)
     std::string cord_;
     int64_t colNum_ = 0;

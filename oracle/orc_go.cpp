@@ -280,20 +280,6 @@ struct GoExec {
         return req;
     }
 
-    int64_t countScanned(const std::vector<VertexID>& vids) {
-        auto it = eng.stores.find(space);
-        if (it == eng.stores.end()) return 0;
-        int32_t numParts = sm.partsNum(space);
-        int64_t n = 0;
-        for (auto v : vids) {
-            for (auto t : edgeTypes) {
-                auto r = it->second.prefix(keys::edgePrefix(idHash(v, numParts), v, t));
-                n += static_cast<int64_t>(r.second - r.first);
-            }
-        }
-        return n;
-    }
-
     bool stepOutLoop() {                                               // :520-606
         while (true) {
             auto returns = getStepOutProps();
@@ -304,10 +290,11 @@ struct GoExec {
             req.filter = pushed;
             req.return_columns = returns;
             res.hopFrontier.push_back(static_cast<int64_t>(starts.size()));
-            res.hopScanned.push_back(countScanned(starts));
             auto tq = std::chrono::steady_clock::now();
             auto resp = eng.getBound(req);
             trace("getBound", tq);
+            // edges the storage scan iterated (the TEPS numerator): counted by the buckets themselves
+            res.hopScanned.push_back(resp.scanned);
             if (!resp.failed_codes.empty()) return fail("Get neighbors failed");
             records.push_back(std::move(resp));
             tq = std::chrono::steady_clock::now();

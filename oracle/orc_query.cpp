@@ -165,14 +165,16 @@ class Processor {
                                                  std::max(eng_->flags.max_handlers_per_req, 1));
         std::vector<std::vector<VertexData>> bucketVertices(buckets.size());
         std::vector<std::vector<std::pair<PartitionID, KVCode>>> codes(buckets.size());
-        std::atomic<int64_t> totalEdges{0};
+        std::atomic<int64_t> totalEdges{0}, scanned{0};
         auto runBucket = [&](size_t b) {
+            int64_t sc = 0;
             for (auto& pv : buckets[b]) {
                 int64_t n = 0;
-                auto rc = processVertex(pv.first, pv.second, bucketVertices[b], n);
+                auto rc = processVertex(pv.first, pv.second, bucketVertices[b], n, sc);
                 totalEdges += n;
                 codes[b].emplace_back(pv.first, rc);
             }
+            scanned += sc;
         };
         int threads = std::max(1, eng_->flags.threads);
         if (threads == 1 || buckets.size() == 1) {
@@ -196,6 +198,7 @@ class Processor {
         }
         for (auto& bv : bucketVertices) for (auto& v : bv) resp.vertices.push_back(std::move(v));
         resp.total_edges = static_cast<int32_t>(totalEdges.load());
+        resp.scanned = scanned.load();
         for (auto& kv : vertexSchema_) resp.vertex_schema[kv.first] = kv.second;
         for (auto& kv : edgeSchema_) resp.edge_schema[kv.first] = kv.second;
         return resp;
@@ -420,22 +423,24 @@ class Processor {
 
     // collectEdgeProps (.inl:478-610) with processEdgeImpl's proc (QueryBoundProcessor.cpp:18-63)
     KVCode processEdgeImpl(PartitionID part, VertexID vid, EdgeType edgeType,
-                           const std::vector<PropContext>& props, FilterContext& fctx, VertexData& vdata) {
+                           const std::vector<PropContext>& props, FilterContext& fctx, VertexData& vdata,
+                           int64_t& scanned) {
         bool onlyStructure = onlyStructures_[edgeType];
-        std::shared_ptr<Schema> currEdgeSchema;
+        const Schema* currEdgeSchema = nullptr;
         if (!onlyStructure) {
             auto it = edgeSchema_.find(edgeType);
             if (it == edgeSchema_.end()) return KVCode::ERR_EDGE_NOT_FOUND;
-            currEdgeSchema = it->second;
+            currEdgeSchema = it->second.get();
         }
         if (!kv_ || !kv_->hasPart(part)) return KVCode::ERR_PART_NOT_FOUND;
         auto range = kv_->prefix(keys::edgePrefix(part, vid, edgeType));
+        scanned += static_cast<int64_t>(range.second - range.first);   // harness count, not reference logic
         std::vector<IdAndProp> edges;
         EdgeRanking lastRank = -1;
         VertexID lastDst = 0;
         bool firstLoop = true;
         int cnt = 0;
-        auto schema = sm_.getEdgeSchema(space_, std::abs(edgeType));
+        const auto& schema = sm_.getEdgeSchema(space_, std::abs(edgeType));
         auto ttl = edgeTTL_.find(edgeType);
         bool hasTTL = ttl != edgeTTL_.end();
         for (size_t i = range.first; i < range.second; i++) {
@@ -511,7 +516,7 @@ class Processor {
         return KVCode::SUCCEEDED;
     }
 
-    KVCode processVertex(PartitionID part, VertexID vid, std::vector<VertexData>& out, int64_t& nEdges) {
+    KVCode processVertex(PartitionID part, VertexID vid, std::vector<VertexData>& out, int64_t& nEdges, int64_t& scanned) {
         VertexData v;                                                    // QueryBoundProcessor.cpp:173-234
         v.vertex_id = vid;
         FilterContext fctx;
@@ -528,7 +533,7 @@ class Processor {
         if (onlyVertexProps_) { out.push_back(std::move(v)); return KVCode::SUCCEEDED; }
         for (auto& ec : edgeContexts_) {
             if (ec.second.empty()) continue;
-            auto ret = processEdgeImpl(part, vid, ec.first, ec.second, fctx, v);
+            auto ret = processEdgeImpl(part, vid, ec.first, ec.second, fctx, v, scanned);
             if (ret != KVCode::SUCCEEDED) return ret;
         }
         if (!v.edge_data.empty()) {

@@ -39,6 +39,7 @@ struct QueryResponse {
     std::map<EdgeType, std::shared_ptr<Schema>> edge_schema;
     std::vector<VertexData> vertices;
     int32_t total_edges = 0;
+    int64_t scanned = 0;                   // harness: keys under the requested (vertex, type) prefixes (TEPS)
 };
 
 struct StorageFlags {                      // QueryBaseProcessor.cpp:9-13 defaults

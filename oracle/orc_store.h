@@ -28,8 +28,11 @@ class SchemaManager {
         }
     }
     // ver < 0 => latest (AdHocSchemaManager.cpp:51-93 / MetaClient semantics); else exact version.
-    SchemaPtr getTagSchema(GraphSpaceID s, TagID id, SchemaVer ver = -1) const { return find(tags_, s, id, ver); }
-    SchemaPtr getEdgeSchema(GraphSpaceID s, EdgeType id, SchemaVer ver = -1) const { return find(edges_, s, id, ver); }
+    // references into the registry (schemas are added before any query and never removed): the per-edge
+    // lookups of collectEdgeProps copy no shared_ptr, whose reference count every reader thread would
+    // otherwise increment on one cache line (the baseline's threads then serialise on it)
+    const SchemaPtr& getTagSchema(GraphSpaceID s, TagID id, SchemaVer ver = -1) const { return find(tags_, s, id, ver); }
+    const SchemaPtr& getEdgeSchema(GraphSpaceID s, EdgeType id, SchemaVer ver = -1) const { return find(edges_, s, id, ver); }
     StatusOr<TagID> toTagID(GraphSpaceID s, const std::string& name) const {
         auto it = tagNames_.find({s, name});
         if (it == tagNames_.end()) return Status::Error("Tag not found");
@@ -51,14 +54,15 @@ class SchemaManager {
     }
 
  private:
-    using Versions = std::map<SchemaVer, std::shared_ptr<Schema>>;
-    static SchemaPtr find(const std::map<std::pair<GraphSpaceID, int32_t>, Versions>& m,
-                          GraphSpaceID s, int32_t id, SchemaVer ver) {
+    using Versions = std::map<SchemaVer, SchemaPtr>;
+    static const SchemaPtr& find(const std::map<std::pair<GraphSpaceID, int32_t>, Versions>& m,
+                                 GraphSpaceID s, int32_t id, SchemaVer ver) {
+        static const SchemaPtr none;
         auto it = m.find({s, id});
-        if (it == m.end() || it->second.empty()) return nullptr;
+        if (it == m.end() || it->second.empty()) return none;
         if (ver < 0) return it->second.rbegin()->second;
         auto v = it->second.find(ver);
-        return v == it->second.end() ? nullptr : v->second;
+        return v == it->second.end() ? none : v->second;
     }
     std::map<GraphSpaceID, int32_t> parts_;
     std::map<std::pair<GraphSpaceID, int32_t>, Versions> tags_, edges_;
