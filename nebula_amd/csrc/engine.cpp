@@ -401,7 +401,16 @@ std::unique_ptr<DeviceGraph> upload(HostGraph& g, const Space& sp) {
         ds.off = d->upload(s.off.data(), s.off.size());
         ds.dst = uploadNarrow(*d, s.dst, s.dst.size(), ds.dstW, sp.narrow);
         ds.dgid = d->upload(s.dgid.data(), s.dgid.size());
-        ds.rank = uploadNarrow(*d, s.rank, s.rank.size(), ds.rankW, sp.narrow);
+        // one rank for every edge (RMAT: rank 0 everywhere): no column, the value travels in HopSlots
+        const bool rankConst = sp.narrow && !s.rank.empty() &&
+                               std::all_of(s.rank.begin(), s.rank.end(), [&](int64_t r) { return r == s.rank[0]; });
+        ds.rankConst = rankConst ? s.rank[0] : 0;
+        if (rankConst) {
+            ds.rank = nullptr;
+            ds.rankW = narrowWidth(&s.rank[0], 1);
+        } else {
+            ds.rank = uploadNarrow(*d, s.rank, s.rank.size(), ds.rankW, sp.narrow);
+        }
         ds.hasFlags = s.anyFlags ? 1 : 0;
         ds.eflags = s.anyFlags ? d->upload(s.eflags.data(), s.eflags.size()) : nullptr;
         uploadColumns(*d, s.cols, s.dst.size(), sp.narrow);
@@ -977,6 +986,7 @@ HopSlots makeHopSlots(const Space& sp, const DeviceGraph& d, const std::vector<i
         hs.dgid[hs.n] = ds.dgid;
         hs.dst[hs.n] = ds.dst;
         hs.rank[hs.n] = ds.rank;
+        hs.rankC[hs.n] = ds.rankConst;
         hs.dstW[hs.n] = static_cast<int8_t>(ds.dstW);
         hs.rankW[hs.n] = static_cast<int8_t>(ds.rankW);
         hs.eflags[hs.n] = ds.hasFlags ? ds.eflags : nullptr;
@@ -2012,9 +2022,14 @@ JitQuery jitHopQuery(const Space& sp, const HopSlots& hs, const Programs& progs)
     jq.etype0 = hs.n == 1 ? hs.etype[0] : 0;
     jq.dstW = hs.n ? hs.dstW[0] : 0;
     jq.rankW = hs.n ? hs.rankW[0] : 0;
-    for (int s = 1; s < hs.n; s++) {
+    jq.rankConst = hs.n > 0;
+    for (int s = 0; s < hs.n; s++) {
         if (hs.dstW[s] != jq.dstW) jq.dstW = 0;
         if (hs.rankW[s] != jq.rankW) jq.rankW = 0;
+        jq.rankConst = jq.rankConst && hs.rank[s] == nullptr;
+    }
+    if (!jq.rankConst) {                                      // a rank column somewhere: widths per slot
+        for (int s = 0; s < hs.n; s++) if (hs.rank[s] == nullptr) jq.rankW = 0;
     }
     return jq;
 }

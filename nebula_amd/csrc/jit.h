@@ -44,6 +44,7 @@ struct JitQuery {
     bool oneSlot = false;           // the hop expands a single edge-type slot (ONE kernels)
     bool pos32 = false;             // every CSR position of the hop's slots fits 32 bits (ChunkMap P32)
     int dstW = 0, rankW = 0;        // key column widths shared by every slot of the hop (0: per slot)
+    bool rankConst = false;         // no slot of the hop has a rank column (HopSlots::rankC)
     std::vector<int32_t> slots;     // the hop's slots (HostGraph::slots indices)
     bool ttl = false;               // some slot's edge type has TTL info
     int32_t etype0 = 0;             // the only slot's signed type (0: several slots)

@@ -17,6 +17,7 @@ struct HopSlots {
     const void* rank[kMaxSlots];
     int8_t dstW[kMaxSlots];
     int8_t rankW[kMaxSlots];
+    int64_t rankC[kMaxSlots];           // the slot's one rank when rank[s] == nullptr (no rank column in HBM)
     const uint8_t* eflags[kMaxSlots];   // per-edge EF_* flags, nullptr when the slot has none
     int32_t colBase[kMaxSlots];         // first DCol of the slot in the column table
 };

@@ -863,6 +863,7 @@ __global__ __launch_bounds__(256) void k_copy_batch(CopyBatch b) {
 // ------------------------------------------------------------------------------ final hop (interpreter)
 struct VmEv {
     static constexpr int kEager = -1;                 // YIELD evaluated in the write pass
+    static constexpr bool kRankConst = false;         // rank columns read per slot (or its constant)
     static constexpr bool kPos32 = false;             // 64-bit CSR positions in the chunk map
     static constexpr bool kMask = true;               // reads FinalArgs::mask when set
     static constexpr int kDstW = 0, kRankW = 0;       // key column widths read per slot

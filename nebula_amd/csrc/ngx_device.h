@@ -49,9 +49,10 @@ struct DSlot {
     const uint64_t* off;   // V + 1
     const void* dst;       // dst vids at dstW bytes (1 / 2 / 4 / 8, sign-extended on load)
     const uint32_t* dgid;
-    const void* rank;      // ranks at rankW bytes
+    const void* rank;      // ranks at rankW bytes; nullptr when every edge of the slot has rank rankConst
     const uint8_t* eflags;
     int32_t dstW, rankW;
+    int64_t rankConst;
 };
 
 
