@@ -132,7 +132,7 @@ struct ngx_ctx {
     std::string lastError;
     std::mutex mu;
     // scratch
-    DBuf visited, F0, F1, estart, chunkFirst, tileSums, counters, lbStatus, seedPart, seedVid;
+    DBuf visited, F0, F1, estart, ebase, chunkFirst, tileSums, counters, lbStatus, seedPart, seedVid;
     DBuf cmpStatus[2];                                  // compaction tile / wave totals (kernels.h CompactArgs)
     DBuf frontierBits;                                  // the pull's frontier bitmap over global rows
     DBuf oSrc, oDst, oRank, oType, oEntry, progBuf, sendBits, recvBits, vcells, misc, oColDesc, edgeMask;
@@ -220,7 +220,7 @@ struct ngx_ctx {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
         spaces.clear();
-        for (DBuf* b : {&visited, &F0, &F1, &estart, &tileSums, &counters, &lbStatus, &seedPart, &seedVid, &oSrc,
+        for (DBuf* b : {&visited, &F0, &F1, &estart, &ebase, &tileSums, &counters, &lbStatus, &seedPart, &seedVid, &oSrc,
                         &oDst, &oRank, &oType, &oEntry, &chunkFirst, &oColDesc, &progBuf, &sendBits, &recvBits, &resvTab, &resvCtl,
                         &vcells, &misc, &edgeMask, &cmpStatus[0], &cmpStatus[1], &frontierBits, &oFlags, &rowCols, &rowLen,
                         &rowOff, &rowBytes, &pullSeg, &pullCtl, &dkTable, &dkKeep, &dkPre, &dSrc, &dDst, &dRank,
@@ -897,20 +897,26 @@ uint64_t awaitPub(ngx_ctx* c, const Publish& p, const uint64_t* devCopy, uint64_
     };
     if (!p.slot) { errBits(); return readScalar(c, devCopy); }
     auto t0 = std::chrono::steady_clock::now();
+    // kernels.h Publish: the words are taken once the tag matches them
+    auto take = [&](uint64_t& v) {
+        const uint64_t tag = __atomic_load_n(&c->pin[1], __ATOMIC_ACQUIRE);
+        v = __atomic_load_n(&c->pin[0], __ATOMIC_ACQUIRE);
+        const uint64_t x = __atomic_load_n(&c->pin[2], __ATOMIC_ACQUIRE);
+        if (tag != pubTag(p.seq, v, x)) return false;
+        if (extra) *extra = x;
+        return true;
+    };
+    uint64_t v = 0;
     for (uint32_t i = 0;; i++) {
-        if (__atomic_load_n(&c->pin[1], __ATOMIC_ACQUIRE) == p.seq) {
+        if (take(v)) {
             c->hmark("pub");
-            if (extra) *extra = __atomic_load_n(&c->pin[2], __ATOMIC_RELAXED);
-            return __atomic_load_n(&c->pin[0], __ATOMIC_RELAXED);
+            return v;
         }
         __builtin_ia32_pause();
         if ((i & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
     }
     HIP_OK(hipStreamSynchronize(c->stream));
-    if (__atomic_load_n(&c->pin[1], __ATOMIC_ACQUIRE) == p.seq) {
-        if (extra) *extra = __atomic_load_n(&c->pin[2], __ATOMIC_RELAXED);
-        return __atomic_load_n(&c->pin[0], __ATOMIC_RELAXED);
-    }
+    if (take(v)) return v;
     errBits();
     return readScalar(c, devCopy);
 }
@@ -2432,6 +2438,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         c->F0.get<uint32_t>(rowsCap);
         c->F1.get<uint32_t>(rowsCap);
         c->estart.get<uint64_t>(rowsCap * static_cast<uint64_t>(hs.n) + 1);
+        c->ebase.get<uint64_t>(rowsCap * static_cast<uint64_t>(hs.n) + 1);
         c->chunkFirst.get<uint64_t>(std::max<uint64_t>((slotEdges * mult + kChunk - 1) / kChunk + 1, cfCap));
     }
     bool haveHeads = false;                                    // chunkFirst of the next hop already built
@@ -2452,6 +2459,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     if (!fusedSeed) HIP_OK(hipMemsetAsync(counters, 0, 64, c->stream));
     uint32_t* F = c->F0.get<uint32_t>(std::max<uint64_t>(nF, 1));
     bool haveEstart = false;                                   // estart[] / E of the next hop already built
+    bool haveEbase = false;                                    // ... and its entries' CSR positions (ebase[])
     uint64_t fusedE = 0;
     if (nF) {
         // the fused seed kernel reads the seeds from the mapped page-locked stage; else a device copy
@@ -2469,6 +2477,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             // lookup + degrees + scan + chunk heads of the seed hop in one workgroup; E published (no
             // stream round trip); the first hop's final-kernel words cleared on the way
             uint64_t* est0 = c->estart.get<uint64_t>(nEnt0 + 1);
+            uint64_t* eb0 = c->ebase.get<uint64_t>(nEnt0 + 1);
             Publish pub = nextPub(c);
             // seeds may repeat (no DISTINCT): E <= slot edges x the largest multiplicity
             const uint64_t mult = std::max<uint64_t>(maxMultiplicity(svids), 1);
@@ -2476,11 +2485,12 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             uint64_t* cf = c->chunkFirst.get<uint64_t>(std::max(cf0, cfCap));
             c->timed("seed", nF * 12 + nEnt0 * 24, [&] {
                 if (launchSeedFrontierCf(dp_, dv, nF, d.vindex, hs, F, est0, pub, cf, std::max(cf0, cfCap), nullptr, 0, errFlag,
-                                         c->stream, dynStats, counters))
+                                         c->stream, dynStats, counters, eb0))
                     throw Error{NGX_E_DEVICE, "seed"};
             });
             fusedE = dyn ? slotEdges * mult : awaitPub(c, pub, est0 + nEnt0);   // dyn: an upper bound
             haveEstart = true;
+            haveEbase = true;
             haveHeads = true;
         } else {
             c->timed("lookup", nF * 12, [&] {
@@ -2523,6 +2533,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         bool isFinal = h == steps;
         uint64_t nEnt = nF * static_cast<uint64_t>(hs.n);
         uint64_t* estart = c->estart.get<uint64_t>(nEnt + 1);
+        const uint64_t* ebase = haveEbase ? c->ebase.get<uint64_t>(nEnt + 1) : nullptr;
         uint64_t* tiles = c->tileSums.get<uint64_t>((std::max<uint64_t>(nEnt, 1) + kTile - 1) / kTile + 1);
         uint64_t E = 0;
         if (haveEstart) {
@@ -2535,6 +2546,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             E = awaitPub(c, pub, estart + nEnt);
         }
         haveEstart = false;
+        haveEbase = false;
         if (isFinal && pushInvalid && nF) return fail(c, NGX_E_QUERY, "Get neighbors failed");
         if (!dyn) {                                              // dyn: read back after the last hop
             R.hopFrontier.push_back(nF);
@@ -2553,6 +2565,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         // the hop's storage request: which edges the processor emits (collectEdgeProps, .inl:501-608)
         FinalArgs a{};
         a.F = F; a.estart = estart; a.chunkFirst = chunkFirst; a.nEnt = nEnt; a.E = E; a.hs = hs;
+        a.ebase = ebase;
         a.vid = d.vid; a.V = d.V; a.gbase = d.gbase;
         a.env = VmEnv{d.dslots, d.dtags, d.dcols, dp.pool, errFlag + 1, now, dstTags, dstCols};
         a.P = (isFinal && progs.P >= 0) ? dp.code + progs.P : nullptr;
@@ -2628,6 +2641,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                 if (launchChunkFirst(est2, nEnt2, cf2, c->stream, nullptr, 0)) throw Error{NGX_E_DEVICE, "chunk first"};
                 HIP_OK(hipStreamSynchronize(c->stream));       // f2 / in2 leave scope
                 a.F = dF2; a.fin = dIn2; a.estart = est2; a.chunkFirst = cf2; a.nEnt = nEnt2; a.E = Ef;
+                a.ebase = nullptr;
                 a.env.input = rw->input;
             }
             // outputs sized for every edge passing (rows are written in the same launch), plus the groups'
@@ -2780,7 +2794,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         } else if ((!pull || dyn) && E) {
             c->timed("expand", dyn ? 0 : E * 8, [&] {
                 if (launchExpandMark(F, estart, chunkFirst, nEnt, E, hs, marks, ep, pos32, c->stream, mask,
-                                     dynTotal, dyn ? pullMinE : ~0ULL))
+                                     dynTotal, dyn ? pullMinE : ~0ULL, ebase))
                     throw Error{NGX_E_DEVICE, "expand"};
             });
         }
@@ -2806,6 +2820,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             ca.hs = hs;
             ca.outF = Fn;
             ca.estart = c->estart.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
+            ca.ebase = c->ebase.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
             ca.chunkFirst = c->chunkFirst.get<uint64_t>(cfCap);
             ca.cfCap = cfCap;
             ca.tileSum = cmpTile;
@@ -2823,6 +2838,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                 if (launchCompactLb(ca, c->stream)) throw Error{NGX_E_DEVICE, "compact"};
             });
             haveEstart = true;
+            haveEbase = true;
             haveHeads = true;
             if (dyn) {                                          // upper bounds; the device has the real ones
                 nF = d.V;

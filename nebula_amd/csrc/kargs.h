@@ -45,6 +45,7 @@ struct FinalArgs {
     const uint32_t* F;                  // frontier rows
     const uint64_t* estart;             // exclusive prefix of entry degrees, [nEnt] = E
     const uint64_t* chunkFirst;         // entry holding the first edge of each CE-edge chunk
+    const uint64_t* ebase;              // optional: per entry, its CSR position (hs.off[s][F[i]]); null: read off[]
     uint64_t nEnt;
     uint64_t E;
     HopSlots hs;

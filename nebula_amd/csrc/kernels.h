@@ -7,11 +7,31 @@
 
 namespace ngx {
 
-// host-mapped publication slot of a scan total: slot[0] = value, slot[1] = seq (written last)
+// host-mapped publication slot of a scan total: slot[0] = value, slot[2] = an extra word (the final
+// hop's error bits), slot[1] = pubTag(seq, value, extra). The three are relaxed system-scope stores: a
+// release would make the kernel write back every dirty L2 line first (buffer_wbl2, measured on the
+// critical path of the seed / compaction / close kernels), and the host needs no device data ordered
+// before the value, only the value itself, which it accepts when slot[1] matches the tag of what it
+// read (a slot caught between stores mismatches and is polled again).
 struct Publish {
     uint64_t* slot;
     uint64_t seq;
 };
+__host__ __device__ inline uint64_t pubMix(uint64_t x) {
+    x ^= x >> 31;
+    x *= 0x7fb5d329728ea185ULL;
+    x ^= x >> 27;
+    x *= 0x81dadef4bc2dd44dULL;
+    return x ^ (x >> 33);
+}
+__host__ __device__ inline uint64_t pubTag(uint64_t seq, uint64_t value, uint64_t extra) {
+    return pubMix(seq ^ pubMix(value + 0x9e3779b97f4a7c15ULL) ^ pubMix(extra ^ 0x2545f4914f6cdd1dULL) * 3);
+}
+__device__ inline void publishWords(uint64_t* slot, uint64_t seq, uint64_t value, uint64_t extra) {
+    __hip_atomic_store(slot, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(slot + 2, extra, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(slot + 1, pubTag(seq, value, extra), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // (part, vid) -> shard vertex row: open-addressing table (linear probing, power-of-two capacity
 // >= 2V, built at commit) so a seed lookup is ~1 probe instead of a binary search over V rows
@@ -52,7 +72,8 @@ int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst
 constexpr uint64_t kDynGrid = 2048;                // workgroups of a device-driven (grid-stride) launch
 int launchExpandMark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst, uint64_t nEnt, uint64_t E,
                      const HopSlots& hs, uint8_t* visited, uint8_t epoch, bool pos32, hipStream_t s,
-                     const uint8_t* mask = nullptr, const uint64_t* dyn = nullptr, uint64_t pullMinE = ~0ULL);
+                     const uint8_t* mask = nullptr, const uint64_t* dyn = nullptr, uint64_t pullMinE = ~0ULL,
+                     const uint64_t* ebase = nullptr);   // ebase: FinalArgs::ebase
 // storage outcome per hop edge (a.E entries of out: 1 = emitted) for the max-edges / TTL mask path;
 // a's F / estart / chunkFirst / hs / env / P / propsMask / ttl fields are read
 int launchStoragePass(const FinalArgs& a, uint8_t* out, hipStream_t s);
@@ -83,6 +104,7 @@ struct CompactArgs {
     HopSlots hs;
     uint32_t* outF;
     uint64_t* estart;
+    uint64_t* ebase;                    // optional: the entries' CSR positions (FinalArgs::ebase)
     uint64_t* chunkFirst;
     uint64_t cfCap;                     // entries of chunkFirst (overflow sets err[3])
     uint64_t* tileSum;                  // one word per tile (written by the count launch)
@@ -105,7 +127,8 @@ int launchCompactLb(const CompactArgs& a, hipStream_t s);
 int launchSeedFrontierCf(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, const HopSlots& hs,
                          uint32_t* F, uint64_t* estart, Publish pub, uint64_t* chunkFirst, uint64_t cfCap,
                          uint64_t* zero, uint32_t nzero, uint32_t* err, hipStream_t s, uint64_t* packedOut = nullptr,
-                         uint64_t* zero8 = nullptr);     // zero8: 8 words cleared first (the query's counters)
+                         uint64_t* zero8 = nullptr,      // zero8: 8 words cleared first (the query's counters)
+                         uint64_t* ebase = nullptr);     // ebase: the entries' CSR positions (FinalArgs::ebase)
 // QueryResponse rows of GetNeighbors (storage.thrift IdAndProp.props): per returned edge, the RowWriter
 // row of its type's response edge schema (QueryBoundProcessor.cpp:38-43 with collectProps,
 // QueryBaseProcessor.inl:325-399). Two launches: write == false stores each row's length in rowLen,

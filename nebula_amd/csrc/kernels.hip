@@ -128,10 +128,7 @@ __global__ __launch_bounds__(1024) void k_scan_tiles(uint64_t* sums, uint64_t nt
     if (threadIdx.x == 0) {
         *total = sm[16];
         if (tail) tail[(sm[16] >> kFdShift) * static_cast<uint64_t>(ns)] = sm[16] & kFdMask;
-        if (pub.slot) {
-            __hip_atomic_store(pub.slot, sm[16], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(pub.slot + 1, pub.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        if (pub.slot) publishWords(pub.slot, pub.seq, sm[16], 0);
     }
 }
 
@@ -220,7 +217,7 @@ __global__ __launch_bounds__(1024) void k_seed_frontier(const int32_t* qpart, co
                                                         HopSlots hs, uint32_t* F, uint64_t* estart, Publish pub,
                                                         uint64_t* chunkFirst, uint64_t cfCap, uint64_t* zero,
                                                         uint32_t nzero, uint32_t* err, uint64_t* packedOut,
-                                                        uint64_t* zero8) {
+                                                        uint64_t* zero8, uint64_t* ebase) {
     if (CF && threadIdx.x < nzero) zero[threadIdx.x * kDoneOff] = 0;
     if (CF && zero8 != nullptr && threadIdx.x >= 64 && threadIdx.x < 72) zero8[threadIdx.x - 64] = 0;
     __shared__ uint64_t sm[1024 / 64 + 1];
@@ -265,7 +262,9 @@ __global__ __launch_bounds__(1024) void k_seed_frontier(const int32_t* qpart, co
         for (int s = 0; s < hs.n; s++) {
             estart[i * hs.n + s] = pre;
             if (rows[k] == kNoRow) continue;
-            uint64_t d = hs.off[s][rows[k] + 1] - hs.off[s][rows[k]];
+            const uint64_t o = hs.off[s][rows[k]];
+            if (ebase) ebase[i * hs.n + s] = o;
+            uint64_t d = hs.off[s][rows[k] + 1] - o;
             if (CF) writeChunkHeads(chunkFirst, cfCap, i * hs.n + s, pre, d, err);
             pre += d;
         }
@@ -273,10 +272,7 @@ __global__ __launch_bounds__(1024) void k_seed_frontier(const int32_t* qpart, co
     if (threadIdx.x == 0) {
         estart[n * hs.n] = sm[16];
         if (packedOut) *packedOut = (n << kDynShift) | sm[16];       // device-driven hops read this
-        if (pub.slot) {
-            __hip_atomic_store(pub.slot, sm[16], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(pub.slot + 1, pub.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        if (pub.slot) publishWords(pub.slot, pub.seq, sm[16], 0);
     }
 }
 
@@ -305,7 +301,7 @@ template <bool ONE, bool P32, bool MASK>
 __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst,
                                                     uint64_t nEnt, uint64_t E, HopSlots hs, uint8_t* visited,
                                                     uint8_t epoch, const uint8_t* mask, const uint64_t* dyn,
-                                                    uint64_t pullMinE) {
+                                                    uint64_t pullMinE, const uint64_t* ebase) {
     __shared__ ChunkMap<ONE, false, P32> m;
     // direct-mapped LDS filter of the rows this workgroup already marked: a repeated destination
     // (hubs of a power-law graph) costs an LDS probe instead of another L2 byte-store transaction
@@ -323,7 +319,7 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
     for (uint32_t chunk = blockIdx.x; chunk < nChunks; chunk += gridDim.x) {
     const uint64_t base = static_cast<uint64_t>(chunk) * CE;
     const uint32_t cnt = static_cast<uint32_t>(E - base < CE ? E - base : CE);
-    buildMap<ONE, false, P32>(estart, chunkFirst, nEnt, chunk, nChunks, base, cnt, F, hs, m);
+    buildMap<ONE, false, P32>(estart, chunkFirst, nEnt, chunk, nChunks, base, cnt, F, hs, m, ebase);
     uint32_t g[CITEMS];
 #pragma unroll
     for (int k = 0; k < CITEMS; k++) {
@@ -473,10 +469,7 @@ __global__ __launch_bounds__(WG) void k_compact_write(CompactArgs a) {
         const uint64_t incl = pre + a.waveSum[tile * NW + wid];
         a.estart[(incl >> kFdShift) * static_cast<uint64_t>(ns)] = incl & kFdMask;
         *a.total = incl;
-        if (a.pub.slot) {
-            __hip_atomic_store(a.pub.slot, incl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(a.pub.slot + 1, a.pub.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        if (a.pub.slot) publishWords(a.pub.slot, a.pub.seq, incl, 0);
     }
     if (tile == 0 && threadIdx.x < a.nzero) a.zero[threadIdx.x * kDoneOff] = 0;
     if (__ballot(flags != 0) == 0) return;              // wave-uniform: every lane stays for the scans below
@@ -499,11 +492,14 @@ __global__ __launch_bounds__(WG) void k_compact_write(CompactArgs a) {
         a.outF[f] = static_cast<uint32_t>(r);
         if (ONE) {
             a.estart[f] = e;
+            if (a.ebase) a.ebase[f] = a.hs.off[0][r];          // L1/L2 hit: waveDegrees read it
             writeChunkHeads(a.chunkFirst, a.cfCap, f, e, deg[k], a.err);
         } else {
             for (int s = 0; s < ns; s++) {
-                const uint64_t d = a.hs.off[s][r + 1] - a.hs.off[s][r];
+                const uint64_t o = a.hs.off[s][r];
+                const uint64_t d = a.hs.off[s][r + 1] - o;
                 a.estart[f * ns + s] = e;
+                if (a.ebase) a.ebase[f * ns + s] = o;
                 writeChunkHeads(a.chunkFirst, a.cfCap, f * ns + s, e, d, a.err);
                 e += d;
             }
@@ -971,9 +967,7 @@ __global__ __launch_bounds__(WG) void k_final_close(FinalArgs a) {
                 uint64_t bits = 0;
                 for (int k = 0; k < 4; k++)
                     bits |= static_cast<uint64_t>(__hip_atomic_load(a.err + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) << k;
-                __hip_atomic_store(a.rowsPub, R, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_store(a.rowsPub + 2, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_store(a.rowsPub + 1, a.rowsSeq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                publishWords(a.rowsPub, a.rowsSeq, R, bits);
             }
         }
     }
@@ -1036,7 +1030,7 @@ __global__ __launch_bounds__(WG) void k_storage_pass(FinalArgs a, uint8_t* out) 
     __shared__ ChunkMap<ONE, false, false> m;
     const uint64_t base = static_cast<uint64_t>(blockIdx.x) * CE;
     const uint32_t cnt = static_cast<uint32_t>(a.E - base < CE ? a.E - base : CE);
-    buildMap<ONE, false, false>(a.estart, a.chunkFirst, a.nEnt, blockIdx.x, gridDim.x, base, cnt, a.F, a.hs, m);
+    buildMap<ONE, false, false>(a.estart, a.chunkFirst, a.nEnt, blockIdx.x, gridDim.x, base, cnt, a.F, a.hs, m, a.ebase);
     for (int k = 0; k < CITEMS; k++) {
         uint32_t p = threadIdx.x + k * WG;
         if (p >= cnt) continue;
@@ -1194,17 +1188,17 @@ int launchSeedFrontier(const int32_t* qpart, const int64_t* qvid, uint64_t n, VI
                        uint32_t* F, uint64_t* estart, Publish pub, hipStream_t s) {
     if (n * static_cast<uint64_t>(hs.n) > kSeedFuseMax || n > kSeedFuseMax || idx.slots == nullptr) return 1;
     hipLaunchKernelGGL(k_seed_frontier<false>, dim3(1), dim3(1024), 0, s, qpart, qvid, n, idx, hs, F, estart, pub,
-                       nullptr, 0, nullptr, 0u, nullptr, nullptr, nullptr);
+                       nullptr, 0, nullptr, 0u, nullptr, nullptr, nullptr, nullptr);
     return static_cast<int>(hipGetLastError());
 }
 
 int launchSeedFrontierCf(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, const HopSlots& hs,
                          uint32_t* F, uint64_t* estart, Publish pub, uint64_t* chunkFirst, uint64_t cfCap,
                          uint64_t* zero, uint32_t nzero, uint32_t* err, hipStream_t s, uint64_t* packedOut,
-                         uint64_t* zero8) {
+                         uint64_t* zero8, uint64_t* ebase) {
     if (n * static_cast<uint64_t>(hs.n) > kSeedFuseMax || n > kSeedFuseMax || idx.slots == nullptr || nzero > 64) return 1;
     hipLaunchKernelGGL(k_seed_frontier<true>, dim3(1), dim3(1024), 0, s, qpart, qvid, n, idx, hs, F, estart, pub,
-                       chunkFirst, cfCap, zero, nzero, err, packedOut, zero8);
+                       chunkFirst, cfCap, zero, nzero, err, packedOut, zero8, ebase);
     return static_cast<int>(hipGetLastError());
 }
 
@@ -1219,12 +1213,12 @@ int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst
 
 int launchExpandMark(const uint32_t* F, const uint64_t* estart, const uint64_t* chunkFirst, uint64_t nEnt, uint64_t E,
                      const HopSlots& hs, uint8_t* visited, uint8_t epoch, bool pos32, hipStream_t s, const uint8_t* mask,
-                     const uint64_t* dyn, uint64_t pullMinE) {
+                     const uint64_t* dyn, uint64_t pullMinE, const uint64_t* ebase) {
     if (E == 0) return 0;
     // dyn: E is an upper bound here; the grid strides (kDynGrid workgroups at most)
     dim3 grid(static_cast<unsigned>(std::min<uint64_t>((E + CE - 1) / CE, dyn ? kDynGrid : ~0u)));
 #define NGX_EXPAND(ONE, P32, MASK) hipLaunchKernelGGL((k_expand_mark<ONE, P32, MASK>), grid, dim3(WG), 0, s, F, estart, \
-                                                    chunkFirst, nEnt, E, hs, visited, epoch, mask, dyn, pullMinE)
+                                                    chunkFirst, nEnt, E, hs, visited, epoch, mask, dyn, pullMinE, ebase)
     if (mask) {
         if (hs.n == 1) NGX_EXPAND(true, false, true);
         else NGX_EXPAND(false, false, true);
