@@ -59,6 +59,8 @@ def parse():
     p.add_argument("--host-exchange", action="store_true",
                    help="rehearsal of the N > 1 path on one GPU: every rank on device 0, frontier exchange "
                         "through the host collective (gloo) instead of RCCL")
+    p.add_argument("--flag", action="append", default=[], metavar="NAME=VALUE",
+                   help="engine flag (ngx_set_flag) set before the run, e.g. dyn_hops=1; repeatable")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch of the dominant kernel (from profiles/)")
     return p.parse_args()
@@ -127,6 +129,9 @@ def main():
                         threads=args.threads)
     log(f"[rank {rank}] generated {rows.n} rows of RMAT scale {scale} in {time.time() - t0:.1f}s")
     eng = engine.Engine(device, rank, world, uid, exchange=xchg)
+    for f in args.flag:
+        name, _, val = f.partition("=")
+        eng.set_flag(name, int(val))
     eng.add_space(datagen.RMAT_SPACE, args.parts)
     for is_edge, sid, name, fields in datagen.rmat_schemas():
         eng.add_schema(datagen.RMAT_SPACE, is_edge, sid, name, fields)
@@ -324,7 +329,8 @@ def main():
                        "edge_layout": "out-edges + in-edges (-e)" if with_in else "out-edges",
                        "parallelism": f"{world} shard(s), part % {world}, "
                                       + ("host (gloo) exchange, all shards on GPU 0 (rehearsal)" if args.host_exchange
-                                         else "RCCL bitmap all-to-all per hop")},
+                                         else "RCCL bitmap all-to-all per hop"),
+                       **({"engine_flags": args.flag} if args.flag else {})},
             "roofline": roof,
             "cpu_baseline": cpu,
             "edges_per_step": edges // args.steps,

@@ -2315,7 +2315,12 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     uint8_t* const marksA = c->visited.get<uint8_t>(2 * vAl);
     PullArgs pa{};                                              // pull expansion (kernels.h launchPull)
     // world > 1: every shard pulls its own rows against the all-gathered frontier bitmap; the mirrors
-    // and the decision are global (findMirrorsGlobal, one all-gather per intermediate hop)
+    // and the decision are global (findMirrorsGlobal, one all-gather per intermediate hop). pullGather:
+    // whether the shards hold that per-hop all-gather, from values every shard has alike (the query,
+    // the world), so all of them enter it; what a shard itself can do (its rows, limits, flags) travels
+    // inside it
+    const bool pullGather = c->world > 1 && !rw && hs.n >= 1 && hs.n <= kPullMaxSlots && d.vglobal < (1ULL << 31) &&
+                            c->world <= kMaxWorld;
     bool pullable = !rw && c->pullFactor > 0 && (c->world == 1 || (d.vglobal < (1ULL << 31) && c->world <= kMaxWorld)) &&
                     hs.n >= 1 && hs.n <= kPullMaxSlots && d.V < (1ULL << 32) && d.mirror.size() == d.slots.size();
     if (pullable) {
@@ -2372,7 +2377,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     if (lbCompact) {
         const uint64_t tiles = (d.V + kCompactTile - 1) / kCompactTile + 1;
         cmpTile = c->cmpStatus[0].get<uint64_t>(tiles);
-        cmpWave = c->cmpStatus[1].get<uint64_t>(tiles * (kCompactTile / 1024));
+        cmpWave = c->cmpStatus[1].get<uint64_t>(tiles * (kCompactTile / 256));   // a word per wave (kernels.hip CNW)
     }
     // the pull reads the frontier as a bitmap over global rows, written by the compaction that built it
     // (or from the frontier list for the seed frontier); the pull's segment counter is cleared by the
@@ -2736,18 +2741,20 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         // (TTL / max-edges) decides which edges count
         // dyn: both expansions are enqueued and the device takes the one its E selects (pullMinE)
         bool pull = dyn ? pullable : pullable && !mask && E && E * 100 >= static_cast<uint64_t>(c->pullFactor) * d.V;
-        if (!dyn && pullable && c->world > 1) {
-            // the hop's edges over every shard, and whether every shard can pull (no storage mask)
-            const uint64_t rec[2] = {E, mask ? 0u : 1u};
+        if (!dyn && pullGather) {
+            // the hop's edges over every shard, whether every shard can pull (its pull state built, no
+            // storage mask) and rank 0's pull_factor (one threshold for all)
+            const uint64_t rec[3] = {E, (pullable && !mask) ? 1u : 0u, static_cast<uint64_t>(std::max<int64_t>(c->pullFactor, 0))};
             const std::vector<uint8_t> all = gatherHost(c, rec, sizeof(rec));
-            uint64_t eAll = 0, can = 1;
+            uint64_t eAll = 0, can = 1, pf = 0;
             for (int w = 0; w < c->world; w++) {
-                uint64_t r[2];
+                uint64_t r[3];
                 std::memcpy(r, all.data() + w * sizeof(rec), sizeof(rec));
                 eAll += r[0];
                 can &= r[1];
+                if (w == 0) pf = r[2];
             }
-            pull = can && eAll && eAll * 100 >= static_cast<uint64_t>(c->pullFactor) * d.vglobal;
+            pull = can && pf > 0 && eAll && eAll * 100 >= pf * d.vglobal;
         }
         // the hop's output marks (pull and push alike; the pull reads the frontier from the bitmap)
         uint8_t* const marks = marksA;

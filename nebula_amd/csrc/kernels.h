@@ -157,6 +157,19 @@ int launchScanU64(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tileS
 // v[0 .. n) -> exclusive prefix in place, v[n] = total (one 1024-thread workgroup: n up to ~1e6)
 int launchScanInPlace(uint64_t* v, uint64_t n, hipStream_t s);
 
+// k_final_close_cols: the arrays a close moves (kind 0: plain, w bytes; 1: 8-byte string values
+// rebased with their arena slots; 2: 8-byte word w of each row's string-arena block)
+struct CloseCol {
+    void* p;
+    int32_t w;
+    int32_t kind;
+};
+constexpr int kCloseMaxCols = 32;
+struct CloseCols {
+    CloseCol c[kCloseMaxCols];
+    int32_t n;
+};
+
 // final hop, one pass (interpreter kernel). a.oEntry set (GetNeighbors): a.lbStatus zeroed, ceil(E /
 // kChunk) + 1 words; outputs sized for a.oBase + a.E rows; rows in edge order, rows written = the
 // inclusive status of the last chunk. Else (GO): the kResv words of a.lbStatus zeroed, outputs sized for

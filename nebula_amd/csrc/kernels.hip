@@ -181,15 +181,22 @@ __global__ void k_lookup(const int32_t* qpart, const int64_t* qvid, uint64_t n, 
 
 // linear probing, two slots per round trip: both loads issue before either is compared (most keys
 // resolve in the first pair at the index's load factor)
+// Two slots per round trip, each one 16-byte load, both issued before either is examined, and the
+// outcome picked by selects (a probe written with early returns let the compiler split each slot
+// into a row load and a key load behind branches: four dependent loads per probe pair, r04 ISA).
+__device__ __forceinline__ uint4 vindexSlot(const VIndex& idx, uint64_t h) {
+    return reinterpret_cast<const uint4*>(idx.slots)[h];
+}
 __device__ __forceinline__ uint32_t vindexFind(const VIndex& idx, int32_t part, int64_t vid) {
     uint64_t h = vindexHash(part, vid) & idx.mask;
+    const uint32_t vlo = static_cast<uint32_t>(vid), vhi = static_cast<uint32_t>(static_cast<uint64_t>(vid) >> 32);
     for (uint64_t probe = 0; probe <= idx.mask; probe += 2) {
-        const VIndexSlot a = idx.slots[h];
-        const VIndexSlot b = idx.slots[(h + 1) & idx.mask];
-        if (a.row == kNoRow) return kNoRow;
-        if (a.vid == vid && a.part == part) return a.row;
-        if (b.row == kNoRow) return kNoRow;
-        if (b.vid == vid && b.part == part) return b.row;
+        const uint4 a = vindexSlot(idx, h), b = vindexSlot(idx, (h + 1) & idx.mask);
+        const bool aHit = a.x == vlo && a.y == vhi && a.z == static_cast<uint32_t>(part) && a.w != kNoRow;
+        const bool bHit = b.x == vlo && b.y == vhi && b.z == static_cast<uint32_t>(part) && b.w != kNoRow;
+        const bool done = aHit || a.w == kNoRow || bHit || b.w == kNoRow;   // found, or an empty slot ends the run
+        const uint32_t r = aHit ? a.w : a.w == kNoRow ? kNoRow : bHit ? b.w : kNoRow;
+        if (done) return r;
         h = (h + 2) & idx.mask;
     }
     return kNoRow;
@@ -225,6 +232,7 @@ __global__ __launch_bounds__(1024) void k_seed_frontier(const int32_t* qpart, co
     const uint64_t per = (n + 1023) / 1024;
     const uint64_t lo = threadIdx.x * per;
     uint32_t rows[kPer];
+    uint64_t b0[kPer], d0[kPer];                  // slot 0's CSR base and degree per seed (kept for the writes)
     uint64_t sum = 0;
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
@@ -237,8 +245,12 @@ __global__ __launch_bounds__(1024) void k_seed_frontier(const int32_t* qpart, co
     }
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
+        b0[k] = d0[k] = 0;
         if (rows[k] == kNoRow) continue;
-        for (int s = 0; s < hs.n; s++) sum += hs.off[s][rows[k] + 1] - hs.off[s][rows[k]];
+        b0[k] = hs.off[0][rows[k]];
+        d0[k] = hs.off[0][rows[k] + 1] - b0[k];
+        sum += d0[k];
+        for (int s = 1; s < hs.n; s++) sum += hs.off[s][rows[k] + 1] - hs.off[s][rows[k]];
     }
     int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint64_t x = sum;
@@ -262,9 +274,9 @@ __global__ __launch_bounds__(1024) void k_seed_frontier(const int32_t* qpart, co
         for (int s = 0; s < hs.n; s++) {
             estart[i * hs.n + s] = pre;
             if (rows[k] == kNoRow) continue;
-            const uint64_t o = hs.off[s][rows[k]];
+            const uint64_t o = s == 0 ? b0[k] : hs.off[s][rows[k]];
             if (ebase) ebase[i * hs.n + s] = o;
-            uint64_t d = hs.off[s][rows[k] + 1] - o;
+            const uint64_t d = s == 0 ? d0[k] : hs.off[s][rows[k] + 1] - o;
             if (CF) writeChunkHeads(chunkFirst, cfCap, i * hs.n + s, pre, d, err);
             pre += d;
         }
@@ -348,12 +360,17 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
 
 // ------------------------------------------------------------------------------ compaction
 // visited[row] == epoch -> next frontier + its entries' estart + the next hop's chunk heads, two
-// launches (kernels.h CompactArgs). Wave w of tile t owns rows t * 4096 + w * 1024 + k * 64 + lane,
-// k < 16, so the marks (1 B per lane) and the CSR offsets (8 B per lane) of one k are one coalesced
+// launches (kernels.h CompactArgs). Wave w of tile t owns rows t * 4096 + w * 256 + k * 64 + lane,
+// k < 4, so the marks (1 B per lane) and the CSR offsets (8 B per lane) of one k are one coalesced
 // wave access, and rows leave in row order (k-major, ballot prefix inside k).
 // (r02 gave each thread 16 consecutive rows: its offset loads put the 64 lanes of a wave on 64 cache
 // lines, 16 times, and the address unit bounded the pass; a single-pass decoupled look-back over
 // tiles taken by ticket then spent 20-38 us per launch on the 586 ticket atomics and the polling.)
+// 1024-thread workgroups: a 4096-row tile over 16 waves of 4 rows per lane (r03's 4 waves of 16
+// rows left 2.3 waves per SIMD at C2, each wave issuing 16 scans one after the other)
+constexpr int CWG = 1024;
+constexpr int CNW = CWG / 64;
+constexpr int CIT = TILE / CWG;
 __device__ __forceinline__ uint64_t waveInclScan(uint64_t x, int lane) {
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -377,65 +394,73 @@ __device__ __forceinline__ uint64_t rowDegree(const HopSlots& hs, uint64_t r) {
 
 // the wave's 16 mark flags (bit k: row wbase + 64 k + lane)
 __device__ __forceinline__ uint32_t waveFlags(const CompactArgs& a, uint64_t wbase, int lane) {
-    uint8_t mk[ITEMS];
+    uint8_t mk[CIT];
 #pragma unroll
-    for (int k = 0; k < ITEMS; k++) {
+    for (int k = 0; k < CIT; k++) {
         const uint64_t r = wbase + k * 64 + lane;
         mk[k] = a.visited[r < a.V ? r : a.V - 1];
     }
     uint32_t flags = 0;
 #pragma unroll
-    for (int k = 0; k < ITEMS; k++) flags |= (mk[k] == a.epoch && wbase + k * 64 + lane < a.V ? 1u : 0u) << k;
+    for (int k = 0; k < CIT; k++) flags |= (mk[k] == a.epoch && wbase + k * 64 + lane < a.V ? 1u : 0u) << k;
     return flags;
 }
 
 // degrees of the wave's flagged rows (0 elsewhere), every load issued before the first use
+// (ONE: also each row's CSR base in ob[], for the write launch's ebase[])
 template <bool ONE>
 __device__ __forceinline__ void waveDegrees(const CompactArgs& a, uint64_t wbase, int lane, uint32_t flags,
-                                            uint64_t (&deg)[ITEMS]) {
+                                            uint64_t (&deg)[CIT], uint64_t* ob = nullptr) {
 #pragma unroll
-    for (int k = 0; k < ITEMS; k++) {
+    for (int k = 0; k < CIT; k++) {
         const bool m = (flags >> k) & 1u;
-        const uint64_t d = rowDegree<ONE>(a.hs, m ? wbase + k * 64 + lane : 0);
-        deg[k] = m ? d : 0;
+        const uint64_t r = m ? wbase + k * 64 + lane : 0;
+        if (ONE) {
+            const uint64_t o0 = a.hs.off[0][r], o1 = a.hs.off[0][r + 1];
+            deg[k] = m ? o1 - o0 : 0;
+            if (ob) ob[k] = o0;
+        } else {
+            const uint64_t d = rowDegree<ONE>(a.hs, r);
+            deg[k] = m ? d : 0;
+        }
     }
 }
 
 // launch 1: per tile and per wave the packed (rows << kFdShift | degrees) total; the bitmap words
 template <bool ONE>
-__global__ __launch_bounds__(WG) void k_compact_count(CompactArgs a) {
-    __shared__ uint64_t sWave[NW];
+__global__ __launch_bounds__(CWG) void k_compact_count(CompactArgs a) {
+    __shared__ uint64_t sWave[CNW];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint64_t wbase = static_cast<uint64_t>(blockIdx.x) * TILE + static_cast<uint64_t>(wid) * (64 * ITEMS);
+    const uint64_t wbase = static_cast<uint64_t>(blockIdx.x) * TILE + static_cast<uint64_t>(wid) * (64 * CIT);
     if (blockIdx.x == 0 && threadIdx.x == 0 && a.clear32 != nullptr) *a.clear32 = 0;
     const uint32_t flags = waveFlags(a, wbase, lane);
-    uint64_t deg[ITEMS];
+    uint64_t deg[CIT];
     waveDegrees<ONE>(a, wbase, lane, flags, deg);
     uint64_t dsum = 0;
 #pragma unroll
-    for (int k = 0; k < ITEMS; k++) dsum += deg[k];
+    for (int k = 0; k < CIT; k++) dsum += deg[k];
     if (a.bits != nullptr) {
         // word k of the wave = rows wbase + 64 k .. + 63; lane k stores it
         uint64_t w = 0;
 #pragma unroll
-        for (int k = 0; k < ITEMS; k++) {
+        for (int k = 0; k < CIT; k++) {
             const uint64_t b = __ballot((flags >> k) & 1u);
             if (lane == k) w = b;
         }
-        if (lane < ITEMS && wbase + static_cast<uint64_t>(lane) * 64 < a.V) a.bits[(wbase >> 6) + lane] = w;
+        if (lane < CIT && wbase + static_cast<uint64_t>(lane) * 64 < a.V) a.bits[(wbase >> 6) + lane] = w;
     }
     uint64_t packed = (static_cast<uint64_t>(__popc(flags)) << kFdShift) | dsum;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) packed += __shfl_xor(packed, o, 64);
     if (lane == 0) {
         sWave[wid] = packed;
-        a.waveSum[static_cast<uint64_t>(blockIdx.x) * NW + wid] = packed;
+        a.waveSum[static_cast<uint64_t>(blockIdx.x) * CNW + wid] = packed;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         uint64_t t = 0;
 #pragma unroll
-        for (int w = 0; w < NW; w++) t += sWave[w];
+        for (int w = 0; w < CNW; w++) t += sWave[w];
         a.tileSum[blockIdx.x] = t;
     }
 }
@@ -444,15 +469,15 @@ __global__ __launch_bounds__(WG) void k_compact_count(CompactArgs a) {
 // launch 1's words, nothing waited for), then the rows in order: positions from each k's ballot and a
 // wave scan of its degrees. The last tile writes the totals (estart[|F| * ns] = E, *total, publish).
 template <bool ONE>
-__global__ __launch_bounds__(WG) void k_compact_write(CompactArgs a) {
+__global__ __launch_bounds__(CWG) void k_compact_write(CompactArgs a) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint64_t tile = blockIdx.x;
-    const uint64_t wbase = tile * TILE + static_cast<uint64_t>(wid) * (64 * ITEMS);
+    const uint64_t wbase = tile * TILE + static_cast<uint64_t>(wid) * (64 * CIT);
     const int ns = a.hs.n;
     const uint32_t flags = waveFlags(a, wbase, lane);
     // the totals of the tiles before this one: 8 loads in flight per lane (a dependent loop of loads
     // cost 10 us at C2's 586 tiles)
-    uint64_t pre = lane < wid ? a.waveSum[tile * NW + lane] : 0;
+    uint64_t pre = lane < wid ? a.waveSum[tile * CNW + lane] : 0;
     for (uint64_t t0 = 0; t0 < tile; t0 += 8 * 64) {
         uint64_t v[8];
 #pragma unroll
@@ -465,20 +490,20 @@ __global__ __launch_bounds__(WG) void k_compact_write(CompactArgs a) {
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) pre += __shfl_xor(pre, o, 64);
-    if (tile == gridDim.x - 1 && wid == NW - 1 && lane == 0) {
-        const uint64_t incl = pre + a.waveSum[tile * NW + wid];
+    if (tile == gridDim.x - 1 && wid == CNW - 1 && lane == 0) {
+        const uint64_t incl = pre + a.waveSum[tile * CNW + wid];
         a.estart[(incl >> kFdShift) * static_cast<uint64_t>(ns)] = incl & kFdMask;
         *a.total = incl;
         if (a.pub.slot) publishWords(a.pub.slot, a.pub.seq, incl, 0);
     }
     if (tile == 0 && threadIdx.x < a.nzero) a.zero[threadIdx.x * kDoneOff] = 0;
     if (__ballot(flags != 0) == 0) return;              // wave-uniform: every lane stays for the scans below
-    uint64_t deg[ITEMS];
-    waveDegrees<ONE>(a, wbase, lane, flags, deg);
+    uint64_t deg[CIT], ob[CIT];
+    waveDegrees<ONE>(a, wbase, lane, flags, deg, ONE ? ob : nullptr);
     uint64_t fk = pre >> kFdShift, ek = pre & kFdMask;     // running start of group k
     const uint64_t below = (1ULL << lane) - 1;
 #pragma unroll
-    for (int k = 0; k < ITEMS; k++) {
+    for (int k = 0; k < CIT; k++) {
         const bool m = (flags >> k) & 1u;
         const uint64_t ball = __ballot(m);
         if (ball == 0) continue;
@@ -492,7 +517,7 @@ __global__ __launch_bounds__(WG) void k_compact_write(CompactArgs a) {
         a.outF[f] = static_cast<uint32_t>(r);
         if (ONE) {
             a.estart[f] = e;
-            if (a.ebase) a.ebase[f] = a.hs.off[0][r];          // L1/L2 hit: waveDegrees read it
+            if (a.ebase) a.ebase[f] = ob[k];
             writeChunkHeads(a.chunkFirst, a.cfCap, f, e, deg[k], a.err);
         } else {
             for (int s = 0; s < ns; s++) {
@@ -909,58 +934,52 @@ __global__ __launch_bounds__(WG) void k_final_in(FinalArgs a) { finalBody<VmEv, 
 // ended, so every error atomic of it has landed), keeps R in the control words and clears the other
 // set of counters for the next launch: no count of finished workgroups (another same-address stream).
 // The moves complete in the stream's order, before any later work on the context's stream.
-__device__ __forceinline__ void moveW(void* p, int32_t w, uint64_t from, uint64_t to) {
-    switch (w) {
-        case 1: gst<uint8_t>(p, to, gld<uint8_t>(p, from)); break;
-        case 2: gst<uint16_t>(p, to, gld<uint16_t>(p, from)); break;
-        case 4: gst<uint32_t>(p, to, gld<uint32_t>(p, from)); break;
-        default: gst<uint64_t>(p, to, gld<uint64_t>(p, from)); break;
-    }
-}
-
-__global__ __launch_bounds__(WG) void k_final_close(FinalArgs a) {
-    __shared__ uint64_t hLo[kResvMaxGroups], hHi[kResvMaxGroups], gV[kResvMaxGroups];
-    __shared__ uint64_t sR, sP, sM;
-    __shared__ int sNh;
+struct CloseHead {
+    uint64_t hLo[kResvMaxGroups], hHi[kResvMaxGroups], gV[kResvMaxGroups];
+    uint64_t R, P, M;
+    int nh;
+};
+// every workgroup: the groups' counts and last blocks (one load round trip), the holes sorted, R and
+// M; workgroup (0, 0) also publishes R and clears the next launch's counters
+__device__ __forceinline__ void closeHead(const FinalArgs& a, CloseHead& h, bool first) {
     const uint64_t B = 1ULL << a.resvShift, st = a.resvStride;
     const uint32_t G = a.resvG;
-    // every group's count and last block at once (one load round trip, not G dependent ones)
     if (threadIdx.x < G) {
         const uint32_t g = threadIdx.x;
         const uint64_t v = lbLoad(a.resvCtl + (1 + g) * st);
-        gV[g] = v;
-        hLo[g] = hHi[g] = 0;
+        h.gV[g] = v;
+        h.hLo[g] = h.hHi[g] = 0;
         if (v & (B - 1)) {
             const uint64_t k = v >> a.resvShift;
             const uint64_t e = k < a.resvTB ? lbLoad(a.resvTab + static_cast<uint64_t>(g) * a.resvTB + k) : 0;
             if ((e >> 32) != a.resvSeq) {
                 atomicOr(a.err + 3, 1u);                    // every reserved block is published: cannot happen
             } else {
-                hLo[g] = ((e & 0xFFFFFFFFULL) << a.resvShift) + (v & (B - 1));
-                hHi[g] = ((e & 0xFFFFFFFFULL) + 1) << a.resvShift;
+                h.hLo[g] = ((e & 0xFFFFFFFFULL) << a.resvShift) + (v & (B - 1));
+                h.hHi[g] = ((e & 0xFFFFFFFFULL) + 1) << a.resvShift;
             }
         }
     }
-    if (threadIdx.x == WG - 1) sP = lbLoad(a.resvCtl);
+    if (threadIdx.x == WG - 1) h.P = lbLoad(a.resvCtl);
     __syncthreads();
     if (threadIdx.x == 0) {
         uint64_t R = 0;
         int nh = 0;
         for (uint32_t g = 0; g < G; g++) {                  // holes sorted by position (insertion sort)
-            R += gV[g];
-            if (hHi[g] == 0) continue;
-            const uint64_t lo = hLo[g], hi = hHi[g];
+            R += h.gV[g];
+            if (h.hHi[g] == 0) continue;
+            const uint64_t lo = h.hLo[g], hi = h.hHi[g];
             int j = nh++;
-            while (j > 0 && hLo[j - 1] > lo) { hLo[j] = hLo[j - 1]; hHi[j] = hHi[j - 1]; j--; }
-            hLo[j] = lo;
-            hHi[j] = hi;
+            while (j > 0 && h.hLo[j - 1] > lo) { h.hLo[j] = h.hLo[j - 1]; h.hHi[j] = h.hHi[j - 1]; j--; }
+            h.hLo[j] = lo;
+            h.hHi[j] = hi;
         }
         uint64_t M = 0;
-        for (int j = 0; j < nh; j++) M += hLo[j] < R ? (hHi[j] < R ? hHi[j] : R) - hLo[j] : 0;
-        sR = R;
-        sM = M;
-        sNh = nh;
-        if (blockIdx.x == 0) {
+        for (int j = 0; j < nh; j++) M += h.hLo[j] < R ? (h.hHi[j] < R ? h.hHi[j] : R) - h.hLo[j] : 0;
+        h.R = R;
+        h.M = M;
+        h.nh = nh;
+        if (first) {
             lbStore(a.resvCtl + (1 + G) * st, R);           // the row count (device copy; dyn hops read it)
             for (uint32_t g = 0; g <= G; g++) lbStore(a.resvNext + g * st, 0);   // the next launch's counters
             if (a.rowsPub != nullptr) {
@@ -972,53 +991,162 @@ __global__ __launch_bounds__(WG) void k_final_close(FinalArgs a) {
         }
     }
     __syncthreads();
-    const uint64_t R = sR, P = sP, M = sM;
-    const int nh = sNh;
-    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * WG + threadIdx.x;
-    if (i >= M) return;
-    uint64_t to = ~0ULL, acc = 0;                           // the i-th hole below R
-    for (int j = 0; j < nh && hLo[j] < R; j++) {
-        const uint64_t len = (hHi[j] < R ? hHi[j] : R) - hLo[j];
-        if (i < acc + len) { to = hLo[j] + (i - acc); break; }
+}
+
+// move i (< M): the i-th hole row below R (to) and the i-th occupied row in [R, P) (from); false if
+// the counts disagree (cannot happen)
+__device__ __forceinline__ bool closePair(const CloseHead& h, uint64_t i, uint64_t& to, uint64_t& from) {
+    const uint64_t R = h.R;
+    to = ~0ULL;
+    uint64_t acc = 0;
+    for (int j = 0; j < h.nh && h.hLo[j] < R; j++) {
+        const uint64_t len = (h.hHi[j] < R ? h.hHi[j] : R) - h.hLo[j];
+        if (i < acc + len) { to = h.hLo[j] + (i - acc); break; }
         acc += len;
     }
-    uint64_t from = ~0ULL, cur = R, left = i;               // the i-th occupied row in [R, P)
-    for (int j = 0; j <= nh; j++) {
-        if (j < nh && hHi[j] <= R) continue;
-        const uint64_t segEnd = j < nh ? hLo[j] : P;
+    from = ~0ULL;
+    uint64_t cur = R, left = i;
+    for (int j = 0; j <= h.nh; j++) {
+        if (j < h.nh && h.hHi[j] <= R) continue;
+        const uint64_t segEnd = j < h.nh ? h.hLo[j] : h.P;
         if (segEnd > cur) {
             if (left < segEnd - cur) { from = cur + left; break; }
             left -= segEnd - cur;
         }
-        if (j < nh && hHi[j] > cur) cur = hHi[j];
+        if (j < h.nh && h.hHi[j] > cur) cur = h.hHi[j];
     }
-    if (to == ~0ULL || from == ~0ULL) { atomicOr(a.err + 3, 1u); return; }
+    return to != ~0ULL && from != ~0ULL;
+}
+
+__device__ __forceinline__ void closeMove(const FinalArgs& a, uint64_t from, uint64_t to);
+// fallback (more columns than CloseCols holds): a thread per moved row, every column of it
+__global__ __launch_bounds__(WG) void k_final_close(FinalArgs a) {
+    __shared__ CloseHead h;
+    closeHead(a, h, blockIdx.x == 0);
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * WG + threadIdx.x; i < h.M; i += static_cast<uint64_t>(gridDim.x) * WG) {
+        uint64_t to, from;
+        if (!closePair(h, i, to, from)) { atomicOr(a.err + 3, 1u); return; }
+        closeMove(a, from, to);
+    }
+}
+
+// A workgroup column (blockIdx.y) of one moved array: each thread moves kCloseBatch rows of it, every
+// load of the batch issued before its stores (one width per launch row, no branch between them).
+constexpr int kCloseBatch = 8;
+template <typename T, int KIND>
+__device__ __forceinline__ void closeColumn(const FinalArgs& a, const CloseHead& h, const CloseCol& col) {
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * WG;
+    for (uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * WG + threadIdx.x; i0 < h.M; i0 += stride * kCloseBatch) {
+        uint64_t to[kCloseBatch], from[kCloseBatch];
+        T v[kCloseBatch];
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < kCloseBatch; k++) {
+            const uint64_t i = i0 + k * stride;
+            to[k] = from[k] = 0;
+            if (i < h.M) ok = closePair(h, i, to[k], from[k]) && ok;
+            to[k] += a.oBase;
+            from[k] += a.oBase;
+        }
+        if (!ok) { atomicOr(a.err + 3, 1u); return; }
+#pragma unroll
+        for (int k = 0; k < kCloseBatch; k++) {
+            const uint64_t i = i0 + k * stride;
+            if (KIND == 2) v[k] = i < h.M ? gld<T>(a.strOut, ((from[k] - a.oBase) * a.nStrOut * kStrBuildBytes) / 8 + col.w) : T(0);
+            else v[k] = i < h.M ? gld<T>(col.p, from[k]) : T(0);
+        }
+#pragma unroll
+        for (int k = 0; k < kCloseBatch; k++) {
+            const uint64_t i = i0 + k * stride;
+            if (i >= h.M) continue;
+            if (KIND == 2) {
+                gst<T>(a.strOut, ((to[k] - a.oBase) * a.nStrOut * kStrBuildBytes) / 8 + col.w, v[k]);
+            } else if (KIND == 1) {
+                // a string value pointing into the row's own arena slots moves with them
+                uint64_t ux = static_cast<uint64_t>(v[k]);
+                const uint64_t slotBytes = static_cast<uint64_t>(a.nStrOut) * kStrBuildBytes;
+                const uint64_t sFrom = reinterpret_cast<uint64_t>(strSlot(a, from[k], 0));
+                const uint64_t sTo = reinterpret_cast<uint64_t>(strSlot(a, to[k], 0));
+                if (ux >= sFrom && ux < sFrom + slotBytes) ux = ux - sFrom + sTo;
+                gst<T>(col.p, to[k], static_cast<T>(ux));
+            } else {
+                gst<T>(col.p, to[k], v[k]);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(WG) void k_final_close_cols(FinalArgs a, CloseCols cc) {
+    __shared__ CloseHead h;
+    closeHead(a, h, blockIdx.x == 0 && blockIdx.y == 0);
+    const CloseCol col = cc.c[blockIdx.y];
+    if (col.kind == 2) closeColumn<uint64_t, 2>(a, h, col);
+    else if (col.kind == 1) closeColumn<uint64_t, 1>(a, h, col);
+    else if (col.w == 1) closeColumn<uint8_t, 0>(a, h, col);
+    else if (col.w == 2) closeColumn<uint16_t, 0>(a, h, col);
+    else if (col.w == 4) closeColumn<uint32_t, 0>(a, h, col);
+    else closeColumn<uint64_t, 0>(a, h, col);
+}
+
+__device__ __forceinline__ void closeMove(const FinalArgs& a, uint64_t from, uint64_t to) {
     from += a.oBase;
     to += a.oBase;
-    if (a.oSrc) moveW(a.oSrc, a.oSrcW, from, to);
-    if (a.oDst) moveW(a.oDst, a.oDstW, from, to);
-    if (a.oRank) moveW(a.oRank, a.oRankW, from, to);
-    if (a.oType) moveW(a.oType, 4, from, to);
-    if (a.oEntry) moveW(a.oEntry, 4, from, to);
-    if (a.oFlags) moveW(a.oFlags, 1, from, to);
-    // strings the row's YIELD columns built live in its slots of the result string arena: they move
-    // with the row, and a value pointing into them is rebased
+    // every load of the row issued before its first store (a load after a store to another array
+    // waits for it: the compiler cannot tell the arrays apart), in batches of registers
     const uint64_t slotBytes = static_cast<uint64_t>(a.nStrOut) * kStrBuildBytes;
     char* const sFrom = a.strOut ? strSlot(a, from, 0) : nullptr;
     char* const sTo = a.strOut ? strSlot(a, to, 0) : nullptr;
-    for (uint64_t b = 0; sFrom && b < slotBytes; b += 8) gst<uint64_t>(sTo, b / 8, gld<uint64_t>(sFrom, b / 8));
-    for (int y = 0; y < a.nY; y++) {
-        const OutCol& oc = outCol(a, y);
-        // a key column aliased to a row array moved with it
-        if (oc.x && oc.x != a.oSrc && oc.x != a.oDst && oc.x != a.oRank) {
-            int64_t x = oc.w == 8 ? gld<int64_t>(oc.x, from) : loadW(oc.x, oc.w, from);
-            const uint64_t ux = static_cast<uint64_t>(x);
-            if (oc.len && sFrom && ux >= reinterpret_cast<uint64_t>(sFrom) && ux < reinterpret_cast<uint64_t>(sFrom) + slotBytes)
-                x = static_cast<int64_t>(ux - reinterpret_cast<uint64_t>(sFrom) + reinterpret_cast<uint64_t>(sTo));
-            storeW(oc.x, oc.w, to, x);
+    {
+        const int64_t v0 = a.oSrc ? loadW(a.oSrc, a.oSrcW, from) : 0;
+        const int64_t v1 = a.oDst ? loadW(a.oDst, a.oDstW, from) : 0;
+        const int64_t v2 = a.oRank ? loadW(a.oRank, a.oRankW, from) : 0;
+        const int32_t v3 = a.oType ? gld<int32_t>(a.oType, from) : 0;
+        const uint32_t v4 = a.oEntry ? gld<uint32_t>(a.oEntry, from) : 0;
+        const uint8_t v5 = a.oFlags ? gld<uint8_t>(a.oFlags, from) : 0;
+        if (a.oSrc) storeW(a.oSrc, a.oSrcW, to, v0);
+        if (a.oDst) storeW(a.oDst, a.oDstW, to, v1);
+        if (a.oRank) storeW(a.oRank, a.oRankW, to, v2);
+        if (a.oType) gst<int32_t>(a.oType, to, v3);
+        if (a.oEntry) gst<uint32_t>(a.oEntry, to, v4);
+        if (a.oFlags) gst<uint8_t>(a.oFlags, to, v5);
+    }
+    // strings the row's YIELD columns built live in its slots of the result string arena: they move
+    // with the row, and a value pointing into them is rebased
+    for (uint64_t b = 0; sFrom && b < slotBytes; b += 64) {
+        uint64_t w[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) w[k] = b + 8 * k < slotBytes ? gld<uint64_t>(sFrom, b / 8 + k) : 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) if (b + 8 * k < slotBytes) gst<uint64_t>(sTo, b / 8 + k, w[k]);
+    }
+    constexpr int kB = 4;                                   // YIELD columns per batch
+    for (int y0 = 0; y0 < a.nY; y0 += kB) {
+        int64_t x[kB];
+        uint32_t len[kB];
+        uint8_t t[kB];
+#pragma unroll
+        for (int k = 0; k < kB; k++) {
+            x[k] = 0; len[k] = 0; t[k] = 0;
+            if (y0 + k >= a.nY) continue;
+            const OutCol& oc = outCol(a, y0 + k);
+            // a key column aliased to a row array moved with it
+            if (oc.x && oc.x != a.oSrc && oc.x != a.oDst && oc.x != a.oRank) x[k] = loadW(oc.x, oc.w, from);
+            if (oc.len) len[k] = gld<uint32_t>(oc.len, from);
+            if (oc.t) t[k] = gld<uint8_t>(oc.t, from);
         }
-        if (oc.len) moveW(oc.len, 4, from, to);
-        if (oc.t) moveW(oc.t, 1, from, to);
+#pragma unroll
+        for (int k = 0; k < kB; k++) {
+            if (y0 + k >= a.nY) continue;
+            const OutCol& oc = outCol(a, y0 + k);
+            if (oc.x && oc.x != a.oSrc && oc.x != a.oDst && oc.x != a.oRank) {
+                const uint64_t ux = static_cast<uint64_t>(x[k]);
+                if (oc.len && sFrom && ux >= reinterpret_cast<uint64_t>(sFrom) && ux < reinterpret_cast<uint64_t>(sFrom) + slotBytes)
+                    x[k] = static_cast<int64_t>(ux - reinterpret_cast<uint64_t>(sFrom) + reinterpret_cast<uint64_t>(sTo));
+                storeW(oc.x, oc.w, to, x[k]);
+            }
+            if (oc.len) gst<uint32_t>(oc.len, to, len[k]);
+            if (oc.t) gst<uint8_t>(oc.t, to, t[k]);
+        }
     }
 }
 
@@ -1261,11 +1389,11 @@ int launchCompactLb(const CompactArgs& a, hipStream_t s) {
     const uint64_t nt = std::max<uint64_t>((a.V + TILE - 1) / TILE, 1);
     dim3 grid(static_cast<unsigned>(nt));
     if (a.hs.n == 1) {
-        hipLaunchKernelGGL((k_compact_count<true>), grid, dim3(WG), 0, s, a);
-        hipLaunchKernelGGL((k_compact_write<true>), grid, dim3(WG), 0, s, a);
+        hipLaunchKernelGGL((k_compact_count<true>), grid, dim3(CWG), 0, s, a);
+        hipLaunchKernelGGL((k_compact_write<true>), grid, dim3(CWG), 0, s, a);
     } else {
-        hipLaunchKernelGGL((k_compact_count<false>), grid, dim3(WG), 0, s, a);
-        hipLaunchKernelGGL((k_compact_write<false>), grid, dim3(WG), 0, s, a);
+        hipLaunchKernelGGL((k_compact_count<false>), grid, dim3(CWG), 0, s, a);
+        hipLaunchKernelGGL((k_compact_write<false>), grid, dim3(CWG), 0, s, a);
     }
     return static_cast<int>(hipGetLastError());
 }
@@ -1314,8 +1442,40 @@ int launchFinal(const FinalArgs& a, hipStream_t s, unsigned g) {
 }
 
 int launchFinalClose(const FinalArgs& a, hipStream_t s) {
-    const unsigned grid = static_cast<unsigned>((resvSlack(a) + WG - 1) / WG);   // a thread per row that may move
-    hipLaunchKernelGGL(k_final_close, dim3(grid), dim3(WG), 0, s, a);
+    // the moved arrays, one launch row each: row arrays, per-row type / entry / flags, the YIELD
+    // columns (values, lengths, types) that are not aliases of a row array, the string arena's words
+    CloseCols cc{};
+    bool fits = a.nY <= kInlineCols;
+    auto add = [&](void* p, int32_t w, int32_t kind) {
+        if (!p) return;
+        if (cc.n >= kCloseMaxCols) { fits = false; return; }
+        cc.c[cc.n++] = CloseCol{p, w, kind};
+    };
+    add(a.oSrc, a.oSrcW, 0);
+    add(a.oDst, a.oDstW, 0);
+    add(a.oRank, a.oRankW, 0);
+    add(a.oType, 4, 0);
+    add(a.oEntry, 4, 0);
+    add(a.oFlags, 1, 0);
+    for (int y = 0; fits && y < a.nY; y++) {
+        const OutCol& oc = a.oColsIn[y];
+        if (oc.x && oc.x != a.oSrc && oc.x != a.oDst && oc.x != a.oRank)
+            add(oc.x, oc.w, (oc.len && a.strOut && oc.w == 8) ? 1 : 0);
+        add(oc.len, 4, 0);
+        add(oc.t, 1, 0);
+    }
+    if (a.strOut) {
+        const uint64_t words = static_cast<uint64_t>(a.nStrOut) * kStrBuildBytes / 8;
+        for (uint64_t w = 0; fits && w < words; w++) add(a.strOut, static_cast<int32_t>(w), 2);
+    }
+    if (fits && cc.n > 0) {
+        // 8 rows per thread over the rows that may move
+        const unsigned gx = static_cast<unsigned>((resvSlack(a) + WG * kCloseBatch - 1) / (WG * kCloseBatch));
+        hipLaunchKernelGGL(k_final_close_cols, dim3(gx, static_cast<unsigned>(cc.n)), dim3(WG), 0, s, a, cc);
+    } else {
+        const unsigned grid = static_cast<unsigned>((resvSlack(a) + WG - 1) / WG);   // a thread per row that may move
+        hipLaunchKernelGGL(k_final_close, dim3(grid), dim3(WG), 0, s, a);
+    }
     return static_cast<int>(hipGetLastError());
 }
 

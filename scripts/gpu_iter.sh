@@ -1,7 +1,8 @@
 #!/bin/bash
 # Iteration run on the GPU box: a pytest selection, then bench.py once per environment variant.
 # Usage: bash scripts/gpu_iter.sh "<pytest args>" "<VAR=val ...>" ["<VAR=val ...>" ...]
-# ("-" as the pytest args skips the tests; "none" as a variant runs the bench with no extra env)
+# ("-" as the pytest args skips the tests; "none" as a variant runs the bench with no extra env;
+# "args:<bench args>" passes bench arguments instead, e.g. "args:--flag dyn_hops=1")
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -18,9 +19,14 @@ i=0
 for v in "$@"; do
     i=$((i + 1))
     envs=""
-    [ "$v" != "none" ] && envs="$v"
-    echo "[bench $i] $envs"
-    env $envs timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --cpu-budget 0 \
+    bargs=""
+    case "$v" in
+        none) ;;
+        args:*) bargs="${v#args:}" ;;
+        *) envs="$v" ;;
+    esac
+    echo "[bench $i] $envs $bargs"
+    env $envs timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --cpu-budget 0 $bargs \
         > gpurun_out/bench_v$i.json 2> gpurun_out/bench_v$i.err || { echo "bench $i failed"; tail -30 gpurun_out/bench_v$i.err; exit 1; }
     python3 -c "
 import json,sys

@@ -126,7 +126,8 @@ def main():
             res.append({"ok": o.ok, "error": o.error, "rows": [list(map(list, x)) for x in o.rows],
                         "pipe_walks": e.get_flag("pipe_walks") - walks})
             continue
-        e.set_flag("pull_factor", q.get("pull_factor", default_pf))
+        pf = q.get("pull_factor", default_pf)
+        e.set_flag("pull_factor", pf[rank] if isinstance(pf, list) else pf)     # a list: per rank
         pulls = e.get_flag("pull_hops")
         r = e.go(datagen.RMAT_SPACE, ngql.parse_go(q["text"]), pushdown=q.get("pushdown", True), columnar=True,
                  rows=False, digest_fn=oracle.digest_columns)

@@ -203,6 +203,36 @@ def test_multishard_go_matches_oracle(tmp_path, world, scale):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
+def test_multishard_pull_decision_is_collective(tmp_path):
+    """World 2 where the shards disagree about pulling: rank 0 cannot (pull_factor 0), rank 1 would
+    pull every hop (pull_factor 1). Every shard still enters each intermediate hop's pull all-gather
+    (engine.cpp pullGather) and sends whether it can pull, so both push: no collective mismatch, rows
+    == the oracle's. With both at 1 the same queries pull."""
+    from nebula_amd import datagen
+    from oracle import oracle
+    from tests import fixtures
+
+    scale = 11
+    ds = fixtures.RmatDataset(scale, with_in=True, with_tag=True)
+    o = oracle.Oracle()
+    o.set_flags(threads=8)
+    ds.load_oracle(o)
+    queries = []
+    for i, text in enumerate(["GO 3 STEPS FROM {S} OVER e WHERE e.p0 < 50 YIELD e._dst, e._rank, e.p0, e.p1",
+                              "GO 2 STEPS FROM {S} OVER e REVERSELY YIELD e._dst, e.p1"]):
+        seeds = datagen.sample_vids(700 + i, 1 << scale, 30)
+        queries.append({"text": text.replace("{S}", ", ".join(str(int(v)) for v in seeds)), "pushdown": True})
+    mixed = [dict(q, pull_factor=[0, 1]) for q in queries]
+    both = [dict(q, pull_factor=[1, 1]) for q in queries]
+    shards, digests = _run_shards(tmp_path, 2, scale, mixed + both, timeout=300)
+    _check_merged(o, ds.space, mixed + both, shards, digests)
+    n = len(mixed)
+    assert [r["pull_hops"] for s in shards for r in s[:n]] == [0] * (2 * n)
+    assert all(s[k]["pull_hops"] >= 1 for s in shards for k in range(n, 2 * n))
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
 def test_multishard_csr_load_matches_oracle(tmp_path):
     """World 8 with every shard bulk-loaded through ngx_load_csr (datagen.rmat_csr: the C3 at-size test's
     input path) against the single-process oracle loaded from the same graph's KV rows: the columnar
