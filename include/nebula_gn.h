@@ -424,6 +424,14 @@ int32_t ngx_kernel_stats(ngx_ctx* ctx, const ngx_kernel_stat** out, int32_t* n);
  *   "rccl_timeout_ms"     deadline of every RCCL collective (default 120000; env NGX_RCCL_TIMEOUT_MS).
  *          On a timeout or an asynchronous RCCL error the communicator is aborted, the call returns
  *          NGX_E_DEVICE and every later call on the context fails (the caller exits).
+ *   "trace_go"  graphd's FLAGS_trace_go (GoExecutor.cpp:559-569, 834-836): 1 logs each step's frontier,
+ *          scanned edges, next frontier and time, and the total row count, to stderr (default 0).
+ *   "dyn_hops"  0 (default) / 1: device-driven hops at world 1 (hop totals passed between kernels on the
+ *          device, upper-bound grids, no host round trip per hop). Same results; measured slower at C2.
+ *   "narrow_columns"  1 (default): integer columns, dst and rank stored at the narrowest width holding
+ *          every value (applies at the next commit); 0: 8 bytes each. Same results.
+ *   "compact_lane_rows"  rows per lane of the next-frontier compaction: 0 (default) = 4; 8 / 16 fewer,
+ *          fatter waves (measured slower at C2). Same results.
  * Read-only counters for ngx_get_flag: "jit_compiled", "jit_hits", "jit_failed", "jit_compile_us",
  * "jit_cached", "jit_evicted". */
 int32_t ngx_set_flag(ngx_ctx* ctx, const char* name, int64_t value);

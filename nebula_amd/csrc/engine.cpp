@@ -187,6 +187,7 @@ struct ngx_ctx {
     // pull expansion (kernels.h launchPull): segment queue + its counters, kept zero between launches
     DBuf pullSeg, pullCtl;
     uint64_t pullSegWords = 0;
+    int32_t compactLaneRows = 0;                        // compaction rows per lane: 0 = by shard size, else 4 / 8 / 16
     int64_t pullFactor = 200;                           // pull when 100 x hop edges >= pullFactor x shard rows (0: never)
     uint64_t pullHops = 0;
     // device-driven hops (no host round trip per hop). Off by default: on MI355X the upper-bound grids
@@ -1551,6 +1552,11 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
     if (n == "enable_reservoir_sampling") { c->reservoirSampling = value != 0; return NGX_OK; }
     if (n == "narrow_columns") { c->narrowColumns = value != 0; return NGX_OK; }
     if (n == "trace_go") { c->traceGo = value != 0; return NGX_OK; }
+    if (n == "compact_lane_rows") {
+        if (value != 0 && value != 4 && value != 8 && value != 16) return fail(c, NGX_E_BAD_ARGUMENT, "compact_lane_rows: 0, 4, 8 or 16");
+        c->compactLaneRows = static_cast<int32_t>(value);
+        return NGX_OK;
+    }
     if (n == "jit_wait") { c->jit.drain(); return NGX_OK; }
     return fail(c, NGX_E_BAD_ARGUMENT, "unknown flag " + n);
 }
@@ -1568,6 +1574,7 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "enable_reservoir_sampling") *value = c->reservoirSampling ? 1 : 0;
     else if (n == "narrow_columns") *value = c->narrowColumns ? 1 : 0;
     else if (n == "trace_go") *value = c->traceGo ? 1 : 0;
+    else if (n == "compact_lane_rows") *value = c->compactLaneRows;
     else if (n == "pull_hops") *value = static_cast<int64_t>(c->pullHops);
     else if (n == "pipe_walks") *value = static_cast<int64_t>(c->pipeWalks);
     else if (n == "jit_compiled") *value = static_cast<int64_t>(c->jit.compiled);
@@ -2841,6 +2848,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             ca.nzero = 0;
             ca.err = errFlag;
             ca.epoch = ep;
+            ca.laneRows = c->compactLaneRows;
             c->timed("compact_degrees", 0, [&] {
                 if (launchCompactLb(ca, c->stream)) throw Error{NGX_E_DEVICE, "compact"};
             });

@@ -51,11 +51,8 @@ __host__ __device__ inline uint64_t vindexHash(int32_t part, int64_t vid) {
     return h ^ (h >> 32);
 }
 
-// seed hop in ONE single-workgroup launch (n seeds, n * hs.n <= kSeedFuseMax entries): lookup through
-// the index -> F, entry degrees -> estart (n * hs.n + 1 entries, the last = E), E published
+// seed hop (n seeds, n * hs.n <= kSeedFuseMax entries): launchSeedFrontierCf below
 constexpr uint64_t kSeedFuseMax = 4096;
-int launchSeedFrontier(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, const HopSlots& hs,
-                       uint32_t* F, uint64_t* estart, Publish pub, hipStream_t s);
 
 int launchIndexLookup(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, uint32_t* out, hipStream_t s);
 int launchLookup(const int32_t* qpart, const int64_t* qvid, uint64_t n, const int32_t* vpart, const int64_t* vid,
@@ -117,9 +114,10 @@ struct CompactArgs {
     uint32_t* err;
     uint8_t epoch;
     uint64_t* bits;                     // optional frontier bitmap of this shard's rows (V / 64 words, rounded up)
+    int32_t laneRows;                   // rows per lane, 4 / 8 / 16; 0: the launcher picks by V (kernels.hip)
 };
 constexpr uint64_t kCompactLbMaxV = 1ULL << (62 - kFdShift);
-constexpr uint64_t kCompactTile = 4096;     // rows per compaction tile (256 threads x 16 rows)
+constexpr uint64_t kCompactTile = 4096;     // the smallest compaction tile (1024 threads x 4 rows; 8 or 16 per lane on larger shards): sizes the per-tile words
 // GO final kernel words: kargs.h (kResv*, kDoneOff). The seed / compaction kernels clear zero[k * kDoneOff]
 // for k < nzero.
 int launchCompactLb(const CompactArgs& a, hipStream_t s);
@@ -165,6 +163,18 @@ struct CloseCol {
     int32_t kind;
 };
 constexpr int kCloseMaxCols = 32;
+// the FinalArgs fields k_final_close_cols reads (same names and meaning)
+struct CloseArgs {
+    uint64_t* resvCtl;
+    uint64_t* resvTab;
+    uint64_t* resvNext;
+    uint32_t* err;
+    uint64_t* rowsPub;
+    uint64_t rowsSeq;
+    char* strOut;
+    uint64_t oBase;
+    uint32_t resvTB, resvSeq, resvG, resvShift, resvStride, nStrOut;
+};
 struct CloseCols {
     CloseCol c[kCloseMaxCols];
     int32_t n;

@@ -217,72 +217,70 @@ __device__ __forceinline__ void writeChunkHeads(uint64_t* cf, uint64_t cap, uint
     }
 }
 
-// 1024 threads; thread t owns seeds [t*per, t*per + per) and their entries (contiguous)
-// CF: also the hop's chunk heads (chunkFirst, k_chunk_first's job) and the words zero[0 .. nzero)
-template <bool CF>
-__global__ __launch_bounds__(1024) void k_seed_frontier(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx,
-                                                        HopSlots hs, uint32_t* F, uint64_t* estart, Publish pub,
-                                                        uint64_t* chunkFirst, uint64_t cfCap, uint64_t* zero,
-                                                        uint32_t nzero, uint32_t* err, uint64_t* packedOut,
-                                                        uint64_t* zero8, uint64_t* ebase) {
-    if (CF && threadIdx.x < nzero) zero[threadIdx.x * kDoneOff] = 0;
-    if (CF && zero8 != nullptr && threadIdx.x >= 64 && threadIdx.x < 72) zero8[threadIdx.x - 64] = 0;
+// Seed hop in two launches. A single workgroup doing the lookups measured ~1.5 us per dependent step
+// (tools/mb_latency.hip: 1024 random loads from one CU queue behind its own miss handling), 14 us in
+// all; spread over 64-thread workgroups on as many CUs each step costs about one memory latency.
+// Launch 1 (a thread per seed): (part, vid) -> row through the index, F[i], and per entry its degree
+// (into estart, turned into offsets by launch 2) and CSR base (ebase); block 0 clears zero[] / zero8.
+__global__ __launch_bounds__(64) void k_seed_lookup(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx,
+                                                    HopSlots hs, uint32_t* F, uint64_t* deg, uint64_t* ebase,
+                                                    uint64_t* zero, uint32_t nzero, uint64_t* zero8) {
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < nzero) zero[threadIdx.x * kDoneOff] = 0;
+        if (zero8 != nullptr && threadIdx.x < 8) zero8[threadIdx.x] = 0;
+    }
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 64 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t r = vindexFind(idx, qpart[i], qvid[i]);
+    F[i] = r;
+    const uint64_t rr = r == kNoRow ? 0 : r;                    // every load issued, the result selected
+    for (int s = 0; s < hs.n; s++) {
+        const uint64_t o0 = hs.off[s][rr], o1 = hs.off[s][rr + 1];
+        deg[i * hs.n + s] = r == kNoRow ? 0 : o1 - o0;
+        if (ebase) ebase[i * hs.n + s] = o0;
+    }
+}
+
+// Launch 2 (one 1024-thread workgroup, nEnt <= kSeedFuseMax): the entries' degrees -> exclusive offsets
+// in place, E = estart[nEnt], the hop's chunk heads, E published (and packed with |F| for dyn hops)
+__global__ __launch_bounds__(1024) void k_seed_scan(uint64_t n, int ns, uint64_t* estart, Publish pub,
+                                                    uint64_t* chunkFirst, uint64_t cfCap, uint32_t* err,
+                                                    uint64_t* packedOut) {
     __shared__ uint64_t sm[1024 / 64 + 1];
     constexpr int kPer = static_cast<int>(kSeedFuseMax / 1024);
-    const uint64_t per = (n + 1023) / 1024;
-    const uint64_t lo = threadIdx.x * per;
-    uint32_t rows[kPer];
-    uint64_t b0[kPer], d0[kPer];                  // slot 0's CSR base and degree per seed (kept for the writes)
+    const uint64_t nEnt = n * static_cast<uint64_t>(ns);
+    const uint64_t lo = threadIdx.x * static_cast<uint64_t>(kPer);
+    uint64_t d[kPer];
     uint64_t sum = 0;
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
-        rows[k] = kNoRow;
-        uint64_t i = lo + k;
-        if (k < static_cast<int>(per) && i < n) {
-            rows[k] = vindexFind(idx, qpart[i], qvid[i]);
-            F[i] = rows[k];
-        }
+        d[k] = lo + k < nEnt ? estart[lo + k] : 0;
+        sum += d[k];
     }
-#pragma unroll
-    for (int k = 0; k < kPer; k++) {
-        b0[k] = d0[k] = 0;
-        if (rows[k] == kNoRow) continue;
-        b0[k] = hs.off[0][rows[k]];
-        d0[k] = hs.off[0][rows[k] + 1] - b0[k];
-        sum += d0[k];
-        for (int s = 1; s < hs.n; s++) sum += hs.off[s][rows[k] + 1] - hs.off[s][rows[k]];
-    }
-    int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint64_t x = sum;
     for (int o = 1; o < 64; o <<= 1) {
-        uint64_t y = __shfl_up(x, o, 64);
+        const uint64_t y = __shfl_up(x, o, 64);
         if (lane >= o) x += y;
     }
     if (lane == 63) sm[wid] = x;
     __syncthreads();
     if (threadIdx.x == 0) {
         uint64_t acc = 0;
-        for (int w = 0; w < 16; w++) { uint64_t t = sm[w]; sm[w] = acc; acc += t; }
+        for (int w = 0; w < 16; w++) { const uint64_t t = sm[w]; sm[w] = acc; acc += t; }
         sm[16] = acc;
     }
     __syncthreads();
     uint64_t pre = sm[wid] + x - sum;
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
-        uint64_t i = lo + k;
-        if (k >= static_cast<int>(per) || i >= n) continue;
-        for (int s = 0; s < hs.n; s++) {
-            estart[i * hs.n + s] = pre;
-            if (rows[k] == kNoRow) continue;
-            const uint64_t o = s == 0 ? b0[k] : hs.off[s][rows[k]];
-            if (ebase) ebase[i * hs.n + s] = o;
-            const uint64_t d = s == 0 ? d0[k] : hs.off[s][rows[k] + 1] - o;
-            if (CF) writeChunkHeads(chunkFirst, cfCap, i * hs.n + s, pre, d, err);
-            pre += d;
-        }
+        if (lo + k >= nEnt) break;
+        estart[lo + k] = pre;
+        writeChunkHeads(chunkFirst, cfCap, lo + k, pre, d[k], err);
+        pre += d[k];
     }
     if (threadIdx.x == 0) {
-        estart[n * hs.n] = sm[16];
+        estart[nEnt] = sm[16];
         if (packedOut) *packedOut = (n << kDynShift) | sm[16];       // device-driven hops read this
         if (pub.slot) publishWords(pub.slot, pub.seq, sm[16], 0);
     }
@@ -360,17 +358,17 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
 
 // ------------------------------------------------------------------------------ compaction
 // visited[row] == epoch -> next frontier + its entries' estart + the next hop's chunk heads, two
-// launches (kernels.h CompactArgs). Wave w of tile t owns rows t * 4096 + w * 256 + k * 64 + lane,
-// k < 4, so the marks (1 B per lane) and the CSR offsets (8 B per lane) of one k are one coalesced
+// launches (kernels.h CompactArgs). Wave w of tile t owns rows t * 1024 CIT + w * 64 CIT + k * 64 +
+// lane, k < CIT, so the marks (1 B per lane) and the CSR offsets (8 B per lane) of one k are one coalesced
 // wave access, and rows leave in row order (k-major, ballot prefix inside k).
 // (r02 gave each thread 16 consecutive rows: its offset loads put the 64 lanes of a wave on 64 cache
 // lines, 16 times, and the address unit bounded the pass; a single-pass decoupled look-back over
 // tiles taken by ticket then spent 20-38 us per launch on the 586 ticket atomics and the polling.)
 // 1024-thread workgroups: a 4096-row tile over 16 waves of 4 rows per lane (r03's 4 waves of 16
 // rows left 2.3 waves per SIMD at C2, each wave issuing 16 scans one after the other)
+// CIT rows per lane (4 by default; 8 or 16 by the flag compact_lane_rows, tested for parity)
 constexpr int CWG = 1024;
 constexpr int CNW = CWG / 64;
-constexpr int CIT = TILE / CWG;
 __device__ __forceinline__ uint64_t waveInclScan(uint64_t x, int lane) {
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -393,6 +391,7 @@ __device__ __forceinline__ uint64_t rowDegree(const HopSlots& hs, uint64_t r) {
 }
 
 // the wave's 16 mark flags (bit k: row wbase + 64 k + lane)
+template <int CIT>
 __device__ __forceinline__ uint32_t waveFlags(const CompactArgs& a, uint64_t wbase, int lane) {
     uint8_t mk[CIT];
 #pragma unroll
@@ -408,7 +407,7 @@ __device__ __forceinline__ uint32_t waveFlags(const CompactArgs& a, uint64_t wba
 
 // degrees of the wave's flagged rows (0 elsewhere), every load issued before the first use
 // (ONE: also each row's CSR base in ob[], for the write launch's ebase[])
-template <bool ONE>
+template <bool ONE, int CIT>
 __device__ __forceinline__ void waveDegrees(const CompactArgs& a, uint64_t wbase, int lane, uint32_t flags,
                                             uint64_t (&deg)[CIT], uint64_t* ob = nullptr) {
 #pragma unroll
@@ -427,15 +426,15 @@ __device__ __forceinline__ void waveDegrees(const CompactArgs& a, uint64_t wbase
 }
 
 // launch 1: per tile and per wave the packed (rows << kFdShift | degrees) total; the bitmap words
-template <bool ONE>
+template <bool ONE, int CIT>
 __global__ __launch_bounds__(CWG) void k_compact_count(CompactArgs a) {
     __shared__ uint64_t sWave[CNW];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint64_t wbase = static_cast<uint64_t>(blockIdx.x) * TILE + static_cast<uint64_t>(wid) * (64 * CIT);
+    const uint64_t wbase = static_cast<uint64_t>(blockIdx.x) * (CWG * CIT) + static_cast<uint64_t>(wid) * (64 * CIT);
     if (blockIdx.x == 0 && threadIdx.x == 0 && a.clear32 != nullptr) *a.clear32 = 0;
-    const uint32_t flags = waveFlags(a, wbase, lane);
+    const uint32_t flags = waveFlags<CIT>(a, wbase, lane);
     uint64_t deg[CIT];
-    waveDegrees<ONE>(a, wbase, lane, flags, deg);
+    waveDegrees<ONE, CIT>(a, wbase, lane, flags, deg);
     uint64_t dsum = 0;
 #pragma unroll
     for (int k = 0; k < CIT; k++) dsum += deg[k];
@@ -468,13 +467,13 @@ __global__ __launch_bounds__(CWG) void k_compact_count(CompactArgs a) {
 // launch 2: the wave's start = the tiles before it + the waves before it in its tile (summed from
 // launch 1's words, nothing waited for), then the rows in order: positions from each k's ballot and a
 // wave scan of its degrees. The last tile writes the totals (estart[|F| * ns] = E, *total, publish).
-template <bool ONE>
+template <bool ONE, int CIT>
 __global__ __launch_bounds__(CWG) void k_compact_write(CompactArgs a) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint64_t tile = blockIdx.x;
-    const uint64_t wbase = tile * TILE + static_cast<uint64_t>(wid) * (64 * CIT);
+    const uint64_t wbase = tile * (CWG * CIT) + static_cast<uint64_t>(wid) * (64 * CIT);
     const int ns = a.hs.n;
-    const uint32_t flags = waveFlags(a, wbase, lane);
+    const uint32_t flags = waveFlags<CIT>(a, wbase, lane);
     // the totals of the tiles before this one: 8 loads in flight per lane (a dependent loop of loads
     // cost 10 us at C2's 586 tiles)
     uint64_t pre = lane < wid ? a.waveSum[tile * CNW + lane] : 0;
@@ -499,7 +498,7 @@ __global__ __launch_bounds__(CWG) void k_compact_write(CompactArgs a) {
     if (tile == 0 && threadIdx.x < a.nzero) a.zero[threadIdx.x * kDoneOff] = 0;
     if (__ballot(flags != 0) == 0) return;              // wave-uniform: every lane stays for the scans below
     uint64_t deg[CIT], ob[CIT];
-    waveDegrees<ONE>(a, wbase, lane, flags, deg, ONE ? ob : nullptr);
+    waveDegrees<ONE, CIT>(a, wbase, lane, flags, deg, ONE ? ob : nullptr);
     uint64_t fk = pre >> kFdShift, ek = pre & kFdMask;     // running start of group k
     const uint64_t below = (1ULL << lane) - 1;
 #pragma unroll
@@ -940,18 +939,22 @@ struct CloseHead {
     int nh;
 };
 // every workgroup: the groups' counts and last blocks (one load round trip), the holes sorted, R and
-// M; workgroup (0, 0) also publishes R and clears the next launch's counters
-__device__ __forceinline__ void closeHead(const FinalArgs& a, CloseHead& h, bool first) {
+// M; workgroup (0, 0) also publishes R and clears the next launch's counters. Plain loads: the words
+// were last written by the final kernel (an earlier launch on the stream), and every workgroup reads
+// the same 17 of them — as device-scope atomic loads each went to the memory side, one same-address
+// queue for ~1300 workgroups (r04 SQ pass: 10 us per wave, 13 us per close)
+template <class A>
+__device__ __forceinline__ void closeHead(const A& a, CloseHead& h, bool first) {
     const uint64_t B = 1ULL << a.resvShift, st = a.resvStride;
     const uint32_t G = a.resvG;
     if (threadIdx.x < G) {
         const uint32_t g = threadIdx.x;
-        const uint64_t v = lbLoad(a.resvCtl + (1 + g) * st);
+        const uint64_t v = gld<uint64_t>(a.resvCtl, (1 + g) * st);
         h.gV[g] = v;
         h.hLo[g] = h.hHi[g] = 0;
         if (v & (B - 1)) {
             const uint64_t k = v >> a.resvShift;
-            const uint64_t e = k < a.resvTB ? lbLoad(a.resvTab + static_cast<uint64_t>(g) * a.resvTB + k) : 0;
+            const uint64_t e = k < a.resvTB ? gld<uint64_t>(a.resvTab, static_cast<uint64_t>(g) * a.resvTB + k) : 0;
             if ((e >> 32) != a.resvSeq) {
                 atomicOr(a.err + 3, 1u);                    // every reserved block is published: cannot happen
             } else {
@@ -960,7 +963,7 @@ __device__ __forceinline__ void closeHead(const FinalArgs& a, CloseHead& h, bool
             }
         }
     }
-    if (threadIdx.x == WG - 1) h.P = lbLoad(a.resvCtl);
+    if (threadIdx.x == WG - 1) h.P = gld<uint64_t>(a.resvCtl, 0);
     __syncthreads();
     if (threadIdx.x == 0) {
         uint64_t R = 0;
@@ -1034,7 +1037,7 @@ __global__ __launch_bounds__(WG) void k_final_close(FinalArgs a) {
 // load of the batch issued before its stores (one width per launch row, no branch between them).
 constexpr int kCloseBatch = 8;
 template <typename T, int KIND>
-__device__ __forceinline__ void closeColumn(const FinalArgs& a, const CloseHead& h, const CloseCol& col) {
+__device__ __forceinline__ void closeColumn(const CloseArgs& a, const CloseHead& h, const CloseCol& col) {
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * WG;
     for (uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * WG + threadIdx.x; i0 < h.M; i0 += stride * kCloseBatch) {
         uint64_t to[kCloseBatch], from[kCloseBatch];
@@ -1065,8 +1068,8 @@ __device__ __forceinline__ void closeColumn(const FinalArgs& a, const CloseHead&
                 // a string value pointing into the row's own arena slots moves with them
                 uint64_t ux = static_cast<uint64_t>(v[k]);
                 const uint64_t slotBytes = static_cast<uint64_t>(a.nStrOut) * kStrBuildBytes;
-                const uint64_t sFrom = reinterpret_cast<uint64_t>(strSlot(a, from[k], 0));
-                const uint64_t sTo = reinterpret_cast<uint64_t>(strSlot(a, to[k], 0));
+                const uint64_t sFrom = reinterpret_cast<uint64_t>(a.strOut) + (from[k] - a.oBase) * slotBytes;
+                const uint64_t sTo = reinterpret_cast<uint64_t>(a.strOut) + (to[k] - a.oBase) * slotBytes;
                 if (ux >= sFrom && ux < sFrom + slotBytes) ux = ux - sFrom + sTo;
                 gst<T>(col.p, to[k], static_cast<T>(ux));
             } else {
@@ -1076,7 +1079,9 @@ __device__ __forceinline__ void closeColumn(const FinalArgs& a, const CloseHead&
     }
 }
 
-__global__ __launch_bounds__(WG) void k_final_close_cols(FinalArgs a, CloseCols cc) {
+// (its own small argument block: the fields sit in two cache lines, where FinalArgs spreads the ones
+// the close reads over 2.3 KB of kernel arguments, each line a scalar-cache miss on every CU)
+__global__ __launch_bounds__(WG) void k_final_close_cols(CloseArgs a, CloseCols cc) {
     __shared__ CloseHead h;
     closeHead(a, h, blockIdx.x == 0 && blockIdx.y == 0);
     const CloseCol col = cc.c[blockIdx.y];
@@ -1312,21 +1317,15 @@ int launchDegreeScan(const uint32_t* F, uint64_t nEnt, const HopSlots& hs, uint6
     return scan3(DegreeIn{F, hs}, nEnt, WriteEstart{estart}, tileSums, estart + nEnt, s, nullptr, 0, pub);
 }
 
-int launchSeedFrontier(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, const HopSlots& hs,
-                       uint32_t* F, uint64_t* estart, Publish pub, hipStream_t s) {
-    if (n * static_cast<uint64_t>(hs.n) > kSeedFuseMax || n > kSeedFuseMax || idx.slots == nullptr) return 1;
-    hipLaunchKernelGGL(k_seed_frontier<false>, dim3(1), dim3(1024), 0, s, qpart, qvid, n, idx, hs, F, estart, pub,
-                       nullptr, 0, nullptr, 0u, nullptr, nullptr, nullptr, nullptr);
-    return static_cast<int>(hipGetLastError());
-}
-
 int launchSeedFrontierCf(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, const HopSlots& hs,
                          uint32_t* F, uint64_t* estart, Publish pub, uint64_t* chunkFirst, uint64_t cfCap,
                          uint64_t* zero, uint32_t nzero, uint32_t* err, hipStream_t s, uint64_t* packedOut,
                          uint64_t* zero8, uint64_t* ebase) {
     if (n * static_cast<uint64_t>(hs.n) > kSeedFuseMax || n > kSeedFuseMax || idx.slots == nullptr || nzero > 64) return 1;
-    hipLaunchKernelGGL(k_seed_frontier<true>, dim3(1), dim3(1024), 0, s, qpart, qvid, n, idx, hs, F, estart, pub,
-                       chunkFirst, cfCap, zero, nzero, err, packedOut, zero8, ebase);
+    const unsigned g = static_cast<unsigned>(std::max<uint64_t>((n + 63) / 64, 1));   // block 0 also clears
+    hipLaunchKernelGGL(k_seed_lookup, dim3(g), dim3(64), 0, s, qpart, qvid, n, idx, hs,
+                       F, estart, ebase, zero, nzero, zero8);
+    hipLaunchKernelGGL(k_seed_scan, dim3(1), dim3(1024), 0, s, n, hs.n, estart, pub, chunkFirst, cfCap, err, packedOut);
     return static_cast<int>(hipGetLastError());
 }
 
@@ -1386,15 +1385,26 @@ int launchCompactDegrees(const uint8_t* visited, uint64_t gbase, uint64_t V, uin
 
 int launchCompactLb(const CompactArgs& a, hipStream_t s) {
     if (a.V >= kCompactLbMaxV || a.nzero > WG) return 1;
-    const uint64_t nt = std::max<uint64_t>((a.V + TILE - 1) / TILE, 1);
-    dim3 grid(static_cast<unsigned>(nt));
+    // rows per lane: 4 unless the flag forces 8 or 16 (measured at C2: 8 rows per lane, every wave
+    // resident at once, 48 vs 46 us per step for 4 with a second round of waves)
+    const int cit = a.laneRows != 0 ? a.laneRows : 4;
+    const uint64_t tile = static_cast<uint64_t>(CWG) * cit;
+    const dim3 grid(static_cast<unsigned>(std::max<uint64_t>((a.V + tile - 1) / tile, 1)));
+#define NGX_COMPACT(ONE, CIT)                                                              \
+    do {                                                                                   \
+        hipLaunchKernelGGL((k_compact_count<ONE, CIT>), grid, dim3(CWG), 0, s, a);         \
+        hipLaunchKernelGGL((k_compact_write<ONE, CIT>), grid, dim3(CWG), 0, s, a);         \
+    } while (0)
     if (a.hs.n == 1) {
-        hipLaunchKernelGGL((k_compact_count<true>), grid, dim3(CWG), 0, s, a);
-        hipLaunchKernelGGL((k_compact_write<true>), grid, dim3(CWG), 0, s, a);
+        if (cit == 4) NGX_COMPACT(true, 4);
+        else if (cit == 8) NGX_COMPACT(true, 8);
+        else NGX_COMPACT(true, 16);
     } else {
-        hipLaunchKernelGGL((k_compact_count<false>), grid, dim3(CWG), 0, s, a);
-        hipLaunchKernelGGL((k_compact_write<false>), grid, dim3(CWG), 0, s, a);
+        if (cit == 4) NGX_COMPACT(false, 4);
+        else if (cit == 8) NGX_COMPACT(false, 8);
+        else NGX_COMPACT(false, 16);
     }
+#undef NGX_COMPACT
     return static_cast<int>(hipGetLastError());
 }
 
@@ -1469,9 +1479,24 @@ int launchFinalClose(const FinalArgs& a, hipStream_t s) {
         for (uint64_t w = 0; fits && w < words; w++) add(a.strOut, static_cast<int32_t>(w), 2);
     }
     if (fits && cc.n > 0) {
+        CloseArgs ca{};
+        ca.resvCtl = a.resvCtl;
+        ca.resvTab = a.resvTab;
+        ca.resvNext = a.resvNext;
+        ca.err = a.err;
+        ca.rowsPub = a.rowsPub;
+        ca.rowsSeq = a.rowsSeq;
+        ca.strOut = a.strOut;
+        ca.oBase = a.oBase;
+        ca.resvTB = a.resvTB;
+        ca.resvSeq = a.resvSeq;
+        ca.resvG = a.resvG;
+        ca.resvShift = a.resvShift;
+        ca.resvStride = a.resvStride;
+        ca.nStrOut = a.nStrOut;
         // 8 rows per thread over the rows that may move
         const unsigned gx = static_cast<unsigned>((resvSlack(a) + WG * kCloseBatch - 1) / (WG * kCloseBatch));
-        hipLaunchKernelGGL(k_final_close_cols, dim3(gx, static_cast<unsigned>(cc.n)), dim3(WG), 0, s, a, cc);
+        hipLaunchKernelGGL(k_final_close_cols, dim3(gx, static_cast<unsigned>(cc.n)), dim3(WG), 0, s, ca, cc);
     } else {
         const unsigned grid = static_cast<unsigned>((resvSlack(a) + WG - 1) / WG);   // a thread per row that may move
         hipLaunchKernelGGL(k_final_close, dim3(grid), dim3(WG), 0, s, a);

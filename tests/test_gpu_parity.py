@@ -319,6 +319,28 @@ def test_rmat16_bench_query(rmat16, sel):
     assert fixtures.normalize_cells(got.rows) == fixtures.normalize_cells(ref.rows)
 
 
+@pytest.mark.parametrize("lane_rows", [4, 8, 16])
+def test_compaction_lane_rows(rmat16, rmat, lane_rows):
+    """The next-frontier compaction at each rows-per-lane width (flag compact_lane_rows, default 4):
+    the bench query at scale 16 (one edge type) and a BIDIRECT query at
+    scale 12 with in-edges (two slots per frontier row) give the oracle's rows and per-hop scans."""
+    cases = [(rmat16, datagen.rmat_seeds(16, 300, 16, 42, 99, threads=8),
+              "GO 3 STEPS FROM {S} OVER e WHERE e.p0 < 50 YIELD e._dst, e._rank, e.p0, e.p1"),
+             (rmat, datagen.sample_vids(99, 1 << 12, 40),
+              "GO 3 STEPS FROM {S} OVER e BIDIRECT WHERE e.p0 > 60 YIELD e._dst, e.p1")]
+    for (ds, o, e), seeds, text in cases:
+        s = ngql.parse_go(text.replace("{S}", ", ".join(str(int(v)) for v in seeds)))
+        e.set_flag("compact_lane_rows", lane_rows)
+        try:
+            got = e.go(ds.space, s)
+        finally:
+            e.set_flag("compact_lane_rows", 0)
+        ref = o.go(ds.space, s)
+        assert ref.ok and got.ok, (got.error, ref.error)
+        assert got.hop_edges == ref.hop_scanned
+        assert fixtures.normalize_cells(got.rows) == fixtures.normalize_cells(ref.rows)
+
+
 # --------------------------------------------------------------------------- C4: power law + supernodes
 PL_QUERIES = [
     "GO 2 STEPS FROM {S} OVER pl REVERSELY YIELD pl._dst, pl.w, pl.score",
