@@ -177,7 +177,7 @@ struct ngx_ctx {
             return n;
         }
         void release() { if (p) (void)hipHostFree(p); p = nullptr; cap = 0; }
-    } hostStage, inStage;
+    } hostStage, inStage, seedStage;
     size_t progStageBytes = 0;                          // bytes of inStage holding this call's programs                               // results D2H / query inputs H2D (programs, seeds)
     std::vector<ColBuf> oCols;                          // result columns (columnar, HBM)
     std::vector<ColBuf> dCols;                          // DISTINCT: the other half of each column's double buffer
@@ -230,6 +230,7 @@ struct ngx_ctx {
         for (auto& cb : dCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         hostStage.release();
         inStage.release();
+        seedStage.release();
         for (auto e : eventPool) (void)hipEventDestroy(e);
         if (comm) (void)ncclCommDestroy(comm);
         if (pin) (void)hipHostFree(pin);
@@ -511,15 +512,13 @@ uint64_t maxMultiplicity(const std::vector<int64_t>& v) {
     return best;
 }
 
-// seeds (vids then parts) into one device block with one copy; dvid holds n * 12 bytes
+// seeds (vids then parts) into one device block with one copy; dvid holds n * 12 bytes. The seeds
+// have their own page-locked stage: the seed hop is launched before the programs are staged
+// (runGo), so the two must not share a block that may move when it grows.
 void stageSeeds(ngx_ctx* c, const std::vector<int32_t>& parts, const std::vector<int64_t>& vids, int32_t* dpart,
                 int64_t* dvid) {
     const size_t n = vids.size();
-    const size_t progBytes = (c->progStageBytes + 63) & ~size_t(63);
-    // the stage may move when it grows: the programs' copy was issued from the old one, so wait for it
-    if (c->inStage.cap < progBytes + n * 12 + 64) HIP_OK(hipStreamSynchronize(c->stream));
-    char* host = c->inStage.getKeep(progBytes + n * 12 + 64, progBytes);
-    char* hp = host + progBytes;
+    char* hp = c->seedStage.get(n * 12 + 64);             // the previous call has synchronised with its copies
     std::memcpy(hp, vids.data(), n * 8);
     std::memcpy(hp + n * 8, parts.data(), n * 4);
     if (reinterpret_cast<char*>(dpart) == reinterpret_cast<char*>(dvid) + n * 8) {
@@ -530,21 +529,19 @@ void stageSeeds(ngx_ctx* c, const std::vector<int32_t>& parts, const std::vector
     }
 }
 
-// seeds (vids then parts) into the page-locked input stage after the programs, returned as device-visible
-// pointers into that (mapped) stage: the seed kernel reads them over the bus, no copy launch. False when
-// the stage cannot be mapped (the caller copies instead).
+// seeds (vids then parts) into the page-locked seed stage, returned as device-visible pointers into it
+// (mapped): the seed kernel reads them over the bus, no copy launch. False when the stage cannot be
+// mapped (the caller copies instead).
 bool stageSeedsMapped(ngx_ctx* c, const std::vector<int32_t>& parts, const std::vector<int64_t>& vids, const int32_t*& hpart,
                       const int64_t*& hvid) {
     const size_t n = vids.size();
-    const size_t progBytes = (c->progStageBytes + 63) & ~size_t(63);
-    if (c->inStage.cap < progBytes + n * 12 + 64) HIP_OK(hipStreamSynchronize(c->stream));
-    char* host = c->inStage.getKeep(progBytes + n * 12 + 64, progBytes);
+    char* host = c->seedStage.get(n * 12 + 64);
     char* dev = nullptr;
-    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&dev), c->inStage.p, 0) != hipSuccess || dev == nullptr) return false;
-    std::memcpy(host + progBytes, vids.data(), n * 8);
-    std::memcpy(host + progBytes + n * 8, parts.data(), n * 4);
-    hvid = reinterpret_cast<const int64_t*>(dev + progBytes);
-    hpart = reinterpret_cast<const int32_t*>(dev + progBytes + n * 8);
+    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&dev), c->seedStage.p, 0) != hipSuccess || dev == nullptr) return false;
+    std::memcpy(host, vids.data(), n * 8);
+    std::memcpy(host + n * 8, parts.data(), n * 4);
+    hvid = reinterpret_cast<const int64_t*>(dev);
+    hpart = reinterpret_cast<const int32_t*>(dev + n * 8);
     return true;
 }
 
@@ -2177,8 +2174,6 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     const DCol* dstCols = dstReplica ? d.rcols : d.dcols;
     std::vector<int32_t> ySlotType(progs.yOff.size(), 0);
     c->hmark("compile");
-    DevPrograms dp = uploadPrograms(c, progs, ySlotType, gp.colTypes);
-    c->hmark("upload");
     // WHERE fully pushed: for edges whose storage filter ran, graphd's re-evaluation is implied
     bool wIsP = pushHere && gp.where && encodeExpr(*gp.pushed) == encodeExpr(*gp.where);
     std::vector<int32_t> hopTypes;
@@ -2219,35 +2214,6 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             if (!col.allValid || !(col.type == T_INT || col.type == T_VID || col.type == T_TIMESTAMP)) continue;
             if (col.width == 1 || col.width == 2 || col.width == 4) yW[y] = col.width;
         }
-    }
-    // per-query straight-line kernels (jit.cpp); the interpreter kernels otherwise
-    std::shared_ptr<const JitKernels> jk, jkNoP;             // jkNoP: record hops before the last (no pushdown)
-    std::vector<int64_t> jitKc;                              // their literal table (FinalArgs::kc/kl)
-    std::vector<uint32_t> jitKl;
-    c->jitNote.clear();
-    c->jit.releaseRetired(c->stream);                        // modules evicted by earlier queries
-    if (c->jitOn) {
-        JitQuery jq = jitHopQuery(sp, hs, progs);
-        jq.yColType = gp.colTypes;
-        jq.yKey = yAlias;
-        jq.dstReplica = dstReplica;
-        jq.rowMask = rowMask;
-        for (int k = 0; k < 3; k++) jq.outW[k] = outW[k];
-        if (compact) jq.yW = yW;
-        jq.input = rw && rw->perRow;
-        jitSlotConsts(jq, jitKc, jitKl);
-        std::string jerr;
-        // kernels cached by query shape: the source is generated only on a miss
-        jk = c->jit.get(jitShapeKey(sp, jq), [&] { return jitSource(sp, jq); }, jerr);
-        if (jk && jq.P.present && recordFrom < steps) {
-            jq.P = JitProgram{};
-            jkNoP = c->jit.get(jitShapeKey(sp, jq), [&] { return jitSource(sp, jq); }, jerr);
-            if (!jkNoP) jk = nullptr;
-        } else {
-            jkNoP = jk;
-        }
-        if (!jk) c->jitNote = jerr.empty() ? "jit: unsupported program" : jerr;
-        c->hmark("jit");
     }
     // algorithmic-byte model inputs: k_f prop columns read by the filter, k_y yielded
     uint64_t ky = 0, kfBytes = 0;
@@ -2509,6 +2475,39 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                 if (launchLookup(dp_, dv, nF, d.vpart, d.vid, d.V, F, c->stream)) throw Error{NGX_E_DEVICE, "lookup"};
             });
         }
+    }
+    // the programs and the generated kernels, prepared while the seed hop runs (only the record hops
+    // read them)
+    DevPrograms dp = uploadPrograms(c, progs, ySlotType, gp.colTypes);
+    c->hmark("upload");
+    // per-query straight-line kernels (jit.cpp); the interpreter kernels otherwise
+    std::shared_ptr<const JitKernels> jk, jkNoP;             // jkNoP: record hops before the last (no pushdown)
+    std::vector<int64_t> jitKc;                              // their literal table (FinalArgs::kc/kl)
+    std::vector<uint32_t> jitKl;
+    c->jitNote.clear();
+    c->jit.releaseRetired(c->stream);                        // modules evicted by earlier queries
+    if (c->jitOn) {
+        JitQuery jq = jitHopQuery(sp, hs, progs);
+        jq.yColType = gp.colTypes;
+        jq.yKey = yAlias;
+        jq.dstReplica = dstReplica;
+        jq.rowMask = rowMask;
+        for (int k = 0; k < 3; k++) jq.outW[k] = outW[k];
+        if (compact) jq.yW = yW;
+        jq.input = rw && rw->perRow;
+        jitSlotConsts(jq, jitKc, jitKl);
+        std::string jerr;
+        // kernels cached by query shape: the source is generated only on a miss
+        jk = c->jit.get(jitShapeKey(sp, jq), [&] { return jitSource(sp, jq); }, jerr);
+        if (jk && jq.P.present && recordFrom < steps) {
+            jq.P = JitProgram{};
+            jkNoP = c->jit.get(jitShapeKey(sp, jq), [&] { return jitSource(sp, jq); }, jerr);
+            if (!jkNoP) jk = nullptr;
+        } else {
+            jkNoP = jk;
+        }
+        if (!jk) c->jitNote = jerr.empty() ? "jit: unsupported program" : jerr;
+        c->hmark("jit");
     }
     // multi-root walk: root sets over rows, the seed frontier's from the starts' bits
     uint64_t* rootsCur = nullptr;

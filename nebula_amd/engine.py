@@ -523,15 +523,19 @@ class Engine:
             strings = ctypes.string_at(r.strings, r.strings_len) if r.strings_len else b""
             n = r.nrows
             if on_device:
-                res = GoResult(ok=rc == 0, error=err, code=rc, col_types=[r.col_types[i] for i in range(r.ncols)],
+                # pointer slices (one C loop each) rather than an element access per index: this path
+                # runs once per bench step
+                nh, nc = r.nhops, r.ncols
+                xb = r.hop_exchange_bytes
+                res = GoResult(ok=rc == 0, error=err, code=rc, col_types=r.col_types[:nc] if nc else [],
                                rows=[], nrows=n, host_prep_ms=r.host_prep_ms, host_tail_ms=r.host_tail_ms,
-                               hop_frontier=[r.hop_frontier[i] for i in range(r.nhops)],
-                               hop_edges=[r.hop_edges[i] for i in range(r.nhops)],
-                               hop_next=[r.hop_next[i] for i in range(r.nhops)],
-                               hop_xchg=[r.hop_exchange_bytes[i] for i in range(r.nhops)] if r.hop_exchange_bytes else [],
+                               hop_frontier=r.hop_frontier[:nh] if nh else [],
+                               hop_edges=r.hop_edges[:nh] if nh else [],
+                               hop_next=r.hop_next[:nh] if nh else [],
+                               hop_xchg=xb[:nh] if xb and nh else [],
                                device_ms=r.device_ms)
                 if rc == 0 and r.dev_col_w:
-                    res.dev_widths = ([r.dev_key_w[k] for k in range(3)], [r.dev_col_w[c] for c in range(r.ncols)])
+                    res.dev_widths = (r.dev_key_w[:3], r.dev_col_w[:nc] if nc else [])
                 if fetch and rc == 0:
                     kw = res.dev_widths[0] if res.dev_widths else [8, 8, 8]
                     cw = res.dev_widths[1] if res.dev_widths else [8] * r.ncols
