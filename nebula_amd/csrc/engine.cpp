@@ -2439,6 +2439,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     bool haveEstart = false;                                   // estart[] / E of the next hop already built
     bool haveEbase = false;                                    // ... and its entries' CSR positions (ebase[])
     uint64_t fusedE = 0;
+    Publish seedPub{nullptr, 0};                               // the fused seed hop's E, awaited after the host prep
+    const uint64_t* seedE = nullptr;
     if (nF) {
         // the fused seed kernel reads the seeds from the mapped page-locked stage; else a device copy
         const int64_t* dv = nullptr;
@@ -2466,7 +2468,12 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                                          c->stream, dynStats, counters, eb0))
                     throw Error{NGX_E_DEVICE, "seed"};
             });
-            fusedE = dyn ? slotEdges * mult : awaitPub(c, pub, est0 + nEnt0);   // dyn: an upper bound
+            if (dyn) {
+                fusedE = slotEdges * mult;                     // an upper bound: the device has the real E
+            } else {
+                seedPub = pub;
+                seedE = est0 + nEnt0;
+            }
             haveEstart = true;
             haveEbase = true;
             haveHeads = true;
@@ -2509,6 +2516,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         if (!jk) c->jitNote = jerr.empty() ? "jit: unsupported program" : jerr;
         c->hmark("jit");
     }
+    if (seedE) fusedE = awaitPub(c, seedPub, seedE);           // the seed hop ran under the host prep above
     // multi-root walk: root sets over rows, the seed frontier's from the starts' bits
     uint64_t* rootsCur = nullptr;
     uint64_t* rootsNext = nullptr;
