@@ -299,7 +299,7 @@ def main():
                 # real memory throughput (frac above credits the algorithmic bytes)
                 "frac_counter": round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 4) if traffic and avg_s > 0 else None,
                 # the same figure with every field at the width it is stored / written at (compact results:
-                # 6 B / scanned edge, 18 B / row at C2): the least this layout must move
+                # 5 B / scanned edge, 17 B / row at C2, the rank a constant column): the least this layout must move
                 "stored_width": {"algo_bytes_per_launch": stored,
                                  "frac": round(stored / avg_s / 1e9 / HBM_PEAK_GBS, 4) if avg_s > 0 else None,
                                  "compact_results": not args.no_compact}}

@@ -364,6 +364,11 @@ typedef struct {
      * (8 unless plan.compact_results; then 1, 2, 4 or 8, signed integers below 8) */
     int32_t dev_key_w[3];
     const int32_t* dev_col_w;          /* ncols entries */
+    /* compact_results: a width of 0 in dev_key_w / dev_col_w marks a constant column — the array is NULL
+     * and every row holds dev_key_const[k] / dev_col_const[c] (the rank when every edge of the OVER
+     * types has the same rank: nothing is written per row) */
+    int64_t dev_key_const[3];
+    const int64_t* dev_col_const;      /* ncols entries */
 } ngx_go_result;
 
 int32_t ngx_go(ngx_ctx* ctx, const ngx_go_plan* plan, ngx_go_result** out);

@@ -954,6 +954,7 @@ struct GoResultHolder {
     const int64_t *rowSrcView = nullptr, *rowDstView = nullptr, *rowRankView = nullptr;
     const int32_t* rowTypeView = nullptr;
     std::vector<int32_t> devColW;                               // result_on_device: bytes per dev_cols[c].x
+    std::vector<int64_t> devColConst;                           // ... and the value of a constant one (width 0)
 };
 struct GnResultHolder {
     ngx_gn_result r{};
@@ -1903,7 +1904,8 @@ std::vector<int32_t> keyAliases(const Programs& progs, const std::vector<int32_t
 // size the result columns for `cap` rows (keeping `keep`) and upload their descriptors; aliased
 // key columns (keyAliases) point at oSrc/oDst/oRank, which must already be sized
 void prepareCols(ngx_ctx* c, FinalArgs& a, const std::vector<ColSpec>& spec, uint64_t cap, uint64_t keep,
-                 const std::vector<int32_t>& alias = {}, const std::vector<int32_t>* widths = nullptr) {
+                 const std::vector<int32_t>& alias = {}, const std::vector<int32_t>* widths = nullptr,
+                 bool rankConst = false) {
     if (c->oCols.size() < spec.size()) c->oCols.resize(spec.size());
     c->oColView.assign(spec.size(), OutCol{nullptr, nullptr, nullptr, 8, 0});
     for (size_t y = 0; widths && y < spec.size() && y < widths->size(); y++) c->oColView[y].w = (*widths)[y];
@@ -1911,7 +1913,8 @@ void prepareCols(ngx_ctx* c, FinalArgs& a, const std::vector<ColSpec>& spec, uin
         auto& cb = c->oCols[y];
         if (y < alias.size() && alias[y] >= 0) {
             DBuf& kb = alias[y] == 0 ? c->oSrc : alias[y] == 1 ? c->oDst : c->oRank;
-            c->oColView[y].x = static_cast<int64_t*>(kb.p);
+            // a constant rank is stored nowhere (the kernels skip a column without an array)
+            c->oColView[y].x = (alias[y] == 2 && rankConst) ? nullptr : static_cast<int64_t*>(kb.p);
             continue;
         }
         growKeep(c, cb.x, cap * 8, keep * 8);
@@ -2191,6 +2194,12 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     // (src: of the shard's vid table), and a YIELD column that copies one stored integer column of the
     // only OVER type, present in every row, at that column's width; every other column at 8 bytes
     const bool compact = p.compact_results && p.result_on_device && !p.distinct && rw == nullptr;
+    // compact results over slots whose every rank is one value (no rank column in HBM, HopSlots::rankC):
+    // the rank is a constant column of the result (width 0), no byte per row
+    bool rankConst = compact && hs.n > 0;
+    for (int s = 0; rankConst && s < hs.n; s++)
+        rankConst = hs.rank[s] == nullptr && hs.rankC[s] == hs.rankC[0];
+    if (rankConst) rowMask &= ~4;
     int32_t outW[3] = {8, 8, 8};
     std::vector<int32_t> yW(progs.yOff.size(), 8);
     if (compact) {
@@ -2250,7 +2259,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         kfBytes += 8 * (wr.srcTag.size() + wr.dstTag.size());
     }
     // per scanned edge: dst + rank (8 B each in §8d; compact: their stored widths) + the filter props
-    const uint64_t keyReadBytes = compact ? static_cast<uint64_t>(outW[1] + outW[2]) : 16u;
+    const uint64_t keyReadBytes = compact ? static_cast<uint64_t>(outW[1] + (rankConst ? 0 : outW[2])) : 16u;
     // bytes written per passing edge: the row arrays and the k_y yielded props, 8 B each (§8d); compact
     // results count each at the width it is written at
     uint64_t rowBytes = 0;
@@ -2671,7 +2680,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             growKeep(c, c->oDst, cap * 8, totalRows * 8);
             growKeep(c, c->oRank, cap * 8, totalRows * 8);
             growKeep(c, c->oType, cap * 4, totalRows * 4);
-            prepareCols(c, a, colSpec, cap, totalRows, yAlias, compact ? &yW : nullptr);
+            prepareCols(c, a, colSpec, cap, totalRows, yAlias, compact ? &yW : nullptr, rankConst);
             a.oBase = totalRows;
             a.oSrcW = static_cast<int8_t>(outW[0]);
             a.oDstW = static_cast<int8_t>(outW[1]);
@@ -3075,7 +3084,19 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         R.devColW.assign(nY, 8);
         for (int k = 0; k < 3; k++) R.r.dev_key_w[k] = compact ? outW[k] : 8;
         for (int32_t y = 0; compact && y < nY; y++) R.devColW[y] = yW[y];
+        R.devColConst.assign(nY, 0);
+        if (rankConst) {                                      // the rank and the YIELD columns that alias it
+            R.r.dev_key_w[2] = 0;
+            R.r.dev_key_const[2] = hs.rankC[0];
+            for (int32_t y = 0; y < nY; y++) {
+                if (y >= static_cast<int32_t>(yAlias.size()) || yAlias[y] != 2) continue;
+                R.devColW[y] = 0;
+                R.devColConst[y] = hs.rankC[0];
+                R.devCols[y].x = nullptr;
+            }
+        }
         R.r.dev_col_w = R.devColW.data();
+        R.r.dev_col_const = R.devColConst.data();
         return NGX_OK;
     }
     // ---- results to the host: every array in one batch of D2H copies into page-locked staging

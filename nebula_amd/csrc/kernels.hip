@@ -912,7 +912,7 @@ struct VmEv {
                 if (v.t == V_ERR) errs |= 1u;
                 else if (a.yColType != nullptr && !cellTypeOk(a.yColType[y], v.t)) errs |= 4u;
             }
-            storeW(oc.x, oc.w, o, v.x);
+            if (oc.x) storeW(oc.x, oc.w, o, v.x);         // no array: a constant column (aliased rank)
             if (oc.len) gst<uint32_t>(oc.len, o, v.len);
             if (oc.t) gst<uint8_t>(oc.t, o, v.t);
         }

@@ -153,7 +153,8 @@ class GoResultC(ctypes.Structure):
                 ("dev_rank", ctypes.c_void_p), ("dev_type", ctypes.c_void_p), ("dev_cols", ctypes.c_void_p),
                 ("dev_type_const", ctypes.c_int32), ("host_cols", ctypes.c_void_p),
                 ("hop_exchange_bytes", P(c_u64)), ("host_prep_ms", c_dbl), ("host_tail_ms", c_dbl),
-                ("dev_key_w", c_i32 * 3), ("dev_col_w", P(c_i32))]
+                ("dev_key_w", c_i32 * 3), ("dev_col_w", P(c_i32)),
+                ("dev_key_const", c_i64 * 3), ("dev_col_const", P(c_i64))]
 
 
 class Stat(ctypes.Structure):
@@ -301,6 +302,7 @@ class GoResult:
     dev_cols: List[tuple] = field(default_factory=list)
     # on_device: ([src, dst, rank] widths, per-column widths) in bytes; 8 unless compact
     dev_widths: Optional[tuple] = None
+    dev_consts: Optional[tuple] = None       # (key values, column values) of width-0 (constant) columns
     digests: object = None               # columnar + digest_fn: whatever digest_fn returned
     host_prep_ms: float = 0.0            # library host time before the first launch / after the device
     host_tail_ms: float = 0.0
@@ -535,19 +537,27 @@ class Engine:
                                hop_xchg=xb[:nh] if xb and nh else [],
                                device_ms=r.device_ms)
                 if rc == 0 and r.dev_col_w:
+                    # width 0: a constant column (value in dev_key_const / dev_col_const, no array)
                     res.dev_widths = (r.dev_key_w[:3], r.dev_col_w[:nc] if nc else [])
+                    res.dev_consts = (r.dev_key_const[:3], r.dev_col_const[:nc] if nc and r.dev_col_const else [0] * nc)
                 if fetch and rc == 0:
                     kw = res.dev_widths[0] if res.dev_widths else [8, 8, 8]
                     cw = res.dev_widths[1] if res.dev_widths else [8] * r.ncols
-                    res.src = self._d2h_int(r.dev_src, n, kw[0]) if r.dev_src else None
-                    res.dst = self._d2h_int(r.dev_dst, n, kw[1]) if r.dev_dst else None
-                    res.rank = self._d2h_int(r.dev_rank, n, kw[2]) if r.dev_rank else None
+                    kc, cc = res.dev_consts if res.dev_widths else ([0, 0, 0], [0] * r.ncols)
+
+                    def key(ptr, k):
+                        if kw[k] == 0:
+                            return np.full(n, kc[k], np.int64)
+                        return self._d2h_int(ptr, n, kw[k]) if ptr else None
+                    res.src = key(r.dev_src, 0)
+                    res.dst = key(r.dev_dst, 1)
+                    res.rank = key(r.dev_rank, 2)
                     res.etype = (self._d2h(r.dev_type, n, np.int32) if r.dev_type
                                  else np.full(n, r.dev_type_const, np.int32))   # one OVER type: no column
                     cols = ctypes.cast(r.dev_cols, P(DevColumn)) if r.dev_cols else None
                     for c in range(r.ncols):
                         dc = cols[c]
-                        res.dev_cols.append((self._d2h_int(dc.x, n, cw[c]),
+                        res.dev_cols.append((np.full(n, cc[c], np.int64) if cw[c] == 0 else self._d2h_int(dc.x, n, cw[c]),
                                              self._d2h(dc.len, n, np.uint32) if dc.len else None,
                                              self._d2h(dc.type, n, np.uint8) if dc.type else None))
                 return res

@@ -19,19 +19,20 @@ from tests import fixtures
 pytestmark = pytest.mark.gpu
 
 QUERIES = [
-    # (query, expected key widths, expected column widths); None: not checked
+    # (query, expected key widths, expected column widths); None: not checked. Every rank of the RMAT
+    # graph is 0, so the rank is a constant column (width 0, ngx_go_result.dev_key_const): no bytes
     ("GO 3 STEPS FROM {S} OVER e WHERE e.p0 < 50 YIELD e._dst, e._rank, e.p0, e.p1",
-     [2, 2, 1], [2, 1, 1, 8]),
+     [2, 2, 0], [2, 0, 1, 8]),
     ("GO 1 TO 3 STEPS FROM {S} OVER e WHERE e.p0 % 7 == 1 YIELD e._src, e._dst, e.p0, e.p0 + 1, e.p1 % 1000",
-     [2, 2, 1], [2, 2, 1, 8, 8]),
+     [2, 2, 0], [2, 2, 1, 8, 8]),
     ("GO 2 STEPS FROM {S} OVER e REVERSELY YIELD e._dst, e.p1, e.p0, $^.vt.v0, $^.vt.name",
-     [2, 2, 1], [2, 8, 1, 8, 8]),
+     [2, 2, 0], [2, 8, 1, 8, 8]),
     ("GO 2 STEPS FROM {S} OVER e BIDIRECT WHERE e.p0 > 80 YIELD e._dst, e.p0, e._rank",
-     [2, 2, 1], [2, 8, 1]),                 # two slots: aliased keys compact, e.p0 at 8 bytes
+     [2, 2, 0], [2, 8, 0]),                 # two slots: aliased keys compact, e.p0 at 8 bytes
     ("GO 2 STEPS FROM {S} OVER e YIELD DISTINCT e._dst, e.p0",
      [8, 8, 8], [8, 8]),
     ("GO 3 STEPS FROM {S} OVER e WHERE $$.vt.v0 > 10 YIELD e.p0, $$.vt.v0, e._dst",
-     [2, 2, 1], [1, 8, 2]),
+     [2, 2, 0], [1, 8, 2]),
 ]
 
 
@@ -75,6 +76,8 @@ def test_compact_equals_wide(rmat12, qi, jit):
         assert comp.dev_widths[0] == key_w
     if col_w is not None:
         assert comp.dev_widths[1] == col_w
+    if comp.dev_widths[0][2] == 0:                  # a constant rank: its value, and no array behind it
+        assert comp.dev_consts[0][2] == 0
     # rows land in chunk completion order (final_kernels.h, !ORDERED): compare the sorted rows over the
     # row arrays and every column without per-row lengths / types (strings are pointers into arenas)
     def table(r):

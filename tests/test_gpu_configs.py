@@ -118,7 +118,9 @@ def test_c2_bench_step_vs_oracle(c2):
     got = e.go(ds.space, s, on_device=True, fetch=True, compact=True)
     assert got.ok and got.hop_edges == ref.hop_scanned
     key_w, col_w = got.dev_widths
-    assert key_w == [4, 4, 1] and col_w == [4, 1, 1, 8]      # src / dst vids < 2^31, rank 0, p0 < 100
+    # src / dst vids < 2^31, p0 < 100; every rank 0: a constant column (width 0, no bytes per row)
+    assert key_w == [4, 4, 0] and col_w == [4, 0, 1, 8]
+    assert got.dev_consts[0][2] == 0 and got.dev_consts[1][1] == 0
     cols = [np.ascontiguousarray(x) for x, _, _ in got.dev_cols]
     assert all(ln is None and t is None for _, ln, t in got.dev_cols)
     digests = oracle.digest_columns(got.col_types, got.nrows, [c.ctypes.data for c in cols], [None] * 4, [None] * 4)
