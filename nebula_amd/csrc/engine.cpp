@@ -885,7 +885,7 @@ Publish nextPub(ngx_ctx* c) {
 // the stream, and read the device copy if the slot still disagrees. extra (final-hop publications):
 // the word published beside the value (the query's error bits), or read from errDev on the fallback.
 uint64_t awaitPub(ngx_ctx* c, const Publish& p, const uint64_t* devCopy, uint64_t* extra = nullptr,
-                  const uint32_t* errDev = nullptr) {
+                  const uint32_t* errDev = nullptr, uint64_t* extra2 = nullptr, const uint64_t* extra2Dev = nullptr) {
     auto errBits = [&] {
         if (!extra) return;
         uint32_t f[4];
@@ -900,8 +900,10 @@ uint64_t awaitPub(ngx_ctx* c, const Publish& p, const uint64_t* devCopy, uint64_
         const uint64_t tag = __atomic_load_n(&c->pin[1], __ATOMIC_ACQUIRE);
         v = __atomic_load_n(&c->pin[0], __ATOMIC_ACQUIRE);
         const uint64_t x = __atomic_load_n(&c->pin[2], __ATOMIC_ACQUIRE);
-        if (tag != pubTag(p.seq, v, x)) return false;
+        const uint64_t x2 = __atomic_load_n(&c->pin[3], __ATOMIC_ACQUIRE);
+        if (tag != pubTag(p.seq, v, x, x2)) return false;
         if (extra) *extra = x;
+        if (extra2) *extra2 = x2;
         return true;
     };
     uint64_t v = 0;
@@ -916,6 +918,7 @@ uint64_t awaitPub(ngx_ctx* c, const Publish& p, const uint64_t* devCopy, uint64_
     HIP_OK(hipStreamSynchronize(c->stream));
     if (take(v)) return v;
     errBits();
+    if (extra2) *extra2 = extra2Dev ? readScalar(c, extra2Dev) : 0;
     return readScalar(c, devCopy);
 }
 
@@ -2411,7 +2414,14 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     const bool dyn = !rw && c->dynHops && c->world == 1 && lbCompact && hs.n > 0 && !capped && recordFrom == steps && !pushInvalid &&
                      !intermediateChecks && !svids.empty() && svids.size() <= kSeedFuseMax &&
                      svids.size() * static_cast<uint64_t>(hs.n) <= kSeedFuseMax && d.vindex.slots != nullptr;
-    uint64_t* dynStats = dyn ? c->dynStats.get<uint64_t>(steps + 2) : nullptr;
+    // The final hop's grid and E from the device (finalDev): the compaction before it keeps its packed
+    // (|F|, E) in dynStats and publishes nothing, the final kernel strides an upper-bound grid over the
+    // real chunks (a device-driven hop measured as fast as a host-sized one), and k_final_close publishes
+    // that hop's totals beside the row count: one host round trip fewer. One shard, one record hop (the
+    // last), outputs sized for every edge of the slots, no string arena, no storage mask on it.
+    const bool finalDev = !dyn && !rw && c->world == 1 && lbCompact && hs.n > 0 && steps >= 2 && recordFrom == steps &&
+                          !pushInvalid && !capped && nStrOut == 0;
+    uint64_t* dynStats = (dyn || finalDev) ? c->dynStats.get<uint64_t>(steps + 2) : nullptr;
     const uint64_t pullMinE = pullable ? (static_cast<uint64_t>(c->pullFactor) * d.V + 99) / 100 : ~0ULL;
     if (dyn && c->epoch + 2 * static_cast<uint64_t>(steps) + 4 > 255) {   // no epoch wrap inside the query
         HIP_OK(hipMemsetAsync(c->visited.p, 0, c->visitedSize, c->stream));
@@ -2559,6 +2569,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         if (c->traceGo) hopT.push_back(std::chrono::steady_clock::now());
         bool isRecord = h >= recordFrom;
         bool isFinal = h == steps;
+        const bool devE = finalDev && isFinal;                   // E below is an upper bound; the device has it
         uint64_t nEnt = nF * static_cast<uint64_t>(hs.n);
         uint64_t* estart = c->estart.get<uint64_t>(nEnt + 1);
         const uint64_t* ebase = haveEbase ? c->ebase.get<uint64_t>(nEnt + 1) : nullptr;
@@ -2580,7 +2591,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             R.hopFrontier.push_back(nF);
             R.hopEdges.push_back(E);
         }
-        const uint64_t* dynTotal = dyn ? dynStats + (h - 1) : nullptr;   // this hop's (|F|, E), device side
+        const uint64_t* dynTotal = (dyn || devE) ? dynStats + (h - 1) : nullptr;   // this hop's (|F|, E), device side
         uint64_t chunks = (E + kChunk - 1) / kChunk;
         uint64_t* chunkFirst = c->chunkFirst.get<uint64_t>(std::max<uint64_t>(chunks, 1));
         if (E && !haveHeads) {
@@ -2718,7 +2729,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             a.resvTab = resvTable(c, static_cast<uint64_t>(a.resvTB) * a.resvG);
             if (++c->resvSeq == 0) c->resvSeq = 1;
             a.resvSeq = c->resvSeq;
-            c->timed("final", dyn ? 0 : Ef * (keyReadBytes + kfBytes), [&] {
+            c->timed("final", (dyn || devE) ? 0 : Ef * (keyReadBytes + kfBytes), [&] {
                 if (grid == 0) return;
                 if (kj) {
                     void* args[] = {&a};
@@ -2733,8 +2744,18 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             });
             if (!dyn) {
                 // GO: the row count and the query's error bits so far, published by k_final_close
-                uint64_t nrows = awaitPub(c, rowsPub, c->resvRows, &finalErrBits, errFlag);
+                uint64_t fin = 0;                               // devE: this hop's packed (|F|, E)
+                uint64_t nrows = awaitPub(c, rowsPub, c->resvRows, &finalErrBits, errFlag, devE ? &fin : nullptr,
+                                          devE ? dynTotal : nullptr);
                 haveFinalErrs = true;
+                if (devE) {                                     // the hop's statistics, known now
+                    const uint64_t fF = fin >> kDynShift, fE = fin & kDynMask;
+                    R.hopFrontier.back() = fF;
+                    R.hopEdges.back() = fE;
+                    if (!R.hopNext.empty()) R.hopNext.back() = fF;
+                    c->addBytes("final", fE * (keyReadBytes + kfBytes));
+                    c->addBytes("compact_degrees", fF * 8 + fF * static_cast<uint64_t>(hs.n) * 24);
+                }
                 c->addBytes("final", nrows * rowBytes);
                 if (rw && !rw->perRow) {                        // the rows' src vids -> their roots
                     RootWalk::Hop hop;
@@ -2858,8 +2879,9 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             ca.clear32 = pullable ? pa.ctl : nullptr;
             ca.bits = lbits;
             haveBits = lbits != nullptr;
-            ca.total = dyn ? dynStats + h : counters + 2;
-            ca.pub = dyn ? Publish{nullptr, 0} : nextPub(c);
+            const bool devNext = finalDev && h + 1 == steps;      // the next hop is the device-sized final one
+            ca.total = (dyn || devNext) ? dynStats + h : counters + 2;
+            ca.pub = (dyn || devNext) ? Publish{nullptr, 0} : nextPub(c);
             ca.zero = nullptr;
             ca.nzero = 0;
             ca.err = errFlag;
@@ -2871,7 +2893,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             haveEstart = true;
             haveEbase = true;
             haveHeads = true;
-            if (dyn) {                                          // upper bounds; the device has the real ones
+            if (dyn || devNext) {                               // upper bounds; the device has the real ones
                 nF = d.V;
                 fusedE = slotEdges;
             } else {

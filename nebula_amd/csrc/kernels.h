@@ -24,13 +24,16 @@ __host__ __device__ inline uint64_t pubMix(uint64_t x) {
     x *= 0x81dadef4bc2dd44dULL;
     return x ^ (x >> 33);
 }
-__host__ __device__ inline uint64_t pubTag(uint64_t seq, uint64_t value, uint64_t extra) {
-    return pubMix(seq ^ pubMix(value + 0x9e3779b97f4a7c15ULL) ^ pubMix(extra ^ 0x2545f4914f6cdd1dULL) * 3);
+__host__ __device__ inline uint64_t pubTag(uint64_t seq, uint64_t value, uint64_t extra, uint64_t extra2) {
+    return pubMix(seq ^ pubMix(value + 0x9e3779b97f4a7c15ULL) ^ pubMix(extra ^ 0x2545f4914f6cdd1dULL) * 3 ^
+                  pubMix(extra2 + 0x632be59bd9b4e019ULL) * 5);
 }
-__device__ inline void publishWords(uint64_t* slot, uint64_t seq, uint64_t value, uint64_t extra) {
+// slot[3]: a second extra word (the final hop's packed (|F|, E) when its grid came from the device)
+__device__ inline void publishWords(uint64_t* slot, uint64_t seq, uint64_t value, uint64_t extra, uint64_t extra2 = 0) {
     __hip_atomic_store(slot, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(slot + 2, extra, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(slot + 1, pubTag(seq, value, extra), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(slot + 3, extra2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(slot + 1, pubTag(seq, value, extra, extra2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // (part, vid) -> shard vertex row: open-addressing table (linear probing, power-of-two capacity
@@ -173,6 +176,7 @@ struct CloseArgs {
     uint64_t rowsSeq;
     char* strOut;
     uint64_t oBase;
+    const uint64_t* dynTotal;           // the final hop's packed (|F|, E) on the device, published beside R
     uint32_t resvTB, resvSeq, resvG, resvShift, resvStride, nStrOut;
 };
 struct CloseCols {

@@ -989,7 +989,7 @@ __device__ __forceinline__ void closeHead(const A& a, CloseHead& h, bool first) 
                 uint64_t bits = 0;
                 for (int k = 0; k < 4; k++)
                     bits |= static_cast<uint64_t>(__hip_atomic_load(a.err + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) << k;
-                publishWords(a.rowsPub, a.rowsSeq, R, bits);
+                publishWords(a.rowsPub, a.rowsSeq, R, bits, a.dynTotal ? gld<uint64_t>(a.dynTotal, 0) : 0);
             }
         }
     }
@@ -1488,6 +1488,7 @@ int launchFinalClose(const FinalArgs& a, hipStream_t s) {
         ca.rowsSeq = a.rowsSeq;
         ca.strOut = a.strOut;
         ca.oBase = a.oBase;
+        ca.dynTotal = a.dynTotal;
         ca.resvTB = a.resvTB;
         ca.resvSeq = a.resvSeq;
         ca.resvG = a.resvG;
