@@ -3597,8 +3597,11 @@ void encodeEdgeRows(ngx_ctx* c, const FinalArgs& a, uint64_t nrows,
     if (launchEncodeRows(e, true, c->stream)) throw Error{NGX_E_DEVICE, "rows"};
     R.edgePropsOff.resize(nrows + 1);
     R.edgeProps.resize(total);
-    HIP_OK(hipMemcpyAsync(R.edgePropsOff.data(), off, (nrows + 1) * 8, hipMemcpyDeviceToHost, c->stream));
-    if (total) HIP_OK(hipMemcpyAsync(R.edgeProps.data(), e.out, total, hipMemcpyDeviceToHost, c->stream));
+    // the rows into pageable vectors: wait for the encode launch, then plain synchronous copies (an
+    // asynchronous copy into pageable memory is staged by the runtime; keep the order explicit)
+    HIP_OK(hipStreamSynchronize(c->stream));
+    HIP_OK(hipMemcpy(R.edgePropsOff.data(), off, (nrows + 1) * 8, hipMemcpyDeviceToHost));
+    if (total) HIP_OK(hipMemcpy(R.edgeProps.data(), e.out, total, hipMemcpyDeviceToHost));
 }
 
 // TagData rows (QueryBoundProcessor.cpp:175-204): per request vid, per tag of the response in order, the
