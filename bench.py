@@ -184,7 +184,8 @@ def main():
     dev_ms = 0.0
     hop_edges = None
     hop_xchg = None
-    final_8d = 0
+    final_8d = final_edges = final_rows = 0
+    p1_width = None
     prep_ms = tail_ms = 0.0
     for i in range(args.steps):
         r = step(plans[args.warmup + i])
@@ -195,6 +196,10 @@ def main():
         hop_edges = r.hop_edges
         hop_xchg = r.hop_xchg
         final_8d += 24 * r.hop_edges[-1] + 40 * r.nrows
+        final_edges += r.hop_edges[-1]
+        final_rows += r.nrows
+        if r.dev_widths and len(r.dev_widths[1]) >= 4:
+            p1_width = r.dev_widths[1][3]               # YIELD e._dst, e._rank, e.p0, e.p1: p1's width
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t_start
@@ -263,13 +268,19 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.SUM)
         edges, result_rows, xchg_bytes_all = int(e[0]), int(e[1]), int(e[2])
 
-    # dominant kernel roofline (algorithmic bytes / HIP-event time)
+    # dominant kernel roofline. `frac` = the bytes the kernel must move on this layout (a
+    # fraction <= 1 of the bytes the kernel actually moves) / its HIP-event launch time / 8 TB/s. For the
+    # final hop that is the library's stored-width count (dst 4 B + p0 1 B per scanned edge, rank a
+    # constant column: 0 B; 17 B written per row) plus the YIELD-only column p1 read at whole 128-B lines:
+    # a line of 128 / w values is fetched when any of its edges passes, 1 - (1 - f)^(128 / w) of the
+    # lines at pass fraction f (random at C2: every line). SURVEY.md §8d's figure (every field 8 B) is
+    # kept beside it as frac_8d, a TEPS-equivalent credit, not a bandwidth.
     hbm = {k: v for k, v in stats.items() if k not in NOT_HBM}
     dom = max(hbm.items(), key=lambda kv: kv[1][1]) if hbm else None
     roof = None
+    final_fix = 0
     if dom:
         name, (launches, ms, algo) = dom
-        achieved = algo / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         traffic = None
         # the committed PMC bytes were measured on the N = 1 C2 step: other workloads report none
         if os.path.exists(args.traffic) and world == 1 and scale == 22 and not args.yield_only:
@@ -282,30 +293,44 @@ def main():
                 traffic = None
         avg_s = ms * 1e-3 / max(launches, 1)
         stored = algo // max(launches, 1)             # the library's count: fields at their stored widths
+        must, algo8, line_note = stored, stored, None
         if name == "final" and final_8d and launches:
-            # SURVEY.md §8d's per-unit figure (every field 8 bytes): 24 B per scanned edge of the last hop
-            # (dst, rank, the filter prop) + 40 B per result row (src, dst, rank, p0, p1); one final launch
-            # per step, the profiled pass re-runs the timed steps
+            # the profiled pass re-runs the timed steps: one final launch per step
             algo8 = final_8d // args.steps
-            final_fix = final_8d * launches // args.steps - algo   # path bytes: the final hop at §8d
-            achieved = algo8 / avg_s / 1e9 if avg_s > 0 else 0.0
-        else:
-            algo8, final_fix = stored, 0
+            e_last = max(final_edges // args.steps, 1)
+            rows_last = final_rows // args.steps
+            f = min(1.0, rows_last / e_last)
+            w = p1_width or 8
+            lines = 1.0 - (1.0 - f) ** (128 // w)
+            p1_bytes = int(e_last * w * lines)
+            must = stored + p1_bytes
+            line_note = {"p1_width": w, "pass_fraction": round(f, 4), "p1_lines_read": round(lines, 6),
+                         "p1_line_bytes": p1_bytes}
+            final_fix = (must - stored) * launches
+        gbs = lambda b: b / avg_s / 1e9 if avg_s > 0 else 0.0
+        achieved = gbs(must)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": name,
                 "launches": launches, "avg_launch_us": round(ms * 1e3 / max(launches, 1), 2),
-                "algo_bytes_per_launch": algo8, "bytes_model": "SURVEY.md §8d: 24 B / scanned edge + 40 B / row",
+                "algo_bytes_per_launch": must,
+                "bytes_model": "bytes the final hop must move: scanned-edge reads at stored widths (dst, filter "
+                               "column p0; constant rank 0 B) + result rows at written widths + the YIELD-only "
+                               "column p1 at whole 128-B lines",
+                "p1_lines": line_note,
                 # the HBM bytes the PMC counters measured per launch over this launch time: the kernel's
-                # real memory throughput (frac above credits the algorithmic bytes)
+                # real memory throughput
                 "frac_counter": round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 4) if traffic and avg_s > 0 else None,
-                # the same figure with every field at the width it is stored / written at (compact results:
-                # 5 B / scanned edge, 17 B / row at C2, the rank a constant column): the least this layout must move
+                "traffic_over_must": round(traffic / must, 3) if traffic and must else None,
+                # the same launch credited per SURVEY.md §8d (24 B / scanned edge + 40 B / row, every field
+                # 8 B): a TEPS-equivalent credit, above the bytes the kernel moves with narrow columns
+                "frac_8d": round(gbs(algo8) / HBM_PEAK_GBS, 4), "algo_bytes_8d": algo8,
+                # stored widths without the p1 lines (the library's own per-kernel count)
                 "stored_width": {"algo_bytes_per_launch": stored,
-                                 "frac": round(stored / avg_s / 1e9 / HBM_PEAK_GBS, 4) if avg_s > 0 else None,
+                                 "frac": round(gbs(stored) / HBM_PEAK_GBS, 4) if avg_s > 0 else None,
                                  "compact_results": not args.no_compact}}
     all_ms = sum(v[1] for v in hbm.values())
     all_bytes_stored = sum(v[2] for v in hbm.values())
-    all_bytes = all_bytes_stored + (final_fix if roof else 0)
+    all_bytes = all_bytes_stored + final_fix
 
     cpu = None
     if keep_rows:
@@ -351,6 +376,8 @@ def main():
                               "note": "same query with the rows copied to host memory: columnar arrays in "
                                       "page-locked staging (host_columnar), or typed ColumnValue cells"},
             "jit": jit,
+            # every kernel's library byte count (stored widths; a pulled hop credited with what the pull
+            # reads: 9 B per row, not its scanned edges), the final hop as in `roofline`
             "path_roofline": {"algo_bytes": all_bytes, "algo_bytes_stored_width": all_bytes_stored,
                               "kernel_ms": round(all_ms, 3),
                               "frac": round(all_bytes / (all_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if all_ms else None,

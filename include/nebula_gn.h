@@ -379,6 +379,15 @@ void ngx_go_result_free(ngx_go_result* r);
 int32_t ngx_device_to_host(ngx_ctx* ctx, void* dst, const void* src, uint64_t bytes);
 /* Wait until all work issued on the context has completed (result_on_device arrays fully written). */
 int32_t ngx_synchronize(ngx_ctx* ctx);
+/* Order-independent digest of a device-resident GO result (result_on_device), computed on the device
+ * without copying the rows: per row h = m(...m(m(S ^ src) ^ v0)... ^ v(ncols-1)), m = splitmix64's
+ * finalizer, S = 0x9E3779B97F4A7C15, src the row's src vid and v_c the value bits of YIELD column c
+ * (integers sign-extended from their stored width, a constant column's value); out[0] = sum of h mod
+ * 2^64, out[1] = XOR of h, out[2] = rows. Integer / double / bool columns only (NGX_E_UNSUPPORTED for
+ * string or untyped columns). A verification hook: two result multisets of any size compare by their
+ * digests (tests/test_gpu_c3.py checks the 1 G-row C3 results against the generator's edges this way).
+ * Call it before any other call on the context (the result arrays are valid until then). */
+int32_t ngx_go_result_digest(ngx_ctx* ctx, const ngx_go_result* r, uint64_t out[3]);
 
 /* ---------------------------------------------------------------- measurement hooks */
 /* Per-kernel device times of the last ngx_go (HIP events on the engine stream), for bench.py. */

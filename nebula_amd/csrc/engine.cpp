@@ -82,6 +82,15 @@ struct DeviceGraph {
 
 namespace {
 
+// Debugging aid (flag "poison_buffers", process-wide; NGX_POISON=1 sets it at load, for a whole test
+// suite): every device scratch buffer allocated from then on starts as kPoisonByte bytes, so a kernel
+// that reads a word no kernel of the query wrote sees garbage instead of whatever an earlier query left
+// there (tests/test_gpu_poison.py). The fill is ordered before any use: the engine's stream is
+// non-blocking, so a fill on the null stream left running could land after the first copy or kernel
+// that writes the buffer; hence the device synchronisation.
+std::atomic<bool> gPoison{std::getenv("NGX_POISON") != nullptr && std::getenv("NGX_POISON")[0] == '1'};
+constexpr int kPoisonByte = 0xA5;
+
 // growable device buffer
 struct DBuf {
     void* p = nullptr;
@@ -95,6 +104,10 @@ struct DBuf {
             size_t c = std::max(bytes, cap * 3 / 2);
             HIP_OK(hipMalloc(&p, c));
             cap = c;
+            if (gPoison.load(std::memory_order_relaxed)) {
+                HIP_OK(hipMemset(p, kPoisonByte, c));
+                HIP_OK(hipDeviceSynchronize());
+            }
         }
         return static_cast<T*>(p);
     }
@@ -139,7 +152,9 @@ struct ngx_ctx {
     DBuf resvTab, resvCtl;                              // GO final hop: block tables, counters (kargs.h resv*)
     uint64_t resvTabWords = 0;
     uint32_t resvSeq = 0, resvLastG = 0, resvLastStride = 0, resvParity = 0;
-    const uint64_t* resvRows = nullptr;                 // the last GO final launch's row count (device word)
+    const uint64_t* resvRows = nullptr;                 // this query's last GO final launch's row count (device word)
+    uint64_t strArenaMax = uint64_t(8) << 30;           // bytes of one record hop's result string arena (flag str_arena_max)
+    bool resvClosePending = false;                      // counters handed out, their k_final_close not enqueued
     DBuf oFlags, rowCols, rowLen, rowOff, rowBytes;     // GetNeighbors response rows (encode_rows)
     DBuf dkTable, dkKeep, dkPre, dSrc, dDst, dRank, dType;   // YIELD DISTINCT (table, marks, compacted rows)
     std::vector<DBuf> strArena;                         // result string arenas, one per record hop (FinalArgs::strOut)
@@ -190,6 +205,17 @@ struct ngx_ctx {
     int32_t compactLaneRows = 0;                        // compaction rows per lane: 0 = by shard size, else 4 / 8 / 16
     int64_t pullFactor = 200;                           // pull when 100 x hop edges >= pullFactor x shard rows (0: never)
     uint64_t pullHops = 0;
+    // sparse intermediate hops (kernels.h SparseArgs): a push hop with E * sparseFactor <= V builds the next
+    // frontier in the expansion itself (flag "sparse_factor", 0 = never, < 0 = every push hop; read-only
+    // "sparse_hops")
+    int64_t sparseFactor = 16;
+    uint64_t sparseHops = 0;
+    DBuf sparseCtl;                                     // the sparse kernel's counters, kept zero between launches
+    DBuf estart2, ebase2, chunkFirst2;                  // the next hop's entry arrays while the sparse kernel reads this hop's
+    // the frontier bitmap is known to be all zero (a sparse hop's dedup set starts from it): set by a
+    // compaction that wrote zeros, cleared by every other writer
+    bool bitsClean = false;
+    const void* bitsCleanPtr = nullptr;
     // device-driven hops (no host round trip per hop). Off by default: on MI355X the upper-bound grids
     // and the idle launch of the expansion not taken cost what the round trips saved (C2 step: device
     // 680 vs 656 us, profiles/r02_dyn_*); kept as an option ("dyn_hops", NGX_DYN_HOPS=1)
@@ -225,7 +251,7 @@ struct ngx_ctx {
                         &oDst, &oRank, &oType, &oEntry, &chunkFirst, &oColDesc, &progBuf, &sendBits, &recvBits, &resvTab, &resvCtl,
                         &vcells, &misc, &edgeMask, &cmpStatus[0], &cmpStatus[1], &frontierBits, &oFlags, &rowCols, &rowLen,
                         &rowOff, &rowBytes, &pullSeg, &pullCtl, &dkTable, &dkKeep, &dkPre, &dSrc, &dDst, &dRank,
-                        &dType, &dynStats}) b->release();
+                        &dType, &dynStats, &sparseCtl, &estart2, &ebase2, &chunkFirst2}) b->release();
         for (auto& cb : oCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         for (auto& cb : dCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         hostStage.release();
@@ -1523,6 +1549,39 @@ int32_t ngx_synchronize(ngx_ctx* c) {
     return NGX_OK;
 }
 
+int32_t ngx_go_result_digest(ngx_ctx* c, const ngx_go_result* r, uint64_t out[3]) {
+    if (!c || !r || !out) return NGX_E_BAD_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    try {
+        HIP_OK(hipSetDevice(c->device));
+        if (r->code != NGX_OK || (r->nrows && !r->dev_cols && r->ncols)) return fail(c, NGX_E_BAD_ARGUMENT, "digest: not a device-resident result");
+        if (r->ncols > kDigestMaxCols) return fail(c, NGX_E_UNSUPPORTED, "digest: more than 16 YIELD columns");
+        DigestArgs a{};
+        a.n = r->nrows;
+        a.ncols = r->ncols;
+        a.x[0] = r->dev_src;
+        a.w[0] = r->dev_key_w[0];
+        a.c[0] = r->dev_key_const[0];
+        if (a.n && a.w[0] != 0 && !a.x[0]) return fail(c, NGX_E_UNSUPPORTED, "digest: no src row array (yield_only)");
+        for (int32_t k = 0; k < r->ncols; k++) {
+            const ngx_dev_column& dc = r->dev_cols[k];
+            if (dc.len || dc.type) return fail(c, NGX_E_UNSUPPORTED, "digest: string or untyped YIELD column");
+            a.x[k + 1] = dc.x;
+            a.w[k + 1] = r->dev_col_w ? r->dev_col_w[k] : 8;
+            a.c[k + 1] = r->dev_col_const ? r->dev_col_const[k] : 0;
+            if (a.n && a.w[k + 1] != 0 && !dc.x) return fail(c, NGX_E_BAD_ARGUMENT, "digest: column without values");
+        }
+        uint64_t* dev = c->misc.get<uint64_t>(3);
+        a.out = dev;
+        if (launchRowDigest(a, c->stream)) throw Error{NGX_E_DEVICE, "row digest"};
+        HIP_OK(hipMemcpyAsync(out, dev, 24, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipStreamSynchronize(c->stream));
+    } catch (const Error& e) {
+        return fail(c, e.code, e.msg);
+    }
+    return NGX_OK;
+}
+
 int32_t ngx_set_profiling(ngx_ctx* c, int32_t on) {
     std::lock_guard<std::mutex> g(c->mu);
     c->prof = on != 0;
@@ -1543,12 +1602,15 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
     std::lock_guard<std::mutex> g(c->mu);
     std::string n = name ? name : "";
     if (n == "jit") { c->jitOn = value != 0; return NGX_OK; }
+    if (n == "poison_buffers") { gPoison.store(value != 0); return NGX_OK; }
+    if (n == "str_arena_max") { c->strArenaMax = value > 0 ? static_cast<uint64_t>(value) : (uint64_t(8) << 30); return NGX_OK; }
     if (n == "rccl_timeout_ms") { c->rcclTimeoutMs = value < 1 ? 1 : value; return NGX_OK; }
     if (n == "max_edge_returned_per_vertex") { c->maxEdgesPerVertex = value <= 0 ? INT32_MAX : value; return NGX_OK; }
     if (n == "jit_cache_capacity") { c->jit.capacity = value < 1 ? 1 : static_cast<size_t>(value); return NGX_OK; }
     if (n == "pull_factor") { c->pullFactor = value < 0 ? 0 : value; return NGX_OK; }
     if (n == "jit_async") { c->jit.async = value != 0; c->jit.device = c->device; return NGX_OK; }
     if (n == "dyn_hops") { c->dynHops = value != 0; return NGX_OK; }
+    if (n == "sparse_factor") { c->sparseFactor = value < 0 ? -1 : value; return NGX_OK; }
     if (n == "device_libm") { c->deviceLibm = value != 0; return NGX_OK; }
     if (n == "enable_reservoir_sampling") { c->reservoirSampling = value != 0; return NGX_OK; }
     if (n == "narrow_columns") { c->narrowColumns = value != 0; return NGX_OK; }
@@ -1566,6 +1628,8 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     std::lock_guard<std::mutex> g(c->mu);
     std::string n = name ? name : "";
     if (n == "jit") *value = c->jitOn ? 1 : 0;
+    else if (n == "poison_buffers") *value = gPoison.load() ? 1 : 0;
+    else if (n == "str_arena_max") *value = static_cast<int64_t>(c->strArenaMax);
     else if (n == "rccl_timeout_ms") *value = c->rcclTimeoutMs;
     else if (n == "max_edge_returned_per_vertex") *value = c->maxEdgesPerVertex;
     else if (n == "pull_factor") *value = c->pullFactor;
@@ -1577,6 +1641,8 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "trace_go") *value = c->traceGo ? 1 : 0;
     else if (n == "compact_lane_rows") *value = c->compactLaneRows;
     else if (n == "pull_hops") *value = static_cast<int64_t>(c->pullHops);
+    else if (n == "sparse_hops") *value = static_cast<int64_t>(c->sparseHops);
+    else if (n == "sparse_factor") *value = c->sparseFactor;
     else if (n == "pipe_walks") *value = static_cast<int64_t>(c->pipeWalks);
     else if (n == "jit_compiled") *value = static_cast<int64_t>(c->jit.compiled);
     else if (n == "jit_hits") *value = static_cast<int64_t>(c->jit.hits);
@@ -1849,7 +1915,6 @@ void growKeep(ngx_ctx* c, DBuf& b, size_t bytes, size_t keep) {
 // the final kernel's look-back words: ticket / row counter, one status per chunk, the done counter
 // (chunks + 2 words); zeroed by the hop's k_chunk_first launch
 uint64_t lookBackWords(uint64_t chunks) { return chunks + 2; }
-constexpr uint64_t kStrArenaMax = uint64_t(8) << 30;   // bytes of one record hop's result string arena
 uint64_t* lookBack(ngx_ctx* c, uint64_t chunks) { return c->lbStatus.get<uint64_t>(lookBackWords(chunks)); }
 // the GO final hop's block tables (kargs.h kResv*): entries carry the launch's tag, so the table is
 // cleared only when it is (re)allocated
@@ -1872,10 +1937,13 @@ void resvGeometry(ngx_ctx* c, FinalArgs& a) {
     uint64_t* base = static_cast<uint64_t*>(c->resvCtl.p);
     a.resvCtl = base + c->resvParity * words;
     a.resvNext = base + (1 - c->resvParity) * words;
+    // a query that bailed out between the last hand-out and its k_final_close (string-arena limit, a
+    // throw) left this set uncleared: clear it here instead
+    if (c->resvClosePending) HIP_OK(hipMemsetAsync(a.resvCtl, 0, words * 8, c->stream));
+    c->resvClosePending = true;                                 // until launchFinalClose is enqueued
     c->resvParity ^= 1;
     c->resvLastG = a.resvG;
     c->resvLastStride = a.resvStride;
-    c->resvRows = a.resvCtl + (a.resvG + 1) * static_cast<uint64_t>(a.resvStride);
 }
 uint64_t* resvTable(ngx_ctx* c, uint64_t words) {
     if (c->resvTabWords < words || c->resvTab.p == nullptr) {
@@ -2095,6 +2163,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     c->hmark("in");
     RoctxRange queryRange("ngx_go");
     DeviceGraph& d = *sp.dev;
+    c->resvRows = nullptr;                                       // set by this query's final launches only
     const int64_t now = p.now_sec > 0 ? p.now_sec : static_cast<int64_t>(std::time(nullptr));   // WallClock
     GoPlan gp;
     int32_t rc = prepareGo(c, sp, p, gp, in);
@@ -2368,7 +2437,19 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     // (or from the frontier list for the seed frontier); the pull's segment counter is cleared by the
     // compaction after it
     if (!lbCompact) pullable = false;
-    uint64_t* fbits = pullable ? c->frontierBits.get<uint64_t>(vAl / 64 + 1) : nullptr;
+    // sparse hops: one shard (its rows are the global rows), the frontier bitmap as the dedup set
+    const bool sparseOk = c->world == 1 && lbCompact && !rw && c->sparseFactor != 0 && hs.n > 0 && d.gbase == 0 &&
+                          d.vglobal == d.V && d.V < (1ULL << 32);
+    uint64_t* fbits = (pullable || sparseOk) ? c->frontierBits.get<uint64_t>(vAl / 64 + 1) : nullptr;
+    if (sparseOk) {
+        // both sets of entry arrays at full size now: no buffer a kernel of this query reads is regrown later
+        const uint64_t n = d.V * static_cast<uint64_t>(hs.n) + 1;
+        c->estart.get<uint64_t>(n);
+        c->estart2.get<uint64_t>(n);
+        c->ebase.get<uint64_t>(n);
+        c->ebase2.get<uint64_t>(n);
+        c->chunkFirst2.get<uint64_t>(cfCap);
+    }
     // world > 1: the compaction writes this shard's bitmap (local rows), gathered into fbits when a hop
     // pulls; segWords = the largest shard's words (the all-gather block)
     uint64_t segWords = 0;
@@ -2710,10 +2791,10 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             a.nStrOut = nStrOut;
             a.strOutMask = strOutMask;
             if (nStrOut) {
-                // one 64-byte slot per (edge, building column): past kStrArenaMax the caller's CPU path
+                // one 64-byte slot per (edge, building column): past str_arena_max the caller's CPU path
                 // runs the query instead of a device allocation failure
                 const uint64_t arenaBytes = (Ef + resvSlack(a)) * nStrOut * static_cast<uint64_t>(kStrBuildBytes);
-                if (arenaBytes > kStrArenaMax)
+                if (arenaBytes > c->strArenaMax)
                     return fail(c, NGX_E_UNSUPPORTED, "built strings of " + std::to_string(Ef) + " edges exceed the device string arena");
                 if (c->strArena.size() <= arenas.size()) c->strArena.resize(arenas.size() + 1);
                 a.strOut = c->strArena[arenas.size()].get<char>((Ef + resvSlack(a)) * nStrOut * static_cast<uint64_t>(kStrBuildBytes));
@@ -2742,6 +2823,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             c->timed("final_close", 0, [&] {
                 if (launchFinalClose(a, c->stream)) throw Error{NGX_E_DEVICE, "final close"};
             });
+            c->resvClosePending = false;
+            c->resvRows = a.resvCtl + (a.resvG + 1) * static_cast<uint64_t>(a.resvStride);
             if (!dyn) {
                 // GO: the row count and the query's error bits so far, published by k_final_close
                 uint64_t fin = 0;                               // devE: this hop's packed (|F|, E)
@@ -2802,7 +2885,11 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         }
         // the hop's output marks (pull and push alike; the pull reads the frontier from the bitmap)
         uint8_t* const marks = marksA;
+        // sparse: this push hop's expansion builds the next frontier itself (no compaction sweep)
+        const bool sparse = sparseOk && !dyn && !pull && !mask && E > 0 &&
+                            (c->sparseFactor < 0 || static_cast<unsigned __int128>(E) * static_cast<uint64_t>(c->sparseFactor) <= d.V);
         if (pull && !haveBits) {                                // the seed frontier: bitmap from its list
+            c->bitsClean = false;
             HIP_OK(hipMemsetAsync(lbits, 0, (d.V + 63) / 64 * 8, c->stream));
             if (launchMarkBits(F, nF, lbits, c->stream)) throw Error{NGX_E_DEVICE, "mark bits"};
         }
@@ -2842,7 +2929,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                 if (launchExpandRoots(F, nF, hs, rootsCur, rootsNext, marks, ep, c->stream))
                     throw Error{NGX_E_DEVICE, "expand roots"};
             });
-        } else if ((!pull || dyn) && E) {
+        } else if ((!pull || dyn) && E && !sparse) {
             c->timed("expand", dyn ? 0 : E * 8, [&] {
                 if (launchExpandMark(F, estart, chunkFirst, nEnt, E, hs, marks, ep, pos32, c->stream, mask,
                                      dynTotal, dyn ? pullMinE : ~0ULL, ebase))
@@ -2862,7 +2949,50 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         }
         uint32_t* Fn = (F == c->F0.p) ? c->F1.get<uint32_t>(std::max<uint64_t>(d.V, 1)) : c->F0.get<uint32_t>(std::max<uint64_t>(d.V, 1));
         uint64_t* tiles2 = c->tileSums.get<uint64_t>((std::max<uint64_t>(d.V, 1) + kTile - 1) / kTile + 1);
-        if (lbCompact) {
+        if (sparse) {
+            // the bitmap must start all zero: it is the hop's dedup set and then the next frontier's bits
+            if (!c->bitsClean || c->bitsCleanPtr != lbits) HIP_OK(hipMemsetAsync(lbits, 0, (d.V + 63) / 64 * 8, c->stream));
+            c->bitsClean = false;
+            if (!c->sparseCtl.p) {
+                c->sparseCtl.get<uint64_t>(2);
+                HIP_OK(hipMemsetAsync(c->sparseCtl.p, 0, c->sparseCtl.cap, c->stream));
+            }
+            const bool devNext = finalDev && h + 1 == steps;      // the next hop is the device-sized final one
+            SparseArgs sa{};
+            sa.F = F; sa.estart = estart; sa.chunkFirst = chunkFirst; sa.ebase = ebase;
+            sa.nEnt = nEnt; sa.E = E; sa.hs = hs;
+            sa.bits = lbits;
+            sa.outF = Fn;
+            sa.outEst = c->estart2.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
+            sa.outEbase = c->ebase2.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
+            sa.outCf = c->chunkFirst2.get<uint64_t>(cfCap);
+            sa.cfCap = cfCap;
+            sa.ctl = static_cast<uint64_t*>(c->sparseCtl.p);
+            sa.total = devNext ? dynStats + h : counters + 2;
+            sa.pub = devNext ? Publish{nullptr, 0} : nextPub(c);
+            sa.err = errFlag;
+            c->timed("expand_sparse", E * 12, [&] {
+                if (launchExpandSparse(sa, pos32, c->stream)) throw Error{NGX_E_DEVICE, "sparse expand"};
+            });
+            // the next hop reads the arrays just written; this hop's become the spares
+            std::swap(c->estart, c->estart2);
+            std::swap(c->ebase, c->ebase2);
+            std::swap(c->chunkFirst, c->chunkFirst2);
+            haveEstart = true;
+            haveEbase = true;
+            haveHeads = true;
+            haveBits = true;                                    // the bitmap holds exactly the next frontier
+            c->sparseHops++;
+            if (devNext) {
+                nF = d.V;
+                fusedE = slotEdges;
+            } else {
+                uint64_t packed = awaitPub(c, sa.pub, counters + 2);
+                nF = packed >> kFdShift;
+                fusedE = packed & kFdMask;
+                c->addBytes("expand_sparse", nF * (4 + 24 * static_cast<uint64_t>(hs.n)));
+            }
+        } else if (lbCompact) {
             // one launch: next frontier + estart + chunk heads; the look-back words of the next
             // compaction cleared on the way
             CompactArgs ca{};
@@ -2878,7 +3008,11 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             ca.waveSum = cmpWave;
             ca.clear32 = pullable ? pa.ctl : nullptr;
             ca.bits = lbits;
-            haveBits = lbits != nullptr;
+            // a bitmap no hop will read (the next hop is the final one, or no hop pulls) is written as
+            // zeros: a later sparse hop then finds it clean without a memset
+            ca.bitsZero = (h + 1 == steps || !pullable) ? 1 : 0;
+            haveBits = lbits != nullptr && !ca.bitsZero;
+            c->bitsClean = false;
             const bool devNext = finalDev && h + 1 == steps;      // the next hop is the device-sized final one
             ca.total = (dyn || devNext) ? dynStats + h : counters + 2;
             ca.pub = (dyn || devNext) ? Publish{nullptr, 0} : nextPub(c);
@@ -2890,6 +3024,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             c->timed("compact_degrees", 0, [&] {
                 if (launchCompactLb(ca, c->stream)) throw Error{NGX_E_DEVICE, "compact"};
             });
+            if (ca.bits && ca.bitsZero) { c->bitsClean = true; c->bitsCleanPtr = ca.bits; }
             haveEstart = true;
             haveEbase = true;
             haveHeads = true;
@@ -3513,6 +3648,9 @@ extern "C" int32_t ngx_go(ngx_ctx* c, const ngx_go_plan* p, ngx_go_result** out)
     } catch (const Error& e) {
         rc = fail(c, e.code, e.msg);
     }
+    // a failed query may leave kernels enqueued that still read the page-locked seed / program stages
+    // the next call rewrites: drain them first
+    if (rc != NGX_OK) (void)hipStreamSynchronize(c->stream);
     R->r.code = rc;
     R->r.ncols = static_cast<int32_t>(R->colTypes.size());
     R->r.col_types = R->colTypes.data();
@@ -3556,10 +3694,66 @@ void addSchema(GnResultHolder& R, const HostSchemaView& hv) {
     R.schemas.push_back(std::move(s));
 }
 
+// poison_buffers: every word k_encode_rows is about to read, checked on the host first — the row's
+// type and flags, and per prop column of its type the value type, and for a string its length and
+// that the pointer lies in a snapshot string column or the query's literal pool. A word no kernel
+// wrote still holds kPoisonByte bytes and fails here (NGX_E_DEVICE) instead of faulting the encoder.
+void checkEncodeInputs(ngx_ctx* c, const RowEncArgs& e, const std::vector<int32_t>& srcs, uint64_t nrows,
+                       const DeviceGraph& d, const DevPrograms& dp, const std::string& pool) {
+    HIP_OK(hipStreamSynchronize(c->stream));
+    auto fetch = [&](const void* dev, size_t bytes) {
+        std::vector<uint8_t> h(bytes);
+        if (bytes && dev) HIP_OK(hipMemcpy(h.data(), dev, bytes, hipMemcpyDeviceToHost));
+        return h;
+    };
+    auto bad = [&](uint64_t i, const std::string& what) {
+        throw Error{NGX_E_DEVICE, "encode_rows: row " + std::to_string(i) + ": " + what + " (unwritten word)"};
+    };
+    std::vector<uint8_t> ty = fetch(e.oType, nrows * 4), fl = fetch(e.oFlags, e.oFlags ? nrows : 0);
+    const int32_t* type = reinterpret_cast<const int32_t*>(ty.data());
+    struct HostCol { std::vector<uint8_t> x, len, t; };
+    std::map<int32_t, HostCol> cols;
+    for (int32_t s : srcs) {
+        if (s < 0 || cols.count(s)) continue;
+        const OutCol& oc = c->oColView.at(static_cast<size_t>(s));
+        cols[s] = HostCol{fetch(oc.x, nrows * 8), fetch(oc.len, oc.len ? nrows * 4 : 0), fetch(oc.t, oc.t ? nrows : 0)};
+    }
+    const uint64_t pb = reinterpret_cast<uint64_t>(dp.pool);
+    auto knownString = [&](uint64_t p, uint32_t len) {
+        if (len == 0) return true;
+        if (p >= pb && p + len <= pb + pool.size()) return true;
+        for (const auto& r : d.strRanges) if (p >= r.dev && p + len <= r.dev + r.len) return true;
+        return false;
+    };
+    for (uint64_t i = 0; i < nrows; i++) {
+        int sl = -1;
+        for (int s = 0; s < e.nslots; s++) if (e.etype[s] == type[i]) sl = s;
+        if (sl < 0) bad(i, "edge type " + std::to_string(type[i]) + " not requested");
+        const uint8_t f = fl.empty() ? 0 : fl[i];
+        if (f & ~(EF_EMPTY_VALUE | EF_BAD_ROW)) bad(i, "flags " + std::to_string(f));
+        if (f & EF_EMPTY_VALUE) continue;
+        for (int32_t j = e.cbeg[sl]; j < e.cbeg[sl + 1]; j++) {
+            const int32_t s = srcs[static_cast<size_t>(j)];
+            if (s < 0) continue;
+            const HostCol& hc = cols[s];
+            int64_t x;
+            std::memcpy(&x, hc.x.data() + i * 8, 8);
+            const uint8_t t = hc.t.empty() ? V_INT : hc.t[i];
+            uint32_t len = 0;
+            if (!hc.len.empty()) std::memcpy(&len, hc.len.data() + i * 4, 4);
+            const std::string col = "column " + std::to_string(s);
+            if (t != V_INT && t != V_DBL && t != V_BOOL && t != V_STR && t != 0xFF) bad(i, col + " value type " + std::to_string(t));
+            if (t == V_STR && !knownString(static_cast<uint64_t>(x), len))
+                bad(i, col + " string pointer / length " + std::to_string(len));
+        }
+    }
+}
+
 // IdAndProp.props of every returned edge, encoded on the device (kernels.hip k_encode_rows): row
 // lengths, their scan, then the bytes; copied to the result on the context's stream
 void encodeEdgeRows(ngx_ctx* c, const FinalArgs& a, uint64_t nrows,
-                    const std::map<int32_t, std::vector<std::pair<int32_t, int32_t>>>& respCols, GnResultHolder& R) {
+                    const std::map<int32_t, std::vector<std::pair<int32_t, int32_t>>>& respCols, GnResultHolder& R,
+                    const DeviceGraph& d, const DevPrograms& dp, const std::string& pool) {
     RowEncArgs e{};
     e.n = nrows;
     e.oType = a.oType;
@@ -3585,6 +3779,10 @@ void encodeEdgeRows(ngx_ctx* c, const FinalArgs& a, uint64_t nrows,
     HIP_OK(hipMemcpyAsync(drc, srcs.data(), srcs.size() * 4, hipMemcpyHostToDevice, c->stream));
     e.rcSrc = drc;
     e.rcType = drc + types.size();
+    if (gPoison.load(std::memory_order_relaxed)) {
+        checkEncodeInputs(c, e, std::vector<int32_t>(srcs.begin(), srcs.begin() + static_cast<std::ptrdiff_t>(types.size())),
+                          nrows, d, dp, pool);
+    }
     uint64_t* len = c->rowLen.get<uint64_t>(nrows + 1);
     uint64_t* off = c->rowOff.get<uint64_t>(nrows + 1);
     uint64_t* tiles = c->tileSums.get<uint64_t>((nrows + kTile - 1) / kTile + 1);
@@ -3919,7 +4117,7 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
             std::memcpy(R.edgeVertex.data(), ex[0].host, nrows * 4);
             std::memcpy(R.edgeType.data(), ex[1].host, nrows * 4);
             std::memcpy(R.edgeDst.data(), ex[2].host, nrows * 8);
-            if (q.encode_rows) encodeEdgeRows(c, a, nrows, respCols, R);
+            if (q.encode_rows) encodeEdgeRows(c, a, nrows, respCols, R, d, dp, progs.pool);
             HIP_OK(hipStreamSynchronize(c->stream));
             c->hmark("d2h");
             // IdAndProp.dst is set only by a `_dst` return column of the edge type (PropsCollector::
@@ -4008,6 +4206,7 @@ extern "C" int32_t ngx_get_neighbors(ngx_ctx* c, const ngx_gn_request* q, ngx_gn
     } catch (const Error& e) {
         rc = fail(c, e.code, e.msg);
     }
+    if (rc != NGX_OK) (void)hipStreamSynchronize(c->stream);     // as ngx_go: no kernel left reading the stages
     c->hmark("end");
     c->hflush();
     if (rc != NGX_OK) R->r.code = rc;

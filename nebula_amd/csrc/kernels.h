@@ -118,7 +118,37 @@ struct CompactArgs {
     uint8_t epoch;
     uint64_t* bits;                     // optional frontier bitmap of this shard's rows (V / 64 words, rounded up)
     int32_t laneRows;                   // rows per lane, 4 / 8 / 16; 0: the launcher picks by V (kernels.hip)
+    int32_t bitsZero;                   // write every word of `bits` as 0 (no hop reads this frontier's bitmap:
+                                        // the next hop is the final one), leaving it clean for a sparse hop
 };
+// Sparse intermediate hop (world 1, push, E far below the shard's rows): the expansion builds the next
+// frontier itself instead of a compaction sweeping every row (kernels.hip k_expand_sparse). Per edge one
+// 64-bit atomicOr on the frontier bitmap (all zero before the launch) dedups the destination and sets the
+// pull's bitmap; the rows whose bit an edge set are the next frontier. Each workgroup reserves its new
+// rows' places and edge offsets with one packed atomicAdd, so every entry gets estart / ebase / chunk
+// heads without a scan; the last workgroup writes the tail estart[|F| ns] = E, the packed total and its
+// publication, and clears the counters. Frontier order = reservation order (a set: GoExecutor keeps the
+// dsts of a hop in an unordered set too, GoExecutor.cpp:675-718).
+struct SparseArgs {
+    const uint32_t* F;
+    const uint64_t* estart;
+    const uint64_t* chunkFirst;
+    const uint64_t* ebase;              // optional (FinalArgs::ebase)
+    uint64_t nEnt;
+    uint64_t E;
+    HopSlots hs;
+    uint64_t* bits;                     // the shard's frontier bitmap, zero before the launch
+    uint32_t* outF;
+    uint64_t* outEst;                   // next hop: estart, |F| * ns + 1 entries
+    uint64_t* outEbase;                 // next hop: the entries' CSR positions, or null
+    uint64_t* outCf;                    // next hop: chunk heads
+    uint64_t cfCap;
+    uint64_t* ctl;                      // [0] packed (rows << kFdShift | edges) reserved, [1] finished workgroups
+    uint64_t* total;                    // device copy of the packed total
+    Publish pub;
+    uint32_t* err;
+};
+int launchExpandSparse(const SparseArgs& a, bool pos32, hipStream_t s);
 constexpr uint64_t kCompactLbMaxV = 1ULL << (62 - kFdShift);
 constexpr uint64_t kCompactTile = 4096;     // the smallest compaction tile (1024 threads x 4 rows; 8 or 16 per lane on larger shards): sizes the per-tile words
 // GO final kernel words: kargs.h (kResv*, kDoneOff). The seed / compaction kernels clear zero[k * kDoneOff]
@@ -157,6 +187,22 @@ int launchEncodeRows(const RowEncArgs& a, bool write, hipStream_t s);
 int launchScanU64(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* tileSums, hipStream_t s);
 // v[0 .. n) -> exclusive prefix in place, v[n] = total (one 1024-thread workgroup: n up to ~1e6)
 int launchScanInPlace(uint64_t* v, uint64_t n, hipStream_t s);
+
+// ngx_go_result_digest: per row h = mix64(... mix64(mix64(kDigestSeed ^ key) ^ col0) ...) over the row's
+// src vid and each listed column's value bits (integers sign-extended from their width w, or the constant
+// c when w == 0); out[0] += h (mod 2^64), out[1] ^= h, out[2] += rows. Order-independent, so two result
+// multisets compare without a sort (oracle/orc_digest.cpp restates it on the host).
+constexpr int kDigestMaxCols = 16;
+constexpr uint64_t kDigestSeed = 0x9E3779B97F4A7C15ULL;
+struct DigestArgs {
+    uint64_t n;
+    int32_t ncols;                      // columns after the key
+    const void* x[kDigestMaxCols + 1];  // [0] the src vids, then the columns
+    int32_t w[kDigestMaxCols + 1];      // bytes per element, 0: constant
+    int64_t c[kDigestMaxCols + 1];
+    uint64_t* out;                      // 3 words, zeroed by the launcher
+};
+int launchRowDigest(const DigestArgs& a, hipStream_t s);
 
 // k_final_close_cols: the arrays a close moves (kind 0: plain, w bytes; 1: 8-byte string values
 // rebased with their arena slots; 2: 8-byte word w of each row's string-arena block)

@@ -446,7 +446,7 @@ __global__ __launch_bounds__(CWG) void k_compact_count(CompactArgs a) {
             const uint64_t b = __ballot((flags >> k) & 1u);
             if (lane == k) w = b;
         }
-        if (lane < CIT && wbase + static_cast<uint64_t>(lane) * 64 < a.V) a.bits[(wbase >> 6) + lane] = w;
+        if (lane < CIT && wbase + static_cast<uint64_t>(lane) * 64 < a.V) a.bits[(wbase >> 6) + lane] = a.bitsZero ? 0 : w;
     }
     uint64_t packed = (static_cast<uint64_t>(__popc(flags)) << kFdShift) | dsum;
 #pragma unroll
@@ -527,6 +527,106 @@ __global__ __launch_bounds__(CWG) void k_compact_write(CompactArgs a) {
                 writeChunkHeads(a.chunkFirst, a.cfCap, f * ns + s, e, d, a.err);
                 e += d;
             }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------ sparse intermediate hop
+// kernels.h SparseArgs. The same edge-balanced chunk map as k_expand_mark; a destination's first edge
+// (the one whose atomicOr set its bit) makes it a row of the next frontier. Loads are issued for every
+// item and selected afterwards (no load under a divergent branch, see the compaction's note below).
+template <bool ONE, bool P32>
+__global__ __launch_bounds__(WG) void k_expand_sparse(SparseArgs a) {
+    __shared__ ChunkMap<ONE, false, P32> m;
+    __shared__ uint64_t sm[NW + 1];
+    __shared__ uint64_t sBase;
+    const uint32_t chunk = blockIdx.x;
+    const uint64_t base = static_cast<uint64_t>(chunk) * CE;
+    const uint32_t cnt = static_cast<uint32_t>(a.E - base < CE ? a.E - base : CE);
+    buildMap<ONE, false, P32>(a.estart, a.chunkFirst, a.nEnt, chunk, gridDim.x, base, cnt, a.F, a.hs, m, a.ebase);
+    uint32_t g[CITEMS];
+#pragma unroll
+    for (int k = 0; k < CITEMS; k++) {
+        const uint32_t p = threadIdx.x + k * WG;
+        g[k] = kNoRow;
+        if (p < cnt) {
+            const uint32_t q = m.at[p];
+            const int s = ONE ? 0 : m.slot[q];
+            const uint64_t pos = P32 ? static_cast<uint64_t>(static_cast<uint32_t>(base + p) + static_cast<uint32_t>(m.pb[q]))
+                                     : static_cast<uint64_t>(static_cast<int64_t>(base + p) + static_cast<int64_t>(m.pb[q]));
+            g[k] = a.hs.dgid[s][pos];
+        }
+    }
+    uint32_t first = 0;                                  // bit k: item k set its destination's bit
+#pragma unroll
+    for (int k = 0; k < CITEMS; k++) {
+        if (g[k] == kNoRow) continue;
+        const unsigned long long bit = 1ULL << (g[k] & 63);
+        const unsigned long long old = atomicOr(reinterpret_cast<unsigned long long*>(a.bits + (g[k] >> 6)), bit);
+        first |= (old & bit) ? 0u : (1u << k);
+    }
+    uint64_t deg[CITEMS], ob[CITEMS];
+#pragma unroll
+    for (int k = 0; k < CITEMS; k++) {
+        const bool f = (first >> k) & 1u;
+        const uint64_t r = f ? g[k] : 0;
+        if (ONE) {
+            const uint64_t o0 = a.hs.off[0][r], o1 = a.hs.off[0][r + 1];
+            deg[k] = f ? o1 - o0 : 0;
+            ob[k] = o0;
+        } else {
+            const uint64_t d = rowDegree<false>(a.hs, r);
+            deg[k] = f ? d : 0;
+            ob[k] = 0;
+        }
+    }
+    uint64_t mine = 0;
+#pragma unroll
+    for (int k = 0; k < CITEMS; k++) mine += ((first >> k) & 1u) ? ((1ULL << kFdShift) | deg[k]) : 0;
+    uint64_t tot;
+    const uint64_t pre = blockExScan(mine, tot, sm);
+    if (threadIdx.x == 0) {
+        sBase = tot ? static_cast<uint64_t>(atomicAdd(reinterpret_cast<unsigned long long*>(a.ctl),
+                                                      static_cast<unsigned long long>(tot)))
+                    : 0;
+    }
+    __syncthreads();
+    const int ns = a.hs.n;
+    const uint64_t at = sBase + pre;
+    uint64_t f = at >> kFdShift, e = at & kFdMask;
+#pragma unroll
+    for (int k = 0; k < CITEMS; k++) {
+        if (!((first >> k) & 1u)) continue;
+        a.outF[f] = g[k];
+        if (ONE) {
+            a.outEst[f] = e;
+            if (a.outEbase) a.outEbase[f] = ob[k];
+            writeChunkHeads(a.outCf, a.cfCap, f, e, deg[k], a.err);
+            e += deg[k];
+        } else {
+            for (int s = 0; s < ns; s++) {
+                const uint64_t o = a.hs.off[s][g[k]];
+                const uint64_t d = a.hs.off[s][g[k] + 1] - o;
+                a.outEst[f * ns + s] = e;
+                if (a.outEbase) a.outEbase[f * ns + s] = o;
+                writeChunkHeads(a.outCf, a.cfCap, f * ns + s, e, d, a.err);
+                e += d;
+            }
+        }
+        f++;
+    }
+    // the last workgroup to finish writes the totals (every reservation has been made by then)
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const uint64_t done = atomicAdd(reinterpret_cast<unsigned long long*>(a.ctl + 1), 1ULL);
+        if (done == gridDim.x - 1) {
+            __threadfence();
+            const uint64_t t = __hip_atomic_load(a.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            a.outEst[(t >> kFdShift) * static_cast<uint64_t>(ns)] = t & kFdMask;
+            *a.total = t;
+            a.ctl[0] = 0;
+            a.ctl[1] = 0;
+            if (a.pub.slot) publishWords(a.pub.slot, a.pub.seq, t, 0);
         }
     }
 }
@@ -1265,6 +1365,48 @@ __global__ void k_encode_rows(RowEncArgs a, int write) {
     rowCord(a, i, sl, ws, offs, nb);
 }
 
+// ------------------------------------------------------------------------------ result digest
+__device__ __forceinline__ uint64_t digestMix(uint64_t z) {        // splitmix64's finalizer
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+
+// a grid-stride pass over the rows; per wave one atomic per word
+__global__ __launch_bounds__(256) void k_row_digest(DigestArgs a) {
+    uint64_t sum = 0, x = 0, cnt = 0;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+        uint64_t h = kDigestSeed;
+        for (int k = 0; k <= a.ncols; k++) {
+            const int64_t v = a.w[k] == 0 ? a.c[k] : loadW(a.x[k], a.w[k], i);
+            h = digestMix(h ^ static_cast<uint64_t>(v));
+        }
+        sum += h;
+        x ^= h;
+        cnt++;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        sum += __shfl_xor(sum, o, 64);
+        x ^= __shfl_xor(x, o, 64);
+        cnt += __shfl_xor(cnt, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0 && cnt) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(a.out), static_cast<unsigned long long>(sum));
+        atomicXor(reinterpret_cast<unsigned long long*>(a.out + 1), static_cast<unsigned long long>(x));
+        atomicAdd(reinterpret_cast<unsigned long long*>(a.out + 2), static_cast<unsigned long long>(cnt));
+    }
+}
+
+int launchRowDigest(const DigestArgs& a, hipStream_t s) {
+    if (hipMemsetAsync(a.out, 0, 24, s) != hipSuccess) return 1;
+    if (a.n == 0) return 0;
+    const uint64_t blocks = std::min<uint64_t>((a.n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_row_digest, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, a);
+    return static_cast<int>(hipGetLastError());
+}
+
 struct ArrIn {
     const uint64_t* v;
     __device__ __forceinline__ uint64_t operator()(uint64_t i) const { return v[i]; }
@@ -1335,6 +1477,16 @@ int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst
     uint64_t n = nEnt > nzero ? nEnt : nzero;
     hipLaunchKernelGGL(k_chunk_first, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, estart, nEnt, chunkFirst,
                        zero, nzero);
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchExpandSparse(const SparseArgs& a, bool pos32, hipStream_t s) {
+    if (a.E == 0) return 1;                              // the host handles an empty hop
+    const dim3 grid(static_cast<unsigned>((a.E + CE - 1) / CE));
+    if (a.hs.n == 1 && pos32) hipLaunchKernelGGL((k_expand_sparse<true, true>), grid, dim3(WG), 0, s, a);
+    else if (a.hs.n == 1) hipLaunchKernelGGL((k_expand_sparse<true, false>), grid, dim3(WG), 0, s, a);
+    else if (pos32) hipLaunchKernelGGL((k_expand_sparse<false, true>), grid, dim3(WG), 0, s, a);
+    else hipLaunchKernelGGL((k_expand_sparse<false, false>), grid, dim3(WG), 0, s, a);
     return static_cast<int>(hipGetLastError());
 }
 

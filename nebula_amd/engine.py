@@ -185,6 +185,7 @@ SIGNATURES = {
     "ngx_go_result_free": (None, [P(GoResultC)]),
     "ngx_set_profiling": (c_i32, [ctypes.c_void_p, c_i32]),
     "ngx_synchronize": (c_i32, [ctypes.c_void_p]),
+    "ngx_go_result_digest": (c_i32, [ctypes.c_void_p, P(GoResultC), P(c_u64)]),
     "ngx_stats": (c_i32, [ctypes.c_void_p, P(P(Stat)), P(c_i32)]),
     "ngx_kernel_stats": (c_i32, [ctypes.c_void_p, P(P(KernelStat)), P(c_i32)]),
     "ngx_set_flag": (c_i32, [ctypes.c_void_p, ctypes.c_char_p, c_i64]),
@@ -304,6 +305,7 @@ class GoResult:
     dev_widths: Optional[tuple] = None
     dev_consts: Optional[tuple] = None       # (key values, column values) of width-0 (constant) columns
     digests: object = None               # columnar + digest_fn: whatever digest_fn returned
+    device_digest: Optional[tuple] = None  # on_device + device_digest: (sum, xor, rows) of the row hashes
     host_prep_ms: float = 0.0            # library host time before the first launch / after the device
     host_tail_ms: float = 0.0
 
@@ -494,7 +496,7 @@ class Engine:
     def go(self, space: int, s: Union[str, ngql.GoSentence], pushdown: bool = True, now_sec: int = 0,
            raise_on_error: bool = False, rows: bool = True, on_device: bool = False, fetch: bool = False,
            columnar: bool = False, digest_fn=None, arrays: bool = True, input=None,
-           yield_only: bool = False, compact: bool = False) -> GoResult:
+           yield_only: bool = False, compact: bool = False, device_digest: bool = False) -> GoResult:
         """Run one GO. rows=False skips decoding cells into Python tuples; on_device=True leaves the
         result rows in HBM (GoResult.nrows and the statistics only); with fetch=True the HBM arrays
         (src/dst/rank/type and the columnar YIELD columns) are copied back into the result.
@@ -504,6 +506,8 @@ class Engine:
         before the result is freed (tests: large-result comparison). FROM $-.col / $var.col reads
         `input' (a nebula_amd.pipeline.Interim; None: no input, no rows). yield_only (with on_device):
         only the YIELD columns are materialised; src / dst / rank arrays only where a column aliases them.
+        device_digest (with on_device): GoResult.device_digest = (sum, xor, rows) of the row hashes, computed
+        on the device (ngx_go_result_digest; oracle.row_digest restates it).
         compact (with on_device): integer result arrays at the widths of the stored columns they copy
         (ngx_go_plan.compact_results); fetch widens them back to int64 (GoResult.dev_widths keeps them)."""
         if isinstance(s, PreparedGo):                       # its own pushdown / result-placement flags
@@ -540,6 +544,12 @@ class Engine:
                     # width 0: a constant column (value in dev_key_const / dev_col_const, no array)
                     res.dev_widths = (r.dev_key_w[:3], r.dev_col_w[:nc] if nc else [])
                     res.dev_consts = (r.dev_key_const[:3], r.dev_col_const[:nc] if nc and r.dev_col_const else [0] * nc)
+                if device_digest and rc == 0:
+                    d3 = (c_u64 * 3)()
+                    drc = self.L.ngx_go_result_digest(self.h, out, d3)
+                    if drc:
+                        raise EngineError(drc, self.L.ngx_last_error(self.h).decode())
+                    res.device_digest = (int(d3[0]), int(d3[1]), int(d3[2]))
                 if fetch and rc == 0:
                     kw = res.dev_widths[0] if res.dev_widths else [8, 8, 8]
                     cw = res.dev_widths[1] if res.dev_widths else [8] * r.ncols

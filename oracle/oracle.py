@@ -68,6 +68,8 @@ def lib():
         L.orc_row_read.restype = vp
         L.orc_row_schema_ver.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
         L.orc_row_schema_ver.restype = ctypes.c_int32
+        L.orc_hop_digest.argtypes = [ctypes.c_uint64, vp, vp, vp, vp, vp, vp, ctypes.c_int64, ctypes.c_int32, u64p]
+        L.orc_row_digest.argtypes = [ctypes.c_uint64, ctypes.c_int32, ctypes.POINTER(vp), u64p]
         L.orc_digest_columns.argtypes = [ctypes.c_int32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.orc_gen_buckets.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]
@@ -415,3 +417,30 @@ class Oracle:
         secs = r.get("d")
         names_out = [r.str().decode() for _ in range(r.get("i"))]
         return GoResult(ok, err, types, out, fr, sc, secs, nrows, dig, names_out)
+
+
+def hop_digest(rows, vid, off, dst, p0, p1, rank=0, threads=1):
+    """Expected (sum, xor, rows) row-hash digests of a record hop's result rows (src, dst, rank, p0, p1)
+    over the out-edges of frontier rows `rows` of a generated CSR shard, for no filter, p0 < 50 and
+    p0 >= 50 (orc_digest.cpp; compared with ngx_go_result_digest of the device result)."""
+    import numpy as np
+    rows = np.ascontiguousarray(rows, dtype=np.int64)
+    vid = np.ascontiguousarray(vid, dtype=np.int64)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    dst = np.ascontiguousarray(dst, dtype=np.int64)
+    p0 = np.ascontiguousarray(p0, dtype=np.int8)
+    p1 = np.ascontiguousarray(p1, dtype=np.int64)
+    out = (ctypes.c_uint64 * 9)()
+    lib().orc_hop_digest(len(rows), rows.ctypes.data, vid.ctypes.data, off.ctypes.data, dst.ctypes.data,
+                         p0.ctypes.data, p1.ctypes.data, int(rank), int(threads), out)
+    return {"all": tuple(out[0:3]), "lt": tuple(out[3:6]), "ge": tuple(out[6:9])}
+
+
+def row_digest(cols):
+    """(sum, xor, rows) of the row hashes of equal-length int64 columns (the first is the src vid)."""
+    import numpy as np
+    cols = [np.ascontiguousarray(c, dtype=np.int64) for c in cols]
+    ptrs = (ctypes.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
+    out = (ctypes.c_uint64 * 3)()
+    lib().orc_row_digest(len(cols[0]) if cols else 0, len(cols), ptrs, out)
+    return tuple(out)

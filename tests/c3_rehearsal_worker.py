@@ -14,7 +14,11 @@ result is checked through properties that hold at any size:
     all-gathered over gloo);
   * without WHERE every scanned edge of the last hop is a row;
   * `WHERE e.p0 < 50` and `WHERE e.p0 >= 50` partition those rows;
-  * every rank takes the same pull decisions (the parent checks that at least one hop pulled).
+  * every rank takes the same pull decisions (the parent checks that at least one hop pulled);
+  * the rows themselves: an order-independent digest (sum and XOR of a 64-bit hash of every row's
+    (src, dst, rank, p0, p1)) of the device result, computed on the device (ngx_go_result_digest), equals
+    the digest of the rows the generator's edges give (oracle.hop_digest over the out-edges of the last
+    hop's frontier rows, filtered by p0), per filter; the parent compares the sums over the shards.
 
 Usage: python tests/c3_rehearsal_worker.py RANK WORLD PORT OUT.json SCALE [out|in] [pull_factor]
 """
@@ -43,6 +47,7 @@ def main():
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
                             timeout=datetime.timedelta(seconds=1800))
     from nebula_amd import datagen, engine, ngql
+    from oracle import oracle
 
     threads = max(1, int(os.environ.get("NGX_HOST_THREADS", "2")))
     res = {"rank": rank}
@@ -55,10 +60,12 @@ def main():
     c = datagen.rmat_csr_build(scale, prefix, rank, world, world, with_in=with_in, threads=threads)
     res["gen_s"] = time.time() - t0
     # the shard's distinct out-edges for the host BFS (independent of the engine): vid -> out-list
-    etype, off, dst, _ = next(s for s in c.slots if s[0] == datagen.RMAT_EDGE)
+    etype, off, dst, props = next(s for s in c.slots if s[0] == datagen.RMAT_EDGE)
     vid = c.vid.copy()
     off = off.copy()
     odst = dst.copy()
+    op0 = props[0].astype(np.int8)                   # p0 in 0..99
+    op1 = props[1].copy()
     log(rank, f"generated {c.nv} vertex rows, {[len(s[2]) for s in c.slots]} edges per slot in {res['gen_s']:.1f}s")
 
     e = engine.Engine(0, rank, world, exchange=engine.dist_exchange())
@@ -84,10 +91,11 @@ def main():
         pulls = e.get_flag("pull_hops")
         t = time.time()
         r = e.go(datagen.RMAT_SPACE, ngql.parse_go(QUERY.replace("{S}", S).replace("{W}", w)), on_device=True,
-                 compact=True)
+                 compact=True, device_digest=True)
         res[name] = {"ok": r.ok, "error": r.error, "nrows": r.nrows, "hop_edges": list(r.hop_edges),
                      "hop_xchg": list(r.hop_xchg), "pull_hops": e.get_flag("pull_hops") - pulls,
-                     "ms": (time.time() - t) * 1e3}
+                     "ms": (time.time() - t) * 1e3,
+                     "digest": [str(x) for x in r.device_digest] if r.device_digest else None}
         log(rank, name, res[name])
     e.close()
 
@@ -105,6 +113,10 @@ def main():
         lo, hi = off[rows].astype(np.int64), off[rows + 1].astype(np.int64)
         bfs.append(int((hi - lo).sum()))
         if h == 2:
+            # the last hop's rows: every out-edge of this shard's frontier rows, hashed as the device
+            # hashes its result rows (src, dst, rank 0, p0, p1), per filter
+            dg = oracle.hop_digest(rows, vid, off, odst, op0, op1, 0, threads)
+            res["host_digest"] = {k: [str(x) for x in v] for k, v in dg.items()}
             break
         lens = hi - lo
         nz = lens > 0

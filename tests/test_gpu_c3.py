@@ -8,7 +8,9 @@ the all-gathered frontier bitmap (k_repack_bits). Reference placement: CreateSpa
 
 No oracle holds 2.1 G edges, so the worker checks properties that hold at any size (its docstring):
 per-hop scan sums == a host BFS over the generator's out-edges, unfiltered rows == last-hop edges,
-`p0 < 50` / `p0 >= 50` partition them, the same pull decisions on every rank, and at least one pull.
+`p0 < 50` / `p0 >= 50` partition them, the same pull decisions on every rank, and at least one pull —
+and the values: the device result's row-multiset digest (ngx_go_result_digest) equals the digest of
+the rows the generator's edges give (oracle.hop_digest), for each filter, summed over the shards.
 The shards are bulk-loaded (ngx_load_csr): tests/test_multishard.py checks at world 8 that this load
 and the KV-row export give the oracle's rows.
 """
@@ -79,6 +81,16 @@ def run_c3(outdir, world=WORLD, scale=SCALE, layout="in", pull_factor=-1, timeou
                       "hop_xchg_rank0": rs[0][name]["hop_xchg"],
                       "pull_hops": [r[name]["pull_hops"] for r in rs],
                       "ms_max": round(max(r[name]["ms"] for r in rs), 1)}
+    M = (1 << 64) - 1
+
+    def total(ds):                                  # the shards' digests merged: sums, XORs, row counts
+        s_, x_, n_ = 0, 0, 0
+        for d in ds:
+            s_, x_, n_ = (s_ + int(d[0])) & M, x_ ^ int(d[1]), n_ + int(d[2])
+        return [str(s_), str(x_), str(n_)]
+    for name in ("lt", "ge", "all"):
+        summ[name]["device_digest"] = total(r[name]["digest"] for r in rs)
+        summ[name]["host_digest"] = total(r["host_digest"][name] for r in rs)
     bfs = [sum(r["bfs_hop_edges"][h] for r in rs) for h in range(3)]
     summ["host_bfs_hop_edges"] = bfs
     checks = {
@@ -88,6 +100,10 @@ def run_c3(outdir, world=WORLD, scale=SCALE, layout="in", pull_factor=-1, timeou
         "both sides non-empty": summ["lt"]["nrows"] > 0 and summ["ge"]["nrows"] > 0,
         "same pull decisions on every rank": all(len(set(summ[n]["pull_hops"])) == 1 for n in ("lt", "ge", "all")),
         "a hop pulled at world > 1": layout != "in" or all(summ[n]["pull_hops"][0] >= 1 for n in ("lt", "ge", "all")),
+        # value parity at size: the rows' multiset digest, device vs the generator's edges
+        "row digests == generator's rows": all(summ[n]["device_digest"] == summ[n]["host_digest"]
+                                               for n in ("lt", "ge", "all")),
+        "digest row counts == nrows": all(int(summ[n]["device_digest"][2]) == summ[n]["nrows"] for n in ("lt", "ge", "all")),
     }
     summ["checks"] = checks
     with open(os.path.join(outdir, "summary.json"), "w") as f:

@@ -92,3 +92,52 @@ def test_trace_go_logs_every_step(nba, capfd):
         assert f"scanned edges {edges}," in ln
     e.go(ds.space, s)
     assert "trace_go" not in capfd.readouterr().err
+
+
+def _rows(r):
+    return sorted(fixtures.normalize_cells(r.rows), key=repr)
+
+
+def test_query_over_string_arena_limit_then_normal_queries(nba):
+    """A GO whose built strings exceed the device string arena (flag str_arena_max, 8 GiB by default)
+    fails with NGX_E_UNSUPPORTED after the row reservation counters were handed out (its final launch
+    never runs). The next queries on the same context must start from clean counters: each equals the
+    oracle (a stale counter set made blocks allocate past the outputs)."""
+    ds, o, e = nba
+    built = ngql.parse_go(fixtures.nba_query(
+        "GO 2 STEPS FROM {P:Tim Duncan}, {P:Tony Parker} OVER like YIELD (string)like.likeness AS s, like._dst"))
+    plain = ngql.parse_go(fixtures.nba_query(GO))
+    for _ in range(3):
+        e.set_flag("str_arena_max", 64)
+        try:
+            with pytest.raises(engine.EngineError) as x:
+                e.go(ds.space, built)
+            assert x.value.code == engine.E_UNSUPPORTED and "string arena" in str(x.value)
+        finally:
+            e.set_flag("str_arena_max", 0)
+        for s in (plain, built):
+            ref, got = o.go(ds.space, s), e.go(ds.space, s)
+            assert ref.ok and got.ok and got.rows
+            assert _rows(got) == _rows(ref)
+
+
+def test_dyn_hops_over_type_without_edges_after_rows():
+    """Device-driven hops (flag dyn_hops) over an edge type that has no edges: no final launch runs, so
+    the row count must be this query's 0, not the count of the query before it."""
+    ds = fixtures.nba()
+    ds.schemas.append(fixtures.SchemaDef(True, 99, "vacant", [("w", fixtures.INT)]))
+    o = oracle.Oracle()
+    ds.load_oracle(o)
+    with engine.Engine(0) as e:
+        ds.load_engine(e)
+        e.set_flag("dyn_hops", 1)
+        full = ngql.parse_go(fixtures.nba_query("GO 2 STEPS FROM {P:Tim Duncan} OVER like YIELD like._dst"))
+        empty = ngql.parse_go(fixtures.nba_query("GO 2 STEPS FROM {P:Tim Duncan} OVER vacant YIELD vacant._dst"))
+        for _ in range(2):
+            got = e.go(ds.space, full)
+            assert got.ok and _rows(got) == _rows(o.go(ds.space, full)) and got.rows
+            got = e.go(ds.space, empty)
+            assert got.ok and got.rows == [] and o.go(ds.space, empty).rows == []
+            dev = e.go(ds.space, empty, on_device=True)
+            assert dev.ok and dev.nrows == 0
+    o.close()

@@ -12,6 +12,7 @@ Results are compared sorted (verifyResult, src/graph/test/TestBase.h:188-233); i
 doubles bit-exact.
 """
 
+import numpy as np
 import pytest
 
 from nebula_amd import datagen, engine, ngql
@@ -422,3 +423,21 @@ def test_snb_compound(snb, qi, pushdown):
         return
     assert got.col_types == ref.col_types
     assert fixtures.normalize_cells(got.rows) == fixtures.normalize_cells(ref.rows)
+
+
+@pytest.mark.parametrize("compact", [True, False])
+def test_rmat_device_digest_matches_oracle_rows(rmat, compact):
+    """ngx_go_result_digest (the device reduction that pins C3's rows by value) over a device-resident
+    result equals the oracle restatement's row hash of the oracle's own rows; with a narrowed / constant
+    column layout (compact) and at 8 bytes."""
+    ds, o, e = rmat
+    seeds = datagen.sample_vids(4242, 1 << ds.scale, 60)
+    for where in ("", " WHERE e.p0 < 50", " WHERE e.p0 >= 50"):
+        q = f"GO 3 STEPS FROM {', '.join(str(int(v)) for v in seeds)} OVER e{where} YIELD e._src, e._dst, e._rank, e.p0, e.p1"
+        s = ngql.parse_go(q)
+        ref = o.go(ds.space, s)
+        got = e.go(ds.space, s, on_device=True, compact=compact, device_digest=True)
+        assert ref.ok and got.ok and got.nrows == len(ref.rows) > 0
+        cols = [np.array([int(r[k][1]) for r in ref.rows], dtype=np.int64) for k in range(5)]
+        # the device hashes the row's src vid, then every YIELD column (here e._src again)
+        assert got.device_digest == oracle.row_digest([cols[0]] + cols)
