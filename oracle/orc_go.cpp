@@ -139,6 +139,11 @@ struct GoExec {
 
     GoExec(const StorageEngine& e, GraphSpaceID sp, const GoSentence& sent, GoFlags f)
         : eng(e), sm(e.schemas), space(sp), s(sent), flags(f) {}
+    ~GoExec() {
+        auto t = std::chrono::steady_clock::now();
+        records.clear();
+        trace("teardown", t);
+    }
 
     bool fail(const std::string& msg) {
         res.ok = false; res.error = msg; res.rows.clear(); res.digests.clear(); res.rowCount = 0;
@@ -285,7 +290,9 @@ struct GoExec {
             auto returns = getStepOutProps();
             std::string pushed;
             if (flags.filter_pushdown && isFinalStep() && s.direction == 0) pushed = filterPushdown;
+            auto tr = std::chrono::steady_clock::now();
             auto req = makeRequest(starts);
+            trace("request", tr);
             req.edge_types = edgeTypes;
             req.filter = pushed;
             req.return_columns = returns;
@@ -306,6 +313,32 @@ struct GoExec {
             const bool track = !isFinalStep() && steps != 1 && s.fromType != 0;
             std::unordered_set<VertexID> set;
             std::set<std::pair<VertexID, VertexID>> curBackTrace;
+            const int T = flags.threads;
+            if (!track && T > 1 && records.back().vertices.size() >= 1024) {
+                // the same set on every thread: thread t inserts the dsts whose hash falls in its
+                // partition (each reads every edge, inserts 1/T of them); the union is the frontier
+                std::vector<std::unordered_set<VertexID>> sets(T);
+                std::vector<std::thread> ts;
+                for (int t = 0; t < T; t++) {
+                    ts.emplace_back([&, t] {
+                        for (auto& vd : records.back().vertices)
+                            for (auto& ed : vd.edge_data)
+                                for (auto& e : ed.edges)
+                                    if (std::hash<VertexID>()(e.dst) % T == static_cast<size_t>(t)) sets[t].insert(e.dst);
+                    });
+                }
+                for (auto& th : ts) th.join();
+                trace("frontier", tq);
+                if (isFinalStep()) return true;
+                starts.clear();
+                for (auto& st : sets) starts.insert(starts.end(), st.begin(), st.end());
+                if (starts.empty()) {
+                    if (!isRecord()) { records.clear(); return true; }
+                    return true;
+                }
+                curStep++;
+                continue;
+            }
             for (auto& vd : records.back().vertices)
                 for (auto& ed : vd.edge_data)
                     for (auto& e : ed.edges) {
@@ -619,7 +652,7 @@ struct GoExec {
         auto tf = std::chrono::steady_clock::now();
         processFinalResult();
         trace("final", tf);
-        return res;
+        return std::move(res);                                         // a member: not copied (7 M rows at C2)
     }
 };
 
