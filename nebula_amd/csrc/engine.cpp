@@ -212,6 +212,11 @@ struct ngx_ctx {
     uint64_t sparseHops = 0;
     DBuf sparseCtl;                                     // the sparse kernel's counters, kept zero between launches
     DBuf estart2, ebase2, chunkFirst2;                  // the next hop's entry arrays while the sparse kernel reads this hop's
+    // world > 1 push hops: frontier exchanged as vid lists instead of bitmaps (flag "xchg_lists": -1 by the
+    // hop's size, 0 bitmaps, 1 lists; read-only "xchg_list_hops")
+    int64_t xchgLists = -1;
+    uint64_t xchgListHops = 0;
+    DBuf xListSend, xListRecv, xCounts;
     // the frontier bitmap is known to be all zero (a sparse hop's dedup set starts from it): set by a
     // compaction that wrote zeros, cleared by every other writer
     bool bitsClean = false;
@@ -251,7 +256,8 @@ struct ngx_ctx {
                         &oDst, &oRank, &oType, &oEntry, &chunkFirst, &oColDesc, &progBuf, &sendBits, &recvBits, &resvTab, &resvCtl,
                         &vcells, &misc, &edgeMask, &cmpStatus[0], &cmpStatus[1], &frontierBits, &oFlags, &rowCols, &rowLen,
                         &rowOff, &rowBytes, &pullSeg, &pullCtl, &dkTable, &dkKeep, &dkPre, &dSrc, &dDst, &dRank,
-                        &dType, &dynStats, &sparseCtl, &estart2, &ebase2, &chunkFirst2}) b->release();
+                        &dType, &dynStats, &sparseCtl, &estart2, &ebase2, &chunkFirst2, &xListSend, &xListRecv,
+                        &xCounts}) b->release();
         for (auto& cb : oCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         for (auto& cb : dCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         hostStage.release();
@@ -1611,6 +1617,7 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
     if (n == "jit_async") { c->jit.async = value != 0; c->jit.device = c->device; return NGX_OK; }
     if (n == "dyn_hops") { c->dynHops = value != 0; return NGX_OK; }
     if (n == "sparse_factor") { c->sparseFactor = value < 0 ? -1 : value; return NGX_OK; }
+    if (n == "xchg_lists") { c->xchgLists = value < 0 ? -1 : (value ? 1 : 0); return NGX_OK; }
     if (n == "device_libm") { c->deviceLibm = value != 0; return NGX_OK; }
     if (n == "enable_reservoir_sampling") { c->reservoirSampling = value != 0; return NGX_OK; }
     if (n == "narrow_columns") { c->narrowColumns = value != 0; return NGX_OK; }
@@ -1642,6 +1649,8 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "compact_lane_rows") *value = c->compactLaneRows;
     else if (n == "pull_hops") *value = static_cast<int64_t>(c->pullHops);
     else if (n == "sparse_hops") *value = static_cast<int64_t>(c->sparseHops);
+    else if (n == "xchg_lists") *value = c->xchgLists;
+    else if (n == "xchg_list_hops") *value = static_cast<int64_t>(c->xchgListHops);
     else if (n == "sparse_factor") *value = c->sparseFactor;
     else if (n == "pipe_walks") *value = static_cast<int64_t>(c->pipeWalks);
     else if (n == "jit_compiled") *value = static_cast<int64_t>(c->jit.compiled);
@@ -1860,6 +1869,77 @@ void exchangeFrontier(ngx_ctx* c, const DeviceGraph& d, uint8_t epoch) {
     }
     xa.bits = recv;
     if (launchMergePeers(xa, c->stream)) throw Error{NGX_E_DEVICE, "merge"};
+}
+
+// The list form (for hops whose frontier is small next to the peers' rows; StorageClient
+// groups a request's vids per host the same way, StorageClient.h:260-290): every shard lists the rows
+// it marked in each peer's range, the shards all-gather their per-peer counts (W words each, so every
+// rank knows what it sends and receives), then send exactly those vids (4 B each) and each owner marks
+// the rows it received. Bytes per hop: 4 x the marked peer rows + the counts, against V / 8 per peer
+// for the bitmaps.
+void exchangeFrontierList(ngx_ctx* c, const DeviceGraph& d, uint8_t epoch) {
+    const int W = c->world;
+    const auto& sb = d.shardBase;
+    uint64_t cap = 1;
+    for (int q = 0; q < W; q++) cap = std::max<uint64_t>(cap, sb[q + 1] - sb[q]);
+    uint32_t* send = c->xListSend.get<uint32_t>(cap * W);
+    unsigned long long* counts = c->xCounts.get<unsigned long long>(static_cast<size_t>(W) * (W + 1));
+    unsigned long long* all = counts + W;
+    HIP_OK(hipMemsetAsync(counts, 0, W * 8, c->stream));
+    ListXchgArgs la{};
+    la.visited = c->visited.get<uint8_t>(d.vglobal);
+    la.epoch = epoch;
+    for (int q = 0; q <= W; q++) la.sb[q] = sb[q];
+    la.world = W;
+    la.rank = c->rank;
+    la.list = send;
+    la.cap = cap;
+    la.counts = counts;
+    if (launchPackLists(la, c->stream)) throw Error{NGX_E_DEVICE, "pack lists"};
+    allGather(c, counts, all, static_cast<uint64_t>(W) * 8);         // all[p * W + q]: p sends q
+    std::vector<uint64_t> m(static_cast<size_t>(W) * W);
+    HIP_OK(hipMemcpyAsync(m.data(), all, m.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    std::vector<uint64_t> roff(W + 1, 0);                              // received list q at roff[q]
+    uint64_t block = 0;
+    for (int q = 0; q < W; q++) {
+        roff[q + 1] = roff[q] + (q == c->rank ? 0 : m[static_cast<size_t>(q) * W + c->rank]);
+        for (int p = 0; p < W; p++) if (p != q) block = std::max<uint64_t>(block, m[static_cast<size_t>(p) * W + q]);
+    }
+    uint32_t* recv = c->xListRecv.get<uint32_t>(std::max<uint64_t>(roff[W], 1));
+    c->lastXchgBytes = static_cast<uint64_t>(W - 1) * W * 8;
+    for (int q = 0; q < W; q++) if (q != c->rank) c->lastXchgBytes += m[static_cast<size_t>(c->rank) * W + q] * 4;
+    if (c->xchg) {
+        // the host collective moves equal blocks: every list padded to the largest count of any pair
+        if (block) {
+            std::vector<uint32_t> hs(block * W, 0), hr(block * W, 0);
+            for (int q = 0; q < W; q++) {
+                const uint64_t n = q == c->rank ? 0 : m[static_cast<size_t>(c->rank) * W + q];
+                if (n) HIP_OK(hipMemcpyAsync(hs.data() + q * block, send + q * cap, n * 4, hipMemcpyDeviceToHost, c->stream));
+            }
+            HIP_OK(hipStreamSynchronize(c->stream));
+            if (c->xchg(c->xchgUser, NGX_XCHG_ALLTOALL, hs.data(), hr.data(), block * 4) != 0)
+                throw Error{NGX_E_DEVICE, "host exchange failed"};
+            std::vector<uint32_t> packed(std::max<uint64_t>(roff[W], 1));
+            for (int q = 0; q < W; q++)
+                std::copy(hr.begin() + q * block, hr.begin() + q * block + (roff[q + 1] - roff[q]), packed.begin() + roff[q]);
+            if (roff[W]) HIP_OK(hipMemcpyAsync(recv, packed.data(), roff[W] * 4, hipMemcpyHostToDevice, c->stream));
+            HIP_OK(hipStreamSynchronize(c->stream));
+        }
+    } else {
+        NCCL_OK(ncclGroupStart());
+        for (int q = 0; q < W; q++) {
+            if (q == c->rank) continue;
+            const uint64_t ns = m[static_cast<size_t>(c->rank) * W + q], nr = roff[q + 1] - roff[q];
+            if (ns) NCCL_OK(ncclSend(send + q * cap, ns * 4, ncclUint8, q, c->comm, c->stream));
+            if (nr) NCCL_OK(ncclRecv(recv + roff[q], nr * 4, ncclUint8, q, c->comm, c->stream));
+        }
+        NCCL_OK(ncclGroupEnd());
+        rcclWait(c, "frontier vid lists");
+    }
+    if (launchMergeList(recv, roff[W], c->visited.get<uint8_t>(d.vglobal) + d.gbase, epoch, c->stream))
+        throw Error{NGX_E_DEVICE, "merge lists"};
+    c->xchgListHops++;
 }
 
 // multi-root walk at world > 1: the expansion OR-ed root sets into next[] over global rows; every
@@ -2868,6 +2948,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         // (TTL / max-edges) decides which edges count
         // dyn: both expansions are enqueued and the device takes the one its E selects (pullMinE)
         bool pull = dyn ? pullable : pullable && !mask && E && E * 100 >= static_cast<uint64_t>(c->pullFactor) * d.V;
+        uint64_t eMaxShard = 0;                                  // the largest shard's E (from the pull gather)
+        bool eMaxKnown = false;
         if (!dyn && pullGather) {
             // the hop's edges over every shard, whether every shard can pull (its pull state built, no
             // storage mask) and rank 0's pull_factor (one threshold for all)
@@ -2878,10 +2960,12 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                 uint64_t r[3];
                 std::memcpy(r, all.data() + w * sizeof(rec), sizeof(rec));
                 eAll += r[0];
+                eMaxShard = std::max(eMaxShard, r[0]);
                 can &= r[1];
                 if (w == 0) pf = r[2];
             }
             pull = can && pf > 0 && eAll && eAll * 100 >= pf * d.vglobal;
+            eMaxKnown = true;
         }
         // the hop's output marks (pull and push alike; the pull reads the frontier from the bitmap)
         uint8_t* const marks = marksA;
@@ -2937,8 +3021,14 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             });
         }
         if (c->world > 1 && !pull) {                            // a pull computed every local row already
+            // vid lists when they are sure to be smaller than the bitmaps: a shard marks at most E rows,
+            // 4 B each, against (peer rows) / 8 B per peer. Every shard decides alike (the gathered E).
+            uint64_t minPeer = ~0ULL;
+            for (int q = 0; q < c->world; q++) minPeer = std::min<uint64_t>(minPeer, d.shardBase[q + 1] - d.shardBase[q]);
+            const bool lists = c->xchgLists > 0 || (c->xchgLists < 0 && eMaxKnown && 32 * eMaxShard < minPeer);
             c->timed("exchange", 0, [&] {
-                exchangeFrontier(c, d, ep);
+                if (lists) exchangeFrontierList(c, d, ep);
+                else exchangeFrontier(c, d, ep);
                 if (rw) {                                       // E == 0: no expansion wrote next[]
                     if (!E) HIP_OK(hipMemsetAsync(rootsNext, 0, std::max<uint64_t>(d.vglobal, 1) * 8, c->stream));
                     exchangeRoots(c, d, rootsNext, rootsCur);   // cur is dead after the expansion
@@ -2962,6 +3052,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             sa.F = F; sa.estart = estart; sa.chunkFirst = chunkFirst; sa.ebase = ebase;
             sa.nEnt = nEnt; sa.E = E; sa.hs = hs;
             sa.bits = lbits;
+            sa.bitWords = (d.V + 63) / 64;
             sa.outF = Fn;
             sa.outEst = c->estart2.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
             sa.outEbase = c->ebase2.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);

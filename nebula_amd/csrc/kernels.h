@@ -138,6 +138,7 @@ struct SparseArgs {
     uint64_t E;
     HopSlots hs;
     uint64_t* bits;                     // the shard's frontier bitmap, zero before the launch
+    uint64_t bitWords;                  // its words
     uint32_t* outF;
     uint64_t* outEst;                   // next hop: estart, |F| * ns + 1 entries
     uint64_t* outEbase;                 // next hop: the entries' CSR positions, or null
@@ -369,6 +370,22 @@ struct ExchangeArgs {
 };
 int launchPackPeers(const ExchangeArgs& a, hipStream_t s);
 int launchMergePeers(const ExchangeArgs& a, hipStream_t s);
+// The list form of the same exchange, for hops whose frontier is far smaller than the peers' rows
+// (counts, then the vids): per peer q != rank the marked rows of q's range as u32 offsets
+// from sb[q], appended to list[q * cap ..] (one atomic per workgroup and peer; counts[q] zeroed by the
+// host first), then each owner marks the rows it received (k_merge_list).
+struct ListXchgArgs {
+    const uint8_t* visited;
+    uint8_t epoch;
+    uint64_t sb[kMaxWorld + 1];
+    int world, rank;
+    uint32_t* list;
+    uint64_t cap;                                    // entries per peer in `list`
+    unsigned long long* counts;                      // world words
+};
+int launchPackLists(const ListXchgArgs& a, hipStream_t s);
+// own[rows[i]] = epoch for i < n
+int launchMergeList(const uint32_t* rows, uint64_t n, uint8_t* own, uint8_t epoch, hipStream_t s);
 
 
 }  // namespace ngx

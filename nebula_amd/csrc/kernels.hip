@@ -557,28 +557,33 @@ __global__ __launch_bounds__(WG) void k_expand_sparse(SparseArgs a) {
             g[k] = a.hs.dgid[s][pos];
         }
     }
-    uint32_t first = 0;                                  // bit k: item k set its destination's bit
-#pragma unroll
-    for (int k = 0; k < CITEMS; k++) {
-        if (g[k] == kNoRow) continue;
-        const unsigned long long bit = 1ULL << (g[k] & 63);
-        const unsigned long long old = atomicOr(reinterpret_cast<unsigned long long*>(a.bits + (g[k] >> 6)), bit);
-        first |= (old & bit) ? 0u : (1u << k);
-    }
+    // every item's atomic and its row's CSR offsets issued together, unconditionally (an atomic with
+    // return under a divergent branch waits on its own; an item without a destination ORs 0 into a word
+    // of its own, so the idle lanes of the last chunk do not queue on one address): one round trip for
+    // the dedup and the degrees
+    unsigned long long old[CITEMS];
     uint64_t deg[CITEMS], ob[CITEMS];
 #pragma unroll
     for (int k = 0; k < CITEMS; k++) {
-        const bool f = (first >> k) & 1u;
-        const uint64_t r = f ? g[k] : 0;
+        const bool v = g[k] != kNoRow;
+        const uint64_t r = v ? g[k] : 0;
+        const uint64_t w = v ? (r >> 6) : (threadIdx.x * CITEMS + k) % a.bitWords;
+        old[k] = atomicOr(reinterpret_cast<unsigned long long*>(a.bits + w), v ? 1ULL << (r & 63) : 0ULL);
         if (ONE) {
             const uint64_t o0 = a.hs.off[0][r], o1 = a.hs.off[0][r + 1];
-            deg[k] = f ? o1 - o0 : 0;
+            deg[k] = o1 - o0;
             ob[k] = o0;
         } else {
-            const uint64_t d = rowDegree<false>(a.hs, r);
-            deg[k] = f ? d : 0;
+            deg[k] = rowDegree<false>(a.hs, r);
             ob[k] = 0;
         }
+    }
+    uint32_t first = 0;                                  // bit k: item k set its destination's bit
+#pragma unroll
+    for (int k = 0; k < CITEMS; k++) {
+        const bool v = g[k] != kNoRow;
+        first |= (v && !(old[k] & (1ULL << (g[k] & 63)))) ? (1u << k) : 0u;
+        deg[k] = ((first >> k) & 1u) ? deg[k] : 0;
     }
     uint64_t mine = 0;
 #pragma unroll
@@ -615,12 +620,13 @@ __global__ __launch_bounds__(WG) void k_expand_sparse(SparseArgs a) {
         }
         f++;
     }
-    // the last workgroup to finish writes the totals (every reservation has been made by then)
+    // the last workgroup to finish writes the totals: every workgroup's reservation returned before its
+    // done increment was issued, so the count it reads is final. No fence: the rows, estart and heads
+    // are read by later launches only (a kernel boundary orders them; an agent-scope fence here would
+    // write back the XCD's L2)
     if (threadIdx.x == 0) {
-        __threadfence();
         const uint64_t done = atomicAdd(reinterpret_cast<unsigned long long*>(a.ctl + 1), 1ULL);
         if (done == gridDim.x - 1) {
-            __threadfence();
             const uint64_t t = __hip_atomic_load(a.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             a.outEst[(t >> kFdShift) * static_cast<uint64_t>(ns)] = t & kFdMask;
             *a.total = t;
@@ -1750,6 +1756,71 @@ int launchMergeRoots(const uint64_t* own, const uint64_t* recv, uint64_t stride,
 int launchVertexCells(const VertexCellArgs& a, hipStream_t s) {
     if (a.n == 0) return 0;
     hipLaunchKernelGGL(k_vertex_cells, dim3(static_cast<unsigned>((a.n + 255) / 256)), dim3(256), 0, s, a);
+    return static_cast<int>(hipGetLastError());
+}
+
+// list pack: 1024 threads x 4 rows per workgroup (row = tile + k * 1024 + thread: coalesced mark loads),
+// blockIdx.y = peer
+__global__ __launch_bounds__(1024) void k_pack_list(ListXchgArgs a) {
+    __shared__ uint64_t sm[1024 / 64 + 1];
+    __shared__ uint64_t sBase;
+    const int q = blockIdx.y;
+    if (q == a.rank) return;
+    const uint64_t n = a.sb[q + 1] - a.sb[q];
+    const uint64_t tile = static_cast<uint64_t>(blockIdx.x) * 4096;
+    if (tile >= n) return;
+    const uint8_t* mk = a.visited + a.sb[q];
+    uint32_t flags = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint64_t r = tile + k * 1024 + threadIdx.x;
+        const uint8_t m = mk[r < n ? r : n - 1];
+        flags |= (r < n && m == a.epoch ? 1u : 0u) << k;
+    }
+    const uint64_t mine = static_cast<uint64_t>(__popc(flags));
+    // block exclusive scan of the per-thread counts
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint64_t x = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sm[wid] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t acc = 0;
+        for (int w = 0; w < 16; w++) { const uint64_t t = sm[w]; sm[w] = acc; acc += t; }
+        sBase = acc ? static_cast<uint64_t>(atomicAdd(a.counts + q, static_cast<unsigned long long>(acc))) : 0;
+    }
+    __syncthreads();
+    uint64_t at = sBase + sm[wid] + x - mine;
+    uint32_t* out = a.list + static_cast<uint64_t>(q) * a.cap;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        if (!((flags >> k) & 1u)) continue;
+        if (at < a.cap) out[at] = static_cast<uint32_t>(tile + k * 1024 + threadIdx.x);
+        at++;
+    }
+}
+
+__global__ void k_merge_list(const uint32_t* rows, uint64_t n, uint8_t* own, uint8_t epoch) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) own[rows[i]] = epoch;
+}
+
+int launchPackLists(const ListXchgArgs& a, hipStream_t s) {
+    uint64_t maxRows = 0;
+    for (int q = 0; q < a.world; q++)
+        if (q != a.rank) maxRows = std::max(maxRows, a.sb[q + 1] - a.sb[q]);
+    if (maxRows == 0 || a.world < 2 || a.world > kMaxWorld) return 0;
+    hipLaunchKernelGGL(k_pack_list, dim3(static_cast<unsigned>((maxRows + 4095) / 4096), a.world), dim3(1024), 0, s, a);
+    return static_cast<int>(hipGetLastError());
+}
+
+int launchMergeList(const uint32_t* rows, uint64_t n, uint8_t* own, uint8_t epoch, hipStream_t s) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_merge_list, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, rows, n, own, epoch);
     return static_cast<int>(hipGetLastError());
 }
 

@@ -188,16 +188,25 @@ def test_multishard_go_matches_oracle(tmp_path, world, scale):
     queries = []
     for i, (text, push) in enumerate(MS_QUERIES):
         seeds = datagen.sample_vids(500 + i, 1 << scale, 30)
-        queries.append({"text": text.replace("{S}", ", ".join(str(int(v)) for v in seeds)), "pushdown": push})
+        queries.append({"text": text.replace("{S}", ", ".join(str(int(v)) for v in seeds)), "pushdown": push,
+                        "xchg_lists": 0})
     # the same queries with every intermediate hop of E >= V / 100 pulled (world > 1 pull: all-gathered
     # frontier bitmap, each shard probing its own rows' in-edges)
     pulled = [dict(q, pull_factor=1) for q in queries] if world != 3 else []
-    shards, digests = _run_shards(tmp_path, world, scale, queries + pulled)
-    _check_merged(o, ds.space, queries + pulled, shards, digests)
+    # and with every hop pushed and its frontier exchanged as vid lists (counts, then the vids: SURVEY
+    # §8e) instead of bitmaps
+    listed = [dict(q, pull_factor=0, xchg_lists=1) for q in queries]
+    shards, digests = _run_shards(tmp_path, world, scale, queries + pulled + listed)
+    _check_merged(o, ds.space, queries + pulled + listed, shards, digests)
     n = len(queries)
+    m = n + len(pulled)
+    for s in shards:
+        assert sum(r["list_hops"] for r in s[m:]) > 0 and sum(r["list_hops"] for r in s[:n]) == 0
+        # list bytes: 4 per exchanged vid plus the counts, below the bitmaps' V / 8 per peer on these hops
+        assert all(r["ok"] for r in s[m:])
     for s in shards:                                     # every shard takes the same pull decisions
-        assert [r["pull_hops"] for r in s[n:]] == [r["pull_hops"] for r in shards[0][n:]]
-    assert not pulled or sum(r["pull_hops"] for r in shards[0][n:]) >= 5
+        assert [r["pull_hops"] for r in s[n:m]] == [r["pull_hops"] for r in shards[0][n:m]]
+    assert not pulled or sum(r["pull_hops"] for r in shards[0][n:m]) >= 5
     assert sum(r["pull_hops"] for r in shards[0][:n]) == sum(r["pull_hops"] for r in shards[1][:n])
 
 
