@@ -532,64 +532,62 @@ __global__ __launch_bounds__(CWG) void k_compact_write(CompactArgs a) {
 }
 
 // ------------------------------------------------------------------------------ sparse intermediate hop
-// kernels.h SparseArgs. The same edge-balanced chunk map as k_expand_mark; a destination's first edge
-// (the one whose atomicOr set its bit) makes it a row of the next frontier. Loads are issued for every
-// item and selected afterwards (no load under a divergent branch, see the compaction's note below).
+// kernels.h SparseArgs. The same edge-balanced chunk map as k_expand_mark, but kSparseSub workgroups
+// per 2048-edge chunk, each taking one 256-edge slice of it (one edge per thread): the hop's atomics
+// spread over kSparseSub times as many CUs. The atomics execute at the memory side and a CU issues them
+// at a bounded rate — with 8 per thread on 24 CUs (C2 hop 1) they took ~10 of 21 us (device
+// timestamps, r05). A destination's first edge (the one whose atomicOr set its bit) makes it a row of
+// the next frontier. Loads and atomics are issued for every lane and selected afterwards (no memory
+// operation under a divergent branch, see the compaction's note below).
+constexpr int kSparseSub = CE / WG;                     // 8 slices of 256 edges per chunk
 template <bool ONE, bool P32>
 __global__ __launch_bounds__(WG) void k_expand_sparse(SparseArgs a) {
     __shared__ ChunkMap<ONE, false, P32> m;
     __shared__ uint64_t sm[NW + 1];
     __shared__ uint64_t sBase;
-    const uint32_t chunk = blockIdx.x;
+    // direct-mapped LDS filter of the destinations this workgroup already sent an atomic for (as in
+    // k_expand_mark): a hub's repeats cost an LDS probe, not another atomic on the hub's word
+    constexpr int kSeenBits = 9;
+    __shared__ uint32_t seen[1 << kSeenBits];
+    for (int p = threadIdx.x; p < (1 << kSeenBits); p += WG) seen[p] = kNoRow;
+    const uint32_t chunk = blockIdx.x / kSparseSub, sub = blockIdx.x % kSparseSub;
+    const uint32_t nChunks = gridDim.x / kSparseSub;
     const uint64_t base = static_cast<uint64_t>(chunk) * CE;
     const uint32_t cnt = static_cast<uint32_t>(a.E - base < CE ? a.E - base : CE);
-    buildMap<ONE, false, P32>(a.estart, a.chunkFirst, a.nEnt, chunk, gridDim.x, base, cnt, a.F, a.hs, m, a.ebase);
-    uint32_t g[CITEMS];
-#pragma unroll
-    for (int k = 0; k < CITEMS; k++) {
-        const uint32_t p = threadIdx.x + k * WG;
-        g[k] = kNoRow;
-        if (p < cnt) {
-            const uint32_t q = m.at[p];
-            const int s = ONE ? 0 : m.slot[q];
-            const uint64_t pos = P32 ? static_cast<uint64_t>(static_cast<uint32_t>(base + p) + static_cast<uint32_t>(m.pb[q]))
-                                     : static_cast<uint64_t>(static_cast<int64_t>(base + p) + static_cast<int64_t>(m.pb[q]));
-            g[k] = a.hs.dgid[s][pos];
-        }
+    buildMap<ONE, false, P32>(a.estart, a.chunkFirst, a.nEnt, chunk, nChunks, base, cnt, a.F, a.hs, m, a.ebase);
+    const uint32_t p = sub * WG + threadIdx.x;          // this lane's edge of the chunk
+    uint32_t g = kNoRow;
+    if (p < cnt) {
+        const uint32_t q = m.at[p];
+        const int s = ONE ? 0 : m.slot[q];
+        const uint64_t pos = P32 ? static_cast<uint64_t>(static_cast<uint32_t>(base + p) + static_cast<uint32_t>(m.pb[q]))
+                                 : static_cast<uint64_t>(static_cast<int64_t>(base + p) + static_cast<int64_t>(m.pb[q]));
+        g = a.hs.dgid[s][pos];
     }
-    // every item's atomic and its row's CSR offsets issued together, unconditionally (an atomic with
-    // return under a divergent branch waits on its own; an item without a destination ORs 0 into a word
-    // of its own, so the idle lanes of the last chunk do not queue on one address): one round trip for
-    // the dedup and the degrees
-    unsigned long long old[CITEMS];
-    uint64_t deg[CITEMS], ob[CITEMS];
-#pragma unroll
-    for (int k = 0; k < CITEMS; k++) {
-        const bool v = g[k] != kNoRow;
-        const uint64_t r = v ? g[k] : 0;
-        const uint64_t w = v ? (r >> 6) : (threadIdx.x * CITEMS + k) % a.bitWords;
-        old[k] = atomicOr(reinterpret_cast<unsigned long long*>(a.bits + w), v ? 1ULL << (r & 63) : 0ULL);
-        if (ONE) {
-            const uint64_t o0 = a.hs.off[0][r], o1 = a.hs.off[0][r + 1];
-            deg[k] = o1 - o0;
-            ob[k] = o0;
-        } else {
-            deg[k] = rowDegree<false>(a.hs, r);
-            ob[k] = 0;
-        }
+    bool need = false;                                   // the destination not yet seen in this workgroup
+    if (g != kNoRow) {
+        const uint32_t h = (g * 2654435761u) >> (32 - kSeenBits);
+        if (seen[h] != g) { seen[h] = g; need = true; }
     }
-    uint32_t first = 0;                                  // bit k: item k set its destination's bit
-#pragma unroll
-    for (int k = 0; k < CITEMS; k++) {
-        const bool v = g[k] != kNoRow;
-        first |= (v && !(old[k] & (1ULL << (g[k] & 63)))) ? (1u << k) : 0u;
-        deg[k] = ((first >> k) & 1u) ? deg[k] : 0;
+    // the atomic and the row's CSR offsets issued together; a lane without one ORs 0 into a word of its
+    // own (no queue on one address). 32-bit words of the 64-bit bitmap (little-endian halves).
+    uint32_t* const bits32 = reinterpret_cast<uint32_t*>(a.bits);
+    const uint64_t r = need ? g : 0;
+    const uint64_t w = need ? (r >> 5) : (static_cast<uint64_t>(blockIdx.x) * WG + threadIdx.x) % (2 * a.bitWords);
+    const uint32_t old = atomicOr(bits32 + w, need ? 1u << (r & 31) : 0u);
+    uint64_t deg, ob;
+    if (ONE) {
+        const uint64_t o0 = a.hs.off[0][r], o1 = a.hs.off[0][r + 1];
+        deg = o1 - o0;
+        ob = o0;
+    } else {
+        deg = rowDegree<false>(a.hs, r);
+        ob = 0;
     }
-    uint64_t mine = 0;
-#pragma unroll
-    for (int k = 0; k < CITEMS; k++) mine += ((first >> k) & 1u) ? ((1ULL << kFdShift) | deg[k]) : 0;
+    const bool first = need && !(old & (1u << (r & 31)));
+    deg = first ? deg : 0;
     uint64_t tot;
-    const uint64_t pre = blockExScan(mine, tot, sm);
+    const uint64_t pre = blockExScan(first ? ((1ULL << kFdShift) | deg) : 0, tot, sm);
     if (threadIdx.x == 0) {
         sBase = tot ? static_cast<uint64_t>(atomicAdd(reinterpret_cast<unsigned long long*>(a.ctl),
                                                       static_cast<unsigned long long>(tot)))
@@ -597,28 +595,25 @@ __global__ __launch_bounds__(WG) void k_expand_sparse(SparseArgs a) {
     }
     __syncthreads();
     const int ns = a.hs.n;
-    const uint64_t at = sBase + pre;
-    uint64_t f = at >> kFdShift, e = at & kFdMask;
-#pragma unroll
-    for (int k = 0; k < CITEMS; k++) {
-        if (!((first >> k) & 1u)) continue;
-        a.outF[f] = g[k];
+    if (first) {
+        const uint64_t at = sBase + pre;
+        const uint64_t f = at >> kFdShift;
+        uint64_t e = at & kFdMask;
+        a.outF[f] = g;
         if (ONE) {
             a.outEst[f] = e;
-            if (a.outEbase) a.outEbase[f] = ob[k];
-            writeChunkHeads(a.outCf, a.cfCap, f, e, deg[k], a.err);
-            e += deg[k];
+            if (a.outEbase) a.outEbase[f] = ob;
+            writeChunkHeads(a.outCf, a.cfCap, f, e, deg, a.err);
         } else {
             for (int s = 0; s < ns; s++) {
-                const uint64_t o = a.hs.off[s][g[k]];
-                const uint64_t d = a.hs.off[s][g[k] + 1] - o;
+                const uint64_t o = a.hs.off[s][g];
+                const uint64_t d = a.hs.off[s][g + 1] - o;
                 a.outEst[f * ns + s] = e;
                 if (a.outEbase) a.outEbase[f * ns + s] = o;
                 writeChunkHeads(a.outCf, a.cfCap, f * ns + s, e, d, a.err);
                 e += d;
             }
         }
-        f++;
     }
     // the last workgroup to finish writes the totals: every workgroup's reservation returned before its
     // done increment was issued, so the count it reads is final. No fence: the rows, estart and heads
@@ -1488,7 +1483,7 @@ int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst
 
 int launchExpandSparse(const SparseArgs& a, bool pos32, hipStream_t s) {
     if (a.E == 0) return 1;                              // the host handles an empty hop
-    const dim3 grid(static_cast<unsigned>((a.E + CE - 1) / CE));
+    const dim3 grid(static_cast<unsigned>((a.E + CE - 1) / CE * kSparseSub));
     if (a.hs.n == 1 && pos32) hipLaunchKernelGGL((k_expand_sparse<true, true>), grid, dim3(WG), 0, s, a);
     else if (a.hs.n == 1) hipLaunchKernelGGL((k_expand_sparse<true, false>), grid, dim3(WG), 0, s, a);
     else if (pos32) hipLaunchKernelGGL((k_expand_sparse<false, true>), grid, dim3(WG), 0, s, a);
