@@ -693,10 +693,16 @@ PairDigest slotDigest(const HostSlot& s, bool transpose, uint64_t gbase = 0) {
 // over s (a frontier reached by expansion holds the hubs first, so most reached rows hit on their
 // first probe). Which in-neighbours are probed first changes nothing but the probe count: the pull
 // computes set membership.
+// Rows without in-edges can never be reached by a pull: they are left out of the image (16 % of C2's
+// rows, 15 % of its slices), so the windows run over the rows that have in-edges, in row order.
 void buildPullHead(const HostGraph& g, int32_t s, int32_t m, DeviceGraph& d, const std::vector<uint32_t>* globalDeg = nullptr) {
     const HostSlot& out = g.slots[s];
     const HostSlot& in = g.slots[m];
-    const uint64_t V = g.vid.size();
+    const uint64_t Vall = g.vid.size();
+    std::vector<uint32_t> live;
+    live.reserve(Vall);
+    for (uint64_t r = 0; r < Vall; r++) if (in.off[r + 1] != in.off[r]) live.push_back(static_cast<uint32_t>(r));
+    const uint64_t V = live.size();
     const uint64_t slices = (V + 63) / 64;
     std::vector<uint32_t> perm(slices * 64, kNoRow), head(slices * 64 * kPullK, kNoRow);
     std::vector<uint8_t> nk(slices, 0);
@@ -705,7 +711,7 @@ void buildPullHead(const HostGraph& g, int32_t s, int32_t m, DeviceGraph& d, con
     // in-neighbours are global rows: world 1 reads the out-degree here, world > 1 the gathered one
     auto outDeg = [&](uint32_t u) -> uint64_t {
         if (globalDeg) return u < globalDeg->size() ? (*globalDeg)[u] : 0;
-        return u < V ? out.off[u + 1] - out.off[u] : 0;
+        return u < Vall ? out.off[u + 1] - out.off[u] : 0;
     };
     parallelRows(windows, [&](uint64_t lo, uint64_t hi, int t) {
         std::vector<std::pair<uint32_t, uint32_t>> rows;        // (head length, row)
@@ -713,9 +719,10 @@ void buildPullHead(const HostGraph& g, int32_t s, int32_t m, DeviceGraph& d, con
         for (uint64_t w = lo; w < hi; w++) {
             const uint64_t r0 = w * kPullWindow, r1 = std::min<uint64_t>(V, r0 + kPullWindow);
             rows.clear();
-            for (uint64_t r = r0; r < r1; r++) {
+            for (uint64_t i = r0; i < r1; i++) {
+                const uint32_t r = live[i];
                 const uint64_t deg = in.off[r + 1] - in.off[r];
-                rows.emplace_back(static_cast<uint32_t>(std::min<uint64_t>(deg, kPullK)), static_cast<uint32_t>(r));
+                rows.emplace_back(static_cast<uint32_t>(std::min<uint64_t>(deg, kPullK)), r);
             }
             std::stable_sort(rows.begin(), rows.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
             for (uint64_t i = 0; i < rows.size(); i++) {
