@@ -193,6 +193,8 @@ struct ngx_ctx {
         }
         void release() { if (p) (void)hipHostFree(p); p = nullptr; cap = 0; }
     } hostStage, inStage, seedStage;
+    std::string progLast;                               // the bytes of the last program upload ...
+    const char* progLastPtr = nullptr;                  // ... and where they went (uploadPrograms skips a repeat)
     size_t progStageBytes = 0;                          // bytes of inStage holding this call's programs                               // results D2H / query inputs H2D (programs, seeds)
     std::vector<ColBuf> oCols;                          // result columns (columnar, HBM)
     std::vector<ColBuf> dCols;                          // DISTINCT: the other half of each column's double buffer
@@ -503,7 +505,9 @@ DevPrograms uploadPrograms(ngx_ctx* c, const Programs& pr, const std::vector<int
     size_t cBytes = yColType.size() * 4;
     size_t poolOff = (codeBytes + yBytes + tBytes + cBytes + 63) & ~size_t(63);
     size_t total = poolOff + pr.pool.size() + 64;
+    const size_t capBefore = c->progBuf.cap;
     char* base = c->progBuf.get<char>(total);
+    if (c->progBuf.cap != capBefore) c->progLastPtr = nullptr;   // a new allocation (maybe at the old address)
     // staged in page-locked memory: the copy is asynchronous (the stage is reused only by the next call,
     // after this one has synchronised with its kernels)
     char* host = c->inStage.get(total);
@@ -514,7 +518,13 @@ DevPrograms uploadPrograms(ngx_ctx* c, const Programs& pr, const std::vector<int
     std::memcpy(host + codeBytes + yBytes, ySlotType.data(), tBytes);
     std::memcpy(host + codeBytes + yBytes + tBytes, yColType.data(), cBytes);
     std::memcpy(host + poolOff, pr.pool.data(), pr.pool.size());
-    HIP_OK(hipMemcpyAsync(base, host, total, hipMemcpyHostToDevice, c->stream));
+    // the same bytes as the last upload into the same buffer (a prepared query run again): nothing to copy
+    // (a copy launch and its dispatch gap, ~7 us of the C2 step on the device timeline)
+    if (base != c->progLastPtr || c->progLast.size() != total || std::memcmp(c->progLast.data(), host, total) != 0) {
+        HIP_OK(hipMemcpyAsync(base, host, total, hipMemcpyHostToDevice, c->stream));
+        c->progLast.assign(host, total);
+        c->progLastPtr = base;
+    }
     DevPrograms d;
     d.code = reinterpret_cast<const Insn*>(base);
     d.yOff = reinterpret_cast<const int32_t*>(base + codeBytes);
@@ -2589,7 +2599,21 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     // last), outputs sized for every edge of the slots, no string arena, no storage mask on it.
     const bool finalDev = !dyn && !rw && c->world == 1 && lbCompact && hs.n > 0 && steps >= 2 && recordFrom == steps &&
                           !pushInvalid && !capped && nStrOut == 0;
-    uint64_t* dynStats = (dyn || finalDev) ? c->dynStats.get<uint64_t>(steps + 2) : nullptr;
+    // Hop 1 as a sparse hop sized on the device (spec1): the fused seed kernel's packed (|F|, E) feeds the
+    // sparse kernel, which strides a fixed grid over the hop's slices, so the host launches hop 1 without
+    // waiting for the seed hop's total (one host round trip fewer). Chosen before E1 is known, from the
+    // seeds x the OVER types' average degree: a wrong guess costs time, never rows (the sparse kernel is
+    // exact for any E).
+    const double e1est = d.V ? static_cast<double>(svids.size()) * static_cast<double>(slotEdges) / static_cast<double>(d.V) : 0.0;
+    const bool spec1 = sparseOk && !dyn && steps >= 2 && recordFrom > 1 && !capped && !intermediateChecks &&
+                       !svids.empty() && svids.size() <= kSeedFuseMax && svids.size() * static_cast<uint64_t>(hs.n) <= kSeedFuseMax &&
+                       d.vindex.slots != nullptr &&
+                       (c->sparseFactor < 0 || e1est * static_cast<double>(c->sparseFactor) <= static_cast<double>(d.V)) &&
+                       !(pullable && e1est * 100.0 >= static_cast<double>(c->pullFactor) * static_cast<double>(d.V)) &&
+                       // a pull factor set below 1 (pull on any hop of E >= V / 100: tests, pull-heavy tuning)
+                       // wants hop 1's direction from its real E, which only the seed hop knows
+                       !(pullable && c->pullFactor < 100);
+    uint64_t* dynStats = (dyn || finalDev || spec1) ? c->dynStats.get<uint64_t>(steps + 2) : nullptr;
     const uint64_t pullMinE = pullable ? (static_cast<uint64_t>(c->pullFactor) * d.V + 99) / 100 : ~0ULL;
     if (dyn && c->epoch + 2 * static_cast<uint64_t>(steps) + 4 > 255) {   // no epoch wrap inside the query
         HIP_OK(hipMemsetAsync(c->visited.p, 0, c->visitedSize, c->stream));
@@ -2703,7 +2727,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         if (!jk) c->jitNote = jerr.empty() ? "jit: unsupported program" : jerr;
         c->hmark("jit");
     }
-    if (seedE) fusedE = awaitPub(c, seedPub, seedE);           // the seed hop ran under the host prep above
+    if (seedE && !spec1) fusedE = awaitPub(c, seedPub, seedE); // the seed hop ran under the host prep above
     // multi-root walk: root sets over rows, the seed frontier's from the starts' bits
     uint64_t* rootsCur = nullptr;
     uint64_t* rootsNext = nullptr;
@@ -2737,6 +2761,58 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         if (c->traceGo) hopT.push_back(std::chrono::steady_clock::now());
         bool isRecord = h >= recordFrom;
         bool isFinal = h == steps;
+        if (spec1 && h == 1) {
+            // the seed hop's frontier expanded by the sparse kernel, its size read on the device
+            if (!c->bitsClean || c->bitsCleanPtr != lbits) HIP_OK(hipMemsetAsync(lbits, 0, (d.V + 63) / 64 * 8, c->stream));
+            c->bitsClean = false;
+            if (!c->sparseCtl.p) {
+                c->sparseCtl.get<uint64_t>(2);
+                HIP_OK(hipMemsetAsync(c->sparseCtl.p, 0, c->sparseCtl.cap, c->stream));
+            }
+            const bool devNext = finalDev && h + 1 == steps;
+            uint32_t* Fn = (F == c->F0.p) ? c->F1.get<uint32_t>(std::max<uint64_t>(d.V, 1)) : c->F0.get<uint32_t>(std::max<uint64_t>(d.V, 1));
+            SparseArgs sa{};
+            sa.F = F; sa.estart = static_cast<const uint64_t*>(c->estart.p); sa.chunkFirst = static_cast<const uint64_t*>(c->chunkFirst.p);
+            sa.ebase = static_cast<const uint64_t*>(c->ebase.p);
+            sa.dynIn = dynStats;                                  // the seed kernel's packed (|F|, E)
+            sa.hs = hs;
+            sa.bits = lbits;
+            sa.bitWords = (d.V + 63) / 64;
+            sa.outF = Fn;
+            sa.outEst = c->estart2.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
+            sa.outEbase = c->ebase2.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
+            sa.outCf = c->chunkFirst2.get<uint64_t>(cfCap);
+            sa.cfCap = cfCap;
+            sa.ctl = static_cast<uint64_t*>(c->sparseCtl.p);
+            sa.total = devNext ? dynStats + h : counters + 2;
+            sa.pub = devNext ? Publish{nullptr, 0} : nextPub(c);
+            sa.err = errFlag;
+            c->timed("expand_sparse", 0, [&] {
+                if (launchExpandSparse(sa, pos32, c->stream)) throw Error{NGX_E_DEVICE, "sparse expand"};
+            });
+            std::swap(c->estart, c->estart2);
+            std::swap(c->ebase, c->ebase2);
+            std::swap(c->chunkFirst, c->chunkFirst2);
+            const uint64_t E1 = awaitPub(c, seedPub, seedE);     // published before the sparse kernel ran
+            R.hopFrontier.push_back(nF);
+            R.hopEdges.push_back(E1);
+            c->addBytes("expand_sparse", E1 * 12);
+            haveEstart = haveEbase = haveHeads = haveBits = true;
+            c->sparseHops++;
+            if (devNext) {
+                nF = d.V;
+                fusedE = slotEdges;
+            } else {
+                const uint64_t packed = awaitPub(c, sa.pub, counters + 2);
+                nF = packed >> kFdShift;
+                fusedE = packed & kFdMask;
+                c->addBytes("expand_sparse", nF * (4 + 24 * static_cast<uint64_t>(hs.n)));
+            }
+            R.hopNext.push_back(nF);
+            F = Fn;
+            if (nF == 0) break;                                    // GO_EXIT: empty frontier
+            continue;
+        }
         const bool devE = finalDev && isFinal;                   // E below is an upper bound; the device has it
         uint64_t nEnt = nF * static_cast<uint64_t>(hs.n);
         uint64_t* estart = c->estart.get<uint64_t>(nEnt + 1);

@@ -136,6 +136,8 @@ struct SparseArgs {
     const uint64_t* ebase;              // optional (FinalArgs::ebase)
     uint64_t nEnt;
     uint64_t E;
+    const uint64_t* dynIn;              // or null: packed (|F| << kDynShift | E) of this hop on the device (the
+                                        // launch is then a fixed grid striding over the hop's slices)
     HopSlots hs;
     uint64_t* bits;                     // the shard's frontier bitmap, zero before the launch
     uint64_t bitWords;                  // its words

@@ -550,70 +550,87 @@ __global__ __launch_bounds__(WG) void k_expand_sparse(SparseArgs a) {
     constexpr int kSeenBits = 9;
     __shared__ uint32_t seen[1 << kSeenBits];
     for (int p = threadIdx.x; p < (1 << kSeenBits); p += WG) seen[p] = kNoRow;
-    const uint32_t chunk = blockIdx.x / kSparseSub, sub = blockIdx.x % kSparseSub;
-    const uint32_t nChunks = gridDim.x / kSparseSub;
-    const uint64_t base = static_cast<uint64_t>(chunk) * CE;
-    const uint32_t cnt = static_cast<uint32_t>(a.E - base < CE ? a.E - base : CE);
-    buildMap<ONE, false, P32>(a.estart, a.chunkFirst, a.nEnt, chunk, nChunks, base, cnt, a.F, a.hs, m, a.ebase);
-    const uint32_t p = sub * WG + threadIdx.x;          // this lane's edge of the chunk
-    uint32_t g = kNoRow;
-    if (p < cnt) {
-        const uint32_t q = m.at[p];
-        const int s = ONE ? 0 : m.slot[q];
-        const uint64_t pos = P32 ? static_cast<uint64_t>(static_cast<uint32_t>(base + p) + static_cast<uint32_t>(m.pb[q]))
-                                 : static_cast<uint64_t>(static_cast<int64_t>(base + p) + static_cast<int64_t>(m.pb[q]));
-        g = a.hs.dgid[s][pos];
+    // the hop's edges: from the arguments, or (dynIn, a hop launched before its size is known on the
+    // host) from the packed (|F|, E) word the kernel that built the frontier wrote; the grid then strides
+    // over the slices
+    uint64_t E = a.E, nEnt = a.nEnt;
+    if (a.dynIn != nullptr) {
+        const uint64_t t = gld<uint64_t>(a.dynIn, 0);
+        E = t & kDynMask;
+        nEnt = (t >> kDynShift) * static_cast<uint64_t>(a.hs.n);
     }
-    bool need = false;                                   // the destination not yet seen in this workgroup
-    if (g != kNoRow) {
-        const uint32_t h = (g * 2654435761u) >> (32 - kSeenBits);
-        if (seen[h] != g) { seen[h] = g; need = true; }
-    }
-    // the atomic and the row's CSR offsets issued together; a lane without one ORs 0 into a word of its
-    // own (no queue on one address). 32-bit words of the 64-bit bitmap (little-endian halves).
-    uint32_t* const bits32 = reinterpret_cast<uint32_t*>(a.bits);
-    const uint64_t r = need ? g : 0;
-    const uint64_t w = need ? (r >> 5) : (static_cast<uint64_t>(blockIdx.x) * WG + threadIdx.x) % (2 * a.bitWords);
-    const uint32_t old = atomicOr(bits32 + w, need ? 1u << (r & 31) : 0u);
-    uint64_t deg, ob;
-    if (ONE) {
-        const uint64_t o0 = a.hs.off[0][r], o1 = a.hs.off[0][r + 1];
-        deg = o1 - o0;
-        ob = o0;
-    } else {
-        deg = rowDegree<false>(a.hs, r);
-        ob = 0;
-    }
-    const bool first = need && !(old & (1u << (r & 31)));
-    deg = first ? deg : 0;
-    uint64_t tot;
-    const uint64_t pre = blockExScan(first ? ((1ULL << kFdShift) | deg) : 0, tot, sm);
-    if (threadIdx.x == 0) {
-        sBase = tot ? static_cast<uint64_t>(atomicAdd(reinterpret_cast<unsigned long long*>(a.ctl),
-                                                      static_cast<unsigned long long>(tot)))
-                    : 0;
-    }
-    __syncthreads();
+    const uint32_t nChunks = static_cast<uint32_t>((E + CE - 1) / CE);
     const int ns = a.hs.n;
-    if (first) {
-        const uint64_t at = sBase + pre;
-        const uint64_t f = at >> kFdShift;
-        uint64_t e = at & kFdMask;
-        a.outF[f] = g;
+    // workgroups past the hop's slices leave at once, without counting themselves done (a same-address
+    // atomic per workgroup of a 1024-workgroup grid cost ~9 us); an empty hop is finished by workgroup 0
+    const uint32_t items = nChunks * kSparseSub;
+    const uint32_t active = items < gridDim.x ? (items ? items : 1u) : gridDim.x;
+    if (blockIdx.x >= active) return;
+    for (uint32_t item = blockIdx.x; item < items; item += gridDim.x) {
+        const uint32_t chunk = item / kSparseSub, sub = item % kSparseSub;
+        const uint64_t base = static_cast<uint64_t>(chunk) * CE;
+        const uint32_t cnt = static_cast<uint32_t>(E - base < CE ? E - base : CE);
+        buildMap<ONE, false, P32>(a.estart, a.chunkFirst, nEnt, chunk, nChunks, base, cnt, a.F, a.hs, m, a.ebase);
+        const uint32_t p = sub * WG + threadIdx.x;          // this lane's edge of the chunk
+        uint32_t g = kNoRow;
+        if (p < cnt) {
+            const uint32_t q = m.at[p];
+            const int s = ONE ? 0 : m.slot[q];
+            const uint64_t pos = P32 ? static_cast<uint64_t>(static_cast<uint32_t>(base + p) + static_cast<uint32_t>(m.pb[q]))
+                                     : static_cast<uint64_t>(static_cast<int64_t>(base + p) + static_cast<int64_t>(m.pb[q]));
+            g = a.hs.dgid[s][pos];
+        }
+        bool need = false;                                   // the destination not yet seen in this workgroup
+        if (g != kNoRow) {
+            const uint32_t h = (g * 2654435761u) >> (32 - kSeenBits);
+            if (seen[h] != g) { seen[h] = g; need = true; }
+        }
+        // the atomic and the row's CSR offsets issued together; a lane without one ORs 0 into a word of its
+        // own (no queue on one address). 32-bit words of the 64-bit bitmap (little-endian halves).
+        uint32_t* const bits32 = reinterpret_cast<uint32_t*>(a.bits);
+        const uint64_t r = need ? g : 0;
+        const uint64_t w = need ? (r >> 5) : (static_cast<uint64_t>(blockIdx.x) * WG + threadIdx.x) % (2 * a.bitWords);
+        const uint32_t old = atomicOr(bits32 + w, need ? 1u << (r & 31) : 0u);
+        uint64_t deg, ob;
         if (ONE) {
-            a.outEst[f] = e;
-            if (a.outEbase) a.outEbase[f] = ob;
-            writeChunkHeads(a.outCf, a.cfCap, f, e, deg, a.err);
+            const uint64_t o0 = a.hs.off[0][r], o1 = a.hs.off[0][r + 1];
+            deg = o1 - o0;
+            ob = o0;
         } else {
-            for (int s = 0; s < ns; s++) {
-                const uint64_t o = a.hs.off[s][g];
-                const uint64_t d = a.hs.off[s][g + 1] - o;
-                a.outEst[f * ns + s] = e;
-                if (a.outEbase) a.outEbase[f * ns + s] = o;
-                writeChunkHeads(a.outCf, a.cfCap, f * ns + s, e, d, a.err);
-                e += d;
+            deg = rowDegree<false>(a.hs, r);
+            ob = 0;
+        }
+        const bool first = need && !(old & (1u << (r & 31)));
+        deg = first ? deg : 0;
+        uint64_t tot;
+        const uint64_t pre = blockExScan(first ? ((1ULL << kFdShift) | deg) : 0, tot, sm);
+        if (threadIdx.x == 0) {
+            sBase = tot ? static_cast<uint64_t>(atomicAdd(reinterpret_cast<unsigned long long*>(a.ctl),
+                                                          static_cast<unsigned long long>(tot)))
+                        : 0;
+        }
+        __syncthreads();
+        if (first) {
+            const uint64_t at = sBase + pre;
+            const uint64_t f = at >> kFdShift;
+            uint64_t e = at & kFdMask;
+            a.outF[f] = g;
+            if (ONE) {
+                a.outEst[f] = e;
+                if (a.outEbase) a.outEbase[f] = ob;
+                writeChunkHeads(a.outCf, a.cfCap, f, e, deg, a.err);
+            } else {
+                for (int s = 0; s < ns; s++) {
+                    const uint64_t o = a.hs.off[s][g];
+                    const uint64_t d = a.hs.off[s][g + 1] - o;
+                    a.outEst[f * ns + s] = e;
+                    if (a.outEbase) a.outEbase[f * ns + s] = o;
+                    writeChunkHeads(a.outCf, a.cfCap, f * ns + s, e, d, a.err);
+                    e += d;
+                }
             }
         }
+        __syncthreads();                                // the chunk map and sBase are rebuilt for the next slice
     }
     // the last workgroup to finish writes the totals: every workgroup's reservation returned before its
     // done increment was issued, so the count it reads is final. No fence: the rows, estart and heads
@@ -621,7 +638,7 @@ __global__ __launch_bounds__(WG) void k_expand_sparse(SparseArgs a) {
     // write back the XCD's L2)
     if (threadIdx.x == 0) {
         const uint64_t done = atomicAdd(reinterpret_cast<unsigned long long*>(a.ctl + 1), 1ULL);
-        if (done == gridDim.x - 1) {
+        if (done == active - 1) {
             const uint64_t t = __hip_atomic_load(a.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             a.outEst[(t >> kFdShift) * static_cast<uint64_t>(ns)] = t & kFdMask;
             *a.total = t;
@@ -1482,8 +1499,9 @@ int launchChunkFirst(const uint64_t* estart, uint64_t nEnt, uint64_t* chunkFirst
 }
 
 int launchExpandSparse(const SparseArgs& a, bool pos32, hipStream_t s) {
-    if (a.E == 0) return 1;                              // the host handles an empty hop
-    const dim3 grid(static_cast<unsigned>((a.E + CE - 1) / CE * kSparseSub));
+    if (a.E == 0 && a.dynIn == nullptr) return 1;       // the host handles an empty hop
+    // dynIn: the hop's size is on the device; a fixed grid (4 workgroups per CU) strides over its slices
+    const dim3 grid(a.dynIn != nullptr ? 1024u : static_cast<unsigned>((a.E + CE - 1) / CE * kSparseSub));
     if (a.hs.n == 1 && pos32) hipLaunchKernelGGL((k_expand_sparse<true, true>), grid, dim3(WG), 0, s, a);
     else if (a.hs.n == 1) hipLaunchKernelGGL((k_expand_sparse<true, false>), grid, dim3(WG), 0, s, a);
     else if (pos32) hipLaunchKernelGGL((k_expand_sparse<false, true>), grid, dim3(WG), 0, s, a);
