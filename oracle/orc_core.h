@@ -254,6 +254,15 @@ class RowReader {
         if (!r->processHeader(row)) return nullptr;
         return r;
     }
+    // make() into an existing reader (its offset vectors keep their capacity): false where make() gives
+    // null. The harness's graphd loop reads millions of rows; a reader per row was three allocations.
+    static bool reset(RowReader& r, const std::string& row, const Schema* schema) {
+        if (!schema) return false;
+        r.schema_ = schema;
+        r.row_ = &row;
+        return r.processHeader(row);
+    }
+    RowReader() = default;
 
     const Schema* getSchema() const { return schema_; }
     int32_t numFields() const { return static_cast<int32_t>(schema_->getNumFields()); }
@@ -389,7 +398,6 @@ class RowReader {
     }
 
  private:
-    RowReader() = default;
     const Schema* schema_ = nullptr;
     const std::string* row_ = nullptr;
     const uint8_t* data_ = nullptr;

@@ -441,7 +441,8 @@ struct GoExec {
         VertexID srcId = 0, dstId = 0;
         EdgeType edgeType = 0;
         const std::vector<TagData>* tagData = nullptr;
-        std::unique_ptr<RowReader> reader;
+        RowReader rd;                                  // the edge's row (reset per edge, no allocation)
+        bool reader = false;
         size_t inputRow = 0;
         Getters g;
         FinalEval(GoExec& ex, const std::map<TagID, std::shared_ptr<Schema>>& ts,
@@ -516,7 +517,7 @@ struct GoExec {
                 }
                 if (prop == "_src") return OptVariant(srcId);
                 if (!reader) return Status::Error("null reader");
-                auto r = RowReader::getPropByName(reader.get(), prop);
+                auto r = RowReader::getPropByName(&rd, prop);
                 if (!r.ok()) return Status::Error("get prop failed");
                 return OptVariant(r.v);
             };
@@ -549,7 +550,7 @@ struct GoExec {
                 auto sit = edgeSchema.find(ev.edgeType);
                 for (auto& e : ed.edges) {
                     ev.dstId = e.dst;
-                    ev.reader = sit != edgeSchema.end() ? RowReader::make(e.props, sit->second) : nullptr;
+                    ev.reader = sit != edgeSchema.end() && RowReader::reset(ev.rd, e.props, sit->second.get());
                     if (filter) {
                         auto v = filter->eval(ev.g);
                         if (!v.ok()) { out.ok = false; out.error = v.status().msg_; return false; }
