@@ -256,13 +256,31 @@ def test_rmat_empty_and_missing_seeds(rmat):
         assert got.ok and got.rows == []
 
 
-def test_rmat_query_error_matches(rmat):
+# (query, the oracle's Status text, the device's failure class): graphd's evaluation of WHERE / YIELD
+# fails the query (GoExecutor.cpp:1277-1294); the device reports the class of the failure, not
+# Expressions.cpp's text, so the kind is pinned on both sides
+# (the WHERE of case 2 runs in graphd only with pushdown off: pushed, a storage filter error skips the
+# edge instead, QueryBaseProcessor.inl:586-602)
+ERROR_CASES = [
+    ("GO FROM 1, 2, 3 OVER e YIELD e.p1 * 9223372036854775807", True, "Out of range", "failed to evaluate"),
+    ("GO FROM 1, 2, 3 OVER e YIELD e.p1 / (e.p0 - e.p0)", True, "Division by zero", "failed to evaluate"),
+    ("GO FROM 1, 2, 3 OVER e WHERE e.p1 % (e.p0 - e.p0) > 1 YIELD e._dst", False, "Division by zero", "failed to evaluate"),
+    ("GO 2 STEPS FROM 1, 2, 3 OVER e YIELD -9223372036854775807 - 1 - e.p0 - 1", True, "Out of range", "failed to evaluate"),
+]
+
+
+@pytest.mark.parametrize("case", range(len(ERROR_CASES)))
+def test_rmat_query_error_matches(rmat, case):
     ds, o, e = rmat
-    # int64 overflow inside YIELD fails the query in graphd
-    s = ngql.parse_go("GO FROM 1, 2, 3 OVER e YIELD e.p1 * 9223372036854775807")
-    ref = o.go(ds.space, s)
-    got = e.go(ds.space, s)
-    assert got.ok == ref.ok
+    q, push, ref_text, dev_text = ERROR_CASES[case]
+    s = ngql.parse_go(q)
+    ref = o.go(ds.space, s, pushdown=push)
+    got = e.go(ds.space, s, pushdown=push)
+    assert not ref.ok and ref_text in ref.error, ref.error
+    assert not got.ok and got.code == engine.E_QUERY and dev_text in got.error, (got.code, got.error)
+    # the same query on the host path that the device refuses nothing of: a good query still runs after it
+    ok = e.go(ds.space, ngql.parse_go("GO FROM 1, 2, 3 OVER e YIELD e.p1"))
+    assert ok.ok
 
 
 def test_rmat_device_results_values(rmat):
