@@ -59,6 +59,9 @@ def parse():
     p.add_argument("--host-exchange", action="store_true",
                    help="rehearsal of the N > 1 path on one GPU: every rank on device 0, frontier exchange "
                         "through the host collective (gloo) instead of RCCL")
+    p.add_argument("--host-loop", choices=["native", "python"], default="native",
+                   help="timed steps driven by one native loop over the prepared plans (ngx_go_batch, as a C++ "
+                        "graphd would) or by a Python call per step")
     p.add_argument("--flag", action="append", default=[], metavar="NAME=VALUE",
                    help="engine flag (ngx_set_flag) set before the run, e.g. dyn_hops=1; repeatable")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -187,10 +190,28 @@ def main():
     final_8d = final_edges = final_rows = 0
     p1_width = None
     prep_ms = tail_ms = 0.0
+    timed = [prepared[(id(plans[args.warmup + i]), True, False)] for i in range(args.steps)]
+    if args.host_loop == "native":
+        # the K steps in one native loop over the prepared plans (ngx_go_batch: each is one ngx_go)
+        for code, nrows, e in eng.go_batch(timed):
+            if code:
+                raise RuntimeError(f"GO failed in the timed loop ({code}): {eng.L.ngx_last_error(eng.h).decode()}")
+            edges += e
+            result_rows += nrows
+    else:
+        for i in range(args.steps):
+            r = step(plans[args.warmup + i])
+            edges += sum(r.hop_edges)
+            result_rows += r.nrows
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    # the same steps again with per-kernel HIP events (their records would perturb the timed loop), one
+    # Python call each: per-step statistics
+    eng.set_profiling(True)
     for i in range(args.steps):
         r = step(plans[args.warmup + i])
-        edges += sum(r.hop_edges)
-        result_rows += r.nrows
+        dev_ms += r.device_ms                            # device time: HIP events, profiled pass only
         prep_ms += r.host_prep_ms
         tail_ms += r.host_tail_ms
         hop_edges = r.hop_edges
@@ -200,13 +221,6 @@ def main():
         final_rows += r.nrows
         if r.dev_widths and len(r.dev_widths[1]) >= 4:
             p1_width = r.dev_widths[1][3]               # YIELD e._dst, e._rank, e.p0, e.p1: p1's width
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t_start
-    # the same steps again with per-kernel HIP events (their records would perturb the timed loop)
-    eng.set_profiling(True)
-    for i in range(args.steps):
-        dev_ms += step(plans[args.warmup + i]).device_ms     # device time: HIP events, profiled pass only
     stats = eng.kernel_stats()
     eng.set_profiling(False)
 
@@ -366,6 +380,7 @@ def main():
             "host_ms_per_step": {"library_prep": round(prep_ms / args.steps, 3), "library_tail": round(tail_ms / args.steps, 3),
                                  "note": "inside ngx_go: before the first launch (plan, programs, seeds) / after the "
                                          "device finished; the rest of ms_per_step - device_ms is the Python caller"},
+            "host_loop": args.host_loop,
             "timed_region": ("seeds on host -> the YIELD columns of every result row in HBM (result_on_device; "
                              + ("yield_only: e._dst / e._rank alias the dst / rank row arrays, no src array"
                                 if args.yield_only else "and the src / dst / rank row arrays") + ")"),

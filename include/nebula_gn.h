@@ -373,6 +373,12 @@ typedef struct {
 
 int32_t ngx_go(ngx_ctx* ctx, const ngx_go_plan* plan, ngx_go_result** out);
 void ngx_go_result_free(ngx_go_result* r);
+/* n GO plans run back to back, each exactly as one ngx_go call whose result is freed at once (a native
+ * host loop: a graphd driving many queries, the bench's timed steps). Per query: its code, result rows
+ * and edges scanned over all hops (codes / nrows / edges may be NULL). Device-resident results of the
+ * last query stay in HBM as ngx_go leaves them. Returns the first code that is not NGX_OK. */
+int32_t ngx_go_batch(ngx_ctx* ctx, const ngx_go_plan* const* plans, int32_t n, int32_t* codes, uint64_t* nrows,
+                     uint64_t* edges);
 
 /* Copy `bytes` from device memory of this context (e.g. a result_on_device array) to host memory,
  * ordered after the context's work. */

@@ -3853,6 +3853,26 @@ extern "C" int32_t ngx_go(ngx_ctx* c, const ngx_go_plan* p, ngx_go_result** out)
     return rc;
 }
 
+// A native host loop over prepared plans: each is exactly one ngx_go (its result freed at once), so a
+// caller that drives many queries (a graphd, the bench) pays no interpreter between them.
+extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int32_t n, int32_t* codes, uint64_t* nrows,
+                                uint64_t* edges) {
+    if (!c || (n > 0 && !plans)) return NGX_E_BAD_ARGUMENT;
+    int32_t first = NGX_OK;
+    for (int32_t i = 0; i < n; i++) {
+        ngx_go_result* r = nullptr;
+        const int32_t rc = ngx_go(c, plans[i], &r);
+        uint64_t e = 0;
+        if (r) for (int32_t h = 0; h < r->nhops; h++) e += r->hop_edges[h];
+        if (codes) codes[i] = rc;
+        if (nrows) nrows[i] = r ? r->nrows : 0;
+        if (edges) edges[i] = e;
+        if (r) ngx_go_result_free(r);
+        if (rc != NGX_OK && first == NGX_OK) first = rc;
+    }
+    return first;
+}
+
 // ============================================================================ GetNeighbors
 namespace {
 

@@ -183,6 +183,7 @@ SIGNATURES = {
     "ngx_gn_result_free": (None, [P(GnResult)]),
     "ngx_go": (c_i32, [ctypes.c_void_p, P(GoPlan), P(P(GoResultC))]),
     "ngx_go_result_free": (None, [P(GoResultC)]),
+    "ngx_go_batch": (c_i32, [ctypes.c_void_p, ctypes.c_void_p, c_i32, P(c_i32), P(c_u64), P(c_u64)]),
     "ngx_set_profiling": (c_i32, [ctypes.c_void_p, c_i32]),
     "ngx_synchronize": (c_i32, [ctypes.c_void_p]),
     "ngx_go_result_digest": (c_i32, [ctypes.c_void_p, P(GoResultC), P(c_u64)]),
@@ -590,6 +591,15 @@ class Engine:
             return res
         finally:
             self.L.ngx_go_result_free(out)
+
+    def go_batch(self, prepared: Sequence["PreparedGo"]):
+        """Run prepared GO plans back to back in one native call (ngx_go_batch): per query (code, result
+        rows, edges scanned over all hops)."""
+        n = len(prepared)
+        arr = (ctypes.POINTER(GoPlan) * max(n, 1))(*[ctypes.pointer(p.plan) for p in prepared])
+        codes, rows, edges = (c_i32 * max(n, 1))(), (c_u64 * max(n, 1))(), (c_u64 * max(n, 1))()
+        self.L.ngx_go_batch(self.h, ctypes.cast(arr, ctypes.c_void_p), n, codes, rows, edges)
+        return [(int(codes[i]), int(rows[i]), int(edges[i])) for i in range(n)]
 
     def prepare_go(self, space: int, s, pushdown: bool = True, now_sec: int = 0, on_device: bool = False,
                    columnar: bool = False, yield_only: bool = False, input=None, compact: bool = False) -> PreparedGo:
