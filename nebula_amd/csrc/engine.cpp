@@ -212,6 +212,7 @@ struct ngx_ctx {
     // "sparse_hops")
     int64_t sparseFactor = 16;
     uint64_t sparseHops = 0;
+    bool pullPredict = false;                           // hop 2 of the last query pulled (world 1): launch it early
     DBuf sparseCtl;                                     // the sparse kernel's counters, kept zero between launches
     DBuf estart2, ebase2, chunkFirst2;                  // the next hop's entry arrays while the sparse kernel reads this hop's
     // world > 1 push hops: frontier exchanged as vid lists instead of bitmaps (flag "xchg_lists": -1 by the
@@ -2650,6 +2651,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     bool haveEstart = false;                                   // estart[] / E of the next hop already built
     bool haveEbase = false;                                    // ... and its entries' CSR positions (ebase[])
     uint64_t fusedE = 0;
+    Publish pendingPub{nullptr, 0};                            // a device-sized hop's total not yet read (spec1)
     Publish seedPub{nullptr, 0};                               // the fused seed hop's E, awaited after the host prep
     const uint64_t* seedE = nullptr;
     if (nF) {
@@ -2799,19 +2801,43 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             c->addBytes("expand_sparse", E1 * 12);
             haveEstart = haveEbase = haveHeads = haveBits = true;
             c->sparseHops++;
+            F = Fn;
             if (devNext) {
                 nF = d.V;
                 fusedE = slotEdges;
+                R.hopNext.push_back(nF);
             } else {
-                const uint64_t packed = awaitPub(c, sa.pub, counters + 2);
-                nF = packed >> kFdShift;
-                fusedE = packed & kFdMask;
-                c->addBytes("expand_sparse", nF * (4 + 24 * static_cast<uint64_t>(hs.n)));
+                pendingPub = sa.pub;                               // read at the next hop's start
             }
-            R.hopNext.push_back(nF);
-            F = Fn;
-            if (nF == 0) break;                                    // GO_EXIT: empty frontier
             continue;
+        }
+        // the previous hop (sparse, sized on the device) published its total and the host has not read it:
+        // if this hop is predicted to pull (the last query's hop 2 did), its pull is launched first, reading
+        // E on the device (it does nothing when E is below the threshold), so the host's wait for the total
+        // overlaps the pull instead of idling the GPU (r05: 12-15 us per C2 step)
+        bool specPull = false;
+        uint8_t specEp = 0;
+        if (pendingPub.slot) {
+            const bool tryPull = !isFinal && pullable && c->world == 1 && c->pullPredict && !capped && !intermediateChecks;
+            if (tryPull) {
+                specEp = nextEpoch(c);
+                pa.out = marksA + d.gbase;
+                pa.ep = specEp;
+                pa.err = errFlag;
+                pa.dyn = counters + 2;                             // the sparse hop's packed (|F|, E)
+                pa.minE = pullMinE;
+                c->timed("pull", d.V * 9 * static_cast<uint64_t>(hs.n), [&] {
+                    if (launchPull(pa, c->stream)) throw Error{NGX_E_DEVICE, "pull"};
+                });
+            }
+            const uint64_t packed = awaitPub(c, pendingPub, counters + 2);
+            pendingPub = Publish{nullptr, 0};
+            nF = packed >> kFdShift;
+            fusedE = packed & kFdMask;
+            c->addBytes("expand_sparse", nF * (4 + 24 * static_cast<uint64_t>(hs.n)));
+            R.hopNext.push_back(nF);
+            if (nF == 0) break;                                    // GO_EXIT: empty frontier
+            specPull = tryPull && fusedE >= pullMinE;
         }
         const bool devE = finalDev && isFinal;                   // E below is an upper bound; the device has it
         uint64_t nEnt = nF * static_cast<uint64_t>(hs.n);
@@ -3031,6 +3057,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         // (TTL / max-edges) decides which edges count
         // dyn: both expansions are enqueued and the device takes the one its E selects (pullMinE)
         bool pull = dyn ? pullable : pullable && !mask && E && E * 100 >= static_cast<uint64_t>(c->pullFactor) * d.V;
+        pull = pull || specPull;                                   // (the same threshold: pullMinE)
+        if (h == 2 && c->world == 1 && !dyn) c->pullPredict = pull;
         uint64_t eMaxShard = 0;                                  // the largest shard's E (from the pull gather)
         bool eMaxKnown = false;
         if (!dyn && pullGather) {
@@ -3076,8 +3104,9 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             c->addBytes("exchange", c->lastXchgBytes);
             R.hopXchg.push_back(c->lastXchgBytes);
         }
-        uint8_t ep = nextEpoch(c);
-        if (pull) {
+        uint8_t ep = specPull ? specEp : nextEpoch(c);
+        if (specPull) c->pullHops++;                               // launched above
+        if (pull && !specPull) {
             pa.out = marks + d.gbase;
             pa.ep = ep;
             pa.err = errFlag;
