@@ -140,6 +140,7 @@ struct ngx_ctx {
     uint64_t pinSeq = 0;                               // words [0, 2): scan totals; [kTailOff ..): query tail
     static constexpr size_t kPinBytes = 1024;
     static constexpr size_t kTailOff = 8;               // k_publish_tail: seq, error bits, extra words
+    static constexpr uint32_t kSeedSlot = 80;           // the seed hop's publication (nextPub)
     void* xchgUser = nullptr;
     std::map<int32_t, std::unique_ptr<Space>> spaces;
     std::string lastError;
@@ -926,9 +927,11 @@ T readScalar(ngx_ctx* c, const T* dev) {
 }
 
 // next publication slot for a scan total (none when the mapped buffer is unavailable)
-Publish nextPub(ngx_ctx* c) {
+// slot 0 (words 0..3) for every publication but the seed hop's, which has slot kSeedSlot of its own: a
+// hop sized on the device publishes while the seed total is still unread (spec1)
+Publish nextPub(ngx_ctx* c, uint32_t slotWord = 0) {
     if (!c->pinDev) return Publish{nullptr, 0};
-    return Publish{c->pinDev, ++c->pinSeq};
+    return Publish{c->pinDev + slotWord, ++c->pinSeq};
 }
 
 // the published scan total: poll the host-mapped slot (no stream round trip); after ~50 ms block on
@@ -946,11 +949,12 @@ uint64_t awaitPub(ngx_ctx* c, const Publish& p, const uint64_t* devCopy, uint64_
     if (!p.slot) { errBits(); return readScalar(c, devCopy); }
     auto t0 = std::chrono::steady_clock::now();
     // kernels.h Publish: the words are taken once the tag matches them
+    uint64_t* const w = c->pin + (p.slot - c->pinDev);            // the slot's host view
     auto take = [&](uint64_t& v) {
-        const uint64_t tag = __atomic_load_n(&c->pin[1], __ATOMIC_ACQUIRE);
-        v = __atomic_load_n(&c->pin[0], __ATOMIC_ACQUIRE);
-        const uint64_t x = __atomic_load_n(&c->pin[2], __ATOMIC_ACQUIRE);
-        const uint64_t x2 = __atomic_load_n(&c->pin[3], __ATOMIC_ACQUIRE);
+        const uint64_t tag = __atomic_load_n(&w[1], __ATOMIC_ACQUIRE);
+        v = __atomic_load_n(&w[0], __ATOMIC_ACQUIRE);
+        const uint64_t x = __atomic_load_n(&w[2], __ATOMIC_ACQUIRE);
+        const uint64_t x2 = __atomic_load_n(&w[3], __ATOMIC_ACQUIRE);
         if (tag != pubTag(p.seq, v, x, x2)) return false;
         if (extra) *extra = x;
         if (extra2) *extra2 = x2;
@@ -2671,7 +2675,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             // stream round trip); the first hop's final-kernel words cleared on the way
             uint64_t* est0 = c->estart.get<uint64_t>(nEnt0 + 1);
             uint64_t* eb0 = c->ebase.get<uint64_t>(nEnt0 + 1);
-            Publish pub = nextPub(c);
+            Publish pub = nextPub(c, ngx_ctx::kSeedSlot);
             // seeds may repeat (no DISTINCT): E <= slot edges x the largest multiplicity
             const uint64_t mult = std::max<uint64_t>(maxMultiplicity(svids), 1);
             const uint64_t cf0 = (slotEdges * mult + kChunk - 1) / kChunk + 1;
