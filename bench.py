@@ -191,8 +191,10 @@ def main():
     p1_width = None
     prep_ms = tail_ms = 0.0
     timed = [prepared[(id(plans[args.warmup + i]), True, False)] for i in range(args.steps)]
+    overlaps = eng.get_flag("batch_overlaps")
     if args.host_loop == "native":
-        # the K steps in one native loop over the prepared plans (ngx_go_batch: each is one ngx_go)
+        # the K steps in one native loop over the prepared plans (ngx_go_batch: each is one ngx_go; the
+        # next query's host work and first hops enqueued while this one's final hop runs)
         for code, nrows, e in eng.go_batch(timed):
             if code:
                 raise RuntimeError(f"GO failed in the timed loop ({code}): {eng.L.ngx_last_error(eng.h).decode()}")
@@ -206,6 +208,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t_start
+    overlaps = eng.get_flag("batch_overlaps") - overlaps
     # the same steps again with per-kernel HIP events (their records would perturb the timed loop), one
     # Python call each: per-step statistics
     eng.set_profiling(True)
@@ -381,6 +384,7 @@ def main():
                                  "note": "inside ngx_go: before the first launch (plan, programs, seeds) / after the "
                                          "device finished; the rest of ms_per_step - device_ms is the Python caller"},
             "host_loop": args.host_loop,
+            "batch_overlaps": overlaps,
             "timed_region": ("seeds on host -> the YIELD columns of every result row in HBM (result_on_device; "
                              + ("yield_only: e._dst / e._rank alias the dst / rank row arrays, no src array"
                                 if args.yield_only else "and the src / dst / rank row arrays") + ")"),

@@ -375,10 +375,14 @@ int32_t ngx_go(ngx_ctx* ctx, const ngx_go_plan* plan, ngx_go_result** out);
 void ngx_go_result_free(ngx_go_result* r);
 /* n GO plans run back to back, each exactly as one ngx_go call whose result is freed at once (a native
  * host loop: a graphd driving many queries, the bench's timed steps). Per query: its code, result rows
- * and edges scanned over all hops (codes / nrows / edges may be NULL). Device-resident results of the
- * last query stay in HBM as ngx_go leaves them. Returns the first code that is not NGX_OK. */
+ * and edges scanned over all hops, and with `digests` (3 words per query) ngx_go_result_digest of its
+ * device-resident result (codes / nrows / edges / digests may be NULL). Consecutive device-resident
+ * plans without DISTINCT or input overlap (flag "batch_pipeline", default 1): the next query's host
+ * preparation and first hops are enqueued while this one's final hop runs; every query's outcome is the
+ * one it has alone. Device-resident results of the last query stay in HBM as ngx_go leaves them.
+ * Returns the first code that is not NGX_OK. */
 int32_t ngx_go_batch(ngx_ctx* ctx, const ngx_go_plan* const* plans, int32_t n, int32_t* codes, uint64_t* nrows,
-                     uint64_t* edges);
+                     uint64_t* edges, uint64_t* digests);
 
 /* Copy `bytes` from device memory of this context (e.g. a result_on_device array) to host memory,
  * ordered after the context's work. */
@@ -452,8 +456,11 @@ int32_t ngx_kernel_stats(ngx_ctx* ctx, const ngx_kernel_stat** out, int32_t* n);
  *          every value (applies at the next commit); 0: 8 bytes each. Same results.
  *   "compact_lane_rows"  rows per lane of the next-frontier compaction: 0 (default) = 4; 8 / 16 fewer,
  *          fatter waves (measured slower at C2). Same results.
+ *   "batch_pipeline"  1 (default): ngx_go_batch overlaps consecutive device-resident queries (the next
+ *          one's host work and first hops enqueued while this one's final hop runs); 0: strictly one
+ *          after the other. Same results.
  * Read-only counters for ngx_get_flag: "jit_compiled", "jit_hits", "jit_failed", "jit_compile_us",
- * "jit_cached", "jit_evicted". */
+ * "jit_cached", "jit_evicted", "batch_overlaps" (queries of ngx_go_batch that overlapped the next). */
 int32_t ngx_set_flag(ngx_ctx* ctx, const char* name, int64_t value);
 int32_t ngx_get_flag(ngx_ctx* ctx, const char* name, int64_t* value);
 /* why the last query ran on the interpreter kernels instead of a generated one ("" if it did not) */

@@ -24,6 +24,9 @@
 #include <thread>
 #include <unordered_set>
 
+#include <sys/mman.h>
+#include <ucontext.h>
+
 #include "exprc.h"
 #include "jit.h"
 #include "kernels.h"
@@ -141,6 +144,12 @@ struct ngx_ctx {
     static constexpr size_t kPinBytes = 1024;
     static constexpr size_t kTailOff = 8;               // k_publish_tail: seq, error bits, extra words
     static constexpr uint32_t kSeedSlot = 80;           // the seed hop's publication (nextPub)
+    static constexpr uint32_t kRowsSlot = 88;           // a record hop's row count (k_final_close)
+    // ngx_go_batch: the next query's host preparation and first hops enqueued while this one's final hop
+    // runs (flag "batch_pipeline"; read-only "batch_overlaps" counts the queries that overlapped)
+    bool batchPipeline = true;
+    struct GoPipe* pipe = nullptr;
+    uint64_t pipeOverlaps = 0;
     void* xchgUser = nullptr;
     std::map<int32_t, std::unique_ptr<Space>> spaces;
     std::string lastError;
@@ -196,7 +205,7 @@ struct ngx_ctx {
     } hostStage, inStage, seedStage;
     std::string progLast;                               // the bytes of the last program upload ...
     const char* progLastPtr = nullptr;                  // ... and where they went (uploadPrograms skips a repeat)
-    size_t progStageBytes = 0;                          // bytes of inStage holding this call's programs                               // results D2H / query inputs H2D (programs, seeds)
+    std::string progImg;                                // this call's program bytes (compared before staging)
     std::vector<ColBuf> oCols;                          // result columns (columnar, HBM)
     std::vector<ColBuf> dCols;                          // DISTINCT: the other half of each column's double buffer
     std::vector<OutCol> oColView;                       // their device pointers, as uploaded to oColDesc
@@ -327,6 +336,32 @@ struct ngx_ctx {
         pending.clear();
         eventNext = 0;
     }
+};
+
+// ngx_go_batch's pipeline. The batch's queries run as coroutines (ucontext) on the calling thread, one
+// at a time, each on a stack of its own. A query whose last final hop is enqueued yields before it waits
+// for the row count (it is "deferred"); the next query then prepares and enqueues its first hops —
+// after the deferred query's final hop in the stream's order — up to its first wait for a device total,
+// and yields back; the deferred query finishes (its row count and result), then the next one goes on.
+// The GPU runs one query's last kernel and the next one's first back to back: the host's result tail,
+// preparation and launch calls overlap the final hop instead of idling the GPU between queries. Only one
+// coroutine runs at any time, so the context needs no lock between them; what the two queries share on
+// the host (publication slots, the row-count device word, the program stage) is kept apart (kRowsSlot,
+// goDeferPoint, uploadPrograms).
+struct GoJob {
+    ucontext_t uc;
+    int32_t idx = 0;
+    int state = 0;
+    bool yieldAtAwait = false;                         // started while another query is deferred
+    int32_t rc = NGX_OK;
+    uint64_t nrows = 0, edges = 0, digest[3] = {0, 0, 0};
+};
+struct GoPipe {
+    enum { kRunning = 0, kDeferred = 1, kFrontDone = 2, kDone = 3 };
+    ucontext_t main;
+    GoJob* cur = nullptr;
+    const ngx_go_plan* const* plans = nullptr;
+    int32_t n = 0;
 };
 
 namespace {
@@ -510,21 +545,24 @@ DevPrograms uploadPrograms(ngx_ctx* c, const Programs& pr, const std::vector<int
     const size_t capBefore = c->progBuf.cap;
     char* base = c->progBuf.get<char>(total);
     if (c->progBuf.cap != capBefore) c->progLastPtr = nullptr;   // a new allocation (maybe at the old address)
-    // staged in page-locked memory: the copy is asynchronous (the stage is reused only by the next call,
-    // after this one has synchronised with its kernels)
-    char* host = c->inStage.get(total);
-    c->progStageBytes = total;
-    std::memset(host, 0, total);
-    std::memcpy(host, pr.code.data(), codeBytes);
-    std::memcpy(host + codeBytes, pr.yOff.data(), yBytes);
-    std::memcpy(host + codeBytes + yBytes, ySlotType.data(), tBytes);
-    std::memcpy(host + codeBytes + yBytes + tBytes, yColType.data(), cBytes);
-    std::memcpy(host + poolOff, pr.pool.data(), pr.pool.size());
+    std::string& img = c->progImg;
+    img.assign(total, '\0');
+    std::memcpy(&img[0], pr.code.data(), codeBytes);
+    std::memcpy(&img[codeBytes], pr.yOff.data(), yBytes);
+    std::memcpy(&img[codeBytes + yBytes], ySlotType.data(), tBytes);
+    std::memcpy(&img[codeBytes + yBytes + tBytes], yColType.data(), cBytes);
+    std::memcpy(&img[poolOff], pr.pool.data(), pr.pool.size());
     // the same bytes as the last upload into the same buffer (a prepared query run again): nothing to copy
     // (a copy launch and its dispatch gap, ~7 us of the C2 step on the device timeline)
-    if (base != c->progLastPtr || c->progLast.size() != total || std::memcmp(c->progLast.data(), host, total) != 0) {
+    if (base != c->progLastPtr || c->progLast != img) {
+        // staged in page-locked memory: the copy is asynchronous (the stage is reused only by the next
+        // call, after this one has synchronised with its kernels — or, in a batch whose previous query is
+        // deferred (goDeferPoint), once that query's work is drained)
+        if (c->pipe && c->pipe->cur && c->pipe->cur->yieldAtAwait) HIP_OK(hipStreamSynchronize(c->stream));
+        char* host = c->inStage.get(total);
+        std::memcpy(host, img.data(), total);
         HIP_OK(hipMemcpyAsync(base, host, total, hipMemcpyHostToDevice, c->stream));
-        c->progLast.assign(host, total);
+        c->progLast = img;
         c->progLastPtr = base;
     }
     DevPrograms d;
@@ -934,6 +972,36 @@ Publish nextPub(ngx_ctx* c, uint32_t slotWord = 0) {
     return Publish{c->pinDev + slotWord, ++c->pinSeq};
 }
 
+// a plan whose host work may overlap another query's final hop (and whose own final hop may be overlapped):
+// device-resident rows without DISTINCT, no input table
+bool pipelinable(const ngx_go_plan& p) {
+    return p.result_on_device && !p.distinct && !p.input_vid_col && p.record_to > 0;
+}
+
+void pipeSwitch(ngx_ctx* c, int state) {
+    GoJob* j = c->pipe->cur;
+    j->state = state;
+    swapcontext(&j->uc, &c->pipe->main);
+    j->state = GoPipe::kRunning;
+}
+
+// awaitPub's first call in a query started while another is deferred: hand the thread back
+void pipeFrontYield(ngx_ctx* c) {
+    GoJob* j = c->pipe ? c->pipe->cur : nullptr;
+    if (!j || !j->yieldAtAwait) return;
+    j->yieldAtAwait = false;
+    pipeSwitch(c, GoPipe::kFrontDone);
+}
+
+// the last final hop's close is enqueued: defer the wait for its row count while the next query starts
+void goDeferPoint(ngx_ctx* c) {
+    GoPipe* P = c->pipe;
+    GoJob* j = P ? P->cur : nullptr;
+    if (!j || j->yieldAtAwait || j->idx + 1 >= P->n || !pipelinable(*P->plans[j->idx + 1])) return;
+    c->pipeOverlaps++;
+    pipeSwitch(c, GoPipe::kDeferred);
+}
+
 // the published scan total: poll the host-mapped slot (no stream round trip); after ~50 ms block on
 // the stream, and read the device copy if the slot still disagrees. extra (final-hop publications):
 // the word published beside the value (the query's error bits), or read from errDev on the fallback.
@@ -946,6 +1014,7 @@ uint64_t awaitPub(ngx_ctx* c, const Publish& p, const uint64_t* devCopy, uint64_
         *extra = 0;
         for (int k = 0; k < 4; k++) *extra |= static_cast<uint64_t>(f[k] != 0) << k;
     };
+    if (c->pipe) pipeFrontYield(c);
     if (!p.slot) { errBits(); return readScalar(c, devCopy); }
     auto t0 = std::chrono::steady_clock::now();
     // kernels.h Publish: the words are taken once the tag matches them
@@ -1577,9 +1646,15 @@ int32_t ngx_synchronize(ngx_ctx* c) {
     return NGX_OK;
 }
 
+static int32_t resultDigest(ngx_ctx* c, const ngx_go_result* r, uint64_t out[3]);
 int32_t ngx_go_result_digest(ngx_ctx* c, const ngx_go_result* r, uint64_t out[3]) {
     if (!c || !r || !out) return NGX_E_BAD_ARGUMENT;
     std::lock_guard<std::mutex> g(c->mu);
+    return resultDigest(c, r, out);
+}
+
+// ngx_go_result_digest under the caller's lock
+static int32_t resultDigest(ngx_ctx* c, const ngx_go_result* r, uint64_t out[3]) {
     try {
         HIP_OK(hipSetDevice(c->device));
         if (r->code != NGX_OK || (r->nrows && !r->dev_cols && r->ncols)) return fail(c, NGX_E_BAD_ARGUMENT, "digest: not a device-resident result");
@@ -1644,6 +1719,7 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
     if (n == "enable_reservoir_sampling") { c->reservoirSampling = value != 0; return NGX_OK; }
     if (n == "narrow_columns") { c->narrowColumns = value != 0; return NGX_OK; }
     if (n == "trace_go") { c->traceGo = value != 0; return NGX_OK; }
+    if (n == "batch_pipeline") { c->batchPipeline = value != 0; return NGX_OK; }
     if (n == "compact_lane_rows") {
         if (value != 0 && value != 4 && value != 8 && value != 16) return fail(c, NGX_E_BAD_ARGUMENT, "compact_lane_rows: 0, 4, 8 or 16");
         c->compactLaneRows = static_cast<int32_t>(value);
@@ -1668,6 +1744,8 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "enable_reservoir_sampling") *value = c->reservoirSampling ? 1 : 0;
     else if (n == "narrow_columns") *value = c->narrowColumns ? 1 : 0;
     else if (n == "trace_go") *value = c->traceGo ? 1 : 0;
+    else if (n == "batch_pipeline") *value = c->batchPipeline ? 1 : 0;
+    else if (n == "batch_overlaps") *value = static_cast<int64_t>(c->pipeOverlaps);
     else if (n == "compact_lane_rows") *value = c->compactLaneRows;
     else if (n == "pull_hops") *value = static_cast<int64_t>(c->pullHops);
     else if (n == "sparse_hops") *value = static_cast<int64_t>(c->sparseHops);
@@ -2700,6 +2778,41 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             });
         }
     }
+    // spec1: hop 1's sparse kernel enqueued right behind the seed hop, before the host prepares the
+    // programs below (the GPU idled ~4 us between the two while the host did that first)
+    SparseArgs sa1{};
+    uint32_t* F1spec = nullptr;
+    const bool devNext1 = spec1 && finalDev && steps == 2;
+    if (spec1) {
+        if (!c->bitsClean || c->bitsCleanPtr != lbits) HIP_OK(hipMemsetAsync(lbits, 0, (d.V + 63) / 64 * 8, c->stream));
+        c->bitsClean = false;
+        if (!c->sparseCtl.p) {
+            c->sparseCtl.get<uint64_t>(2);
+            HIP_OK(hipMemsetAsync(c->sparseCtl.p, 0, c->sparseCtl.cap, c->stream));
+        }
+        F1spec = (F == c->F0.p) ? c->F1.get<uint32_t>(std::max<uint64_t>(d.V, 1)) : c->F0.get<uint32_t>(std::max<uint64_t>(d.V, 1));
+        sa1.F = F; sa1.estart = static_cast<const uint64_t*>(c->estart.p); sa1.chunkFirst = static_cast<const uint64_t*>(c->chunkFirst.p);
+        sa1.ebase = static_cast<const uint64_t*>(c->ebase.p);
+        sa1.dynIn = dynStats;                                      // the seed kernel's packed (|F|, E)
+        sa1.hs = hs;
+        sa1.bits = lbits;
+        sa1.bitWords = (d.V + 63) / 64;
+        sa1.outF = F1spec;
+        sa1.outEst = c->estart2.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
+        sa1.outEbase = c->ebase2.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
+        sa1.outCf = c->chunkFirst2.get<uint64_t>(cfCap);
+        sa1.cfCap = cfCap;
+        sa1.ctl = static_cast<uint64_t*>(c->sparseCtl.p);
+        sa1.total = devNext1 ? dynStats + 1 : counters + 2;
+        sa1.pub = devNext1 ? Publish{nullptr, 0} : nextPub(c);
+        sa1.err = errFlag;
+        c->timed("expand_sparse", 0, [&] {
+            if (launchExpandSparse(sa1, pos32, c->stream)) throw Error{NGX_E_DEVICE, "sparse expand"};
+        });
+        std::swap(c->estart, c->estart2);
+        std::swap(c->ebase, c->ebase2);
+        std::swap(c->chunkFirst, c->chunkFirst2);
+    }
     // the programs and the generated kernels, prepared while the seed hop runs (only the record hops
     // read them)
     DevPrograms dp = uploadPrograms(c, progs, ySlotType, gp.colTypes);
@@ -2768,37 +2881,10 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         bool isRecord = h >= recordFrom;
         bool isFinal = h == steps;
         if (spec1 && h == 1) {
-            // the seed hop's frontier expanded by the sparse kernel, its size read on the device
-            if (!c->bitsClean || c->bitsCleanPtr != lbits) HIP_OK(hipMemsetAsync(lbits, 0, (d.V + 63) / 64 * 8, c->stream));
-            c->bitsClean = false;
-            if (!c->sparseCtl.p) {
-                c->sparseCtl.get<uint64_t>(2);
-                HIP_OK(hipMemsetAsync(c->sparseCtl.p, 0, c->sparseCtl.cap, c->stream));
-            }
-            const bool devNext = finalDev && h + 1 == steps;
-            uint32_t* Fn = (F == c->F0.p) ? c->F1.get<uint32_t>(std::max<uint64_t>(d.V, 1)) : c->F0.get<uint32_t>(std::max<uint64_t>(d.V, 1));
-            SparseArgs sa{};
-            sa.F = F; sa.estart = static_cast<const uint64_t*>(c->estart.p); sa.chunkFirst = static_cast<const uint64_t*>(c->chunkFirst.p);
-            sa.ebase = static_cast<const uint64_t*>(c->ebase.p);
-            sa.dynIn = dynStats;                                  // the seed kernel's packed (|F|, E)
-            sa.hs = hs;
-            sa.bits = lbits;
-            sa.bitWords = (d.V + 63) / 64;
-            sa.outF = Fn;
-            sa.outEst = c->estart2.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
-            sa.outEbase = c->ebase2.get<uint64_t>(d.V * static_cast<uint64_t>(hs.n) + 1);
-            sa.outCf = c->chunkFirst2.get<uint64_t>(cfCap);
-            sa.cfCap = cfCap;
-            sa.ctl = static_cast<uint64_t*>(c->sparseCtl.p);
-            sa.total = devNext ? dynStats + h : counters + 2;
-            sa.pub = devNext ? Publish{nullptr, 0} : nextPub(c);
-            sa.err = errFlag;
-            c->timed("expand_sparse", 0, [&] {
-                if (launchExpandSparse(sa, pos32, c->stream)) throw Error{NGX_E_DEVICE, "sparse expand"};
-            });
-            std::swap(c->estart, c->estart2);
-            std::swap(c->ebase, c->ebase2);
-            std::swap(c->chunkFirst, c->chunkFirst2);
+            // the seed hop's frontier expanded by the sparse kernel (launched above), its size read on the device
+            const bool devNext = devNext1;
+            uint32_t* Fn = F1spec;
+            const SparseArgs& sa = sa1;
             const uint64_t E1 = awaitPub(c, seedPub, seedE);     // published before the sparse kernel ran
             R.hopFrontier.push_back(nF);
             R.hopEdges.push_back(E1);
@@ -2976,7 +3062,9 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             a.oType = constType ? nullptr : static_cast<int32_t*>(c->oType.p);
             a.oEntry = nullptr;
             a.lbStatus = nullptr;
-            Publish rowsPub = dyn ? Publish{nullptr, 0} : nextPub(c);   // k_final_close publishes the row count
+            // k_final_close publishes the row count, in a slot of its own (a batch's next query publishes its
+            // first hops' totals while this one is deferred: goDeferPoint)
+            Publish rowsPub = dyn ? Publish{nullptr, 0} : nextPub(c, ngx_ctx::kRowsSlot);
             a.rowsPub = rowsPub.slot;
             a.rowsSeq = rowsPub.seq;
             a.dynTotal = dynTotal;
@@ -3021,7 +3109,13 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             if (!dyn) {
                 // GO: the row count and the query's error bits so far, published by k_final_close
                 uint64_t fin = 0;                               // devE: this hop's packed (|F|, E)
-                uint64_t nrows = awaitPub(c, rowsPub, c->resvRows, &finalErrBits, errFlag, devE ? &fin : nullptr,
+                const uint64_t* rowsDev = c->resvRows;          // (the next query resets c->resvRows)
+                // ngx_go_batch: the next query starts here, before the wait. Not with a device read-back left
+                // (multi-root walks), string arenas, profiling or host traces, nor at world > 1
+                if (c->pipe && isFinal && rowsPub.slot && !rw && c->world == 1 && nStrOut == 0 && !c->prof && !c->htrace &&
+                    !c->traceGo && pipelinable(p))
+                    goDeferPoint(c);
+                uint64_t nrows = awaitPub(c, rowsPub, rowsDev, &finalErrBits, errFlag, devE ? &fin : nullptr,
                                           devE ? dynTotal : nullptr);
                 haveFinalErrs = true;
                 if (devE) {                                     // the hop's statistics, known now
@@ -3838,8 +3932,10 @@ int32_t runPipe(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R) 
 
 }  // namespace
 
-extern "C" int32_t ngx_go(ngx_ctx* c, const ngx_go_plan* p, ngx_go_result** out) {
-    std::lock_guard<std::mutex> g(c->mu);
+namespace {
+
+// ngx_go under the caller's lock of c->mu
+int32_t goCall(ngx_ctx* c, const ngx_go_plan* p, ngx_go_result** out) {
     auto R = std::make_unique<GoResultHolder>();
     R->tIn = std::chrono::steady_clock::now();
     R->tLaunch = R->tDone = R->tIn;
@@ -3886,23 +3982,135 @@ extern "C" int32_t ngx_go(ngx_ctx* c, const ngx_go_plan* p, ngx_go_result** out)
     return rc;
 }
 
-// A native host loop over prepared plans: each is exactly one ngx_go (its result freed at once), so a
-// caller that drives many queries (a graphd, the bench) pays no interpreter between them.
-extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int32_t n, int32_t* codes, uint64_t* nrows,
-                                uint64_t* edges) {
-    if (!c || (n > 0 && !plans)) return NGX_E_BAD_ARGUMENT;
-    int32_t first = NGX_OK;
-    for (int32_t i = 0; i < n; i++) {
-        ngx_go_result* r = nullptr;
-        const int32_t rc = ngx_go(c, plans[i], &r);
-        uint64_t e = 0;
-        if (r) for (int32_t h = 0; h < r->nhops; h++) e += r->hop_edges[h];
-        if (codes) codes[i] = rc;
-        if (nrows) nrows[i] = r ? r->nrows : 0;
-        if (edges) edges[i] = e;
-        if (r) ngx_go_result_free(r);
-        if (rc != NGX_OK && first == NGX_OK) first = rc;
+// one query of a batch: exactly one ngx_go, its counts (and digest) kept, its result freed at once
+void batchQuery(ngx_ctx* c, const ngx_go_plan* p, GoJob& j, bool digest) {
+    ngx_go_result* r = nullptr;
+    try {
+        j.rc = goCall(c, p, &r);
+        j.nrows = r ? r->nrows : 0;
+        j.edges = 0;
+        if (r) for (int32_t h = 0; h < r->nhops; h++) j.edges += r->hop_edges[h];
+        // a result the digest does not cover (host rows, string columns) keeps zeros
+        if (digest && r && j.rc == NGX_OK && p->result_on_device && resultDigest(c, r, j.digest) != NGX_OK)
+            j.digest[0] = j.digest[1] = j.digest[2] = 0;
+    } catch (...) {                                     // nothing unwinds past a coroutine's entry
+        j.rc = NGX_E_DEVICE;
+        (void)hipStreamSynchronize(c->stream);
     }
+    if (r) ngx_go_result_free(r);
+}
+
+struct BatchCo {
+    ngx_ctx* c;
+    GoPipe* P;
+    bool digest;
+};
+thread_local BatchCo* tBatch = nullptr;
+
+void batchEntry() {
+    BatchCo* b = tBatch;
+    GoJob* j = b->P->cur;
+    batchQuery(b->c, b->P->plans[j->idx], *j, b->digest);
+    j->state = GoPipe::kDone;                           // uc_link: back to the batch loop
+}
+
+// a coroutine stack: 16 MB reserved (pages committed on first touch), a guard page below it
+struct CoStack {
+    void* base = nullptr;
+    size_t bytes = 0;
+    bool make(size_t sz) {
+        const size_t guard = 4096;
+        void* m = mmap(nullptr, sz + guard, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE | MAP_STACK, -1, 0);
+        if (m == MAP_FAILED) return false;
+        (void)mprotect(m, guard, PROT_NONE);
+        base = m;
+        bytes = sz + guard;
+        return true;
+    }
+    ~CoStack() { if (base) munmap(base, bytes); }
+};
+
+}  // namespace
+
+extern "C" int32_t ngx_go(ngx_ctx* c, const ngx_go_plan* p, ngx_go_result** out) {
+    std::lock_guard<std::mutex> g(c->mu);
+    return goCall(c, p, out);
+}
+
+// A native host loop over prepared plans: each is exactly one ngx_go (its result freed at once), so a
+// caller that drives many queries (a graphd, the bench) pays no interpreter between them. Consecutive
+// pipelinable plans overlap (GoPipe above): the next query's host work and first hops are enqueued while
+// this one's final hop runs. Every query's rows, counts and errors are those it has alone.
+extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int32_t n, int32_t* codes, uint64_t* nrows,
+                                uint64_t* edges, uint64_t* digests) {
+    if (!c || (n > 0 && !plans)) return NGX_E_BAD_ARGUMENT;
+    for (int32_t i = 0; i < n; i++) if (!plans[i]) return NGX_E_BAD_ARGUMENT;
+    std::lock_guard<std::mutex> g(c->mu);
+    int32_t first = NGX_OK;
+    auto record = [&](const GoJob& j) {
+        if (codes) codes[j.idx] = j.rc;
+        if (nrows) nrows[j.idx] = j.nrows;
+        if (edges) edges[j.idx] = j.edges;
+        if (digests) for (int k = 0; k < 3; k++) digests[3 * static_cast<size_t>(j.idx) + k] = j.digest[k];
+        if (j.rc != NGX_OK && first == NGX_OK) first = j.rc;
+    };
+    bool pipe = c->batchPipeline && n > 1 && c->world == 1 && !c->prof && !c->htrace && !c->traceGo;
+    CoStack stacks[2];
+    for (int k = 0; pipe && k < 2; k++) pipe = stacks[k].make(16u << 20);
+    if (!pipe) {
+        for (int32_t i = 0; i < n; i++) {
+            GoJob j;
+            j.idx = i;
+            batchQuery(c, plans[i], j, digests != nullptr);
+            record(j);
+        }
+        return first;
+    }
+    GoPipe P;
+    P.plans = plans;
+    P.n = n;
+    BatchCo co{c, &P, digests != nullptr};
+    GoJob jobs[2];
+    auto start = [&](int32_t i, bool front) -> GoJob* {
+        GoJob& j = jobs[i & 1];
+        j = GoJob{};
+        j.idx = i;
+        j.yieldAtAwait = front;
+        getcontext(&j.uc);
+        j.uc.uc_stack.ss_sp = static_cast<char*>(stacks[i & 1].base) + 4096;
+        j.uc.uc_stack.ss_size = stacks[i & 1].bytes - 4096;
+        j.uc.uc_link = &P.main;
+        makecontext(&j.uc, batchEntry, 0);
+        return &j;
+    };
+    auto resume = [&](GoJob* j) {
+        P.cur = j;
+        tBatch = &co;
+        swapcontext(&P.main, &j->uc);
+        P.cur = nullptr;
+        return j->state;
+    };
+    c->pipe = &P;
+    GoJob* a = start(0, false);
+    int st = resume(a);
+    for (;;) {
+        if (st == GoPipe::kDeferred) {
+            // a waits for its row count: the next query runs up to its first wait (or to its end), then a
+            // finishes, then the next one goes on
+            GoJob* b = start(a->idx + 1, true);
+            int sb = resume(b);
+            while (resume(a) != GoPipe::kDone) {}         // a query defers once; nothing else yields it
+            record(*a);
+            a = b;
+            st = sb == GoPipe::kFrontDone ? resume(a) : sb;
+            continue;
+        }
+        record(*a);                                       // kDone
+        if (a->idx + 1 >= n) break;
+        a = start(a->idx + 1, false);
+        st = resume(a);
+    }
+    c->pipe = nullptr;
     return first;
 }
 

@@ -183,7 +183,7 @@ SIGNATURES = {
     "ngx_gn_result_free": (None, [P(GnResult)]),
     "ngx_go": (c_i32, [ctypes.c_void_p, P(GoPlan), P(P(GoResultC))]),
     "ngx_go_result_free": (None, [P(GoResultC)]),
-    "ngx_go_batch": (c_i32, [ctypes.c_void_p, ctypes.c_void_p, c_i32, P(c_i32), P(c_u64), P(c_u64)]),
+    "ngx_go_batch": (c_i32, [ctypes.c_void_p, ctypes.c_void_p, c_i32, P(c_i32), P(c_u64), P(c_u64), P(c_u64)]),
     "ngx_set_profiling": (c_i32, [ctypes.c_void_p, c_i32]),
     "ngx_synchronize": (c_i32, [ctypes.c_void_p]),
     "ngx_go_result_digest": (c_i32, [ctypes.c_void_p, P(GoResultC), P(c_u64)]),
@@ -592,14 +592,19 @@ class Engine:
         finally:
             self.L.ngx_go_result_free(out)
 
-    def go_batch(self, prepared: Sequence["PreparedGo"]):
+    def go_batch(self, prepared: Sequence["PreparedGo"], digests: bool = False):
         """Run prepared GO plans back to back in one native call (ngx_go_batch): per query (code, result
-        rows, edges scanned over all hops)."""
+        rows, edges scanned over all hops), plus with `digests` the device-resident result's digest
+        (sum, xor, count as ngx_go_result_digest; zeros for a failed query)."""
         n = len(prepared)
         arr = (ctypes.POINTER(GoPlan) * max(n, 1))(*[ctypes.pointer(p.plan) for p in prepared])
         codes, rows, edges = (c_i32 * max(n, 1))(), (c_u64 * max(n, 1))(), (c_u64 * max(n, 1))()
-        self.L.ngx_go_batch(self.h, ctypes.cast(arr, ctypes.c_void_p), n, codes, rows, edges)
-        return [(int(codes[i]), int(rows[i]), int(edges[i])) for i in range(n)]
+        dg = (c_u64 * max(3 * n, 1))() if digests else None
+        self.L.ngx_go_batch(self.h, ctypes.cast(arr, ctypes.c_void_p), n, codes, rows, edges, dg)
+        out = [(int(codes[i]), int(rows[i]), int(edges[i])) for i in range(n)]
+        if digests:
+            out = [o + ((int(dg[3 * i]), int(dg[3 * i + 1]), int(dg[3 * i + 2])),) for i, o in enumerate(out)]
+        return out
 
     def prepare_go(self, space: int, s, pushdown: bool = True, now_sec: int = 0, on_device: bool = False,
                    columnar: bool = False, yield_only: bool = False, input=None, compact: bool = False) -> PreparedGo:

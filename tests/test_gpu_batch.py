@@ -1,0 +1,142 @@
+"""ngx_go_batch (the native loop over prepared GO plans) against the same plans run one ngx_go at a time
+and against the oracle, with the batch pipeline on and off.
+
+With "batch_pipeline" on, consecutive device-resident plans overlap: a query whose final hop is enqueued
+yields before it waits for its row count, and the next one prepares and enqueues its first hops (seed,
+sparse and pulled hops, program uploads) behind it on the stream (engine.cpp GoPipe). Every query's code,
+row count, per-hop scanned edges (summed) and the value digest of its device-resident rows
+(ngx_go_result_digest) must be what the query has alone — mixes of pipelinable plans with DISTINCT, host
+results, failing queries, empty frontiers and changing programs, in orders that put each kind before
+and after the others.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from nebula_amd import datagen, engine, ngql
+from oracle import oracle
+from tests import fixtures
+from tests.test_gpu_pull import RMAT_Q
+
+pytestmark = pytest.mark.gpu
+
+EXTRA_Q = [
+    "GO FROM {S} OVER e YIELD e._dst, e.p0",                               # one hop
+    "GO 2 STEPS FROM {S} OVER e WHERE e.p1 % (e.p0 - e.p0) > 1 YIELD e._dst",   # fails (division by zero)
+    "GO 3 STEPS FROM 4398046511104 OVER e YIELD e._dst",                     # no such vertex: no rows
+    "GO 3 STEPS FROM {S} OVER e WHERE e.p0 < 50 YIELD e._src, e._dst, e._rank, e.p0, e.p1",
+]
+
+
+@pytest.fixture(scope="module")
+def rmat():
+    ds = fixtures.RmatDataset(12, with_in=True, with_tag=True)
+    o = oracle.Oracle()
+    o.set_flags(threads=8)
+    ds.load_oracle(o)
+    e = engine.Engine(0)
+    ds.load_engine(e)
+    yield ds, o, e
+    e.close()
+    o.close()
+
+
+def _queries(ds, n_seed_sets=2):
+    out = []
+    for qi, q in enumerate(RMAT_Q + EXTRA_Q):
+        for k in range(n_seed_sets):
+            seeds = datagen.sample_vids(5100 + 10 * qi + k, 1 << ds.scale, (25, 3)[k % 2])
+            out.append(q.replace("{S}", ", ".join(str(int(v)) for v in seeds)))
+    return out
+
+
+def _prepare(e, ds, q, mode):
+    s = ngql.parse_go(q)
+    if mode == "compact":
+        return e.prepare_go(ds.space, s, on_device=True, compact=True)
+    if mode == "device":
+        return e.prepare_go(ds.space, s, on_device=True)
+    return e.prepare_go(ds.space, s)
+
+
+def _alone(e, ds, prep):
+    """(code, rows, edges, digest) of one prepared plan through ngx_go"""
+    on_dev = bool(prep.plan.result_on_device)
+    r = e.go(ds.space, prep, rows=False)
+    dig = (0, 0, 0)
+    if r.ok and on_dev:
+        r2 = e.go(ds.space, prep, rows=False, device_digest=True)
+        dig = r2.device_digest
+    return r.code, r.nrows, int(sum(r.hop_edges)) if r.ok else None, dig
+
+
+@pytest.mark.parametrize("pipeline", [1, 0])
+def test_batch_equals_one_at_a_time(rmat, pipeline):
+    ds, o, e = rmat
+    rng = random.Random(77)
+    qs = _queries(ds)
+    modes = ["compact", "device", "host"]
+    items = [(q, m) for q in qs for m in modes]
+    rng.shuffle(items)
+    # runs of pipelinable plans (the bench's shape) between the mixed ones
+    items = [(q, "compact") for q in qs[:6]] + items + [(q, "compact") for q in qs[-6:]]
+    preps = [_prepare(e, ds, q, m) for q, m in items]
+    want = [_alone(e, ds, p) for p in preps]
+    e.set_flag("batch_pipeline", pipeline)
+    before = e.get_flag("batch_overlaps")
+    got = e.go_batch(preps, digests=True)
+    overlaps = e.get_flag("batch_overlaps") - before
+    e.set_flag("batch_pipeline", 1)
+    for (q, m), w, g in zip(items, want, got):
+        code, rows, edges, dig = g
+        assert code == w[0], (q, m, g, w)
+        if code == 0:
+            assert (rows, edges) == (w[1], w[2]), (q, m)
+            # DISTINCT keeps one row of each group, whichever: its src (hashed with the row) is not fixed
+            if "DISTINCT" not in q:
+                assert tuple(dig) == tuple(w[3]), (q, m)
+    if pipeline:
+        assert overlaps >= 10
+    else:
+        assert overlaps == 0
+
+
+def test_batch_rows_equal_oracle(rmat):
+    """A pipelined run of the bench's query shape: every query's digest equals the oracle's rows."""
+    ds, o, e = rmat
+    preps, refs = [], []
+    for k in range(12):
+        seeds = datagen.sample_vids(6200 + k, 1 << ds.scale, 40)
+        w = (" WHERE e.p0 < 50", "", " WHERE e.p0 >= 50")[k % 3]
+        q = f"GO 3 STEPS FROM {', '.join(str(int(v)) for v in seeds)} OVER e{w} YIELD e._src, e._dst, e._rank, e.p0, e.p1"
+        s = ngql.parse_go(q)
+        ref = o.go(ds.space, s)
+        assert ref.ok
+        cols = [np.array([int(r[c][1]) for r in ref.rows], dtype=np.int64) for c in range(5)]
+        refs.append((len(ref.rows), int(sum(ref.hop_scanned)), oracle.row_digest([cols[0]] + cols)))
+        preps.append(e.prepare_go(ds.space, s, on_device=True, compact=True))
+    before = e.get_flag("batch_overlaps")
+    got = e.go_batch(preps, digests=True)
+    assert e.get_flag("batch_overlaps") - before == len(preps) - 1
+    for (code, rows, edges, dig), (nrows, scanned, rdig) in zip(got, refs):
+        assert code == 0
+        assert (rows, edges) == (nrows, scanned)
+        assert tuple(dig) == tuple(rdig)
+
+
+def test_batch_last_result_stays_on_device(rmat):
+    """The last query's rows are in HBM after the batch, as ngx_go leaves them: a following ngx_go of the
+    same plan returns the same digest, and the context keeps working after a pipelined batch whose last
+    query failed."""
+    ds, o, e = rmat
+    seeds = datagen.sample_vids(31, 1 << ds.scale, 30)
+    q = f"GO 3 STEPS FROM {', '.join(str(int(v)) for v in seeds)} OVER e YIELD e._dst, e.p1"
+    bad = f"GO 2 STEPS FROM {', '.join(str(int(v)) for v in seeds)} OVER e YIELD e.p1 / (e.p0 - e.p0)"
+    p = e.prepare_go(ds.space, ngql.parse_go(q), on_device=True, compact=True)
+    pb = e.prepare_go(ds.space, ngql.parse_go(bad), on_device=True, compact=True)
+    got = e.go_batch([p, p, pb], digests=True)
+    assert [g[0] for g in got] == [0, 0, engine.E_QUERY]
+    alone = e.go(ds.space, p, rows=False, device_digest=True)
+    assert alone.ok and tuple(got[0][3]) == tuple(got[1][3]) == alone.device_digest
+    assert e.go_batch([]) == []
