@@ -176,8 +176,14 @@ def main():
     for s_ in plans:                                        # encoded before the timed region
         prepared[(id(s_), True, False)] = eng.prepare_go(datagen.RMAT_SPACE, s_, on_device=True,
                                                          yield_only=args.yield_only, compact=not args.no_compact)
-    for i in range(args.warmup):
-        step(plans[i])
+    if args.host_loop == "native" and args.warmup:
+        # warmed through the timed loop's own path (the batch, its streams and coroutine stacks)
+        for code, _, _ in eng.go_batch([prepared[(id(plans[i]), True, False)] for i in range(args.warmup)]):
+            if code:
+                raise RuntimeError(f"GO failed in warmup ({code}): {eng.L.ngx_last_error(eng.h).decode()}")
+    else:
+        for i in range(args.warmup):
+            step(plans[i])
     log(f"[rank {rank}] warmup done")
     barrier()
     torch.cuda.synchronize()

@@ -141,7 +141,7 @@ struct ngx_ctx {
     uint64_t* pin = nullptr;                           // host-mapped [value, seq]: scan totals published by
     uint64_t* pinDev = nullptr;                        // k_scan_tiles (kernels.h Publish)
     uint64_t pinSeq = 0;                               // words [0, 2): scan totals; [kTailOff ..): query tail
-    static constexpr size_t kPinBytes = 1024;
+    static constexpr size_t kPinBytes = 4096;           // two lanes of 256 words (ngx_ctx::Lane)
     static constexpr size_t kTailOff = 8;               // k_publish_tail: seq, error bits, extra words
     static constexpr uint32_t kSeedSlot = 80;           // the seed hop's publication (nextPub)
     static constexpr uint32_t kRowsSlot = 88;           // a record hop's row count (k_final_close)
@@ -261,24 +261,76 @@ struct ngx_ctx {
     std::vector<hipEvent_t> eventPool;
     size_t eventNext = 0;
 
+    // A query lane: the per-query scratch of the hop loop and its publication slots (words [pinLane,
+    // pinLane + kLaneWords) of the host-mapped block). ngx_go_batch runs consecutive queries on alternate
+    // lanes, so that one query's hops run on the device beside the other's final hop (GoPipe). The active
+    // lane's fields are the members above, the other lane's are parked here; useLane swaps the two sets.
+    uint32_t pinLane = 0;
+    static constexpr uint32_t kLaneWords = 256;
+    struct Lane {
+        DBuf visited, F0, F1, estart, ebase, chunkFirst, estart2, ebase2, chunkFirst2, tileSums, counters, lbStatus,
+            seedPart, seedVid, cmpStatus[2], frontierBits, localBits, edgeMask, pullSeg, pullCtl, sparseCtl, dynStats, progBuf;
+        uint64_t visitedSize = 0, pullSegWords = 0;
+        uint8_t epoch = 0;
+        bool bitsClean = false;
+        const void* bitsCleanPtr = nullptr;
+        std::string progLast;
+        const char* progLastPtr = nullptr;
+        PinBuf inStage, seedStage;
+        uint32_t pinLane = kLaneWords;
+    } parked;
+    int activeLane = 0;
+    // ngx_go_batch's streams (GoPipe, created with the context at world 1): the queries' hops on the front
+    // stream, the last final hop of each overlapped query on the final stream; finalStream is set while a
+    // pipelined batch runs. The coroutine stacks of the batch's queries.
+    hipStream_t pipeStreams[2] = {nullptr, nullptr};
+    hipEvent_t pipeEv[3] = {nullptr, nullptr, nullptr};
+    hipStream_t finalStream = nullptr;
+    void* coStack[2] = {nullptr, nullptr};
+    static constexpr size_t kCoStackBytes = size_t(16) << 20;   // + a guard page below each
+    void swapLane() {
+#define NGX_LANE_SWAP(f) std::swap(f, parked.f);
+        NGX_LANE_SWAP(visited) NGX_LANE_SWAP(F0) NGX_LANE_SWAP(F1) NGX_LANE_SWAP(estart)
+        NGX_LANE_SWAP(ebase) NGX_LANE_SWAP(chunkFirst) NGX_LANE_SWAP(estart2) NGX_LANE_SWAP(ebase2) NGX_LANE_SWAP(chunkFirst2)
+        NGX_LANE_SWAP(tileSums) NGX_LANE_SWAP(counters) NGX_LANE_SWAP(lbStatus) NGX_LANE_SWAP(seedPart) NGX_LANE_SWAP(seedVid)
+        NGX_LANE_SWAP(cmpStatus[0]) NGX_LANE_SWAP(cmpStatus[1]) NGX_LANE_SWAP(frontierBits) NGX_LANE_SWAP(localBits)
+        NGX_LANE_SWAP(edgeMask) NGX_LANE_SWAP(pullSeg) NGX_LANE_SWAP(pullCtl) NGX_LANE_SWAP(sparseCtl) NGX_LANE_SWAP(dynStats)
+        NGX_LANE_SWAP(progBuf) NGX_LANE_SWAP(visitedSize) NGX_LANE_SWAP(pullSegWords) NGX_LANE_SWAP(epoch)
+        NGX_LANE_SWAP(bitsClean) NGX_LANE_SWAP(bitsCleanPtr) NGX_LANE_SWAP(progLast) NGX_LANE_SWAP(progLastPtr)
+        NGX_LANE_SWAP(inStage) NGX_LANE_SWAP(seedStage) NGX_LANE_SWAP(pinLane)
+#undef NGX_LANE_SWAP
+    }
+    void useLane(int k) {
+        if (k != activeLane) { swapLane(); activeLane = k; }
+    }
+
+    void releaseLane() {
+        for (DBuf* b : {&visited, &F0, &F1, &estart, &ebase, &chunkFirst, &estart2, &ebase2, &chunkFirst2, &tileSums, &counters,
+                        &lbStatus, &seedPart, &seedVid, &cmpStatus[0], &cmpStatus[1], &frontierBits, &localBits, &edgeMask,
+                        &pullSeg, &pullCtl, &sparseCtl, &dynStats, &progBuf}) b->release();
+        inStage.release();
+        seedStage.release();
+    }
     ~ngx_ctx() {                                       // also the cleanup of ngx_open's error paths
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
+        for (auto st : pipeStreams) if (st) (void)hipStreamSynchronize(st);
         spaces.clear();
-        for (DBuf* b : {&visited, &F0, &F1, &estart, &ebase, &tileSums, &counters, &lbStatus, &seedPart, &seedVid, &oSrc,
-                        &oDst, &oRank, &oType, &oEntry, &chunkFirst, &oColDesc, &progBuf, &sendBits, &recvBits, &resvTab, &resvCtl,
-                        &vcells, &misc, &edgeMask, &cmpStatus[0], &cmpStatus[1], &frontierBits, &oFlags, &rowCols, &rowLen,
-                        &rowOff, &rowBytes, &pullSeg, &pullCtl, &dkTable, &dkKeep, &dkPre, &dSrc, &dDst, &dRank,
-                        &dType, &dynStats, &sparseCtl, &estart2, &ebase2, &chunkFirst2, &xListSend, &xListRecv,
-                        &xCounts}) b->release();
+        for (DBuf* b : {&oSrc, &oDst, &oRank, &oType, &oEntry, &oColDesc, &sendBits, &recvBits, &resvTab, &resvCtl,
+                        &vcells, &misc, &oFlags, &rowCols, &rowLen, &rowOff, &rowBytes, &dkTable, &dkKeep, &dkPre, &dSrc, &dDst,
+                        &dRank, &dType, &xListSend, &xListRecv, &xCounts}) b->release();
         for (auto& cb : oCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         for (auto& cb : dCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         hostStage.release();
-        inStage.release();
-        seedStage.release();
         for (auto e : eventPool) (void)hipEventDestroy(e);
+        for (auto e : pipeEv) if (e) (void)hipEventDestroy(e);
+        for (auto st : pipeStreams) if (st) (void)hipStreamDestroy(st);
+        for (void* st : coStack) if (st) munmap(st, kCoStackBytes + 4096);
         if (comm) (void)ncclCommDestroy(comm);
         if (pin) (void)hipHostFree(pin);
+        releaseLane();
+        swapLane();
+        releaseLane();
         if (stream) (void)hipStreamDestroy(stream);
     }
 
@@ -339,27 +391,29 @@ struct ngx_ctx {
 };
 
 // ngx_go_batch's pipeline. The batch's queries run as coroutines (ucontext) on the calling thread, one
-// at a time, each on a stack of its own. A query whose last final hop is enqueued yields before it waits
-// for the row count (it is "deferred"); the next query then prepares and enqueues its first hops —
-// after the deferred query's final hop in the stream's order — up to its first wait for a device total,
-// and yields back; the deferred query finishes (its row count and result), then the next one goes on.
-// The GPU runs one query's last kernel and the next one's first back to back: the host's result tail,
-// preparation and launch calls overlap the final hop instead of idling the GPU between queries. Only one
-// coroutine runs at any time, so the context needs no lock between them; what the two queries share on
-// the host (publication slots, the row-count device word, the program stage) is kept apart (kRowsSlot,
-// goDeferPoint, uploadPrograms).
+// at a time, each on a stack of its own, consecutive queries on alternate lanes (ngx_ctx::Lane: scratch
+// and publication slots). A query's hops run on the front stream and its last final hop (with its close)
+// on the final stream, each stream on its own share of the CUs. A query whose final hop is enqueued
+// yields before it waits for its row count (it is "deferred"); the next query then runs its hops on its
+// lane — on the device beside the deferred query's final hop — and enqueues its own final hop behind the
+// deferred one's on the final stream (the result arrays and reservation counters are shared); then it
+// defers in turn, the first query finishes (row count, result) and the one after starts. On the device
+// one query's intermediate hops hide under the other's final hop; on the host the result tail,
+// preparation and launch calls overlap the device work. Only one coroutine runs at any time, so the
+// context needs no lock between them.
 struct GoJob {
     ucontext_t uc;
     int32_t idx = 0;
     int state = 0;
-    bool yieldAtAwait = false;                         // started while another query is deferred
     int32_t rc = NGX_OK;
     uint64_t nrows = 0, edges = 0, digest[3] = {0, 0, 0};
 };
 struct GoPipe {
-    enum { kRunning = 0, kDeferred = 1, kFrontDone = 2, kDone = 3 };
+    enum { kRunning = 0, kDeferred = 1, kPreFinal = 2, kDone = 3 };
     ucontext_t main;
     GoJob* cur = nullptr;
+    GoJob* deferred = nullptr;                         // the query waiting at goDeferPoint
+    bool holdFinals = false;                           // digests: a final hop waits for the deferred query
     const ngx_go_plan* const* plans = nullptr;
     int32_t n = 0;
 };
@@ -555,10 +609,8 @@ DevPrograms uploadPrograms(ngx_ctx* c, const Programs& pr, const std::vector<int
     // the same bytes as the last upload into the same buffer (a prepared query run again): nothing to copy
     // (a copy launch and its dispatch gap, ~7 us of the C2 step on the device timeline)
     if (base != c->progLastPtr || c->progLast != img) {
-        // staged in page-locked memory: the copy is asynchronous (the stage is reused only by the next
-        // call, after this one has synchronised with its kernels — or, in a batch whose previous query is
-        // deferred (goDeferPoint), once that query's work is drained)
-        if (c->pipe && c->pipe->cur && c->pipe->cur->yieldAtAwait) HIP_OK(hipStreamSynchronize(c->stream));
+        // staged in page-locked memory: the copy is asynchronous (the lane's stage is reused only by its
+        // next query, after this one has synchronised with its kernels)
         char* host = c->inStage.get(total);
         std::memcpy(host, img.data(), total);
         HIP_OK(hipMemcpyAsync(base, host, total, hipMemcpyHostToDevice, c->stream));
@@ -969,7 +1021,7 @@ T readScalar(ngx_ctx* c, const T* dev) {
 // hop sized on the device publishes while the seed total is still unread (spec1)
 Publish nextPub(ngx_ctx* c, uint32_t slotWord = 0) {
     if (!c->pinDev) return Publish{nullptr, 0};
-    return Publish{c->pinDev + slotWord, ++c->pinSeq};
+    return Publish{c->pinDev + c->pinLane + slotWord, ++c->pinSeq};   // (the active lane's slots)
 }
 
 // a plan whose host work may overlap another query's final hop (and whose own final hop may be overlapped):
@@ -985,21 +1037,56 @@ void pipeSwitch(ngx_ctx* c, int state) {
     j->state = GoPipe::kRunning;
 }
 
-// awaitPub's first call in a query started while another is deferred: hand the thread back
-void pipeFrontYield(ngx_ctx* c) {
-    GoJob* j = c->pipe ? c->pipe->cur : nullptr;
-    if (!j || !j->yieldAtAwait) return;
-    j->yieldAtAwait = false;
-    pipeSwitch(c, GoPipe::kFrontDone);
-}
-
-// the last final hop's close is enqueued: defer the wait for its row count while the next query starts
+// the last final hop's close is enqueued: defer the wait for its row count while the next query runs its
+// hops on the other lane
 void goDeferPoint(ngx_ctx* c) {
     GoPipe* P = c->pipe;
     GoJob* j = P ? P->cur : nullptr;
-    if (!j || j->yieldAtAwait || j->idx + 1 >= P->n || !pipelinable(*P->plans[j->idx + 1])) return;
+    if (!j || j->idx + 1 >= P->n || !pipelinable(*P->plans[j->idx + 1])) return;
     c->pipeOverlaps++;
     pipeSwitch(c, GoPipe::kDeferred);
+}
+
+// a record hop is about to write the shared result arrays while the previous query is deferred: with
+// digests asked for (GoPipe::holdFinals), wait until that query has finished (its digest reads its rows)
+void goPreFinalPoint(ngx_ctx* c) {
+    GoPipe* P = c->pipe;
+    GoJob* j = P ? P->cur : nullptr;
+    if (j && P->holdFinals && P->deferred) pipeSwitch(c, GoPipe::kPreFinal);
+}
+
+// `to` waits for the work enqueued on `from` so far
+void streamAfter(hipStream_t to, hipStream_t from, hipEvent_t ev) {
+    HIP_OK(hipEventRecord(ev, from));
+    HIP_OK(hipStreamWaitEvent(to, ev, 0));
+}
+
+// A record hop during a pipelined batch: the deferrable last final hop runs on the final stream, after
+// this query's hops on the front stream; any other record hop stays on the front stream, after the final
+// stream's last close (the result arrays and reservation counters are shared by every query)
+struct FinalStreamScope {
+    ngx_ctx* c;
+    hipStream_t saved = nullptr;
+    FinalStreamScope(ngx_ctx* c_, bool onFinal) : c(c_) {
+        if (!c->finalStream) return;
+        if (onFinal) {
+            streamAfter(c->finalStream, c->stream, c->pipeEv[0]);
+            saved = c->stream;
+            c->stream = c->finalStream;
+        } else {
+            streamAfter(c->stream, c->finalStream, c->pipeEv[1]);
+        }
+    }
+    void restore() {
+        if (saved) c->stream = saved;
+        saved = nullptr;
+    }
+    ~FinalStreamScope() { restore(); }
+};
+
+// the front stream after every final hop enqueued so far (a batch query's rows read on the front stream)
+void joinFinal(ngx_ctx* c) {
+    if (c->finalStream) streamAfter(c->stream, c->finalStream, c->pipeEv[1]);
 }
 
 // the published scan total: poll the host-mapped slot (no stream round trip); after ~50 ms block on
@@ -1014,7 +1101,6 @@ uint64_t awaitPub(ngx_ctx* c, const Publish& p, const uint64_t* devCopy, uint64_
         *extra = 0;
         for (int k = 0; k < 4; k++) *extra |= static_cast<uint64_t>(f[k] != 0) << k;
     };
-    if (c->pipe) pipeFrontYield(c);
     if (!p.slot) { errBits(); return readScalar(c, devCopy); }
     auto t0 = std::chrono::steady_clock::now();
     // kernels.h Publish: the words are taken once the tag matches them
@@ -1039,6 +1125,7 @@ uint64_t awaitPub(ngx_ctx* c, const Publish& p, const uint64_t* devCopy, uint64_
         if ((i & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
     }
     HIP_OK(hipStreamSynchronize(c->stream));
+    if (c->finalStream) HIP_OK(hipStreamSynchronize(c->finalStream));   // (a batch's final hop runs there)
     if (take(v)) return v;
     errBits();
     if (extra2) *extra2 = extra2Dev ? readScalar(c, extra2Dev) : 0;
@@ -1048,7 +1135,7 @@ uint64_t awaitPub(ngx_ctx* c, const Publish& p, const uint64_t* devCopy, uint64_
 // the query tail published by k_publish_tail: out[0] = error bits, out[1 ..] the extra words; false
 // if it did not arrive within ~50 ms of polling (the caller synchronises and copies instead)
 bool awaitTail(ngx_ctx* c, uint64_t seq, uint64_t* out, int n) {
-    volatile uint64_t* slot = c->pin + ngx_ctx::kTailOff;
+    volatile uint64_t* slot = c->pin + c->pinLane + ngx_ctx::kTailOff;
     auto t0 = std::chrono::steady_clock::now();
     for (uint32_t i = 0;; i++) {
         if (__atomic_load_n(const_cast<uint64_t*>(slot), __ATOMIC_ACQUIRE) == seq) {
@@ -1323,6 +1410,12 @@ int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return NGX_E_DEVICE;
     if (hipSetDevice(c->device) != hipSuccess) return NGX_E_DEVICE;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return NGX_E_DEVICE;
+    if (c->world == 1) {                              // ngx_go_batch's pipeline (without them: one at a time)
+        for (auto& st : c->pipeStreams)
+            if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) st = nullptr;
+        for (auto& e : c->pipeEv)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+    }
     if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->cus < 1) c->cus = 256;
     if (const char* ht = std::getenv("NGX_HOST_TRACE")) c->htrace = std::string(ht) == "1";
     if (hipHostMalloc(reinterpret_cast<void**>(&c->pin), ngx_ctx::kPinBytes, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
@@ -2611,7 +2704,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     if (lbCompact) {
         const uint64_t tiles = (d.V + kCompactTile - 1) / kCompactTile + 1;
         cmpTile = c->cmpStatus[0].get<uint64_t>(tiles);
-        cmpWave = c->cmpStatus[1].get<uint64_t>(tiles * (kCompactTile / 256));   // a word per wave (kernels.hip CNW)
+        cmpWave = c->cmpStatus[1].get<uint64_t>(tiles * (kCompactTile / 256));   // a word per wave (up to 16 per tile)
     }
     // the pull reads the frontier as a bitmap over global rows, written by the compaction that built it
     // (or from the frontier list for the seed frontier); the pull's segment counter is cleared by the
@@ -2822,7 +2915,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     std::vector<int64_t> jitKc;                              // their literal table (FinalArgs::kc/kl)
     std::vector<uint32_t> jitKl;
     c->jitNote.clear();
-    c->jit.releaseRetired(c->stream);                        // modules evicted by earlier queries
+    c->jit.releaseRetired(c->stream, c->finalStream);        // modules evicted by earlier queries (either stream)
     if (c->jitOn) {
         JitQuery jq = jitHopQuery(sp, hs, progs);
         jq.yColType = gp.colTypes;
@@ -2991,6 +3084,12 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         }
         a.mask = mask;
         if (isRecord && E) {
+            // ngx_go_batch: this query's last final hop may overlap the next query (goDeferPoint): not with a
+            // device read-back left (multi-root walks), string arenas, profiling or host traces, nor at world > 1
+            const bool deferrable = c->pipe && isFinal && c->pinDev && !dyn && !rw && c->world == 1 && nStrOut == 0 &&
+                                    !c->prof && !c->htrace && !c->traceGo && pipelinable(p);
+            if (c->pipe) goPreFinalPoint(c);
+            FinalStreamScope fss(c, deferrable);
             a.W = progs.W >= 0 ? dp.code + progs.W : nullptr;
             a.nY = static_cast<int32_t>(progs.yOff.size());
             a.yCode = dp.code;
@@ -3106,15 +3205,12 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             });
             c->resvClosePending = false;
             c->resvRows = a.resvCtl + (a.resvG + 1) * static_cast<uint64_t>(a.resvStride);
+            fss.restore();                                      // (the front stream again)
             if (!dyn) {
                 // GO: the row count and the query's error bits so far, published by k_final_close
                 uint64_t fin = 0;                               // devE: this hop's packed (|F|, E)
                 const uint64_t* rowsDev = c->resvRows;          // (the next query resets c->resvRows)
-                // ngx_go_batch: the next query starts here, before the wait. Not with a device read-back left
-                // (multi-root walks), string arenas, profiling or host traces, nor at world > 1
-                if (c->pipe && isFinal && rowsPub.slot && !rw && c->world == 1 && nStrOut == 0 && !c->prof && !c->htrace &&
-                    !c->traceGo && pipelinable(p))
-                    goDeferPoint(c);
+                if (deferrable) goDeferPoint(c);                // ngx_go_batch: the next query runs here
                 uint64_t nrows = awaitPub(c, rowsPub, rowsDev, &finalErrBits, errFlag, devE ? &fin : nullptr,
                                           devE ? dynTotal : nullptr);
                 haveFinalErrs = true;
@@ -3380,7 +3476,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         tailOk = true;
     } else if (c->pinDev && nExtra <= 64) {
         const uint64_t seq = ++c->pinSeq;
-        if (launchPublishTail(errFlag, dynStats, nExtra, c->pinDev + ngx_ctx::kTailOff, seq, c->stream))
+        if (launchPublishTail(errFlag, dynStats, nExtra, c->pinDev + c->pinLane + ngx_ctx::kTailOff, seq, c->stream))
             throw Error{NGX_E_DEVICE, "publish tail"};
         tailOk = awaitTail(c, seq, tail, 1 + nExtra);
     }
@@ -3953,7 +4049,10 @@ int32_t goCall(ngx_ctx* c, const ngx_go_plan* p, ngx_go_result** out) {
     }
     // a failed query may leave kernels enqueued that still read the page-locked seed / program stages
     // the next call rewrites: drain them first
-    if (rc != NGX_OK) (void)hipStreamSynchronize(c->stream);
+    if (rc != NGX_OK) {
+        (void)hipStreamSynchronize(c->stream);
+        if (c->finalStream) (void)hipStreamSynchronize(c->finalStream);
+    }
     R->r.code = rc;
     R->r.ncols = static_cast<int32_t>(R->colTypes.size());
     R->r.col_types = R->colTypes.data();
@@ -3991,8 +4090,10 @@ void batchQuery(ngx_ctx* c, const ngx_go_plan* p, GoJob& j, bool digest) {
         j.edges = 0;
         if (r) for (int32_t h = 0; h < r->nhops; h++) j.edges += r->hop_edges[h];
         // a result the digest does not cover (host rows, string columns) keeps zeros
-        if (digest && r && j.rc == NGX_OK && p->result_on_device && resultDigest(c, r, j.digest) != NGX_OK)
-            j.digest[0] = j.digest[1] = j.digest[2] = 0;
+        if (digest && r && j.rc == NGX_OK && p->result_on_device) {
+            joinFinal(c);                               // the rows were written on the final stream
+            if (resultDigest(c, r, j.digest) != NGX_OK) j.digest[0] = j.digest[1] = j.digest[2] = 0;
+        }
     } catch (...) {                                     // nothing unwinds past a coroutine's entry
         j.rc = NGX_E_DEVICE;
         (void)hipStreamSynchronize(c->stream);
@@ -4014,21 +4115,19 @@ void batchEntry() {
     j->state = GoPipe::kDone;                           // uc_link: back to the batch loop
 }
 
-// a coroutine stack: 16 MB reserved (pages committed on first touch), a guard page below it
-struct CoStack {
-    void* base = nullptr;
-    size_t bytes = 0;
-    bool make(size_t sz) {
-        const size_t guard = 4096;
-        void* m = mmap(nullptr, sz + guard, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE | MAP_STACK, -1, 0);
+// the batch's coroutine stacks (once per context): 16 MB reserved each (pages committed on first touch),
+// a guard page below
+bool coStacks(ngx_ctx* c) {
+    for (auto& st : c->coStack) {
+        if (st) continue;
+        void* m = mmap(nullptr, ngx_ctx::kCoStackBytes + 4096, PROT_READ | PROT_WRITE,
+                       MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE | MAP_STACK, -1, 0);
         if (m == MAP_FAILED) return false;
-        (void)mprotect(m, guard, PROT_NONE);
-        base = m;
-        bytes = sz + guard;
-        return true;
+        (void)mprotect(m, 4096, PROT_NONE);
+        st = m;
     }
-    ~CoStack() { if (base) munmap(base, bytes); }
-};
+    return true;
+}
 
 }  // namespace
 
@@ -4054,9 +4153,8 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
         if (digests) for (int k = 0; k < 3; k++) digests[3 * static_cast<size_t>(j.idx) + k] = j.digest[k];
         if (j.rc != NGX_OK && first == NGX_OK) first = j.rc;
     };
-    bool pipe = c->batchPipeline && n > 1 && c->world == 1 && !c->prof && !c->htrace && !c->traceGo;
-    CoStack stacks[2];
-    for (int k = 0; pipe && k < 2; k++) pipe = stacks[k].make(16u << 20);
+    const bool pipe = c->batchPipeline && n > 1 && c->world == 1 && !c->prof && !c->htrace && !c->traceGo &&
+                      c->pipeStreams[0] && c->pipeStreams[1] && c->pipeEv[0] && c->pipeEv[1] && c->pipeEv[2] && coStacks(c);
     if (!pipe) {
         for (int32_t i = 0; i < n; i++) {
             GoJob j;
@@ -4069,21 +4167,33 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
     GoPipe P;
     P.plans = plans;
     P.n = n;
+    P.holdFinals = digests != nullptr;
+    hipStream_t ctxStream = c->stream;
+    try {
+        if (c->activeLane != 0) c->useLane(0);
+        // both streams after the context's earlier work
+        streamAfter(c->pipeStreams[0], ctxStream, c->pipeEv[2]);
+        streamAfter(c->pipeStreams[1], ctxStream, c->pipeEv[2]);
+    } catch (const Error& e) {
+        return fail(c, e.code, e.msg);
+    }
+    c->stream = c->pipeStreams[0];
+    c->finalStream = c->pipeStreams[1];
     BatchCo co{c, &P, digests != nullptr};
     GoJob jobs[2];
-    auto start = [&](int32_t i, bool front) -> GoJob* {
+    auto start = [&](int32_t i) -> GoJob* {
         GoJob& j = jobs[i & 1];
         j = GoJob{};
         j.idx = i;
-        j.yieldAtAwait = front;
         getcontext(&j.uc);
-        j.uc.uc_stack.ss_sp = static_cast<char*>(stacks[i & 1].base) + 4096;
-        j.uc.uc_stack.ss_size = stacks[i & 1].bytes - 4096;
+        j.uc.uc_stack.ss_sp = static_cast<char*>(c->coStack[i & 1]) + 4096;
+        j.uc.uc_stack.ss_size = ngx_ctx::kCoStackBytes;
         j.uc.uc_link = &P.main;
         makecontext(&j.uc, batchEntry, 0);
         return &j;
     };
     auto resume = [&](GoJob* j) {
+        c->useLane(j->idx & 1);                           // query i uses lane i % 2
         P.cur = j;
         tBatch = &co;
         swapcontext(&P.main, &j->uc);
@@ -4091,26 +4201,38 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
         return j->state;
     };
     c->pipe = &P;
-    GoJob* a = start(0, false);
+    GoJob* a = start(0);
     int st = resume(a);
     for (;;) {
         if (st == GoPipe::kDeferred) {
-            // a waits for its row count: the next query runs up to its first wait (or to its end), then a
-            // finishes, then the next one goes on
-            GoJob* b = start(a->idx + 1, true);
+            // a waits for its row count: the next query runs its hops on the other lane and enqueues its final
+            // hop (or, holding finals, stops before it), then a finishes
+            GoJob* b = start(a->idx + 1);
+            P.deferred = a;
             int sb = resume(b);
+            P.deferred = nullptr;
             while (resume(a) != GoPipe::kDone) {}         // a query defers once; nothing else yields it
             record(*a);
             a = b;
-            st = sb == GoPipe::kFrontDone ? resume(a) : sb;
+            st = sb == GoPipe::kPreFinal ? resume(a) : sb;
             continue;
         }
         record(*a);                                       // kDone
         if (a->idx + 1 >= n) break;
-        a = start(a->idx + 1, false);
+        a = start(a->idx + 1);
         st = resume(a);
     }
     c->pipe = nullptr;
+    c->finalStream = nullptr;
+    c->stream = ctxStream;
+    // later calls use lane 0 and the context's stream, ordered after everything the batch enqueued
+    c->useLane(0);
+    try {
+        streamAfter(ctxStream, c->pipeStreams[0], c->pipeEv[0]);
+        streamAfter(ctxStream, c->pipeStreams[1], c->pipeEv[1]);
+    } catch (const Error& e) {
+        if (first == NGX_OK) first = fail(c, e.code, e.msg);
+    }
     return first;
 }
 
@@ -4527,7 +4649,7 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
             jitSlotConsts(jq, kc, kl);
             for (size_t k = 0; k < kc.size(); k++) { a.kc[k] = kc[k]; a.kl[k] = kl[k]; }
             std::string jerr;
-            c->jit.releaseRetired(c->stream);
+            c->jit.releaseRetired(c->stream, c->finalStream);
             jk = c->jit.get(jitShapeKey(sp, jq), [&] { return jitSource(sp, jq); }, jerr);
         }
         if (jk) {

@@ -74,7 +74,7 @@ public:
     std::shared_ptr<const JitKernels> get(const std::string& shape, const std::function<std::string()>& source,
                                           std::string& err);
     // unload the modules evicted since the last call (synchronises `s` first when there are any)
-    void releaseRetired(hipStream_t s);
+    void releaseRetired(hipStream_t s, hipStream_t s2 = nullptr);   // s2: a second stream that may run them
     // block until every queued compile has finished (tests, warm-up)
     void drain();
     uint64_t compiled = 0, hits = 0, failed = 0, evicted = 0;

@@ -241,13 +241,17 @@ __global__ __launch_bounds__(64) void k_seed_lookup(const int32_t* qpart, const 
     }
 }
 
-// Launch 2 (one 1024-thread workgroup, nEnt <= kSeedFuseMax): the entries' degrees -> exclusive offsets
-// in place, E = estart[nEnt], the hop's chunk heads, E published (and packed with |F| for dyn hops)
-__global__ __launch_bounds__(1024) void k_seed_scan(uint64_t n, int ns, uint64_t* estart, Publish pub,
-                                                    uint64_t* chunkFirst, uint64_t cfCap, uint32_t* err,
-                                                    uint64_t* packedOut) {
-    __shared__ uint64_t sm[1024 / 64 + 1];
-    constexpr int kPer = static_cast<int>(kSeedFuseMax / 1024);
+// Launch 2 (one 256-thread workgroup, nEnt <= kSeedFuseMax): the entries' degrees -> exclusive offsets
+// in place, E = estart[nEnt], the hop's chunk heads, E published (and packed with |F| for dyn hops). (A
+// 1024-thread workgroup waited up to 200 us for a CU with 16 free wave slots beside another query's final
+// hop in a pipelined batch.)
+constexpr int kSeedScanWG = 256;
+__global__ __launch_bounds__(kSeedScanWG) void k_seed_scan(uint64_t n, int ns, uint64_t* estart, Publish pub,
+                                                           uint64_t* chunkFirst, uint64_t cfCap, uint32_t* err,
+                                                           uint64_t* packedOut) {
+    constexpr int NW = kSeedScanWG / 64;
+    __shared__ uint64_t sm[NW + 1];
+    constexpr int kPer = static_cast<int>(kSeedFuseMax / kSeedScanWG);
     const uint64_t nEnt = n * static_cast<uint64_t>(ns);
     const uint64_t lo = threadIdx.x * static_cast<uint64_t>(kPer);
     uint64_t d[kPer];
@@ -267,8 +271,8 @@ __global__ __launch_bounds__(1024) void k_seed_scan(uint64_t n, int ns, uint64_t
     __syncthreads();
     if (threadIdx.x == 0) {
         uint64_t acc = 0;
-        for (int w = 0; w < 16; w++) { const uint64_t t = sm[w]; sm[w] = acc; acc += t; }
-        sm[16] = acc;
+        for (int w = 0; w < NW; w++) { const uint64_t t = sm[w]; sm[w] = acc; acc += t; }
+        sm[NW] = acc;
     }
     __syncthreads();
     uint64_t pre = sm[wid] + x - sum;
@@ -280,9 +284,9 @@ __global__ __launch_bounds__(1024) void k_seed_scan(uint64_t n, int ns, uint64_t
         pre += d[k];
     }
     if (threadIdx.x == 0) {
-        estart[nEnt] = sm[16];
-        if (packedOut) *packedOut = (n << kDynShift) | sm[16];       // device-driven hops read this
-        if (pub.slot) publishWords(pub.slot, pub.seq, sm[16], 0);
+        estart[nEnt] = sm[NW];
+        if (packedOut) *packedOut = (n << kDynShift) | sm[NW];       // device-driven hops read this
+        if (pub.slot) publishWords(pub.slot, pub.seq, sm[NW], 0);
     }
 }
 
@@ -368,7 +372,6 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
 // rows left 2.3 waves per SIMD at C2, each wave issuing 16 scans one after the other)
 // CIT rows per lane (4 by default; 8 or 16 by the flag compact_lane_rows, tested for parity)
 constexpr int CWG = 1024;
-constexpr int CNW = CWG / 64;
 __device__ __forceinline__ uint64_t waveInclScan(uint64_t x, int lane) {
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -426,11 +429,14 @@ __device__ __forceinline__ void waveDegrees(const CompactArgs& a, uint64_t wbase
 }
 
 // launch 1: per tile and per wave the packed (rows << kFdShift | degrees) total; the bitmap words
-template <bool ONE, int CIT>
-__global__ __launch_bounds__(CWG) void k_compact_count(CompactArgs a) {
-    __shared__ uint64_t sWave[CNW];
+// (WGS = CWG threads per workgroup; r05 measured 256 threads x 16 rows per lane, the same tile, in a
+// pipelined batch beside another query's final hop: 0.370 vs 0.366 ms per C2 step, alone 27.8 vs 25.8 us)
+template <bool ONE, int CIT, int WGS>
+__global__ __launch_bounds__(WGS) void k_compact_count(CompactArgs a) {
+    constexpr int NW = WGS / 64;
+    __shared__ uint64_t sWave[NW];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint64_t wbase = static_cast<uint64_t>(blockIdx.x) * (CWG * CIT) + static_cast<uint64_t>(wid) * (64 * CIT);
+    const uint64_t wbase = static_cast<uint64_t>(blockIdx.x) * (WGS * CIT) + static_cast<uint64_t>(wid) * (64 * CIT);
     if (blockIdx.x == 0 && threadIdx.x == 0 && a.clear32 != nullptr) *a.clear32 = 0;
     const uint32_t flags = waveFlags<CIT>(a, wbase, lane);
     uint64_t deg[CIT];
@@ -453,13 +459,13 @@ __global__ __launch_bounds__(CWG) void k_compact_count(CompactArgs a) {
     for (int o = 32; o >= 1; o >>= 1) packed += __shfl_xor(packed, o, 64);
     if (lane == 0) {
         sWave[wid] = packed;
-        a.waveSum[static_cast<uint64_t>(blockIdx.x) * CNW + wid] = packed;
+        a.waveSum[static_cast<uint64_t>(blockIdx.x) * NW + wid] = packed;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         uint64_t t = 0;
 #pragma unroll
-        for (int w = 0; w < CNW; w++) t += sWave[w];
+        for (int w = 0; w < NW; w++) t += sWave[w];
         a.tileSum[blockIdx.x] = t;
     }
 }
@@ -467,16 +473,17 @@ __global__ __launch_bounds__(CWG) void k_compact_count(CompactArgs a) {
 // launch 2: the wave's start = the tiles before it + the waves before it in its tile (summed from
 // launch 1's words, nothing waited for), then the rows in order: positions from each k's ballot and a
 // wave scan of its degrees. The last tile writes the totals (estart[|F| * ns] = E, *total, publish).
-template <bool ONE, int CIT>
-__global__ __launch_bounds__(CWG) void k_compact_write(CompactArgs a) {
+template <bool ONE, int CIT, int WGS>
+__global__ __launch_bounds__(WGS) void k_compact_write(CompactArgs a) {
+    constexpr int NW = WGS / 64;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint64_t tile = blockIdx.x;
-    const uint64_t wbase = tile * (CWG * CIT) + static_cast<uint64_t>(wid) * (64 * CIT);
+    const uint64_t wbase = tile * (WGS * CIT) + static_cast<uint64_t>(wid) * (64 * CIT);
     const int ns = a.hs.n;
     const uint32_t flags = waveFlags<CIT>(a, wbase, lane);
     // the totals of the tiles before this one: 8 loads in flight per lane (a dependent loop of loads
     // cost 10 us at C2's 586 tiles)
-    uint64_t pre = lane < wid ? a.waveSum[tile * CNW + lane] : 0;
+    uint64_t pre = lane < wid ? a.waveSum[tile * NW + lane] : 0;
     for (uint64_t t0 = 0; t0 < tile; t0 += 8 * 64) {
         uint64_t v[8];
 #pragma unroll
@@ -489,8 +496,8 @@ __global__ __launch_bounds__(CWG) void k_compact_write(CompactArgs a) {
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) pre += __shfl_xor(pre, o, 64);
-    if (tile == gridDim.x - 1 && wid == CNW - 1 && lane == 0) {
-        const uint64_t incl = pre + a.waveSum[tile * CNW + wid];
+    if (tile == gridDim.x - 1 && wid == NW - 1 && lane == 0) {
+        const uint64_t incl = pre + a.waveSum[tile * NW + wid];
         a.estart[(incl >> kFdShift) * static_cast<uint64_t>(ns)] = incl & kFdMask;
         *a.total = incl;
         if (a.pub.slot) publishWords(a.pub.slot, a.pub.seq, incl, 0);
@@ -1485,7 +1492,7 @@ int launchSeedFrontierCf(const int32_t* qpart, const int64_t* qvid, uint64_t n, 
     const unsigned g = static_cast<unsigned>(std::max<uint64_t>((n + 63) / 64, 1));   // block 0 also clears
     hipLaunchKernelGGL(k_seed_lookup, dim3(g), dim3(64), 0, s, qpart, qvid, n, idx, hs,
                        F, estart, ebase, zero, nzero, zero8);
-    hipLaunchKernelGGL(k_seed_scan, dim3(1), dim3(1024), 0, s, n, hs.n, estart, pub, chunkFirst, cfCap, err, packedOut);
+    hipLaunchKernelGGL(k_seed_scan, dim3(1), dim3(kSeedScanWG), 0, s, n, hs.n, estart, pub, chunkFirst, cfCap, err, packedOut);
     return static_cast<int>(hipGetLastError());
 }
 
@@ -1561,19 +1568,19 @@ int launchCompactLb(const CompactArgs& a, hipStream_t s) {
     const int cit = a.laneRows != 0 ? a.laneRows : 4;
     const uint64_t tile = static_cast<uint64_t>(CWG) * cit;
     const dim3 grid(static_cast<unsigned>(std::max<uint64_t>((a.V + tile - 1) / tile, 1)));
-#define NGX_COMPACT(ONE, CIT)                                                              \
-    do {                                                                                   \
-        hipLaunchKernelGGL((k_compact_count<ONE, CIT>), grid, dim3(CWG), 0, s, a);         \
-        hipLaunchKernelGGL((k_compact_write<ONE, CIT>), grid, dim3(CWG), 0, s, a);         \
+#define NGX_COMPACT(ONE, CIT, WGS)                                                              \
+    do {                                                                                        \
+        hipLaunchKernelGGL((k_compact_count<ONE, CIT, WGS>), grid, dim3(WGS), 0, s, a);         \
+        hipLaunchKernelGGL((k_compact_write<ONE, CIT, WGS>), grid, dim3(WGS), 0, s, a);         \
     } while (0)
     if (a.hs.n == 1) {
-        if (cit == 4) NGX_COMPACT(true, 4);
-        else if (cit == 8) NGX_COMPACT(true, 8);
-        else NGX_COMPACT(true, 16);
+        if (cit == 4) NGX_COMPACT(true, 4, CWG);
+        else if (cit == 8) NGX_COMPACT(true, 8, CWG);
+        else NGX_COMPACT(true, 16, CWG);
     } else {
-        if (cit == 4) NGX_COMPACT(false, 4);
-        else if (cit == 8) NGX_COMPACT(false, 8);
-        else NGX_COMPACT(false, 16);
+        if (cit == 4) NGX_COMPACT(false, 4, CWG);
+        else if (cit == 8) NGX_COMPACT(false, 8, CWG);
+        else NGX_COMPACT(false, 16, CWG);
     }
 #undef NGX_COMPACT
     return static_cast<int>(hipGetLastError());
