@@ -365,7 +365,7 @@ class RowReader {
     static ErrOrVariant getPropByName(const RowReader* r, const std::string& prop) {
         ErrOrVariant out;
         int64_t idx = r->schema_->getFieldIndex(prop);
-        SupportedType t = r->schema_->getFieldType(prop);
+        SupportedType t = r->schema_->getFieldType(idx);             // = getFieldType(prop): one name scan
         if (idx < 0 && t == UNKNOWN) {
             // unknown name: getFieldType => kInvalidValueType => default case => E_DATA_INVALID
             out.err = ResultType::E_DATA_INVALID;

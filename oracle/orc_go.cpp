@@ -557,6 +557,7 @@ struct GoExec {
                         if (!Expression::asBool(v.value())) continue;
                     }
                     std::vector<Variant> record;
+                    record.reserve(yields.size());
                     for (auto& y : yields) {
                         auto v = y->eval(ev.g);
                         if (!v.ok()) { out.ok = false; out.error = v.status().msg_; return false; }
