@@ -50,9 +50,10 @@ def parse():
     p.add_argument("--cpu-budget", type=float, default=20.0, help="target seconds of oracle GO work (0: skip)")
     p.add_argument("--threads", type=int, default=16, help="host threads for datagen / oracle")
     p.add_argument("--out-only", action="store_true", help="store out-edges only (no -e in-edge slot)")
-    p.add_argument("--yield-only", action="store_true",
-                   help="timed step writes only the YIELD columns (no src row array): measured 428 vs 433 us "
-                        "per final hop, the src stores hide under the loads")
+    p.add_argument("--row-arrays", action="store_true",
+                   help="timed step also writes the src / dst / rank row arrays (GetNeighbors' edge keys) beside "
+                        "the YIELD columns. Default off: GO's result is its YIELD columns (GoExecutor.cpp:1288-1297 "
+                        "builds each record from the yields only); with them the C2 final hop measured 289 vs 250 us")
     p.add_argument("--no-compact", action="store_true",
                    help="timed step writes every result value at 8 bytes (default: compact_results, integer "
                         "arrays at the widths of the stored columns they copy)")
@@ -162,7 +163,7 @@ def main():
         key = (id(s), on_device, columnar)
         if key not in prepared:
             prepared[key] = eng.prepare_go(datagen.RMAT_SPACE, s, on_device=on_device, columnar=columnar,
-                                           yield_only=on_device and args.yield_only,
+                                           yield_only=on_device and not args.row_arrays,
                                            compact=on_device and not args.no_compact)
         r = eng.go(datagen.RMAT_SPACE, prepared[key], rows=rows_, arrays=False)
         if not r.ok:
@@ -175,7 +176,7 @@ def main():
 
     for s_ in plans:                                        # encoded before the timed region
         prepared[(id(s_), True, False)] = eng.prepare_go(datagen.RMAT_SPACE, s_, on_device=True,
-                                                         yield_only=args.yield_only, compact=not args.no_compact)
+                                                         yield_only=not args.row_arrays, compact=not args.no_compact)
     if args.host_loop == "native" and args.warmup:
         # warmed through the timed loop's own path (the batch, its streams and coroutine stacks)
         for code, _, _ in eng.go_batch([prepared[(id(plans[i]), True, False)] for i in range(args.warmup)]):
@@ -294,7 +295,7 @@ def main():
     # dominant kernel roofline. `frac` = the bytes the kernel must move on this layout (a
     # fraction <= 1 of the bytes the kernel actually moves) / its HIP-event launch time / 8 TB/s. For the
     # final hop that is the library's stored-width count (dst 4 B + p0 1 B per scanned edge, rank a
-    # constant column: 0 B; 17 B written per row) plus the YIELD-only column p1 read at whole 128-B lines:
+    # constant column: 0 B; 13 B written per row: dst 4, p0 1, p1 8 — 17 with --row-arrays' src) plus the YIELD-only column p1 read at whole 128-B lines:
     # a line of 128 / w values is fetched when any of its edges passes, 1 - (1 - f)^(128 / w) of the
     # lines at pass fraction f (random at C2: every line). SURVEY.md §8d's figure (every field 8 B) is
     # kept beside it as frac_8d, a TEPS-equivalent credit, not a bandwidth.
@@ -306,11 +307,13 @@ def main():
         name, (launches, ms, algo) = dom
         traffic = None
         # the committed PMC bytes were measured on the N = 1 C2 step: other workloads report none
-        if os.path.exists(args.traffic) and world == 1 and scale == 22 and not args.yield_only:
+        if os.path.exists(args.traffic) and world == 1 and scale == 22:
             try:
                 tj = json.load(open(args.traffic))
-                # and on the same result layout (compact_results changes the final hop's writes)
-                if tj.get("kernel_class") == name and bool(tj.get("compact", False)) == (not args.no_compact):
+                # and on the same result layout (compact_results and the row arrays change the final hop's
+                # writes)
+                if tj.get("kernel_class") == name and bool(tj.get("compact", False)) == (not args.no_compact) \
+                        and bool(tj.get("yield_only", False)) == (not args.row_arrays):
                     traffic = tj.get("bytes_per_launch")
             except Exception:
                 traffic = None
@@ -392,8 +395,9 @@ def main():
             "host_loop": args.host_loop,
             "batch_overlaps": overlaps,
             "timed_region": ("seeds on host -> the YIELD columns of every result row in HBM (result_on_device; "
-                             + ("yield_only: e._dst / e._rank alias the dst / rank row arrays, no src array"
-                                if args.yield_only else "and the src / dst / rank row arrays") + ")"),
+                             + ("and the src / dst / rank row arrays" if args.row_arrays else
+                                "yield_only: the YIELD columns are the result, as GoExecutor's records; e._dst / "
+                                "e._rank alias the dst / rank row arrays, no src array") + ")"),
             "get_neighbors": gn_stats,
             "host_delivery": {"ms_per_step_columnar": round(host_col_ms, 3), "ms_per_step_cells": round(host_cell_ms, 3),
                               "columnar_library_tail_ms": round(col_tail, 3), "columnar_device_ms": round(col_dev, 3),

@@ -141,7 +141,7 @@ struct ngx_ctx {
     uint64_t* pin = nullptr;                           // host-mapped [value, seq]: scan totals published by
     uint64_t* pinDev = nullptr;                        // k_scan_tiles (kernels.h Publish)
     uint64_t pinSeq = 0;                               // words [0, 2): scan totals; [kTailOff ..): query tail
-    static constexpr size_t kPinBytes = 4096;           // two lanes of 256 words (ngx_ctx::Lane)
+    static constexpr size_t kPinBytes = 8192;           // up to four lanes of 256 words (ngx_ctx::Lane)
     static constexpr size_t kTailOff = 8;               // k_publish_tail: seq, error bits, extra words
     static constexpr uint32_t kSeedSlot = 80;           // the seed hop's publication (nextPub)
     static constexpr uint32_t kRowsSlot = 88;           // a record hop's row count (k_final_close)
@@ -262,11 +262,13 @@ struct ngx_ctx {
     size_t eventNext = 0;
 
     // A query lane: the per-query scratch of the hop loop and its publication slots (words [pinLane,
-    // pinLane + kLaneWords) of the host-mapped block). ngx_go_batch runs consecutive queries on alternate
-    // lanes, so that one query's hops run on the device beside the other's final hop (GoPipe). The active
-    // lane's fields are the members above, the other lane's are parked here; useLane swaps the two sets.
+    // pinLane + kLaneWords) of the host-mapped block). ngx_go_batch runs consecutive queries on rotating
+    // lanes, so that one query's hops run on the device beside the earlier queries' final hops (GoPipe).
+    // The active lane's fields are the members above; lane k's are parked in parked[k] while it is not
+    // active (parked[activeLane] holds an empty set); useLane swaps sets.
     uint32_t pinLane = 0;
     static constexpr uint32_t kLaneWords = 256;
+    static constexpr int kMaxLanes = 4;                 // kPinBytes / (8 * kLaneWords)
     struct Lane {
         DBuf visited, F0, F1, estart, ebase, chunkFirst, estart2, ebase2, chunkFirst2, tileSums, counters, lbStatus,
             seedPart, seedVid, cmpStatus[2], frontierBits, localBits, edgeMask, pullSeg, pullCtl, sparseCtl, dynStats, progBuf;
@@ -277,19 +279,22 @@ struct ngx_ctx {
         std::string progLast;
         const char* progLastPtr = nullptr;
         PinBuf inStage, seedStage;
-        uint32_t pinLane = kLaneWords;
-    } parked;
+        uint32_t pinLane = 0;
+    } parked[kMaxLanes];
     int activeLane = 0;
+    // lanes of a pipelined batch (flag "batch_lanes", 2 .. kMaxLanes): up to lanes - 1 queries wait at their
+    // deferral point while the next one runs its hops
+    int32_t batchLanes = 3;
     // ngx_go_batch's streams (GoPipe, created with the context at world 1): the queries' hops on the front
     // stream, the last final hop of each overlapped query on the final stream; finalStream is set while a
-    // pipelined batch runs. The coroutine stacks of the batch's queries.
+    // pipelined batch runs. The coroutine stacks of the batch's queries (one per lane).
     hipStream_t pipeStreams[2] = {nullptr, nullptr};
     hipEvent_t pipeEv[3] = {nullptr, nullptr, nullptr};
     hipStream_t finalStream = nullptr;
-    void* coStack[2] = {nullptr, nullptr};
+    void* coStack[kMaxLanes] = {nullptr, nullptr, nullptr, nullptr};
     static constexpr size_t kCoStackBytes = size_t(16) << 20;   // + a guard page below each
-    void swapLane() {
-#define NGX_LANE_SWAP(f) std::swap(f, parked.f);
+    void swapLane(Lane& L) {
+#define NGX_LANE_SWAP(f) std::swap(f, L.f);
         NGX_LANE_SWAP(visited) NGX_LANE_SWAP(F0) NGX_LANE_SWAP(F1) NGX_LANE_SWAP(estart)
         NGX_LANE_SWAP(ebase) NGX_LANE_SWAP(chunkFirst) NGX_LANE_SWAP(estart2) NGX_LANE_SWAP(ebase2) NGX_LANE_SWAP(chunkFirst2)
         NGX_LANE_SWAP(tileSums) NGX_LANE_SWAP(counters) NGX_LANE_SWAP(lbStatus) NGX_LANE_SWAP(seedPart) NGX_LANE_SWAP(seedVid)
@@ -300,8 +305,14 @@ struct ngx_ctx {
         NGX_LANE_SWAP(inStage) NGX_LANE_SWAP(seedStage) NGX_LANE_SWAP(pinLane)
 #undef NGX_LANE_SWAP
     }
+    void initLanes() {
+        for (int k = 1; k < kMaxLanes; k++) parked[k].pinLane = k * kLaneWords;
+    }
     void useLane(int k) {
-        if (k != activeLane) { swapLane(); activeLane = k; }
+        if (k == activeLane) return;
+        swapLane(parked[activeLane]);                  // park the active lane (the empty set comes in) ...
+        swapLane(parked[k]);                           // ... and bring lane k in (the empty set goes to its slot)
+        activeLane = k;
     }
 
     void releaseLane() {
@@ -329,8 +340,10 @@ struct ngx_ctx {
         if (comm) (void)ncclCommDestroy(comm);
         if (pin) (void)hipHostFree(pin);
         releaseLane();
-        swapLane();
-        releaseLane();
+        for (auto& L : parked) {
+            swapLane(L);
+            releaseLane();
+        }
         if (stream) (void)hipStreamDestroy(stream);
     }
 
@@ -412,7 +425,7 @@ struct GoPipe {
     enum { kRunning = 0, kDeferred = 1, kPreFinal = 2, kDone = 3 };
     ucontext_t main;
     GoJob* cur = nullptr;
-    GoJob* deferred = nullptr;                         // the query waiting at goDeferPoint
+    int ndeferred = 0;                                 // queries waiting at goDeferPoint
     bool holdFinals = false;                           // digests: a final hop waits for the deferred query
     const ngx_go_plan* const* plans = nullptr;
     int32_t n = 0;
@@ -1052,7 +1065,7 @@ void goDeferPoint(ngx_ctx* c) {
 void goPreFinalPoint(ngx_ctx* c) {
     GoPipe* P = c->pipe;
     GoJob* j = P ? P->cur : nullptr;
-    if (j && P->holdFinals && P->deferred) pipeSwitch(c, GoPipe::kPreFinal);
+    if (j && P->holdFinals && P->ndeferred) pipeSwitch(c, GoPipe::kPreFinal);
 }
 
 // `to` waits for the work enqueued on `from` so far
@@ -1400,6 +1413,7 @@ int32_t ngx_get_unique_id(void* out128) {
 int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
     if (!cfg || !out) return NGX_E_BAD_ARGUMENT;
     auto c = std::make_unique<ngx_ctx>();
+    c->initLanes();
     c->device = cfg->device;
     c->rank = cfg->rank;
     c->world = cfg->world < 1 ? 1 : cfg->world;
@@ -1818,6 +1832,11 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
     if (n == "narrow_columns") { c->narrowColumns = value != 0; return NGX_OK; }
     if (n == "trace_go") { c->traceGo = value != 0; return NGX_OK; }
     if (n == "batch_pipeline") { c->batchPipeline = value != 0; return NGX_OK; }
+    if (n == "batch_lanes") {
+        if (value < 2 || value > ngx_ctx::kMaxLanes) return fail(c, NGX_E_BAD_ARGUMENT, "batch_lanes: 2 .. 4");
+        c->batchLanes = static_cast<int32_t>(value);
+        return NGX_OK;
+    }
     if (n == "compact_lane_rows") {
         if (value != 0 && value != 4 && value != 8 && value != 16) return fail(c, NGX_E_BAD_ARGUMENT, "compact_lane_rows: 0, 4, 8 or 16");
         c->compactLaneRows = static_cast<int32_t>(value);
@@ -1843,6 +1862,7 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "narrow_columns") *value = c->narrowColumns ? 1 : 0;
     else if (n == "trace_go") *value = c->traceGo ? 1 : 0;
     else if (n == "batch_pipeline") *value = c->batchPipeline ? 1 : 0;
+    else if (n == "batch_lanes") *value = c->batchLanes;
     else if (n == "batch_overlaps") *value = static_cast<int64_t>(c->pipeOverlaps);
     else if (n == "compact_lane_rows") *value = c->compactLaneRows;
     else if (n == "pull_hops") *value = static_cast<int64_t>(c->pullHops);
@@ -4185,20 +4205,23 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
     c->stream = c->pipeStreams[0];
     c->finalStream = c->pipeStreams[1];
     BatchCo co{c, &P, digests != nullptr};
-    GoJob jobs[2];
+    // query i runs on lane i % lanes with the coroutine stack of that lane; up to lanes - 1 queries wait at
+    // their deferral point (digests: one, its rows are hashed before the next final hop overwrites them)
+    const int lanes = P.holdFinals ? 2 : std::max(2, std::min<int>(c->batchLanes, ngx_ctx::kMaxLanes));
+    GoJob jobs[ngx_ctx::kMaxLanes];
     auto start = [&](int32_t i) -> GoJob* {
-        GoJob& j = jobs[i & 1];
+        GoJob& j = jobs[i % lanes];
         j = GoJob{};
         j.idx = i;
         getcontext(&j.uc);
-        j.uc.uc_stack.ss_sp = static_cast<char*>(c->coStack[i & 1]) + 4096;
+        j.uc.uc_stack.ss_sp = static_cast<char*>(c->coStack[i % lanes]) + 4096;
         j.uc.uc_stack.ss_size = ngx_ctx::kCoStackBytes;
         j.uc.uc_link = &P.main;
         makecontext(&j.uc, batchEntry, 0);
         return &j;
     };
     auto resume = [&](GoJob* j) {
-        c->useLane(j->idx & 1);                           // query i uses lane i % 2
+        c->useLane(j->idx % lanes);
         P.cur = j;
         tBatch = &co;
         swapcontext(&P.main, &j->uc);
@@ -4206,27 +4229,39 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
         return j->state;
     };
     c->pipe = &P;
+    GoJob* waiting[ngx_ctx::kMaxLanes];                 // deferred queries, oldest first
+    int nw = 0;
+    auto finishOldest = [&] {
+        GoJob* d = waiting[0];
+        for (int k = 1; k < nw; k++) waiting[k - 1] = waiting[k];
+        P.ndeferred = --nw;
+        while (resume(d) != GoPipe::kDone) {}             // a query defers once; nothing else yields it
+        record(*d);
+    };
     GoJob* a = start(0);
     int st = resume(a);
     for (;;) {
-        if (st == GoPipe::kDeferred) {
-            // a waits for its row count: the next query runs its hops on the other lane and enqueues its final
-            // hop (or, holding finals, stops before it), then a finishes
-            GoJob* b = start(a->idx + 1);
-            P.deferred = a;
-            int sb = resume(b);
-            P.deferred = nullptr;
-            while (resume(a) != GoPipe::kDone) {}         // a query defers once; nothing else yields it
-            record(*a);
-            a = b;
-            st = sb == GoPipe::kPreFinal ? resume(a) : sb;
+        if (st == GoPipe::kPreFinal) {                   // a's final hop waits for the deferred queries' digests
+            while (nw) finishOldest();
+            st = resume(a);
             continue;
         }
-        record(*a);                                       // kDone
-        if (a->idx + 1 >= n) break;
-        a = start(a->idx + 1);
+        if (st == GoPipe::kDeferred) {
+            // a waits for its row count while the next query runs its hops on its own lane and enqueues its
+            // final hop behind a's; the oldest waiting query finishes first when every other lane is taken
+            waiting[nw] = a;
+            P.ndeferred = ++nw;
+        } else {
+            record(*a);                                   // kDone
+        }
+        const int32_t next = a->idx + 1;
+        if (next >= n) break;
+        // the query that last used the next one's lane (and coroutine) has finished
+        while (nw && waiting[0]->idx + lanes <= next) finishOldest();
+        a = start(next);
         st = resume(a);
     }
+    while (nw) finishOldest();
     c->pipe = nullptr;
     c->finalStream = nullptr;
     c->stream = ctxStream;

@@ -140,3 +140,33 @@ def test_batch_last_result_stays_on_device(rmat):
     alone = e.go(ds.space, p, rows=False, device_digest=True)
     assert alone.ok and tuple(got[0][3]) == tuple(got[1][3]) == alone.device_digest
     assert e.go_batch([]) == []
+
+
+@pytest.mark.parametrize("lanes", [2, 3, 4])
+def test_batch_lanes(rmat, lanes):
+    """Deeper pipelines (flag batch_lanes: up to lanes - 1 queries wait for their row counts while the next
+    one runs its hops on its own lane): every query's code, row count and scanned edges are what it has
+    alone, over mixed plans; the batch's last result stays in HBM, digest equal to the same plan alone."""
+    ds, o, e = rmat
+    rng = random.Random(91 + lanes)
+    qs = _queries(ds)
+    items = [(q, rng.choice(["compact", "compact", "device", "host"])) for q in qs]
+    items = [(q, "compact") for q in qs[:8]] + items + [(q, "compact") for q in qs[-8:]]
+    preps = [_prepare(e, ds, q, m) for q, m in items]
+    want = [_alone(e, ds, p) for p in preps]
+    assert e.get_flag("batch_lanes") == 3
+    e.set_flag("batch_lanes", lanes)
+    try:
+        before = e.get_flag("batch_overlaps")
+        got = e.go_batch(preps)
+        overlaps = e.get_flag("batch_overlaps") - before
+        last = e.go_batch(preps[-3:])
+    finally:
+        e.set_flag("batch_lanes", 3)
+    for (q, m), w, g in list(zip(items, want, got)) + list(zip(items[-3:], want[-3:], last)):
+        assert g[0] == w[0], (q, m, g, w)
+        if g[0] == 0:
+            assert (g[1], g[2]) == (w[1], w[2]), (q, m)
+    assert overlaps >= 10
+    with pytest.raises(Exception):
+        e.set_flag("batch_lanes", 5)

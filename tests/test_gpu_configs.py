@@ -113,19 +113,22 @@ def test_c2_bench_step_vs_oracle(c2):
         e.set_flag("jit", 1)
     # factor 1 pulls every intermediate hop with E >= V / 100 (hop 2 here; hop 1 scans ~1 % of V)
     assert pulls[(1, 1)] >= 1 and pulls[(0, 1)] == 0 and pulls[(default, 1)] >= 1
-    # the bench's own result placement: rows in HBM with compact integer arrays (compact_results),
-    # fetched and widened, digest for digest equal to the oracle's rows
-    got = e.go(ds.space, s, on_device=True, fetch=True, compact=True)
-    assert got.ok and got.hop_edges == ref.hop_scanned
-    key_w, col_w = got.dev_widths
-    # src / dst vids < 2^31, p0 < 100; every rank 0: a constant column (width 0, no bytes per row)
-    assert key_w == [4, 4, 0] and col_w == [4, 0, 1, 8]
-    assert got.dev_consts[0][2] == 0 and got.dev_consts[1][1] == 0
-    cols = [np.ascontiguousarray(x) for x, _, _ in got.dev_cols]
-    assert all(ln is None and t is None for _, ln, t in got.dev_cols)
-    digests = oracle.digest_columns(got.col_types, got.nrows, [c.ctypes.data for c in cols], [None] * 4, [None] * 4)
-    assert got.nrows == ref.nrows and np.array_equal(digests, ref.digests)
-    del cols, got
+    # the bench's own result placement: rows in HBM with compact integer arrays (compact_results), the
+    # YIELD columns only (yield_only: no src row array), fetched and widened, digest for digest equal to
+    # the oracle's rows; and with the row arrays (bench.py --row-arrays)
+    for yield_only in (True, False):
+        got = e.go(ds.space, s, on_device=True, fetch=True, compact=True, yield_only=yield_only)
+        assert got.ok and got.hop_edges == ref.hop_scanned
+        key_w, col_w = got.dev_widths
+        # src / dst vids < 2^31, p0 < 100; every rank 0: a constant column (width 0, no bytes per row)
+        assert col_w == [4, 0, 1, 8] and key_w[1:] == [4, 0]
+        assert yield_only or got.src is not None
+        assert got.dev_consts[1][1] == 0
+        cols = [np.ascontiguousarray(x) for x, _, _ in got.dev_cols]
+        assert all(ln is None and t is None for _, ln, t in got.dev_cols)
+        digests = oracle.digest_columns(got.col_types, got.nrows, [c.ctypes.data for c in cols], [None] * 4, [None] * 4)
+        assert got.nrows == ref.nrows and np.array_equal(digests, ref.digests)
+        del cols, got
 
 
 @pytest.mark.timeout(600)
