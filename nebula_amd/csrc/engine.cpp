@@ -215,6 +215,7 @@ struct ngx_ctx {
     DBuf pullSeg, pullCtl;
     uint64_t pullSegWords = 0;
     int32_t compactLaneRows = 0;                        // compaction rows per lane: 0 = by shard size, else 4 / 8 / 16
+    int32_t compactWg = 0;                              // compaction workgroup threads: 0 = auto, 256 or 1024
     int64_t pullFactor = 200;                           // pull when 100 x hop edges >= pullFactor x shard rows (0: never)
     uint64_t pullHops = 0;
     // sparse intermediate hops (kernels.h SparseArgs): a push hop with E * sparseFactor <= V builds the next
@@ -280,6 +281,14 @@ struct ngx_ctx {
         const char* progLastPtr = nullptr;
         PinBuf inStage, seedStage;
         uint32_t pinLane = 0;
+        // the lane's result rows and their reservation state (a query's final hop writes its lane's arrays,
+        // so its k_final_close may run beside the next query's final hop)
+        DBuf oSrc, oDst, oRank, oType, oColDesc, resvTab, resvCtl;
+        std::vector<ColBuf> oCols;
+        std::vector<OutCol> oColView;
+        uint64_t resvTabWords = 0;
+        uint32_t resvLastG = 0, resvLastStride = 0, resvParity = 0;
+        bool resvClosePending = false;
     } parked[kMaxLanes];
     int activeLane = 0;
     // lanes of a pipelined batch (flag "batch_lanes", 2 .. kMaxLanes): up to lanes - 1 queries wait at their
@@ -288,8 +297,25 @@ struct ngx_ctx {
     // ngx_go_batch's streams (GoPipe, created with the context at world 1): the queries' hops on the front
     // stream, the last final hop of each overlapped query on the final stream; finalStream is set while a
     // pipelined batch runs. The coroutine stacks of the batch's queries (one per lane).
-    hipStream_t pipeStreams[2] = {nullptr, nullptr};
-    hipEvent_t pipeEv[3] = {nullptr, nullptr, nullptr};
+    // [0] front (hops), [1] final (final hops), [2] close (k_final_close of an overlapped final hop, beside
+    // the next query's final hop: the close reads and moves its own lane's rows only)
+    hipStream_t pipeStreams[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t pipeEv[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    // a ring of events for the batch's cross-stream waits: each wait gets an event no later record re-arms
+    // while the wait may be pending (flag batch_event_ring; 0: the fixed pipeEv per role)
+    static constexpr int kPipeRing = 64;
+    hipEvent_t pipeRing[kPipeRing] = {};
+    uint32_t pipeRingNext = 0;
+    bool batchEventRing = true;
+    hipEvent_t pipeEvent(int role) {
+        if (!batchEventRing || !pipeRing[0]) return pipeEv[role];
+        return pipeRing[pipeRingNext++ % kPipeRing];
+    }
+    // set while a pipelined batch runs with flag batch_close_stream (off by default: r05 C2 0.330 vs 0.324
+    // ms per step with it — the next final hop still starts ~14 us after its front-stream dependency, the
+    // cross-queue hand-off, whichever queue the close is on)
+    hipStream_t closeStream = nullptr;
+    bool batchCloseStream = false;
     hipStream_t finalStream = nullptr;
     void* coStack[kMaxLanes] = {nullptr, nullptr, nullptr, nullptr};
     static constexpr size_t kCoStackBytes = size_t(16) << 20;   // + a guard page below each
@@ -303,6 +329,10 @@ struct ngx_ctx {
         NGX_LANE_SWAP(progBuf) NGX_LANE_SWAP(visitedSize) NGX_LANE_SWAP(pullSegWords) NGX_LANE_SWAP(epoch)
         NGX_LANE_SWAP(bitsClean) NGX_LANE_SWAP(bitsCleanPtr) NGX_LANE_SWAP(progLast) NGX_LANE_SWAP(progLastPtr)
         NGX_LANE_SWAP(inStage) NGX_LANE_SWAP(seedStage) NGX_LANE_SWAP(pinLane)
+        NGX_LANE_SWAP(oSrc) NGX_LANE_SWAP(oDst) NGX_LANE_SWAP(oRank) NGX_LANE_SWAP(oType) NGX_LANE_SWAP(oColDesc)
+        NGX_LANE_SWAP(resvTab) NGX_LANE_SWAP(resvCtl) NGX_LANE_SWAP(oCols) NGX_LANE_SWAP(oColView)
+        NGX_LANE_SWAP(resvTabWords) NGX_LANE_SWAP(resvLastG) NGX_LANE_SWAP(resvLastStride) NGX_LANE_SWAP(resvParity)
+        NGX_LANE_SWAP(resvClosePending)
 #undef NGX_LANE_SWAP
     }
     void initLanes() {
@@ -318,7 +348,9 @@ struct ngx_ctx {
     void releaseLane() {
         for (DBuf* b : {&visited, &F0, &F1, &estart, &ebase, &chunkFirst, &estart2, &ebase2, &chunkFirst2, &tileSums, &counters,
                         &lbStatus, &seedPart, &seedVid, &cmpStatus[0], &cmpStatus[1], &frontierBits, &localBits, &edgeMask,
-                        &pullSeg, &pullCtl, &sparseCtl, &dynStats, &progBuf}) b->release();
+                        &pullSeg, &pullCtl, &sparseCtl, &dynStats, &progBuf, &oSrc, &oDst, &oRank, &oType, &oColDesc,
+                        &resvTab, &resvCtl}) b->release();
+        for (auto& cb : oCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         inStage.release();
         seedStage.release();
     }
@@ -327,14 +359,14 @@ struct ngx_ctx {
         if (stream) (void)hipStreamSynchronize(stream);
         for (auto st : pipeStreams) if (st) (void)hipStreamSynchronize(st);
         spaces.clear();
-        for (DBuf* b : {&oSrc, &oDst, &oRank, &oType, &oEntry, &oColDesc, &sendBits, &recvBits, &resvTab, &resvCtl,
+        for (DBuf* b : {&oEntry, &sendBits, &recvBits,
                         &vcells, &misc, &oFlags, &rowCols, &rowLen, &rowOff, &rowBytes, &dkTable, &dkKeep, &dkPre, &dSrc, &dDst,
                         &dRank, &dType, &xListSend, &xListRecv, &xCounts}) b->release();
-        for (auto& cb : oCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         for (auto& cb : dCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         hostStage.release();
         for (auto e : eventPool) (void)hipEventDestroy(e);
         for (auto e : pipeEv) if (e) (void)hipEventDestroy(e);
+        for (auto e : pipeRing) if (e) (void)hipEventDestroy(e);
         for (auto st : pipeStreams) if (st) (void)hipStreamDestroy(st);
         for (void* st : coStack) if (st) munmap(st, kCoStackBytes + 4096);
         if (comm) (void)ncclCommDestroy(comm);
@@ -1075,19 +1107,20 @@ void streamAfter(hipStream_t to, hipStream_t from, hipEvent_t ev) {
 }
 
 // A record hop during a pipelined batch: the deferrable last final hop runs on the final stream, after
-// this query's hops on the front stream; any other record hop stays on the front stream, after the final
-// stream's last close (the result arrays and reservation counters are shared by every query)
+// this query's hops on the front stream, and its k_final_close on the close stream after it; any other
+// record hop stays on the front stream, after every final hop and close enqueued so far
 struct FinalStreamScope {
     ngx_ctx* c;
     hipStream_t saved = nullptr;
     FinalStreamScope(ngx_ctx* c_, bool onFinal) : c(c_) {
         if (!c->finalStream) return;
         if (onFinal) {
-            streamAfter(c->finalStream, c->stream, c->pipeEv[0]);
+            streamAfter(c->finalStream, c->stream, c->pipeEvent(0));
             saved = c->stream;
             c->stream = c->finalStream;
         } else {
-            streamAfter(c->stream, c->finalStream, c->pipeEv[1]);
+            streamAfter(c->stream, c->finalStream, c->pipeEvent(1));
+            if (c->closeStream) streamAfter(c->stream, c->closeStream, c->pipeEvent(3));
         }
     }
     void restore() {
@@ -1099,7 +1132,8 @@ struct FinalStreamScope {
 
 // the front stream after every final hop enqueued so far (a batch query's rows read on the front stream)
 void joinFinal(ngx_ctx* c) {
-    if (c->finalStream) streamAfter(c->stream, c->finalStream, c->pipeEv[1]);
+    if (c->finalStream) streamAfter(c->stream, c->finalStream, c->pipeEvent(1));
+    if (c->closeStream) streamAfter(c->stream, c->closeStream, c->pipeEvent(3));
 }
 
 // the published scan total: poll the host-mapped slot (no stream round trip); after ~50 ms block on
@@ -1139,6 +1173,7 @@ uint64_t awaitPub(ngx_ctx* c, const Publish& p, const uint64_t* devCopy, uint64_
     }
     HIP_OK(hipStreamSynchronize(c->stream));
     if (c->finalStream) HIP_OK(hipStreamSynchronize(c->finalStream));   // (a batch's final hop runs there)
+    if (c->closeStream) HIP_OK(hipStreamSynchronize(c->closeStream));
     if (take(v)) return v;
     errBits();
     if (extra2) *extra2 = extra2Dev ? readScalar(c, extra2Dev) : 0;
@@ -1429,11 +1464,13 @@ int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
         // 0.365 / 0.371 vs 0.374 / 0.412 ms per C2 step with both at the default, same box (r05)
         int prLo = 0, prHi = 0;
         (void)hipDeviceGetStreamPriorityRange(&prLo, &prHi);
-        for (int k = 0; k < 2; k++)
-            if (hipStreamCreateWithPriority(&c->pipeStreams[k], hipStreamNonBlocking, k == 0 ? prHi : prLo) != hipSuccess)
+        for (int k = 0; k < 3; k++)
+            if (hipStreamCreateWithPriority(&c->pipeStreams[k], hipStreamNonBlocking, k == 1 ? prLo : prHi) != hipSuccess)
                 c->pipeStreams[k] = nullptr;
         for (auto& e : c->pipeEv)
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+        for (auto& e : c->pipeRing)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { c->pipeRing[0] = nullptr; break; }
     }
     if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->cus < 1) c->cus = 256;
     if (const char* ht = std::getenv("NGX_HOST_TRACE")) c->htrace = std::string(ht) == "1";
@@ -1777,7 +1814,7 @@ static int32_t resultDigest(ngx_ctx* c, const ngx_go_result* r, uint64_t out[3])
         a.x[0] = r->dev_src;
         a.w[0] = r->dev_key_w[0];
         a.c[0] = r->dev_key_const[0];
-        if (a.n && a.w[0] != 0 && !a.x[0]) return fail(c, NGX_E_UNSUPPORTED, "digest: no src row array (yield_only)");
+        if (!a.x[0]) a.w[0] = 0, a.c[0] = 0;          // yield_only (no src row array): the key hashes as 0
         for (int32_t k = 0; k < r->ncols; k++) {
             const ngx_dev_column& dc = r->dev_cols[k];
             if (dc.len || dc.type) return fail(c, NGX_E_UNSUPPORTED, "digest: string or untyped YIELD column");
@@ -1832,9 +1869,16 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
     if (n == "narrow_columns") { c->narrowColumns = value != 0; return NGX_OK; }
     if (n == "trace_go") { c->traceGo = value != 0; return NGX_OK; }
     if (n == "batch_pipeline") { c->batchPipeline = value != 0; return NGX_OK; }
+    if (n == "batch_close_stream") { c->batchCloseStream = value != 0; return NGX_OK; }
+    if (n == "batch_event_ring") { c->batchEventRing = value != 0; return NGX_OK; }
     if (n == "batch_lanes") {
         if (value < 2 || value > ngx_ctx::kMaxLanes) return fail(c, NGX_E_BAD_ARGUMENT, "batch_lanes: 2 .. 4");
         c->batchLanes = static_cast<int32_t>(value);
+        return NGX_OK;
+    }
+    if (n == "compact_wg") {
+        if (value != 0 && value != 256 && value != 1024) return fail(c, NGX_E_BAD_ARGUMENT, "compact_wg: 0, 256 or 1024");
+        c->compactWg = static_cast<int32_t>(value);
         return NGX_OK;
     }
     if (n == "compact_lane_rows") {
@@ -1863,8 +1907,11 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "trace_go") *value = c->traceGo ? 1 : 0;
     else if (n == "batch_pipeline") *value = c->batchPipeline ? 1 : 0;
     else if (n == "batch_lanes") *value = c->batchLanes;
+    else if (n == "batch_close_stream") *value = c->batchCloseStream ? 1 : 0;
+    else if (n == "batch_event_ring") *value = c->batchEventRing ? 1 : 0;
     else if (n == "batch_overlaps") *value = static_cast<int64_t>(c->pipeOverlaps);
     else if (n == "compact_lane_rows") *value = c->compactLaneRows;
+    else if (n == "compact_wg") *value = c->compactWg;
     else if (n == "pull_hops") *value = static_cast<int64_t>(c->pullHops);
     else if (n == "sparse_hops") *value = static_cast<int64_t>(c->sparseHops);
     else if (n == "xchg_lists") *value = c->xchgLists;
@@ -3224,10 +3271,25 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                     throw Error{NGX_E_DEVICE, "final"};
                 }
             });
-            // the holes of the groups' last blocks closed, the row count published (also for grid 0)
-            c->timed("final_close", 0, [&] {
-                if (launchFinalClose(a, c->stream)) throw Error{NGX_E_DEVICE, "final close"};
-            });
+            // the holes of the groups' last blocks closed, the row count published (also for grid 0). An
+            // overlapped final hop's close runs on the close stream: the next query's final hop (another
+            // lane's rows and counters) starts on the final stream without waiting for it
+            {
+                hipStream_t fs = c->stream;
+                if (deferrable && c->closeStream) {
+                    streamAfter(c->closeStream, fs, c->pipeEvent(4));
+                    c->stream = c->closeStream;
+                }
+                try {
+                    c->timed("final_close", 0, [&] {
+                        if (launchFinalClose(a, c->stream)) throw Error{NGX_E_DEVICE, "final close"};
+                    });
+                } catch (...) {
+                    c->stream = fs;
+                    throw;
+                }
+                c->stream = fs;
+            }
             c->resvClosePending = false;
             c->resvRows = a.resvCtl + (a.resvG + 1) * static_cast<uint64_t>(a.resvStride);
             fss.restore();                                      // (the front stream again)
@@ -3443,6 +3505,9 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             ca.err = errFlag;
             ca.epoch = ep;
             ca.laneRows = c->compactLaneRows;
+            // auto: 256-thread workgroups while a pipelined batch may run another query's final hop beside
+            // this compaction (ngx_go_batch's front stream), 1024 alone (2 us faster there)
+            ca.wgThreads = c->compactWg != 0 ? c->compactWg : (c->finalStream ? 256 : 1024);
             c->timed("compact_degrees", 0, [&] {
                 if (launchCompactLb(ca, c->stream)) throw Error{NGX_E_DEVICE, "compact"};
             });
@@ -4179,7 +4244,8 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
         if (j.rc != NGX_OK && first == NGX_OK) first = j.rc;
     };
     const bool pipe = c->batchPipeline && n > 1 && c->world == 1 && !c->prof && !c->htrace && !c->traceGo &&
-                      c->pipeStreams[0] && c->pipeStreams[1] && c->pipeEv[0] && c->pipeEv[1] && c->pipeEv[2] && coStacks(c);
+                      c->pipeStreams[0] && c->pipeStreams[1] && c->pipeStreams[2] && c->pipeEv[0] && c->pipeEv[1] &&
+                      c->pipeEv[2] && c->pipeEv[3] && c->pipeEv[4] && coStacks(c);
     if (!pipe) {
         for (int32_t i = 0; i < n; i++) {
             GoJob j;
@@ -4192,21 +4258,24 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
     GoPipe P;
     P.plans = plans;
     P.n = n;
-    P.holdFinals = digests != nullptr;
+    // digests need no hold since each lane has its own result rows: a deferred query hashes its rows when it
+    // resumes, and no later final hop writes them (the next query on its lane starts after it finished)
+    P.holdFinals = false;
     hipStream_t ctxStream = c->stream;
     try {
         if (c->activeLane != 0) c->useLane(0);
         // both streams after the context's earlier work
-        streamAfter(c->pipeStreams[0], ctxStream, c->pipeEv[2]);
-        streamAfter(c->pipeStreams[1], ctxStream, c->pipeEv[2]);
+        // every stream after the context's earlier work
+        for (auto st : c->pipeStreams) streamAfter(st, ctxStream, c->pipeEv[2]);
     } catch (const Error& e) {
         return fail(c, e.code, e.msg);
     }
     c->stream = c->pipeStreams[0];
     c->finalStream = c->pipeStreams[1];
+    c->closeStream = c->batchCloseStream ? c->pipeStreams[2] : nullptr;
     BatchCo co{c, &P, digests != nullptr};
     // query i runs on lane i % lanes with the coroutine stack of that lane; up to lanes - 1 queries wait at
-    // their deferral point (digests: one, its rows are hashed before the next final hop overwrites them)
+    // their deferral point (holding finals: one)
     const int lanes = P.holdFinals ? 2 : std::max(2, std::min<int>(c->batchLanes, ngx_ctx::kMaxLanes));
     GoJob jobs[ngx_ctx::kMaxLanes];
     auto start = [&](int32_t i) -> GoJob* {
@@ -4264,12 +4333,14 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
     while (nw) finishOldest();
     c->pipe = nullptr;
     c->finalStream = nullptr;
+    c->closeStream = nullptr;
     c->stream = ctxStream;
     // later calls use lane 0 and the context's stream, ordered after everything the batch enqueued
     c->useLane(0);
     try {
         streamAfter(ctxStream, c->pipeStreams[0], c->pipeEv[0]);
         streamAfter(ctxStream, c->pipeStreams[1], c->pipeEv[1]);
+        streamAfter(ctxStream, c->pipeStreams[2], c->pipeEv[3]);
     } catch (const Error& e) {
         if (first == NGX_OK) first = fail(c, e.code, e.msg);
     }

@@ -118,6 +118,8 @@ struct CompactArgs {
     uint8_t epoch;
     uint64_t* bits;                     // optional frontier bitmap of this shard's rows (V / 64 words, rounded up)
     int32_t laneRows;                   // rows per lane, 4 / 8 / 16; 0: the launcher picks by V (kernels.hip)
+    int32_t wgThreads;                  // 1024 (0) or 256 threads per workgroup (256: 16 rows per lane, the same
+                                        // 4096-row tile; a workgroup that fits beside another query's final hop)
     int32_t bitsZero;                   // write every word of `bits` as 0 (no hop reads this frontier's bitmap:
                                         // the next hop is the final one), leaving it clean for a sparse hop
 };

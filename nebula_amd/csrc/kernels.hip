@@ -1565,15 +1565,22 @@ int launchCompactLb(const CompactArgs& a, hipStream_t s) {
     if (a.V >= kCompactLbMaxV || a.nzero > WG) return 1;
     // rows per lane: 4 unless the flag forces 8 or 16 (measured at C2: 8 rows per lane, every wave
     // resident at once, 48 vs 46 us per step for 4 with a second round of waves)
-    const int cit = a.laneRows != 0 ? a.laneRows : 4;
-    const uint64_t tile = static_cast<uint64_t>(CWG) * cit;
+    // 256-thread workgroups (a pipelined batch: one finds room on a CU beside the other query's final-hop
+    // workgroups, where a 1024-thread one waits for 16 free wave slots — r05 trace: the count launch 185 us
+    // beside the final hop, starved until it drained) take 16 rows per lane, the same 4096-row tile
+    const bool small = a.wgThreads == 256;
+    const int cit = small ? 16 : a.laneRows != 0 ? a.laneRows : 4;
+    const uint64_t tile = static_cast<uint64_t>(small ? 256 : CWG) * cit;
     const dim3 grid(static_cast<unsigned>(std::max<uint64_t>((a.V + tile - 1) / tile, 1)));
 #define NGX_COMPACT(ONE, CIT, WGS)                                                              \
     do {                                                                                        \
         hipLaunchKernelGGL((k_compact_count<ONE, CIT, WGS>), grid, dim3(WGS), 0, s, a);         \
         hipLaunchKernelGGL((k_compact_write<ONE, CIT, WGS>), grid, dim3(WGS), 0, s, a);         \
     } while (0)
-    if (a.hs.n == 1) {
+    if (small) {
+        if (a.hs.n == 1) NGX_COMPACT(true, 16, 256);
+        else NGX_COMPACT(false, 16, 256);
+    } else if (a.hs.n == 1) {
         if (cit == 4) NGX_COMPACT(true, 4, CWG);
         else if (cit == 8) NGX_COMPACT(true, 8, CWG);
         else NGX_COMPACT(true, 16, CWG);

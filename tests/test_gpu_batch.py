@@ -55,6 +55,8 @@ def _prepare(e, ds, q, mode):
     s = ngql.parse_go(q)
     if mode == "compact":
         return e.prepare_go(ds.space, s, on_device=True, compact=True)
+    if mode == "lean":                      # the bench's plans: compact YIELD columns only
+        return e.prepare_go(ds.space, s, on_device=True, compact=True, yield_only=True)
     if mode == "device":
         return e.prepare_go(ds.space, s, on_device=True)
     return e.prepare_go(ds.space, s)
@@ -76,7 +78,7 @@ def test_batch_equals_one_at_a_time(rmat, pipeline):
     ds, o, e = rmat
     rng = random.Random(77)
     qs = _queries(ds)
-    modes = ["compact", "device", "host"]
+    modes = ["lean", "compact", "device", "host"]
     items = [(q, m) for q in qs for m in modes]
     rng.shuffle(items)
     # runs of pipelinable plans (the bench's shape) between the mixed ones
@@ -109,13 +111,20 @@ def test_batch_rows_equal_oracle(rmat):
     for k in range(12):
         seeds = datagen.sample_vids(6200 + k, 1 << ds.scale, 40)
         w = (" WHERE e.p0 < 50", "", " WHERE e.p0 >= 50")[k % 3]
-        q = f"GO 3 STEPS FROM {', '.join(str(int(v)) for v in seeds)} OVER e{w} YIELD e._src, e._dst, e._rank, e.p0, e.p1"
+        # odd k: the bench's plans (yield_only, no e._src: no src row array, the key hashes as 0)
+        ys = "e._dst, e._rank, e.p0, e.p1" if k % 2 else "e._src, e._dst, e._rank, e.p0, e.p1"
+        q = f"GO 3 STEPS FROM {', '.join(str(int(v)) for v in seeds)} OVER e{w} YIELD {ys}"
         s = ngql.parse_go(q)
         ref = o.go(ds.space, s)
         assert ref.ok
-        cols = [np.array([int(r[c][1]) for r in ref.rows], dtype=np.int64) for c in range(5)]
-        refs.append((len(ref.rows), int(sum(ref.hop_scanned)), oracle.row_digest([cols[0]] + cols)))
-        preps.append(e.prepare_go(ds.space, s, on_device=True, compact=True))
+        cols = [np.array([int(r[c][1]) for r in ref.rows], dtype=np.int64) for c in range(len(s.yields))]
+        if k % 2:
+            refs.append((len(ref.rows), int(sum(ref.hop_scanned)),
+                         oracle.row_digest([np.zeros(len(ref.rows), np.int64)] + cols)))
+            preps.append(e.prepare_go(ds.space, s, on_device=True, compact=True, yield_only=True))
+        else:
+            refs.append((len(ref.rows), int(sum(ref.hop_scanned)), oracle.row_digest([cols[0]] + cols)))
+            preps.append(e.prepare_go(ds.space, s, on_device=True, compact=True))
     before = e.get_flag("batch_overlaps")
     got = e.go_batch(preps, digests=True)
     assert e.get_flag("batch_overlaps") - before == len(preps) - 1
@@ -142,31 +151,37 @@ def test_batch_last_result_stays_on_device(rmat):
     assert e.go_batch([]) == []
 
 
+@pytest.mark.parametrize("close_stream", [1, 0])
 @pytest.mark.parametrize("lanes", [2, 3, 4])
-def test_batch_lanes(rmat, lanes):
+def test_batch_lanes(rmat, lanes, close_stream):
     """Deeper pipelines (flag batch_lanes: up to lanes - 1 queries wait for their row counts while the next
-    one runs its hops on its own lane): every query's code, row count and scanned edges are what it has
-    alone, over mixed plans; the batch's last result stays in HBM, digest equal to the same plan alone."""
+    one runs its hops on its own lane and its own result rows), with each overlapped final hop's close on
+    the close stream beside the next final hop (flag batch_close_stream) or behind it: every query's code,
+    row count, scanned edges and row digest are what it has alone, over mixed plans."""
     ds, o, e = rmat
     rng = random.Random(91 + lanes)
     qs = _queries(ds)
-    items = [(q, rng.choice(["compact", "compact", "device", "host"])) for q in qs]
-    items = [(q, "compact") for q in qs[:8]] + items + [(q, "compact") for q in qs[-8:]]
+    items = [(q, rng.choice(["lean", "compact", "device", "host"])) for q in qs]
+    items = [(q, "lean") for q in qs[:8]] + items + [(q, "compact") for q in qs[-8:]]
     preps = [_prepare(e, ds, q, m) for q, m in items]
     want = [_alone(e, ds, p) for p in preps]
-    assert e.get_flag("batch_lanes") == 3
+    assert e.get_flag("batch_lanes") == 3 and e.get_flag("batch_close_stream") == 0
     e.set_flag("batch_lanes", lanes)
+    e.set_flag("batch_close_stream", close_stream)
     try:
         before = e.get_flag("batch_overlaps")
-        got = e.go_batch(preps)
+        got = e.go_batch(preps, digests=True)
         overlaps = e.get_flag("batch_overlaps") - before
-        last = e.go_batch(preps[-3:])
+        plain = e.go_batch(preps[:12])                  # no digests: nothing read back between the queries
     finally:
         e.set_flag("batch_lanes", 3)
-    for (q, m), w, g in list(zip(items, want, got)) + list(zip(items[-3:], want[-3:], last)):
+        e.set_flag("batch_close_stream", 0)
+    for (q, m), w, g in list(zip(items, want, got)) + list(zip(items[:12], want[:12], plain)):
         assert g[0] == w[0], (q, m, g, w)
         if g[0] == 0:
             assert (g[1], g[2]) == (w[1], w[2]), (q, m)
+            if len(g) > 3 and "DISTINCT" not in q:
+                assert tuple(g[3]) == tuple(w[3]), (q, m)
     assert overlaps >= 10
     with pytest.raises(Exception):
         e.set_flag("batch_lanes", 5)

@@ -338,9 +338,10 @@ def test_rmat16_bench_query(rmat16, sel):
     assert fixtures.normalize_cells(got.rows) == fixtures.normalize_cells(ref.rows)
 
 
-@pytest.mark.parametrize("lane_rows", [4, 8, 16])
-def test_compaction_lane_rows(rmat16, rmat, lane_rows):
-    """The next-frontier compaction at each rows-per-lane width (flag compact_lane_rows, default 4):
+@pytest.mark.parametrize("lane_rows,wg", [(4, 1024), (8, 1024), (16, 1024), (0, 256)])
+def test_compaction_lane_rows(rmat16, rmat, lane_rows, wg):
+    """The next-frontier compaction at each rows-per-lane width (flag compact_lane_rows, default 4) and
+    in 256-thread workgroups (flag compact_wg; a pipelined batch's default, 16 rows per lane):
     the bench query at scale 16 (one edge type) and a BIDIRECT query at
     scale 12 with in-edges (two slots per frontier row) give the oracle's rows and per-hop scans."""
     cases = [(rmat16, datagen.rmat_seeds(16, 300, 16, 42, 99, threads=8),
@@ -351,10 +352,12 @@ def test_compaction_lane_rows(rmat16, rmat, lane_rows):
         q = text.replace("{S}", ", ".join(str(int(v)) for v in seeds))
         s = ngql.parse_go(q)
         e.set_flag("compact_lane_rows", lane_rows)
+        e.set_flag("compact_wg", wg)
         try:
             got = e.go(ds.space, s, columnar=True, rows=False, digest_fn=oracle.digest_columns)
         finally:
             e.set_flag("compact_lane_rows", 0)
+            e.set_flag("compact_wg", 0)
         # the oracle's sorted row digests, once per (graph, query) over the widths and modes
         key = (id(o), q)
         if key not in _LANE_REFS:
