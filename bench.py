@@ -41,8 +41,10 @@ def log(*a):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=3)
+    # 100 queries per timed batch (a graphd's stream of sessions): the pipeline's fill and drain (the first
+    # query's hops and the last one's final hop run alone) are ~1 step's time per batch, 10% at 10 steps
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--scale", type=int, default=0, help="RMAT scale (default: 22 at N=1, 26 at N=8, else 22+log2 N)")
     p.add_argument("--ef", type=int, default=16)
     p.add_argument("--seeds", type=int, default=1000)

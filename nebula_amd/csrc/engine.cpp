@@ -297,8 +297,10 @@ struct ngx_ctx {
     // ngx_go_batch's streams (GoPipe, created with the context at world 1): the queries' hops on the front
     // stream, the last final hop of each overlapped query on the final stream; finalStream is set while a
     // pipelined batch runs. The coroutine stacks of the batch's queries (one per lane).
-    // [0] front (hops), [1] final (final hops), [2] close (k_final_close of an overlapped final hop, beside
-    // the next query's final hop: the close reads and moves its own lane's rows only)
+    // [0] front (hops), [1] final (final hops), [2] the second front stream (flag batch_fronts 2: consecutive
+    // queries' hops on alternate front streams, so two queries' hop chains run at once beside a final hop)
+    // or the close stream (k_final_close of an overlapped final hop beside the next query's final hop: the
+    // close reads and moves its own lane's rows only)
     hipStream_t pipeStreams[3] = {nullptr, nullptr, nullptr};
     hipEvent_t pipeEv[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     // a ring of events for the batch's cross-stream waits: each wait gets an event no later record re-arms
@@ -316,6 +318,8 @@ struct ngx_ctx {
     // cross-queue hand-off, whichever queue the close is on)
     hipStream_t closeStream = nullptr;
     bool batchCloseStream = false;
+    int32_t batchFronts = 2;                           // front streams of a pipelined batch (1 or 2)
+    int32_t pipeFronts = 1;                            // ... of the batch that runs
     hipStream_t finalStream = nullptr;
     void* coStack[kMaxLanes] = {nullptr, nullptr, nullptr, nullptr};
     static constexpr size_t kCoStackBytes = size_t(16) << 20;   // + a guard page below each
@@ -1870,6 +1874,11 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
     if (n == "trace_go") { c->traceGo = value != 0; return NGX_OK; }
     if (n == "batch_pipeline") { c->batchPipeline = value != 0; return NGX_OK; }
     if (n == "batch_close_stream") { c->batchCloseStream = value != 0; return NGX_OK; }
+    if (n == "batch_fronts") {
+        if (value != 1 && value != 2) return fail(c, NGX_E_BAD_ARGUMENT, "batch_fronts: 1 or 2");
+        c->batchFronts = static_cast<int32_t>(value);
+        return NGX_OK;
+    }
     if (n == "batch_event_ring") { c->batchEventRing = value != 0; return NGX_OK; }
     if (n == "batch_lanes") {
         if (value < 2 || value > ngx_ctx::kMaxLanes) return fail(c, NGX_E_BAD_ARGUMENT, "batch_lanes: 2 .. 4");
@@ -1908,6 +1917,7 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "batch_pipeline") *value = c->batchPipeline ? 1 : 0;
     else if (n == "batch_lanes") *value = c->batchLanes;
     else if (n == "batch_close_stream") *value = c->batchCloseStream ? 1 : 0;
+    else if (n == "batch_fronts") *value = c->batchFronts;
     else if (n == "batch_event_ring") *value = c->batchEventRing ? 1 : 0;
     else if (n == "batch_overlaps") *value = static_cast<int64_t>(c->pipeOverlaps);
     else if (n == "compact_lane_rows") *value = c->compactLaneRows;
@@ -4272,7 +4282,9 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
     }
     c->stream = c->pipeStreams[0];
     c->finalStream = c->pipeStreams[1];
-    c->closeStream = c->batchCloseStream ? c->pipeStreams[2] : nullptr;
+    // the third stream: a second front stream, or (one front stream) the close stream
+    c->pipeFronts = c->batchFronts == 2 ? 2 : 1;
+    c->closeStream = c->pipeFronts == 1 && c->batchCloseStream ? c->pipeStreams[2] : nullptr;
     BatchCo co{c, &P, digests != nullptr};
     // query i runs on lane i % lanes with the coroutine stack of that lane; up to lanes - 1 queries wait at
     // their deferral point (holding finals: one)
@@ -4291,6 +4303,7 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
     };
     auto resume = [&](GoJob* j) {
         c->useLane(j->idx % lanes);
+        c->stream = c->pipeStreams[c->pipeFronts == 2 && (j->idx & 1) ? 2 : 0];   // query i's hops: front i % fronts
         P.cur = j;
         tBatch = &co;
         swapcontext(&P.main, &j->uc);

@@ -2,16 +2,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp; mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_batch.py -x -q --timeout 120 --timeout-method thread > gpurun_out/t_batch.log 2>&1 || { tail -30 gpurun_out/t_batch.log; exit 1; }
-tail -2 gpurun_out/t_batch.log
-for v in ring noring; do
-  a=""; [ $v = noring ] && a="--flag batch_event_ring=0"
-  timeout -k 10 400 python -u bench.py --steps 50 --warmup 5 --cpu-budget 0 $a > gpurun_out/h_$v.json 2> gpurun_out/h_$v.err || { tail -20 gpurun_out/h_$v.err; exit 1; }
-  python3 -c "
-import json;d=json.load(open('gpurun_out/h_$v.json'));print('$v', d['value'], d['ms_per_step'], d['roofline']['avg_launch_us'], d['roofline']['frac'], d['batch_overlaps'])"
-done
-out=gpurun_out/prof/r05h_pipe; mkdir -p $out
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run -f csv -- \
-    python3 bench.py --steps 20 --warmup 3 --cpu-budget 0 > "$out/bench.json" 2> "$out/bench.err" || { echo "pipe trace failed"; tail -20 "$out/bench.err"; exit 1; }
-python3 scripts/lanes_timeline.py $out/trace --skip 8 --count 4 > $out/timeline.txt || exit 1
-tail -30 $out/timeline.txt
+bash scripts/gpu_suite.sh || exit 1
+bash scripts/profile.sh r05h --flag batch_pipeline=0 || exit 1
+timeout -k 10 400 python -u bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || { tail -20 gpurun_out/bench_default.err; exit 1; }
+cat gpurun_out/bench_default.json | head -c 600

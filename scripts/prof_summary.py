@@ -85,6 +85,8 @@ def main():
             traffic["kernel_class"] = args.kernel_class
             # the result layout the profiled bench ran with (bench.py uses the bytes only for the same one)
             traffic["compact"] = bool(bench and ((bench.get("roofline") or {}).get("stored_width") or {}).get("compact_results"))
+            # ... and whether it wrote the YIELD columns only (bench.py's default since r05; --row-arrays not)
+            traffic["yield_only"] = bool(bench and "yield_only" in (bench.get("timed_region") or ""))
             traffic["kernel_name"] = d["kernel"]
             if d["fetch_bytes_x2"] is not None and d["write_bytes"] is not None:
                 traffic["bytes_per_launch"] = d["fetch_bytes_x2"] + d["write_bytes"]

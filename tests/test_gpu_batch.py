@@ -151,13 +151,13 @@ def test_batch_last_result_stays_on_device(rmat):
     assert e.go_batch([]) == []
 
 
-@pytest.mark.parametrize("close_stream", [1, 0])
-@pytest.mark.parametrize("lanes", [2, 3, 4])
-def test_batch_lanes(rmat, lanes, close_stream):
+@pytest.mark.parametrize("lanes,close_stream,fronts", [(2, 0, 2), (3, 0, 2), (4, 0, 2), (3, 0, 1), (3, 1, 1), (2, 1, 1)])
+def test_batch_lanes(rmat, lanes, close_stream, fronts):
     """Deeper pipelines (flag batch_lanes: up to lanes - 1 queries wait for their row counts while the next
-    one runs its hops on its own lane and its own result rows), with each overlapped final hop's close on
-    the close stream beside the next final hop (flag batch_close_stream) or behind it: every query's code,
-    row count, scanned edges and row digest are what it has alone, over mixed plans."""
+    one runs its hops on its own lane and its own result rows), consecutive queries' hops on two front
+    streams (flag batch_fronts) or one, with each overlapped final hop's close on the close stream beside
+    the next final hop (flag batch_close_stream, one front stream) or behind it: every query's code, row
+    count, scanned edges and row digest are what it has alone, over mixed plans."""
     ds, o, e = rmat
     rng = random.Random(91 + lanes)
     qs = _queries(ds)
@@ -166,8 +166,10 @@ def test_batch_lanes(rmat, lanes, close_stream):
     preps = [_prepare(e, ds, q, m) for q, m in items]
     want = [_alone(e, ds, p) for p in preps]
     assert e.get_flag("batch_lanes") == 3 and e.get_flag("batch_close_stream") == 0
+    assert e.get_flag("batch_fronts") == 2
     e.set_flag("batch_lanes", lanes)
     e.set_flag("batch_close_stream", close_stream)
+    e.set_flag("batch_fronts", fronts)
     try:
         before = e.get_flag("batch_overlaps")
         got = e.go_batch(preps, digests=True)
@@ -176,6 +178,7 @@ def test_batch_lanes(rmat, lanes, close_stream):
     finally:
         e.set_flag("batch_lanes", 3)
         e.set_flag("batch_close_stream", 0)
+        e.set_flag("batch_fronts", 2)
     for (q, m), w, g in list(zip(items, want, got)) + list(zip(items[:12], want[:12], plain)):
         assert g[0] == w[0], (q, m, g, w)
         if g[0] == 0:
