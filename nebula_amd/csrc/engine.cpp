@@ -398,8 +398,22 @@ struct ngx_ctx {
     }
     // host timeline of a query (NGX_HOST_TRACE=1): launches and publication waits, printed per query
     bool htrace = false;
+    // pipelined batch host timeline (NGX_PIPE_TRACE=1): the same marks, tagged with the running query and
+    // kept with absolute CLOCK_MONOTONIC times until the batch ends (the pipeline stays on)
+    bool ptrace = false;
+    int32_t ptraceQuery = -1;
+    std::vector<std::pair<std::string, int64_t>> pmarks;
+    void pmark(const std::string& what) {
+        timespec ts;
+        clock_gettime(CLOCK_MONOTONIC, &ts);
+        pmarks.emplace_back("q" + std::to_string(ptraceQuery) + " " + what,
+                            static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec);
+    }
     std::vector<std::pair<std::string, std::chrono::steady_clock::time_point>> hmarks;
-    void hmark(const std::string& what) { if (htrace) hmarks.emplace_back(what, std::chrono::steady_clock::now()); }
+    void hmark(const std::string& what) {
+        if (htrace) hmarks.emplace_back(what, std::chrono::steady_clock::now());
+        if (ptrace) pmark(what);
+    }
     void hflush() {
         if (!htrace || hmarks.empty()) return;
         std::string line = "[ngx host]";
@@ -412,8 +426,8 @@ struct ngx_ctx {
     template <typename F>
     void timed(const char* name, uint64_t algoBytes, F&& f) {
         RoctxRange range(name);                        // a ROCTX range per kernel class launch (rocprofv3 --marker-trace)
-        if (htrace) hmark(std::string("L:") + name);
-        if (!prof) { f(); if (htrace) hmark(std::string("l:") + name); return; }
+        if (htrace || ptrace) hmark(std::string("L:") + name);
+        if (!prof) { f(); if (htrace || ptrace) hmark(std::string("l:") + name); return; }
         int k = statIndex(name);
         hipEvent_t a = ev(), b = ev();
         HIP_OK(hipEventRecord(a, stream));
@@ -1156,6 +1170,7 @@ uint64_t awaitPub(ngx_ctx* c, const Publish& p, const uint64_t* devCopy, uint64_
     auto t0 = std::chrono::steady_clock::now();
     // kernels.h Publish: the words are taken once the tag matches them
     uint64_t* const w = c->pin + (p.slot - c->pinDev);            // the slot's host view
+    c->hmark("await");
     auto take = [&](uint64_t& v) {
         const uint64_t tag = __atomic_load_n(&w[1], __ATOMIC_ACQUIRE);
         v = __atomic_load_n(&w[0], __ATOMIC_ACQUIRE);
@@ -1478,6 +1493,7 @@ int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
     }
     if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->cus < 1) c->cus = 256;
     if (const char* ht = std::getenv("NGX_HOST_TRACE")) c->htrace = std::string(ht) == "1";
+    if (const char* pt = std::getenv("NGX_PIPE_TRACE")) c->ptrace = std::string(pt) == "1";
     if (hipHostMalloc(reinterpret_cast<void**>(&c->pin), ngx_ctx::kPinBytes, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
         std::memset(c->pin, 0, ngx_ctx::kPinBytes);
         if (hipHostGetDevicePointer(reinterpret_cast<void**>(&c->pinDev), c->pin, 0) != hipSuccess) c->pinDev = nullptr;
@@ -4302,12 +4318,15 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
         return &j;
     };
     auto resume = [&](GoJob* j) {
+        c->ptraceQuery = j->idx;
+        if (c->ptrace) c->pmark("resume");
         c->useLane(j->idx % lanes);
         c->stream = c->pipeStreams[c->pipeFronts == 2 && (j->idx & 1) ? 2 : 0];   // query i's hops: front i % fronts
         P.cur = j;
         tBatch = &co;
         swapcontext(&P.main, &j->uc);
         P.cur = nullptr;
+        if (c->ptrace) c->pmark("yield " + std::to_string(j->state));
         return j->state;
     };
     c->pipe = &P;
@@ -4347,6 +4366,16 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
     c->pipe = nullptr;
     c->finalStream = nullptr;
     c->closeStream = nullptr;
+    if (c->ptrace && !c->pmarks.empty()) {
+        timespec tm, tb;
+        clock_gettime(CLOCK_MONOTONIC, &tm);
+        clock_gettime(CLOCK_BOOTTIME, &tb);
+        std::fprintf(stderr, "[ngx pipe] clocks monotonic %lld boottime %lld\n",
+                     static_cast<long long>(tm.tv_sec) * 1000000000LL + tm.tv_nsec,
+                     static_cast<long long>(tb.tv_sec) * 1000000000LL + tb.tv_nsec);
+        for (auto& m : c->pmarks) std::fprintf(stderr, "[ngx pipe] %lld %s\n", static_cast<long long>(m.second), m.first.c_str());
+        c->pmarks.clear();
+    }
     c->stream = ctxStream;
     // later calls use lane 0 and the context's stream, ordered after everything the batch enqueued
     c->useLane(0);

@@ -2,7 +2,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp; mkdir -p gpurun_out
-bash scripts/gpu_suite.sh || exit 1
-bash scripts/profile.sh r05h --flag batch_pipeline=0 || exit 1
-timeout -k 10 400 python -u bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || { tail -20 gpurun_out/bench_default.err; exit 1; }
-cat gpurun_out/bench_default.json | head -c 600
+out=gpurun_out/prof/r05j_pipe; mkdir -p $out
+NGX_PIPE_TRACE=1 timeout -k 10 300 rocprofv3 --kernel-trace -d "$out/trace" -o run -f csv -- \
+    python3 bench.py --steps 12 --warmup 3 --cpu-budget 0 > "$out/bench.json" 2> "$out/bench.err" || { echo "pipe trace failed"; tail -20 "$out/bench.err"; exit 1; }
+grep -c "ngx pipe" $out/bench.err
