@@ -379,7 +379,8 @@ void ngx_go_result_free(ngx_go_result* r);
  * device-resident result (codes / nrows / edges / digests may be NULL). Consecutive device-resident
  * plans without DISTINCT or input overlap (flag "batch_pipeline", default 1): the next query's host
  * preparation and first hops are enqueued while this one's final hop runs; every query's outcome is the
- * one it has alone. Device-resident results of the last query stay in HBM as ngx_go leaves them.
+ * one it has alone. Device-resident results of the last query stay in HBM as ngx_go leaves them (each
+ * lane has its own result arrays: a batch query's rows stay valid until its lane is reused).
  * Returns the first code that is not NGX_OK. */
 int32_t ngx_go_batch(ngx_ctx* ctx, const ngx_go_plan* const* plans, int32_t n, int32_t* codes, uint64_t* nrows,
                      uint64_t* edges, uint64_t* digests);
@@ -459,6 +460,14 @@ int32_t ngx_kernel_stats(ngx_ctx* ctx, const ngx_kernel_stat** out, int32_t* n);
  *   "batch_pipeline"  1 (default): ngx_go_batch overlaps consecutive device-resident queries (the next
  *          one's host work and first hops enqueued while this one's final hop runs); 0: strictly one
  *          after the other. Same results.
+ *   "batch_lanes"  2 .. 4 (default 3): lanes of scratch and result rows a pipelined batch rotates over; up
+ *          to lanes - 1 queries wait for their row counts while the next one runs its hops. Same results.
+ *   "batch_fronts"  1 or 2 (default 2): streams the batch's hops run on (consecutive queries alternate).
+ *   "batch_close_stream"  0 (default) / 1 (with one front stream): an overlapped final hop's close on a
+ *          stream of its own. Same results.
+ *   "batch_event_ring"  1 (default): each cross-stream wait of a batch takes its own event. Same results.
+ *   "compact_wg"  0 (default: 256 in a pipelined batch, else 1024), 256 or 1024: threads per workgroup of
+ *          the next-frontier compaction. Same results.
  * Read-only counters for ngx_get_flag: "jit_compiled", "jit_hits", "jit_failed", "jit_compile_us",
  * "jit_cached", "jit_evicted", "batch_overlaps" (queries of ngx_go_batch that overlapped the next). */
 int32_t ngx_set_flag(ngx_ctx* ctx, const char* name, int64_t value);
