@@ -94,6 +94,27 @@ namespace {
 std::atomic<bool> gPoison{std::getenv("NGX_POISON") != nullptr && std::getenv("NGX_POISON")[0] == '1'};
 constexpr int kPoisonByte = 0xA5;
 
+// Frees deferred while a pipelined batch runs on this thread: hipFree / hipHostFree wait for the whole
+// device to go idle, so a scratch buffer that grows in the middle of a batch (a lane meeting a larger
+// frontier than its earlier queries) would drain the pipeline (r05 trace: the host stalled 560 us on one
+// growth, both final hops behind it running alone). The batch frees them once at its end.
+thread_local bool tDeferFree = false;
+thread_local std::vector<std::pair<void*, bool>> tGraveyard;   // (pointer, page-locked host memory)
+void freeDevice(void* p) {
+    if (!p) return;
+    if (tDeferFree) tGraveyard.emplace_back(p, false);
+    else (void)hipFree(p);
+}
+void freeHost(void* p) {
+    if (!p) return;
+    if (tDeferFree) tGraveyard.emplace_back(p, true);
+    else (void)hipHostFree(p);
+}
+void drainGraveyard() {
+    for (auto& g : tGraveyard) (void)(g.second ? hipHostFree(g.first) : hipFree(g.first));
+    tGraveyard.clear();
+}
+
 // growable device buffer
 struct DBuf {
     void* p = nullptr;
@@ -102,7 +123,7 @@ struct DBuf {
     T* get(size_t n) {
         size_t bytes = std::max<size_t>(n * sizeof(T), 64);
         if (bytes > cap) {
-            if (p) (void)hipFree(p);
+            freeDevice(p);
             p = nullptr;
             size_t c = std::max(bytes, cap * 3 / 2);
             HIP_OK(hipMalloc(&p, c));
@@ -183,7 +204,7 @@ struct ngx_ctx {
         size_t cap = 0;
         char* get(size_t bytes) {
             if (bytes > cap) {
-                if (p) (void)hipHostFree(p);
+                freeHost(p);
                 p = nullptr;
                 // 25 % headroom: result sizes vary from query to query, and re-pinning a GB-sized
                 // staging block costs more than the copy itself
@@ -301,7 +322,7 @@ struct ngx_ctx {
     // queries' hops on alternate front streams, so two queries' hop chains run at once beside a final hop)
     // or the close stream (k_final_close of an overlapped final hop beside the next query's final hop: the
     // close reads and moves its own lane's rows only)
-    hipStream_t pipeStreams[3] = {nullptr, nullptr, nullptr};
+    hipStream_t pipeStreams[4] = {nullptr, nullptr, nullptr, nullptr};   // + [3] the close stream
     hipEvent_t pipeEv[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     // a ring of events for the batch's cross-stream waits: each wait gets an event no later record re-arms
     // while the wait may be pending (flag batch_event_ring; 0: the fixed pipeEv per role)
@@ -319,6 +340,11 @@ struct ngx_ctx {
     hipStream_t closeStream = nullptr;
     bool batchCloseStream = false;
     int32_t batchFronts = 2;                           // front streams of a pipelined batch (1 or 2)
+    // flag batch_cu_split N > 0: the batch's front streams on N CUs (every CU i with (i / 8) % (256 / N / 8)
+    // == 0, spread over the XCDs), its final stream on the others, so the hops' waves do not take slots
+    // from the final hop (streams created on first use with that split)
+    int32_t batchCuSplit = 0, cuSplitMade = 0;
+    hipStream_t splitStreams[4] = {nullptr, nullptr, nullptr, nullptr};
     int32_t pipeFronts = 1;                            // ... of the batch that runs
     hipStream_t finalStream = nullptr;
     void* coStack[kMaxLanes] = {nullptr, nullptr, nullptr, nullptr};
@@ -362,6 +388,7 @@ struct ngx_ctx {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
         for (auto st : pipeStreams) if (st) (void)hipStreamSynchronize(st);
+        for (auto st : splitStreams) if (st) (void)hipStreamSynchronize(st);
         spaces.clear();
         for (DBuf* b : {&oEntry, &sendBits, &recvBits,
                         &vcells, &misc, &oFlags, &rowCols, &rowLen, &rowOff, &rowBytes, &dkTable, &dkKeep, &dkPre, &dSrc, &dDst,
@@ -372,6 +399,7 @@ struct ngx_ctx {
         for (auto e : pipeEv) if (e) (void)hipEventDestroy(e);
         for (auto e : pipeRing) if (e) (void)hipEventDestroy(e);
         for (auto st : pipeStreams) if (st) (void)hipStreamDestroy(st);
+        for (auto st : splitStreams) if (st) (void)hipStreamDestroy(st);
         for (void* st : coStack) if (st) munmap(st, kCoStackBytes + 4096);
         if (comm) (void)ncclCommDestroy(comm);
         if (pin) (void)hipHostFree(pin);
@@ -1483,7 +1511,7 @@ int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
         // 0.365 / 0.371 vs 0.374 / 0.412 ms per C2 step with both at the default, same box (r05)
         int prLo = 0, prHi = 0;
         (void)hipDeviceGetStreamPriorityRange(&prLo, &prHi);
-        for (int k = 0; k < 3; k++)
+        for (int k = 0; k < 4; k++)
             if (hipStreamCreateWithPriority(&c->pipeStreams[k], hipStreamNonBlocking, k == 1 ? prLo : prHi) != hipSuccess)
                 c->pipeStreams[k] = nullptr;
         for (auto& e : c->pipeEv)
@@ -1890,6 +1918,11 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
     if (n == "trace_go") { c->traceGo = value != 0; return NGX_OK; }
     if (n == "batch_pipeline") { c->batchPipeline = value != 0; return NGX_OK; }
     if (n == "batch_close_stream") { c->batchCloseStream = value != 0; return NGX_OK; }
+    if (n == "batch_cu_split") {
+        if (value != 0 && value != 32 && value != 64 && value != 128) return fail(c, NGX_E_BAD_ARGUMENT, "batch_cu_split: 0, 32, 64 or 128");
+        c->batchCuSplit = static_cast<int32_t>(value);
+        return NGX_OK;
+    }
     if (n == "batch_fronts") {
         if (value != 1 && value != 2) return fail(c, NGX_E_BAD_ARGUMENT, "batch_fronts: 1 or 2");
         c->batchFronts = static_cast<int32_t>(value);
@@ -1934,6 +1967,7 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "batch_lanes") *value = c->batchLanes;
     else if (n == "batch_close_stream") *value = c->batchCloseStream ? 1 : 0;
     else if (n == "batch_fronts") *value = c->batchFronts;
+    else if (n == "batch_cu_split") *value = c->batchCuSplit;
     else if (n == "batch_event_ring") *value = c->batchEventRing ? 1 : 0;
     else if (n == "batch_overlaps") *value = static_cast<int64_t>(c->pipeOverlaps);
     else if (n == "compact_lane_rows") *value = c->compactLaneRows;
@@ -4270,7 +4304,7 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
         if (j.rc != NGX_OK && first == NGX_OK) first = j.rc;
     };
     const bool pipe = c->batchPipeline && n > 1 && c->world == 1 && !c->prof && !c->htrace && !c->traceGo &&
-                      c->pipeStreams[0] && c->pipeStreams[1] && c->pipeStreams[2] && c->pipeEv[0] && c->pipeEv[1] &&
+                      c->pipeStreams[0] && c->pipeStreams[1] && c->pipeStreams[2] && c->pipeStreams[3] && c->pipeEv[0] && c->pipeEv[1] &&
                       c->pipeEv[2] && c->pipeEv[3] && c->pipeEv[4] && coStacks(c);
     if (!pipe) {
         for (int32_t i = 0; i < n; i++) {
@@ -4281,6 +4315,25 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
         }
         return first;
     }
+    // CU split: masked copies of the role streams (front A, final, front B), made once per split
+    if (c->batchCuSplit > 0 && c->cuSplitMade != c->batchCuSplit && c->cus >= 256) {
+        for (auto& st : c->splitStreams) {
+            if (st) { (void)hipStreamSynchronize(st); (void)hipStreamDestroy(st); }
+            st = nullptr;
+        }
+        const int nw = (c->cus + 31) / 32;
+        std::vector<uint32_t> front(nw, 0), fin(nw, 0);
+        const int period = c->cus / c->batchCuSplit;       // one group of 8 CUs of every `period` to the fronts
+        for (int i = 0; i < c->cus; i++) {
+            const bool toFront = (i / 8) % period == 0;
+            (toFront ? front : fin)[i / 32] |= 1u << (i % 32);
+        }
+        bool ok = true;
+        for (int k = 0; k < 4 && ok; k++)
+            ok = hipExtStreamCreateWithCUMask(&c->splitStreams[k], static_cast<uint32_t>(nw), k == 1 ? fin.data() : front.data()) == hipSuccess;
+        c->cuSplitMade = ok ? c->batchCuSplit : 0;
+    }
+    hipStream_t* roles = (c->batchCuSplit > 0 && c->cuSplitMade == c->batchCuSplit) ? c->splitStreams : c->pipeStreams;
     GoPipe P;
     P.plans = plans;
     P.n = n;
@@ -4292,15 +4345,15 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
         if (c->activeLane != 0) c->useLane(0);
         // both streams after the context's earlier work
         // every stream after the context's earlier work
-        for (auto st : c->pipeStreams) streamAfter(st, ctxStream, c->pipeEv[2]);
+        for (int k = 0; k < 4; k++) streamAfter(roles[k], ctxStream, c->pipeEv[2]);
     } catch (const Error& e) {
         return fail(c, e.code, e.msg);
     }
-    c->stream = c->pipeStreams[0];
-    c->finalStream = c->pipeStreams[1];
+    c->stream = roles[0];
+    c->finalStream = roles[1];
     // the third stream: a second front stream, or (one front stream) the close stream
     c->pipeFronts = c->batchFronts == 2 ? 2 : 1;
-    c->closeStream = c->pipeFronts == 1 && c->batchCloseStream ? c->pipeStreams[2] : nullptr;
+    c->closeStream = c->batchCloseStream ? roles[3] : nullptr;
     BatchCo co{c, &P, digests != nullptr};
     // query i runs on lane i % lanes with the coroutine stack of that lane; up to lanes - 1 queries wait at
     // their deferral point (holding finals: one)
@@ -4321,7 +4374,7 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
         c->ptraceQuery = j->idx;
         if (c->ptrace) c->pmark("resume");
         c->useLane(j->idx % lanes);
-        c->stream = c->pipeStreams[c->pipeFronts == 2 && (j->idx & 1) ? 2 : 0];   // query i's hops: front i % fronts
+        c->stream = roles[c->pipeFronts == 2 && (j->idx & 1) ? 2 : 0];   // query i's hops: front i % fronts
         P.cur = j;
         tBatch = &co;
         swapcontext(&P.main, &j->uc);
@@ -4330,6 +4383,7 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
         return j->state;
     };
     c->pipe = &P;
+    tDeferFree = true;                                  // no device-wide wait inside the batch (freeDevice)
     GoJob* waiting[ngx_ctx::kMaxLanes];                 // deferred queries, oldest first
     int nw = 0;
     auto finishOldest = [&] {
@@ -4364,6 +4418,7 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
     }
     while (nw) finishOldest();
     c->pipe = nullptr;
+    tDeferFree = false;
     c->finalStream = nullptr;
     c->closeStream = nullptr;
     if (c->ptrace && !c->pmarks.empty()) {
@@ -4380,12 +4435,14 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
     // later calls use lane 0 and the context's stream, ordered after everything the batch enqueued
     c->useLane(0);
     try {
-        streamAfter(ctxStream, c->pipeStreams[0], c->pipeEv[0]);
-        streamAfter(ctxStream, c->pipeStreams[1], c->pipeEv[1]);
-        streamAfter(ctxStream, c->pipeStreams[2], c->pipeEv[3]);
+        streamAfter(ctxStream, roles[0], c->pipeEv[0]);
+        streamAfter(ctxStream, roles[1], c->pipeEv[1]);
+        streamAfter(ctxStream, roles[2], c->pipeEv[3]);
+        streamAfter(ctxStream, roles[3], c->pipeEv[4]);
     } catch (const Error& e) {
         if (first == NGX_OK) first = fail(c, e.code, e.msg);
     }
+    drainGraveyard();                                   // buffers replaced during the batch (one device wait)
     return first;
 }
 

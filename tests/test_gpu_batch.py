@@ -151,12 +151,13 @@ def test_batch_last_result_stays_on_device(rmat):
     assert e.go_batch([]) == []
 
 
-@pytest.mark.parametrize("lanes,close_stream,fronts", [(2, 0, 2), (3, 0, 2), (4, 0, 2), (3, 0, 1), (3, 1, 1), (2, 1, 1)])
+@pytest.mark.parametrize("lanes,close_stream,fronts", [(2, 0, 2), (3, 0, 2), (4, 0, 2), (3, 0, 1), (3, 1, 1), (2, 1, 1),
+                                                        (3, 1, 2)])
 def test_batch_lanes(rmat, lanes, close_stream, fronts):
     """Deeper pipelines (flag batch_lanes: up to lanes - 1 queries wait for their row counts while the next
     one runs its hops on its own lane and its own result rows), consecutive queries' hops on two front
     streams (flag batch_fronts) or one, with each overlapped final hop's close on the close stream beside
-    the next final hop (flag batch_close_stream, one front stream) or behind it: every query's code, row
+    the next final hop (flag batch_close_stream) or behind it: every query's code, row
     count, scanned edges and row digest are what it has alone, over mixed plans."""
     ds, o, e = rmat
     rng = random.Random(91 + lanes)
