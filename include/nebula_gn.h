@@ -463,8 +463,8 @@ int32_t ngx_kernel_stats(ngx_ctx* ctx, const ngx_kernel_stat** out, int32_t* n);
  *   "batch_lanes"  2 .. 4 (default 3): lanes of scratch and result rows a pipelined batch rotates over; up
  *          to lanes - 1 queries wait for their row counts while the next one runs its hops. Same results.
  *   "batch_fronts"  1 or 2 (default 2): streams the batch's hops run on (consecutive queries alternate).
- *   "batch_close_stream"  0 (default) / 1: an overlapped final hop's close on a stream of its own. Same
- *          results.
+ *   "batch_close_stream"  1 (default) / 0: an overlapped final hop's close on a stream of its own (the
+ *          next final hop does not queue behind it). Same results.
  *   "batch_cu_split"  0 (default) / 32, 64, 128: a batch's hops on that many CUs (groups of 8 spread over
  *          the XCDs), its final hops on the rest. Same results.
  *   "batch_event_ring"  1 (default): each cross-stream wait of a batch takes its own event. Same results.

@@ -334,11 +334,11 @@ struct ngx_ctx {
         if (!batchEventRing || !pipeRing[0]) return pipeEv[role];
         return pipeRing[pipeRingNext++ % kPipeRing];
     }
-    // set while a pipelined batch runs with flag batch_close_stream (off by default: r05 C2 0.330 vs 0.324
-    // ms per step with it — the next final hop still starts ~14 us after its front-stream dependency, the
-    // cross-queue hand-off, whichever queue the close is on)
+    // set while a pipelined batch runs with flag batch_close_stream (default on since the second front
+    // stream: C2 0.310 vs 0.317 ms per step; with one front stream it measured 0.330 vs 0.324, the next final
+    // hop waiting for its front-stream dependency anyway)
     hipStream_t closeStream = nullptr;
-    bool batchCloseStream = false;
+    bool batchCloseStream = true;
     int32_t batchFronts = 2;                           // front streams of a pipelined batch (1 or 2)
     // flag batch_cu_split N > 0: the batch's front streams on N CUs (every CU i with (i / 8) % (256 / N / 8)
     // == 0, spread over the XCDs), its final stream on the others, so the hops' waves do not take slots

@@ -166,7 +166,7 @@ def test_batch_lanes(rmat, lanes, close_stream, fronts):
     items = [(q, "lean") for q in qs[:8]] + items + [(q, "compact") for q in qs[-8:]]
     preps = [_prepare(e, ds, q, m) for q, m in items]
     want = [_alone(e, ds, p) for p in preps]
-    assert e.get_flag("batch_lanes") == 3 and e.get_flag("batch_close_stream") == 0
+    assert e.get_flag("batch_lanes") == 3 and e.get_flag("batch_close_stream") == 1
     assert e.get_flag("batch_fronts") == 2
     e.set_flag("batch_lanes", lanes)
     e.set_flag("batch_close_stream", close_stream)
@@ -178,7 +178,7 @@ def test_batch_lanes(rmat, lanes, close_stream, fronts):
         plain = e.go_batch(preps[:12])                  # no digests: nothing read back between the queries
     finally:
         e.set_flag("batch_lanes", 3)
-        e.set_flag("batch_close_stream", 0)
+        e.set_flag("batch_close_stream", 1)
         e.set_flag("batch_fronts", 2)
     for (q, m), w, g in list(zip(items, want, got)) + list(zip(items[:12], want[:12], plain)):
         assert g[0] == w[0], (q, m, g, w)
