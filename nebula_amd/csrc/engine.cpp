@@ -344,13 +344,6 @@ struct ngx_ctx {
     // == 0, spread over the XCDs), its final stream on the others, so the hops' waves do not take slots
     // from the final hop (streams created on first use with that split)
     int32_t batchCuSplit = 0, cuSplitMade = 0;
-    // flag batch_wait_value: a final hop's wait for its query's hops and a close's wait for its final hop as
-    // a stream write / wait of a monotonic word per producing stream (hipStreamWriteValue64 /
-    // hipStreamWaitValue64 on signal memory) instead of an event record / wait
-    bool batchWaitValue = false;
-    uint64_t* waitWords = nullptr;                     // [4] signal memory, one word per role stream
-    uint64_t waitSeq[4] = {0, 0, 0, 0};
-    hipStream_t waitRoles[4] = {nullptr, nullptr, nullptr, nullptr};
     hipStream_t splitStreams[4] = {nullptr, nullptr, nullptr, nullptr};
     int32_t pipeFronts = 1;                            // ... of the batch that runs
     hipStream_t finalStream = nullptr;
@@ -407,7 +400,6 @@ struct ngx_ctx {
         for (auto e : pipeRing) if (e) (void)hipEventDestroy(e);
         for (auto st : pipeStreams) if (st) (void)hipStreamDestroy(st);
         for (auto st : splitStreams) if (st) (void)hipStreamDestroy(st);
-        if (waitWords) (void)hipFree(waitWords);
         for (void* st : coStack) if (st) munmap(st, kCoStackBytes + 4096);
         if (comm) (void)ncclCommDestroy(comm);
         if (pin) (void)hipHostFree(pin);
@@ -1160,17 +1152,6 @@ void streamAfter(hipStream_t to, hipStream_t from, hipEvent_t ev) {
     HIP_OK(hipStreamWaitEvent(to, ev, 0));
 }
 
-// the same for a batch's hot hand-offs (flag batch_wait_value): `from` bumps its word, `to` waits for it
-void streamAfterRole(ngx_ctx* c, hipStream_t to, hipStream_t from, int role) {
-    int k = -1;
-    if (c->batchWaitValue && c->waitWords)
-        for (int i = 0; i < 4; i++) if (c->waitRoles[i] == from) k = i;
-    if (k < 0) { streamAfter(to, from, c->pipeEvent(role)); return; }
-    const uint64_t v = ++c->waitSeq[k];
-    HIP_OK(hipStreamWriteValue64(from, c->waitWords + k, v, 0));
-    HIP_OK(hipStreamWaitValue64(to, c->waitWords + k, v, hipStreamWaitValueGte, ~0ULL));
-}
-
 // A record hop during a pipelined batch: the deferrable last final hop runs on the final stream, after
 // this query's hops on the front stream, and its k_final_close on the close stream after it; any other
 // record hop stays on the front stream, after every final hop and close enqueued so far
@@ -1180,7 +1161,7 @@ struct FinalStreamScope {
     FinalStreamScope(ngx_ctx* c_, bool onFinal) : c(c_) {
         if (!c->finalStream) return;
         if (onFinal) {
-            streamAfterRole(c, c->finalStream, c->stream, 0);
+            streamAfter(c->finalStream, c->stream, c->pipeEvent(0));
             saved = c->stream;
             c->stream = c->finalStream;
         } else {
@@ -1937,7 +1918,6 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
     if (n == "trace_go") { c->traceGo = value != 0; return NGX_OK; }
     if (n == "batch_pipeline") { c->batchPipeline = value != 0; return NGX_OK; }
     if (n == "batch_close_stream") { c->batchCloseStream = value != 0; return NGX_OK; }
-    if (n == "batch_wait_value") { c->batchWaitValue = value != 0; return NGX_OK; }
     if (n == "batch_cu_split") {
         if (value != 0 && value != 32 && value != 64 && value != 128) return fail(c, NGX_E_BAD_ARGUMENT, "batch_cu_split: 0, 32, 64 or 128");
         c->batchCuSplit = static_cast<int32_t>(value);
@@ -1988,7 +1968,6 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "batch_close_stream") *value = c->batchCloseStream ? 1 : 0;
     else if (n == "batch_fronts") *value = c->batchFronts;
     else if (n == "batch_cu_split") *value = c->batchCuSplit;
-    else if (n == "batch_wait_value") *value = c->batchWaitValue ? 1 : 0;
     else if (n == "batch_event_ring") *value = c->batchEventRing ? 1 : 0;
     else if (n == "batch_overlaps") *value = static_cast<int64_t>(c->pipeOverlaps);
     else if (n == "compact_lane_rows") *value = c->compactLaneRows;
@@ -3358,7 +3337,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             {
                 hipStream_t fs = c->stream;
                 if (deferrable && c->closeStream) {
-                    streamAfterRole(c, c->closeStream, fs, 4);
+                    streamAfter(c->closeStream, fs, c->pipeEvent(4));
                     c->stream = c->closeStream;
                 }
                 try {
@@ -4372,16 +4351,6 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
     }
     c->stream = roles[0];
     c->finalStream = roles[1];
-    if (c->batchWaitValue && !c->waitWords) {
-        void* w = nullptr;
-        if (hipExtMallocWithFlags(&w, 64, hipMallocSignalMemory) == hipSuccess && w) {
-            c->waitWords = static_cast<uint64_t*>(w);
-            HIP_OK(hipMemset(c->waitWords, 0, 32));
-            HIP_OK(hipDeviceSynchronize());
-            for (auto& q : c->waitSeq) q = 0;
-        }
-    }
-    for (int k = 0; k < 4; k++) c->waitRoles[k] = roles[k];
     // the third stream: a second front stream, or (one front stream) the close stream
     c->pipeFronts = c->batchFronts == 2 ? 2 : 1;
     c->closeStream = c->batchCloseStream ? roles[3] : nullptr;

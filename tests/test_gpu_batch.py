@@ -151,10 +151,9 @@ def test_batch_last_result_stays_on_device(rmat):
     assert e.go_batch([]) == []
 
 
-@pytest.mark.parametrize("lanes,close_stream,fronts,wait_value", [(2, 0, 2, 0), (3, 0, 2, 0), (4, 0, 2, 0), (3, 0, 1, 0),
-                                                                   (3, 1, 1, 0), (2, 1, 1, 0), (3, 1, 2, 0), (3, 1, 2, 1),
-                                                                   (2, 0, 1, 1)])
-def test_batch_lanes(rmat, lanes, close_stream, fronts, wait_value):
+@pytest.mark.parametrize("lanes,close_stream,fronts", [(2, 0, 2), (3, 0, 2), (4, 0, 2), (3, 0, 1), (3, 1, 1), (2, 1, 1),
+                                                        (3, 1, 2)])
+def test_batch_lanes(rmat, lanes, close_stream, fronts):
     """Deeper pipelines (flag batch_lanes: up to lanes - 1 queries wait for their row counts while the next
     one runs its hops on its own lane and its own result rows), consecutive queries' hops on two front
     streams (flag batch_fronts) or one, with each overlapped final hop's close on the close stream beside
@@ -172,7 +171,6 @@ def test_batch_lanes(rmat, lanes, close_stream, fronts, wait_value):
     e.set_flag("batch_lanes", lanes)
     e.set_flag("batch_close_stream", close_stream)
     e.set_flag("batch_fronts", fronts)
-    e.set_flag("batch_wait_value", wait_value)
     try:
         before = e.get_flag("batch_overlaps")
         got = e.go_batch(preps, digests=True)
@@ -182,7 +180,6 @@ def test_batch_lanes(rmat, lanes, close_stream, fronts, wait_value):
         e.set_flag("batch_lanes", 3)
         e.set_flag("batch_close_stream", 1)
         e.set_flag("batch_fronts", 2)
-        e.set_flag("batch_wait_value", 0)
     for (q, m), w, g in list(zip(items, want, got)) + list(zip(items[:12], want[:12], plain)):
         assert g[0] == w[0], (q, m, g, w)
         if g[0] == 0:
