@@ -237,6 +237,7 @@ struct ngx_ctx {
     uint64_t pullSegWords = 0;
     int32_t compactLaneRows = 0;                        // compaction rows per lane: 0 = by shard size, else 4 / 8 / 16
     int32_t compactWg = 0;                              // compaction workgroup threads: 0 = auto, 256 or 1024
+    bool finalNtStores = false;                         // generated final hops store result rows non-temporally
     int64_t pullFactor = 200;                           // pull when 100 x hop edges >= pullFactor x shard rows (0: never)
     uint64_t pullHops = 0;
     // sparse intermediate hops (kernels.h SparseArgs): a push hop with E * sparseFactor <= V builds the next
@@ -1934,6 +1935,7 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
         c->batchLanes = static_cast<int32_t>(value);
         return NGX_OK;
     }
+    if (n == "final_nt_stores") { c->finalNtStores = value != 0; return NGX_OK; }
     if (n == "compact_wg") {
         if (value != 0 && value != 256 && value != 1024) return fail(c, NGX_E_BAD_ARGUMENT, "compact_wg: 0, 256 or 1024");
         c->compactWg = static_cast<int32_t>(value);
@@ -1972,6 +1974,7 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "batch_overlaps") *value = static_cast<int64_t>(c->pipeOverlaps);
     else if (n == "compact_lane_rows") *value = c->compactLaneRows;
     else if (n == "compact_wg") *value = c->compactWg;
+    else if (n == "final_nt_stores") *value = c->finalNtStores ? 1 : 0;
     else if (n == "pull_hops") *value = static_cast<int64_t>(c->pullHops);
     else if (n == "sparse_hops") *value = static_cast<int64_t>(c->sparseHops);
     else if (n == "xchg_lists") *value = c->xchgLists;
@@ -3054,6 +3057,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         jq.yKey = yAlias;
         jq.dstReplica = dstReplica;
         jq.rowMask = rowMask;
+        jq.ntStore = c->finalNtStores ? 1 : 0;
         for (int k = 0; k < 3; k++) jq.outW[k] = outW[k];
         if (compact) jq.yW = yW;
         jq.input = rw && rw->perRow;

@@ -60,6 +60,11 @@ template <typename T>
 __device__ __forceinline__ void gst(void* p, uint64_t i, T v) {
     ((__attribute__((address_space(1))) T*)p)[i] = v;
 }
+// a non-temporal (streaming) store: the line is not kept in L2 for reuse
+template <typename T>
+__device__ __forceinline__ void gstNT(void* p, uint64_t i, T v) {
+    __builtin_nontemporal_store(v, &((__attribute__((address_space(1))) T*)p)[i]);
+}
 
 // element i of an integer array stored at its narrowest signed width w (1, 2, 4 or 8 bytes)
 __device__ __forceinline__ int64_t loadW(const void* p, int32_t w, uint64_t i) {
@@ -90,9 +95,13 @@ __device__ __forceinline__ void storeW(void* p, int32_t w, uint64_t i, int64_t v
         default: gst<int64_t>(p, i, v); break;
     }
 }
-template <int W>                        // width known at compile time (generated kernels); 0: runtime w
+template <int W, bool NT = false>      // width known at compile time (generated kernels); 0: runtime w
 __device__ __forceinline__ void storeWT(void* p, int32_t w, uint64_t i, int64_t v) {
-    if constexpr (W == 1) gst<int8_t>(p, i, static_cast<int8_t>(v));
+    if constexpr (NT && W == 1) gstNT<int8_t>(p, i, static_cast<int8_t>(v));
+    else if constexpr (NT && W == 2) gstNT<int16_t>(p, i, static_cast<int16_t>(v));
+    else if constexpr (NT && W == 4) gstNT<int32_t>(p, i, static_cast<int32_t>(v));
+    else if constexpr (NT && W == 8) gstNT<int64_t>(p, i, v);
+    else if constexpr (W == 1) gst<int8_t>(p, i, static_cast<int8_t>(v));
     else if constexpr (W == 2) gst<int16_t>(p, i, static_cast<int16_t>(v));
     else if constexpr (W == 4) gst<int32_t>(p, i, static_cast<int32_t>(v));
     else if constexpr (W == 8) gst<int64_t>(p, i, v);
