@@ -1,4 +1,6 @@
 #!/bin/bash
+# End-of-round GPU call (r05n): the full -m gpu suite, the default bench line (with the CPU baseline),
+# then an A/B of one engine flag against the default. Every step has its own time limit.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp; mkdir -p gpurun_out
