@@ -238,7 +238,6 @@ struct ngx_ctx {
     int32_t compactLaneRows = 0;                        // compaction rows per lane: 0 = by shard size, else 4 / 8 / 16
     int32_t compactWg = 0;                              // compaction workgroup threads: 0 = auto, 256 or 1024
     bool finalNtStores = false;                         // generated final hops store result rows non-temporally
-    uint32_t resvGroups = kResvGroups;                  // GO final hop row-reservation groups (flag resv_groups: 8 or 16)
     int64_t pullFactor = 200;                           // pull when 100 x hop edges >= pullFactor x shard rows (0: never)
     uint64_t pullHops = 0;
     // sparse intermediate hops (kernels.h SparseArgs): a push hop with E * sparseFactor <= V builds the next
@@ -1937,11 +1936,6 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
         return NGX_OK;
     }
     if (n == "final_nt_stores") { c->finalNtStores = value != 0; return NGX_OK; }
-    if (n == "resv_groups") {
-        if (value != 8 && value != 16) return fail(c, NGX_E_BAD_ARGUMENT, "resv_groups: 8 or 16");
-        c->resvGroups = static_cast<uint32_t>(value);
-        return NGX_OK;
-    }
     if (n == "compact_wg") {
         if (value != 0 && value != 256 && value != 1024) return fail(c, NGX_E_BAD_ARGUMENT, "compact_wg: 0, 256 or 1024");
         c->compactWg = static_cast<int32_t>(value);
@@ -1981,7 +1975,6 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "compact_lane_rows") *value = c->compactLaneRows;
     else if (n == "compact_wg") *value = c->compactWg;
     else if (n == "final_nt_stores") *value = c->finalNtStores ? 1 : 0;
-    else if (n == "resv_groups") *value = c->resvGroups;
     else if (n == "pull_hops") *value = static_cast<int64_t>(c->pullHops);
     else if (n == "sparse_hops") *value = static_cast<int64_t>(c->sparseHops);
     else if (n == "xchg_lists") *value = c->xchgLists;
@@ -2338,7 +2331,7 @@ uint64_t* lookBack(ngx_ctx* c, uint64_t chunks) { return c->lbStatus.get<uint64_
 // allocations), 8 x 32 K 346 / 15, 8 x 64 K 325 / 15, 8 x 128 K 320 / 18, 16 x 32 K 326 / 24, 32 x 8 K
 // 347 / 83, 64 x 4 K 339 / 193 (the close kernel moves up to G blocks of rows)
 void resvGeometry(ngx_ctx* c, FinalArgs& a) {
-    a.resvG = c->resvGroups;
+    a.resvG = kResvGroups;
     a.resvShift = kResvShift;
     a.resvStride = 32;                                          // counters 256 B apart
     // two sets of counters: a launch uses one and its k_final_close clears the other for the next

@@ -189,22 +189,3 @@ def test_batch_lanes(rmat, lanes, close_stream, fronts):
     assert overlaps >= 10
     with pytest.raises(Exception):
         e.set_flag("batch_lanes", 5)
-
-
-def test_resv_groups_16(rmat):
-    """The final hop's rows reserved over 16 groups (flag resv_groups; two per XCD) instead of 8: every
-    plan's code, rows, edges and row digest as with 8, one at a time and in a pipelined batch."""
-    ds, o, e = rmat
-    qs = _queries(ds)
-    preps = [_prepare(e, ds, q, m) for q in qs for m in ("lean", "compact")]
-    want = [_alone(e, ds, p) for p in preps]
-    e.set_flag("resv_groups", 16)
-    try:
-        alone = [_alone(e, ds, p) for p in preps]
-        got = e.go_batch(preps, digests=True)
-    finally:
-        e.set_flag("resv_groups", 8)
-    for w, a, g in zip(want, alone, got):
-        assert a[:3] == w[:3] and g[0] == w[0]
-        if w[0] == 0:
-            assert a[3] == w[3] and (g[1], g[2]) == (w[1], w[2]) and tuple(g[3]) == tuple(w[3])
