@@ -379,8 +379,13 @@ void ngx_go_result_free(ngx_go_result* r);
  * device-resident result (codes / nrows / edges / digests may be NULL). Consecutive device-resident
  * plans without DISTINCT or input overlap (flag "batch_pipeline", default 1): the next query's host
  * preparation and first hops are enqueued while this one's final hop runs; every query's outcome is the
- * one it has alone. Device-resident results of the last query stay in HBM as ngx_go leaves them (each
- * lane has its own result arrays: a batch query's rows stay valid until its lane is reused).
+ * one it has alone. Every query's ngx_go_result is freed inside the call: only the codes, row counts,
+ * scanned edges and digests come back (no result handle). Memory: a pipelined batch runs query i on lane
+ * i % batch_lanes, and each lane keeps its own scratch (visited marks, frontiers, entry arrays sized by
+ * the shard) and result arrays (sized for every edge of the final hop's slots) after the call, so the
+ * context's steady HBM use is up to batch_lanes times ngx_go's; flag "release_lanes" = 1 frees the parked
+ * lanes now, "batch_release_lanes" = 1 after every batch ("released_lane_bytes" counts what was freed).
+ * A call that fails before any query runs (a NULL plan) writes its code for every query.
  * Returns the first code that is not NGX_OK. */
 int32_t ngx_go_batch(ngx_ctx* ctx, const ngx_go_plan* const* plans, int32_t n, int32_t* codes, uint64_t* nrows,
                      uint64_t* edges, uint64_t* digests);

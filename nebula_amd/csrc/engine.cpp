@@ -116,9 +116,11 @@ void drainGraveyard() {
 }
 
 // growable device buffer
+std::atomic<uint64_t> gDBufGen{0};
 struct DBuf {
     void* p = nullptr;
     size_t cap = 0;
+    uint64_t gen = 0;                                   // unique per allocation (hipMalloc may hand back a freed address)
     template <typename T>
     T* get(size_t n) {
         size_t bytes = std::max<size_t>(n * sizeof(T), 64);
@@ -128,6 +130,7 @@ struct DBuf {
             size_t c = std::max(bytes, cap * 3 / 2);
             HIP_OK(hipMalloc(&p, c));
             cap = c;
+            gen = gDBufGen.fetch_add(1, std::memory_order_relaxed) + 1;
             if (gPoison.load(std::memory_order_relaxed)) {
                 HIP_OK(hipMemset(p, kPoisonByte, c));
                 HIP_OK(hipDeviceSynchronize());
@@ -135,7 +138,7 @@ struct DBuf {
         }
         return static_cast<T*>(p);
     }
-    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; gen = 0; }
 };
 
 struct Timer {
@@ -238,6 +241,7 @@ struct ngx_ctx {
     int32_t compactLaneRows = 0;                        // compaction rows per lane: 0 = by shard size, else 4 / 8 / 16
     int32_t compactWg = 0;                              // compaction workgroup threads: 0 = auto, 256 or 1024
     bool finalNtStores = false;                         // generated final hops store result rows non-temporally
+    uint32_t resvGroups = kResvGroups;                  // GO final hop row-reservation groups (flag resv_groups, 1 .. kResvMaxGroups)
     int64_t pullFactor = 200;                           // pull when 100 x hop edges >= pullFactor x shard rows (0: never)
     uint64_t pullHops = 0;
     // sparse intermediate hops (kernels.h SparseArgs): a push hop with E * sparseFactor <= V builds the next
@@ -254,9 +258,11 @@ struct ngx_ctx {
     uint64_t xchgListHops = 0;
     DBuf xListSend, xListRecv, xCounts;
     // the frontier bitmap is known to be all zero (a sparse hop's dedup set starts from it): set by a
-    // compaction that wrote zeros, cleared by every other writer
+    // compaction that wrote zeros, cleared by every other writer. Keyed on the allocation (pointer and
+    // DBuf::gen) and the words zeroed: a query in a space with more rows needs more zero words
     bool bitsClean = false;
     const void* bitsCleanPtr = nullptr;
+    uint64_t bitsCleanGen = 0, bitsCleanWords = 0;
     // device-driven hops (no host round trip per hop). Off by default: on MI355X the upper-bound grids
     // and the idle launch of the expansion not taken cost what the round trips saved (C2 step: device
     // 680 vs 656 us, profiles/r02_dyn_*); kept as an option ("dyn_hops", NGX_DYN_HOPS=1)
@@ -299,6 +305,7 @@ struct ngx_ctx {
         uint8_t epoch = 0;
         bool bitsClean = false;
         const void* bitsCleanPtr = nullptr;
+        uint64_t bitsCleanGen = 0, bitsCleanWords = 0;
         std::string progLast;
         const char* progLastPtr = nullptr;
         PinBuf inStage, seedStage;
@@ -358,7 +365,7 @@ struct ngx_ctx {
         NGX_LANE_SWAP(cmpStatus[0]) NGX_LANE_SWAP(cmpStatus[1]) NGX_LANE_SWAP(frontierBits) NGX_LANE_SWAP(localBits)
         NGX_LANE_SWAP(edgeMask) NGX_LANE_SWAP(pullSeg) NGX_LANE_SWAP(pullCtl) NGX_LANE_SWAP(sparseCtl) NGX_LANE_SWAP(dynStats)
         NGX_LANE_SWAP(progBuf) NGX_LANE_SWAP(visitedSize) NGX_LANE_SWAP(pullSegWords) NGX_LANE_SWAP(epoch)
-        NGX_LANE_SWAP(bitsClean) NGX_LANE_SWAP(bitsCleanPtr) NGX_LANE_SWAP(progLast) NGX_LANE_SWAP(progLastPtr)
+        NGX_LANE_SWAP(bitsClean) NGX_LANE_SWAP(bitsCleanPtr) NGX_LANE_SWAP(bitsCleanGen) NGX_LANE_SWAP(bitsCleanWords) NGX_LANE_SWAP(progLast) NGX_LANE_SWAP(progLastPtr)
         NGX_LANE_SWAP(inStage) NGX_LANE_SWAP(seedStage) NGX_LANE_SWAP(pinLane)
         NGX_LANE_SWAP(oSrc) NGX_LANE_SWAP(oDst) NGX_LANE_SWAP(oRank) NGX_LANE_SWAP(oType) NGX_LANE_SWAP(oColDesc)
         NGX_LANE_SWAP(resvTab) NGX_LANE_SWAP(resvCtl) NGX_LANE_SWAP(oCols) NGX_LANE_SWAP(oColView)
@@ -385,6 +392,40 @@ struct ngx_ctx {
         inStage.release();
         seedStage.release();
     }
+    // the parked lanes' scratch and result rows freed (flag batch_release_lanes, or release_lanes = 1 once):
+    // a pipelined batch leaves lanes 1 .. kMaxLanes - 1 holding buffers as large as lane 0's. Called with no
+    // batch running; hipFree waits for the work that still reads them.
+    uint64_t releaseParked() {
+        uint64_t freed = 0;
+        const int was = activeLane;
+        for (int k = 0; k < kMaxLanes; k++) {
+            if (k == was) continue;
+            useLane(k);
+            for (DBuf* b : {&visited, &F0, &F1, &estart, &ebase, &chunkFirst, &estart2, &ebase2, &chunkFirst2, &tileSums,
+                            &counters, &lbStatus, &seedPart, &seedVid, &cmpStatus[0], &cmpStatus[1], &frontierBits,
+                            &localBits, &edgeMask, &pullSeg, &pullCtl, &sparseCtl, &dynStats, &progBuf, &oSrc, &oDst, &oRank,
+                            &oType, &oColDesc, &resvTab, &resvCtl})
+                freed += b->cap;
+            for (auto& cb : oCols) freed += cb.x.cap + cb.len.cap + cb.t.cap;
+            releaseLane();
+            oCols.clear();
+            oColView.clear();
+            visitedSize = pullSegWords = 0;
+            epoch = 0;
+            bitsClean = false;
+            bitsCleanPtr = nullptr;
+            bitsCleanGen = bitsCleanWords = 0;
+            progLast.clear();
+            progLastPtr = nullptr;
+            resvTabWords = 0;
+            resvLastG = resvLastStride = resvParity = 0;
+            resvClosePending = false;
+        }
+        useLane(was);
+        return freed;
+    }
+    uint64_t releasedBytes = 0;
+    bool batchReleaseLanes = false;
     ~ngx_ctx() {                                       // also the cleanup of ngx_open's error paths
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
@@ -1930,12 +1971,23 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
         return NGX_OK;
     }
     if (n == "batch_event_ring") { c->batchEventRing = value != 0; return NGX_OK; }
+    if (n == "batch_release_lanes") { c->batchReleaseLanes = value != 0; return NGX_OK; }
+    if (n == "release_lanes") {                       // action: free the parked lanes' buffers now
+        if (value) c->releasedBytes += c->releaseParked();
+        return NGX_OK;
+    }
     if (n == "batch_lanes") {
         if (value < 2 || value > ngx_ctx::kMaxLanes) return fail(c, NGX_E_BAD_ARGUMENT, "batch_lanes: 2 .. 4");
         c->batchLanes = static_cast<int32_t>(value);
         return NGX_OK;
     }
     if (n == "final_nt_stores") { c->finalNtStores = value != 0; return NGX_OK; }
+    if (n == "resv_groups") {
+        if (value < 1 || value > static_cast<int64_t>(kResvMaxGroups))
+            return fail(c, NGX_E_BAD_ARGUMENT, "resv_groups: 1 .. " + std::to_string(kResvMaxGroups));
+        c->resvGroups = static_cast<uint32_t>(value);
+        return NGX_OK;
+    }
     if (n == "compact_wg") {
         if (value != 0 && value != 256 && value != 1024) return fail(c, NGX_E_BAD_ARGUMENT, "compact_wg: 0, 256 or 1024");
         c->compactWg = static_cast<int32_t>(value);
@@ -1967,6 +2019,8 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "trace_go") *value = c->traceGo ? 1 : 0;
     else if (n == "batch_pipeline") *value = c->batchPipeline ? 1 : 0;
     else if (n == "batch_lanes") *value = c->batchLanes;
+    else if (n == "batch_release_lanes") *value = c->batchReleaseLanes ? 1 : 0;
+    else if (n == "released_lane_bytes") *value = static_cast<int64_t>(c->releasedBytes);
     else if (n == "batch_close_stream") *value = c->batchCloseStream ? 1 : 0;
     else if (n == "batch_fronts") *value = c->batchFronts;
     else if (n == "batch_cu_split") *value = c->batchCuSplit;
@@ -1975,6 +2029,7 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "compact_lane_rows") *value = c->compactLaneRows;
     else if (n == "compact_wg") *value = c->compactWg;
     else if (n == "final_nt_stores") *value = c->finalNtStores ? 1 : 0;
+    else if (n == "resv_groups") *value = c->resvGroups;
     else if (n == "pull_hops") *value = static_cast<int64_t>(c->pullHops);
     else if (n == "sparse_hops") *value = static_cast<int64_t>(c->sparseHops);
     else if (n == "xchg_lists") *value = c->xchgLists;
@@ -2331,7 +2386,7 @@ uint64_t* lookBack(ngx_ctx* c, uint64_t chunks) { return c->lbStatus.get<uint64_
 // allocations), 8 x 32 K 346 / 15, 8 x 64 K 325 / 15, 8 x 128 K 320 / 18, 16 x 32 K 326 / 24, 32 x 8 K
 // 347 / 83, 64 x 4 K 339 / 193 (the close kernel moves up to G blocks of rows)
 void resvGeometry(ngx_ctx* c, FinalArgs& a) {
-    a.resvG = kResvGroups;
+    a.resvG = c->resvGroups;
     a.resvShift = kResvShift;
     a.resvStride = 32;                                          // counters 256 B apart
     // two sets of counters: a launch uses one and its k_final_close clears the other for the next
@@ -2352,6 +2407,20 @@ void resvGeometry(ngx_ctx* c, FinalArgs& a) {
     c->resvParity ^= 1;
     c->resvLastG = a.resvG;
     c->resvLastStride = a.resvStride;
+}
+// the frontier bitmap's zero state (ngx_ctx::bitsClean): `bits` is one of the context's bitmaps
+static uint64_t bitsGen(const ngx_ctx* c, const void* bits) {
+    return bits == c->frontierBits.p ? c->frontierBits.gen : bits == c->localBits.p ? c->localBits.gen : 0;
+}
+bool bitsKnownZero(const ngx_ctx* c, const void* bits, uint64_t words) {
+    return c->bitsClean && bits != nullptr && c->bitsCleanPtr == bits && c->bitsCleanGen == bitsGen(c, bits) &&
+           c->bitsCleanGen != 0 && c->bitsCleanWords >= words;
+}
+void markBitsZero(ngx_ctx* c, const void* bits, uint64_t words) {
+    c->bitsClean = true;
+    c->bitsCleanPtr = bits;
+    c->bitsCleanGen = bitsGen(c, bits);
+    c->bitsCleanWords = words;
 }
 uint64_t* resvTable(ngx_ctx* c, uint64_t words) {
     if (c->resvTabWords < words || c->resvTab.p == nullptr) {
@@ -3012,7 +3081,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     uint32_t* F1spec = nullptr;
     const bool devNext1 = spec1 && finalDev && steps == 2;
     if (spec1) {
-        if (!c->bitsClean || c->bitsCleanPtr != lbits) HIP_OK(hipMemsetAsync(lbits, 0, (d.V + 63) / 64 * 8, c->stream));
+        if (!bitsKnownZero(c, lbits, (d.V + 63) / 64)) HIP_OK(hipMemsetAsync(lbits, 0, (d.V + 63) / 64 * 8, c->stream));
         c->bitsClean = false;
         if (!c->sparseCtl.p) {
             c->sparseCtl.get<uint64_t>(2);
@@ -3498,7 +3567,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         uint64_t* tiles2 = c->tileSums.get<uint64_t>((std::max<uint64_t>(d.V, 1) + kTile - 1) / kTile + 1);
         if (sparse) {
             // the bitmap must start all zero: it is the hop's dedup set and then the next frontier's bits
-            if (!c->bitsClean || c->bitsCleanPtr != lbits) HIP_OK(hipMemsetAsync(lbits, 0, (d.V + 63) / 64 * 8, c->stream));
+            if (!bitsKnownZero(c, lbits, (d.V + 63) / 64)) HIP_OK(hipMemsetAsync(lbits, 0, (d.V + 63) / 64 * 8, c->stream));
             c->bitsClean = false;
             if (!c->sparseCtl.p) {
                 c->sparseCtl.get<uint64_t>(2);
@@ -3575,7 +3644,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             c->timed("compact_degrees", 0, [&] {
                 if (launchCompactLb(ca, c->stream)) throw Error{NGX_E_DEVICE, "compact"};
             });
-            if (ca.bits && ca.bitsZero) { c->bitsClean = true; c->bitsCleanPtr = ca.bits; }
+            if (ca.bits && ca.bitsZero) markBitsZero(c, ca.bits, (d.V + 63) / 64);
             haveEstart = true;
             haveEbase = true;
             haveHeads = true;
@@ -4296,8 +4365,15 @@ extern "C" int32_t ngx_go(ngx_ctx* c, const ngx_go_plan* p, ngx_go_result** out)
 // this one's final hop runs. Every query's rows, counts and errors are those it has alone.
 extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int32_t n, int32_t* codes, uint64_t* nrows,
                                 uint64_t* edges, uint64_t* digests) {
-    if (!c || (n > 0 && !plans)) return NGX_E_BAD_ARGUMENT;
-    for (int32_t i = 0; i < n; i++) if (!plans[i]) return NGX_E_BAD_ARGUMENT;
+    // a call that fails before a query runs reports its code for every query (never zero-filled success)
+    auto failAll = [&](int32_t rc) {
+        for (int32_t i = 0; codes && i < n; i++) codes[i] = rc;
+        for (int32_t i = 0; nrows && i < n; i++) nrows[i] = 0;
+        for (int32_t i = 0; edges && i < n; i++) edges[i] = 0;
+        return rc;
+    };
+    if (!c || (n > 0 && !plans)) return failAll(NGX_E_BAD_ARGUMENT);
+    for (int32_t i = 0; i < n; i++) if (!plans[i]) return failAll(fail(c, NGX_E_BAD_ARGUMENT, "go_batch: null plan"));
     std::lock_guard<std::mutex> g(c->mu);
     int32_t first = NGX_OK;
     auto record = [&](const GoJob& j) {
@@ -4351,7 +4427,7 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
         // every stream after the context's earlier work
         for (int k = 0; k < 4; k++) streamAfter(roles[k], ctxStream, c->pipeEv[2]);
     } catch (const Error& e) {
-        return fail(c, e.code, e.msg);
+        return failAll(fail(c, e.code, e.msg));
     }
     c->stream = roles[0];
     c->finalStream = roles[1];
@@ -4447,6 +4523,7 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
         if (first == NGX_OK) first = fail(c, e.code, e.msg);
     }
     drainGraveyard();                                   // buffers replaced during the batch (one device wait)
+    if (c->batchReleaseLanes) c->releasedBytes += c->releaseParked();
     return first;
 }
 

@@ -600,7 +600,9 @@ class Engine:
         arr = (ctypes.POINTER(GoPlan) * max(n, 1))(*[ctypes.pointer(p.plan) for p in prepared])
         codes, rows, edges = (c_i32 * max(n, 1))(), (c_u64 * max(n, 1))(), (c_u64 * max(n, 1))()
         dg = (c_u64 * max(3 * n, 1))() if digests else None
-        self.L.ngx_go_batch(self.h, ctypes.cast(arr, ctypes.c_void_p), n, codes, rows, edges, dg)
+        rc = self.L.ngx_go_batch(self.h, ctypes.cast(arr, ctypes.c_void_p), n, codes, rows, edges, dg)
+        if rc != 0 and all(codes[i] == 0 for i in range(n)):
+            raise EngineError(rc, "go_batch: " + self.L.ngx_last_error(self.h).decode())
         out = [(int(codes[i]), int(rows[i]), int(edges[i])) for i in range(n)]
         if digests:
             out = [o + ((int(dg[3 * i]), int(dg[3 * i + 1]), int(dg[3 * i + 2])),) for i, o in enumerate(out)]

@@ -189,3 +189,94 @@ def test_batch_lanes(rmat, lanes, close_stream, fronts):
     assert overlaps >= 10
     with pytest.raises(Exception):
         e.set_flag("batch_lanes", 5)
+
+
+def _digest_fixed(q, mode):
+    """A DISTINCT result keeps one row of each group, whichever came first (GoExecutor.cpp:1298-1305): the
+    YIELD columns are fixed, the src vid of the row kept is not. The lean plans (yield_only) hash no src."""
+    return "DISTINCT" not in q or mode == "lean"
+
+
+@pytest.mark.parametrize("groups", [16, 4, 1, 64])
+def test_resv_groups(rmat, groups):
+    """The final hop's rows reserved over another number of groups (flag resv_groups; 8 = a group per XCD
+    by default): every plan's code, rows, edges and row digest as with 8, one at a time and in a pipelined
+    batch. (Round 5 saw a digest differ at 16 groups: it was a DISTINCT plan whose digest hashes the src of
+    whichever row of a group DISTINCT keeps, which the row placement decides, not a misplaced row.)"""
+    ds, o, e = rmat
+    qs = _queries(ds)
+    items = [(q, m) for q in qs for m in ("lean", "compact")]
+    preps = [_prepare(e, ds, q, m) for q, m in items]
+    want = [_alone(e, ds, p) for p in preps]
+    e.set_flag("resv_groups", groups)
+    try:
+        assert e.get_flag("resv_groups") == groups
+        alone = [_alone(e, ds, p) for p in preps]
+        got = e.go_batch(preps, digests=True)
+    finally:
+        e.set_flag("resv_groups", 8)
+    for (q, m), w, a, g in zip(items, want, alone, got):
+        assert a[:3] == w[:3] and g[0] == w[0], (q, m)
+        if w[0] == 0:
+            assert (g[1], g[2]) == (w[1], w[2]), (q, m)
+            if _digest_fixed(q, m):
+                assert a[3] == w[3] and tuple(g[3]) == tuple(w[3]), (q, m)
+
+
+def test_resv_groups_switch(rmat):
+    """8 -> 16 -> 8 -> 3 groups on one context, a batch after each switch (the counters are reallocated,
+    the block table keeps entries of other geometries, tagged by launch): the bench's query shape equals
+    the oracle's rows every time."""
+    ds, o, e = rmat
+    preps, refs = [], []
+    for k in range(4):
+        seeds = datagen.sample_vids(7300 + k, 1 << ds.scale, 40)
+        q = f"GO 3 STEPS FROM {', '.join(str(int(v)) for v in seeds)} OVER e WHERE e.p0 < 50 YIELD e._dst, e._rank, e.p0, e.p1"
+        s = ngql.parse_go(q)
+        ref = o.go(ds.space, s)
+        assert ref.ok
+        cols = [np.array([int(r[c][1]) for r in ref.rows], dtype=np.int64) for c in range(len(s.yields))]
+        refs.append((len(ref.rows), int(sum(ref.hop_scanned)), oracle.row_digest([np.zeros(len(ref.rows), np.int64)] + cols)))
+        preps.append(e.prepare_go(ds.space, s, on_device=True, compact=True, yield_only=True))
+    try:
+        for groups in (8, 16, 8, 3, 8):
+            e.set_flag("resv_groups", groups)
+            got = e.go_batch(preps + preps, digests=True)
+            for (code, rows, edges, dig), ref in zip(got, refs + refs):
+                assert code == 0 and (rows, edges, tuple(dig)) == (ref[0], ref[1], tuple(ref[2])), groups
+            r = e.go(ds.space, preps[0], rows=False, device_digest=True)
+            assert r.ok and (r.nrows, tuple(r.device_digest)) == (refs[0][0], tuple(refs[0][2])), groups
+    finally:
+        e.set_flag("resv_groups", 8)
+
+
+def test_release_parked_lanes(rmat):
+    """the parked lanes' scratch and result rows are freed on request (flag release_lanes, or
+    batch_release_lanes after every batch), and later batches give the same outcomes."""
+    ds, o, e = rmat
+    qs = _queries(ds)[:8]
+    preps = [_prepare(e, ds, q, "lean") for q in qs]
+    first = e.go_batch(preps, digests=True)
+    before = e.get_flag("released_lane_bytes")
+    e.set_flag("release_lanes", 1)
+    assert e.get_flag("released_lane_bytes") > before
+    assert e.go_batch(preps, digests=True) == first
+    e.set_flag("batch_release_lanes", 1)
+    try:
+        mid = e.get_flag("released_lane_bytes")
+        assert e.go_batch(preps, digests=True) == first
+        assert e.get_flag("released_lane_bytes") > mid
+        assert e.go_batch(preps, digests=True) == first
+    finally:
+        e.set_flag("batch_release_lanes", 0)
+
+
+def test_batch_bad_plan_reports_every_query():
+    """a batch that fails before any query runs (a null plan) reports the error for every
+    query; the Python wrapper raises instead of returning zero-filled successes."""
+    import ctypes
+    with engine.Engine(0) as e:
+        codes = (ctypes.c_int32 * 2)()
+        arr = (ctypes.c_void_p * 2)(None, None)
+        rc = e.L.ngx_go_batch(e.h, ctypes.cast(arr, ctypes.c_void_p), 2, codes, None, None, None)
+        assert rc != 0 and list(codes) == [rc, rc]

@@ -155,3 +155,35 @@ def test_sparse_gotest_nba():
                 r = e.go(ds.space, ngql.parse_go(q))
                 assert fixtures.normalize_cells(r.rows) == ([] if case.get("empty") else fixtures.nba_expected(case["rows"]))
     o.close()
+
+
+def test_sparse_bitmap_clean_state_across_spaces():
+    """the frontier bitmap's zero state is keyed on the allocation and the words a
+    compaction zeroed, not on the pointer alone. A GO 2 STEPS in the larger space leaves its sparse hop's
+    bits set over its rows; a GO 3 STEPS in the smaller space clears only its own words, then its hop-2
+    compaction writes them as zeros and marks the bitmap clean; the larger space's next sparse hop must
+    still clear the words past the smaller space's rows, or its dedup sees stale bits and drops rows."""
+    big = fixtures.RmatDataset(13, with_in=True)
+    small = fixtures.GenDataset(datagen.RMAT_SPACE + 7, 100, datagen.rmat(10, 16, 43, 100, True, False),
+                                datagen.rmat_schemas(False))
+    o = oracle.Oracle()
+    o.set_flags(threads=8)
+    big.load_oracle(o)
+    small.load_oracle(o)
+    with engine.Engine(0) as e:
+        big.load_engine(e)
+        small.load_engine(e)
+        e.set_flag("pull_factor", 0)
+        e.set_flag("sparse_factor", 16)
+        sb = datagen.sample_vids(11, 1 << 13, 4)
+        ss = datagen.sample_vids(12, 1 << 10, 30)
+        qb = f"GO 2 STEPS FROM {', '.join(str(int(v)) for v in sb)} OVER e YIELD e._src, e._dst, e.p0"
+        qs = f"GO 3 STEPS FROM {', '.join(str(int(v)) for v in ss)} OVER e YIELD e._dst, e.p1"
+        for space, q in [(big.space, qb), (small.space, qs), (big.space, qb), (small.space, qs), (big.space, qb)]:
+            s = ngql.parse_go(q)
+            got, ref = e.go(space, s), o.go(space, s)
+            assert got.ok and ref.ok
+            assert got.hop_edges == ref.hop_scanned
+            assert fixtures.normalize_cells(got.rows) == fixtures.normalize_cells(ref.rows)
+        assert e.get_flag("sparse_hops") >= 3
+    o.close()

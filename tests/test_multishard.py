@@ -196,12 +196,27 @@ def test_multishard_go_matches_oracle(tmp_path, world, scale):
     # and with every hop pushed and its frontier exchanged as vid lists (counts, then the vids: SURVEY
     # §8e) instead of bitmaps
     listed = [dict(q, pull_factor=0, xchg_lists=1) for q in queries]
-    shards, digests = _run_shards(tmp_path, world, scale, queries + pulled + listed)
-    _check_merged(o, ds.space, queries + pulled + listed, shards, digests)
+    # and with the defaults (xchg_lists -1: lists or bitmaps chosen per hop by size, pull factor 200), one
+    # seed for the small frontiers lists favour and 300 for the large ones bitmaps favour
+    auto = []
+    for i, (text, push) in enumerate(MS_QUERIES):
+        for k, ns in enumerate((1, 300)):
+            seeds = datagen.sample_vids(800 + 2 * i + k, 1 << scale, ns)
+            auto.append({"text": text.replace("{S}", ", ".join(str(int(v)) for v in seeds)), "pushdown": push})
+    shards, digests = _run_shards(tmp_path, world, scale, queries + pulled + listed + auto)
+    _check_merged(o, ds.space, queries + pulled + listed + auto, shards, digests)
     n = len(queries)
     m = n + len(pulled)
+    a0 = m + len(listed)
     for s in shards:
-        assert sum(r["list_hops"] for r in s[m:]) > 0 and sum(r["list_hops"] for r in s[:n]) == 0
+        assert sum(r["list_hops"] for r in s[m:a0]) > 0 and sum(r["list_hops"] for r in s[:n]) == 0
+        # default mode: both exchange forms occur over the queries (a hop with exchanged bytes that is
+        # neither a list hop nor a pulled hop sent bitmaps)
+        lists = sum(r["list_hops"] for r in s[a0:])
+        bitmaps = sum(sum(1 for x in r["hop_xchg"] if x > 0) - r["list_hops"] - r["pull_hops"] for r in s[a0:] if r["ok"])
+        assert lists > 0 and bitmaps > 0, (lists, bitmaps)
+    for s in shards:                                     # the default mode takes the same decisions everywhere
+        assert [r["list_hops"] for r in s[a0:]] == [r["list_hops"] for r in shards[0][a0:]]
         # list bytes: 4 per exchanged vid plus the counts, below the bitmaps' V / 8 per peer on these hops
         assert all(r["ok"] for r in s[m:])
     for s in shards:                                     # every shard takes the same pull decisions
