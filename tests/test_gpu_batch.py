@@ -193,8 +193,9 @@ def test_batch_lanes(rmat, lanes, close_stream, fronts):
 
 def _digest_fixed(q, mode):
     """A DISTINCT result keeps one row of each group, whichever came first (GoExecutor.cpp:1298-1305): the
-    YIELD columns are fixed, the src vid of the row kept is not. The lean plans (yield_only) hash no src."""
-    return "DISTINCT" not in q or mode == "lean"
+    YIELD columns are fixed, the src vid of the row kept is not, and the device digest hashes it (DISTINCT
+    plans keep the src row array: yield_only does not apply to them). Their rows are compared as cells."""
+    return "DISTINCT" not in q
 
 
 @pytest.mark.parametrize("groups", [16, 4, 1, 64])
@@ -221,6 +222,15 @@ def test_resv_groups(rmat, groups):
             assert (g[1], g[2]) == (w[1], w[2]), (q, m)
             if _digest_fixed(q, m):
                 assert a[3] == w[3] and tuple(g[3]) == tuple(w[3]), (q, m)
+    # DISTINCT: the YIELD cells (host rows) are the oracle's under either group count
+    for q in {q for q, _ in items if not _digest_fixed(q, "")}:
+        s = ngql.parse_go(q)
+        ref = o.go(ds.space, s)
+        for gr in (groups, 8):
+            e.set_flag("resv_groups", gr)
+            got = e.go(ds.space, s)
+            assert got.ok and ref.ok
+            assert fixtures.normalize_cells(got.rows) == fixtures.normalize_cells(ref.rows), (q, gr)
 
 
 def test_resv_groups_switch(rmat):
