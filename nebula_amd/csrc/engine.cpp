@@ -355,6 +355,11 @@ struct ngx_ctx {
     hipStream_t splitStreams[4] = {nullptr, nullptr, nullptr, nullptr};
     int32_t pipeFronts = 1;                            // ... of the batch that runs
     hipStream_t finalStream = nullptr;
+    // flag batch_finals 2: consecutive queries' final hops on two final streams (the close after its final
+    // hop on the same stream, no close stream), so one final hop starts while the other drains its tail;
+    // finalCur is the running query's
+    int32_t batchFinals = 1;
+    hipStream_t finalStream2 = nullptr, finalCur = nullptr;
     void* coStack[kMaxLanes] = {nullptr, nullptr, nullptr, nullptr};
     static constexpr size_t kCoStackBytes = size_t(16) << 20;   // + a guard page below each
     void swapLane(Lane& L) {
@@ -1203,11 +1208,13 @@ struct FinalStreamScope {
     FinalStreamScope(ngx_ctx* c_, bool onFinal) : c(c_) {
         if (!c->finalStream) return;
         if (onFinal) {
-            streamAfter(c->finalStream, c->stream, c->pipeEvent(0));
+            hipStream_t fs = c->finalCur ? c->finalCur : c->finalStream;
+            streamAfter(fs, c->stream, c->pipeEvent(0));
             saved = c->stream;
-            c->stream = c->finalStream;
+            c->stream = fs;
         } else {
             streamAfter(c->stream, c->finalStream, c->pipeEvent(1));
+            if (c->finalStream2) streamAfter(c->stream, c->finalStream2, c->pipeEvent(1));
             if (c->closeStream) streamAfter(c->stream, c->closeStream, c->pipeEvent(3));
         }
     }
@@ -1221,6 +1228,7 @@ struct FinalStreamScope {
 // the front stream after every final hop enqueued so far (a batch query's rows read on the front stream)
 void joinFinal(ngx_ctx* c) {
     if (c->finalStream) streamAfter(c->stream, c->finalStream, c->pipeEvent(1));
+    if (c->finalStream2) streamAfter(c->stream, c->finalStream2, c->pipeEvent(1));
     if (c->closeStream) streamAfter(c->stream, c->closeStream, c->pipeEvent(3));
 }
 
@@ -1262,6 +1270,7 @@ uint64_t awaitPub(ngx_ctx* c, const Publish& p, const uint64_t* devCopy, uint64_
     }
     HIP_OK(hipStreamSynchronize(c->stream));
     if (c->finalStream) HIP_OK(hipStreamSynchronize(c->finalStream));   // (a batch's final hop runs there)
+    if (c->finalStream2) HIP_OK(hipStreamSynchronize(c->finalStream2));
     if (c->closeStream) HIP_OK(hipStreamSynchronize(c->closeStream));
     if (take(v)) return v;
     errBits();
@@ -1971,6 +1980,11 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
         return NGX_OK;
     }
     if (n == "batch_event_ring") { c->batchEventRing = value != 0; return NGX_OK; }
+    if (n == "batch_finals") {
+        if (value != 1 && value != 2) return fail(c, NGX_E_BAD_ARGUMENT, "batch_finals: 1 or 2");
+        c->batchFinals = static_cast<int32_t>(value);
+        return NGX_OK;
+    }
     if (n == "batch_release_lanes") { c->batchReleaseLanes = value != 0; return NGX_OK; }
     if (n == "release_lanes") {                       // action: free the parked lanes' buffers now
         if (value) c->releasedBytes += c->releaseParked();
@@ -2019,6 +2033,7 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "trace_go") *value = c->traceGo ? 1 : 0;
     else if (n == "batch_pipeline") *value = c->batchPipeline ? 1 : 0;
     else if (n == "batch_lanes") *value = c->batchLanes;
+    else if (n == "batch_finals") *value = c->batchFinals;
     else if (n == "batch_release_lanes") *value = c->batchReleaseLanes ? 1 : 0;
     else if (n == "released_lane_bytes") *value = static_cast<int64_t>(c->releasedBytes);
     else if (n == "batch_close_stream") *value = c->batchCloseStream ? 1 : 0;
@@ -3119,7 +3134,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     std::vector<int64_t> jitKc;                              // their literal table (FinalArgs::kc/kl)
     std::vector<uint32_t> jitKl;
     c->jitNote.clear();
-    c->jit.releaseRetired(c->stream, c->finalStream);        // modules evicted by earlier queries (either stream)
+    c->jit.releaseRetired(c->stream, c->finalStream, c->finalStream2);        // modules evicted by earlier queries (either stream)
     if (c->jitOn) {
         JitQuery jq = jitHopQuery(sp, hs, progs);
         jq.yColType = gp.colTypes;
@@ -4275,6 +4290,7 @@ int32_t goCall(ngx_ctx* c, const ngx_go_plan* p, ngx_go_result** out) {
     if (rc != NGX_OK) {
         (void)hipStreamSynchronize(c->stream);
         if (c->finalStream) (void)hipStreamSynchronize(c->finalStream);
+        if (c->finalStream2) (void)hipStreamSynchronize(c->finalStream2);
     }
     R->r.code = rc;
     R->r.ncols = static_cast<int32_t>(R->colTypes.size());
@@ -4434,6 +4450,10 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
     // the third stream: a second front stream, or (one front stream) the close stream
     c->pipeFronts = c->batchFronts == 2 ? 2 : 1;
     c->closeStream = c->batchCloseStream ? roles[3] : nullptr;
+    // two final streams: the fourth role stream is the second final stream; each close follows its final
+    // hop on that hop's stream
+    c->finalStream2 = c->batchFinals == 2 ? roles[3] : nullptr;
+    if (c->finalStream2) c->closeStream = nullptr;
     BatchCo co{c, &P, digests != nullptr};
     // query i runs on lane i % lanes with the coroutine stack of that lane; up to lanes - 1 queries wait at
     // their deferral point (holding finals: one)
@@ -4455,6 +4475,7 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
         if (c->ptrace) c->pmark("resume");
         c->useLane(j->idx % lanes);
         c->stream = roles[c->pipeFronts == 2 && (j->idx & 1) ? 2 : 0];   // query i's hops: front i % fronts
+        c->finalCur = (c->finalStream2 && (j->idx & 1)) ? c->finalStream2 : c->finalStream;   // its final hop
         P.cur = j;
         tBatch = &co;
         swapcontext(&P.main, &j->uc);
@@ -4500,6 +4521,8 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
     c->pipe = nullptr;
     tDeferFree = false;
     c->finalStream = nullptr;
+    c->finalStream2 = nullptr;
+    c->finalCur = nullptr;
     c->closeStream = nullptr;
     if (c->ptrace && !c->pmarks.empty()) {
         timespec tm, tb;
@@ -4940,7 +4963,7 @@ int32_t runGetNeighbors(ngx_ctx* c, Space& sp, const ngx_gn_request& q, GnResult
             jitSlotConsts(jq, kc, kl);
             for (size_t k = 0; k < kc.size(); k++) { a.kc[k] = kc[k]; a.kl[k] = kl[k]; }
             std::string jerr;
-            c->jit.releaseRetired(c->stream, c->finalStream);
+            c->jit.releaseRetired(c->stream, c->finalStream, c->finalStream2);
             jk = c->jit.get(jitShapeKey(sp, jq), [&] { return jitSource(sp, jq); }, jerr);
         }
         if (jk) {

@@ -75,7 +75,7 @@ public:
     std::shared_ptr<const JitKernels> get(const std::string& shape, const std::function<std::string()>& source,
                                           std::string& err);
     // unload the modules evicted since the last call (synchronises `s` first when there are any)
-    void releaseRetired(hipStream_t s, hipStream_t s2 = nullptr);   // s2: a second stream that may run them
+    void releaseRetired(hipStream_t s, hipStream_t s2 = nullptr, hipStream_t s3 = nullptr);   // s2, s3: other streams that may run them
     // block until every queued compile has finished (tests, warm-up)
     void drain();
     uint64_t compiled = 0, hits = 0, failed = 0, evicted = 0;

@@ -290,3 +290,36 @@ def test_batch_bad_plan_reports_every_query():
         arr = (ctypes.c_void_p * 2)(None, None)
         rc = e.L.ngx_go_batch(e.h, ctypes.cast(arr, ctypes.c_void_p), 2, codes, None, None, None)
         assert rc != 0 and list(codes) == [rc, rc]
+
+
+@pytest.mark.parametrize("lanes,fronts", [(3, 2), (4, 2), (3, 1)])
+def test_batch_two_final_streams(rmat, lanes, fronts):
+    """Flag batch_finals 2: consecutive queries' final hops on two final streams (each close after its own
+    final hop on that stream), so two final hops of different lanes may run at once: every query's code,
+    rows, scanned edges and digest are what it has alone."""
+    ds, o, e = rmat
+    rng = random.Random(191 + lanes)
+    qs = _queries(ds)
+    items = [(q, rng.choice(["lean", "compact", "device", "host"])) for q in qs]
+    items = [(q, "lean") for q in qs[:8]] + items + [(q, "compact") for q in qs[-8:]]
+    preps = [_prepare(e, ds, q, m) for q, m in items]
+    want = [_alone(e, ds, p) for p in preps]
+    e.set_flag("batch_finals", 2)
+    e.set_flag("batch_lanes", lanes)
+    e.set_flag("batch_fronts", fronts)
+    try:
+        before = e.get_flag("batch_overlaps")
+        got = e.go_batch(preps, digests=True)
+        overlaps = e.get_flag("batch_overlaps") - before
+        plain = e.go_batch(preps[:12])
+    finally:
+        e.set_flag("batch_finals", 1)
+        e.set_flag("batch_lanes", 3)
+        e.set_flag("batch_fronts", 2)
+    for (q, m), w, g in list(zip(items, want, got)) + list(zip(items[:12], want[:12], plain)):
+        assert g[0] == w[0], (q, m, g, w)
+        if g[0] == 0:
+            assert (g[1], g[2]) == (w[1], w[2]), (q, m)
+            if len(g) > 3 and "DISTINCT" not in q:
+                assert tuple(g[3]) == tuple(w[3]), (q, m)
+    assert overlaps >= 10

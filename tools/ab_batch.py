@@ -1,0 +1,92 @@
+"""In-process A/B of engine flags on bench.py's timed loop (C2 graph loaded once, through ngx_load_csr).
+
+bench.py pays ~50 s of KV load + commit per run, and two runs on the same box differ by a few percent;
+this tool builds the C2 shard once and times bench.py's exact timed step — `go_batch` over the same 20
+prepared plans (seeds rmat_seeds(22, 1000, 16, 42, 42 + i)), after a 5-plan warmup batch — alternately
+per variant, R rounds, and prints the median and spread of ms per step for each variant.
+
+Usage (GPU box): python tools/ab_batch.py [--rounds 8] [--steps 20] VARIANT ...
+  VARIANT = "base" or comma-separated NAME=VALUE engine flags, e.g. "batch_finals=2,batch_lanes=4"
+"""
+import argparse
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+QUERY = "GO 3 STEPS FROM {S} OVER e WHERE e.p0 < 50 YIELD e._dst, e._rank, e.p0, e.p1"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("variants", nargs="+")
+    ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--scale", type=int, default=22)
+    ap.add_argument("--threads", type=int, default=16)
+    args = ap.parse_args()
+    import torch
+    from nebula_amd import datagen, engine, ngql
+    torch.cuda.set_device(0)
+    t0 = time.time()
+    c = datagen.rmat_csr(args.scale, 16, 42, 100, with_in=True, threads=args.threads)
+    eng = engine.Engine(0)
+    eng.add_space(datagen.RMAT_SPACE, 100)
+    for is_edge, sid, name, fields in datagen.rmat_schemas():
+        eng.add_schema(datagen.RMAT_SPACE, is_edge, sid, name, fields)
+    eng.load_csr(datagen.RMAT_SPACE, c.vpart, c.vid, c.slots)
+    eng.commit(datagen.RMAT_SPACE)
+    c.free()
+    print(f"[ab] C2 shard loaded in {time.time() - t0:.1f}s", flush=True)
+
+    def plan(i):
+        seeds = datagen.rmat_seeds(args.scale, 1000, 16, 42, 42 + i, threads=args.threads)
+        s = ngql.parse_go(QUERY.replace("{S}", ", ".join(str(int(v)) for v in seeds)))
+        return eng.prepare_go(datagen.RMAT_SPACE, s, on_device=True, yield_only=True, compact=True)
+
+    preps = [plan(i) for i in range(args.warmup + args.steps)]
+    warm, timed = preps[:args.warmup], preps[args.warmup:]
+    edges = None
+    parsed = []
+    for v in args.variants:
+        flags = []
+        if v != "base":
+            for kv in v.split(","):
+                n, _, val = kv.partition("=")
+                flags.append((n, int(val)))
+        parsed.append((v, flags))
+    defaults = {n: eng.get_flag(n) for _, fl in parsed for n, _ in fl}
+    res = {v: [] for v, _ in parsed}
+    for r in range(args.rounds):
+        for v, flags in (parsed if r % 2 == 0 else parsed[::-1]):
+            for n, val in flags:
+                eng.set_flag(n, val)
+            for code, _, _ in eng.go_batch(warm):
+                assert code == 0
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            out = eng.go_batch(timed)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t
+            assert all(o[0] == 0 for o in out), out
+            e = sum(o[2] for o in out)
+            assert edges is None or e == edges
+            edges = e
+            res[v].append(dt * 1e3 / args.steps)
+            for n, _ in flags:
+                eng.set_flag(n, defaults[n])
+        print(f"[ab] round {r}: " + "  ".join(f"{v} {res[v][-1]:.4f}" for v, _ in parsed), flush=True)
+    for v, _ in parsed:
+        x = res[v]
+        med = statistics.median(x)
+        print(f"[ab] {v:40s} median {med:.4f} ms/step  min {min(x):.4f}  max {max(x):.4f}  "
+              f"TEPS {edges / args.steps / (med * 1e-3):.4g}", flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
