@@ -322,7 +322,7 @@ struct ngx_ctx {
     int activeLane = 0;
     // lanes of a pipelined batch (flag "batch_lanes", 2 .. kMaxLanes): up to lanes - 1 queries wait at their
     // deferral point while the next one runs its hops
-    int32_t batchLanes = 3;
+    int32_t batchLanes = 4;                            // r06, two final streams: 4 lanes 0.299 vs 3 lanes 0.303 ms per step
     // ngx_go_batch's streams (GoPipe, created with the context at world 1): the queries' hops on the front
     // stream, the last final hop of each overlapped query on the final stream; finalStream is set while a
     // pipelined batch runs. The coroutine stacks of the batch's queries (one per lane).
@@ -358,7 +358,13 @@ struct ngx_ctx {
     // flag batch_finals 2: consecutive queries' final hops on two final streams (the close after its final
     // hop on the same stream, no close stream), so one final hop starts while the other drains its tail;
     // finalCur is the running query's
-    int32_t batchFinals = 1;
+    int32_t batchFinals = 2;
+    // per lane: the event after its last overlapped final hop's close. The lane's next final hop waits for it:
+    // that close still moves the earlier query's rows inside the lane's result arrays and reads its block
+    // table after the earlier query has read its row count (published by the close's first workgroup), and
+    // with two final streams nothing else orders the two (r06: a C2 batch at 4 groups failed on it)
+    hipEvent_t laneCloseEv[kMaxLanes] = {nullptr, nullptr, nullptr, nullptr};
+    bool laneClosePending[kMaxLanes] = {false, false, false, false};                           // C2: 0.302 vs 0.309 ms per step (tools/ab_batch.py, 10 rounds)
     hipStream_t finalStream2 = nullptr, finalCur = nullptr;
     void* coStack[kMaxLanes] = {nullptr, nullptr, nullptr, nullptr};
     static constexpr size_t kCoStackBytes = size_t(16) << 20;   // + a guard page below each
@@ -444,6 +450,7 @@ struct ngx_ctx {
         hostStage.release();
         for (auto e : eventPool) (void)hipEventDestroy(e);
         for (auto e : pipeEv) if (e) (void)hipEventDestroy(e);
+        for (auto e : laneCloseEv) if (e) (void)hipEventDestroy(e);
         for (auto e : pipeRing) if (e) (void)hipEventDestroy(e);
         for (auto st : pipeStreams) if (st) (void)hipStreamDestroy(st);
         for (auto st : splitStreams) if (st) (void)hipStreamDestroy(st);
@@ -1210,6 +1217,7 @@ struct FinalStreamScope {
         if (onFinal) {
             hipStream_t fs = c->finalCur ? c->finalCur : c->finalStream;
             streamAfter(fs, c->stream, c->pipeEvent(0));
+            if (c->laneClosePending[c->activeLane]) HIP_OK(hipStreamWaitEvent(fs, c->laneCloseEv[c->activeLane], 0));
             saved = c->stream;
             c->stream = fs;
         } else {
@@ -3432,6 +3440,12 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                     c->timed("final_close", 0, [&] {
                         if (launchFinalClose(a, c->stream)) throw Error{NGX_E_DEVICE, "final close"};
                     });
+                    if (deferrable) {                          // the lane's next final hop waits for this close
+                        hipEvent_t& ev = c->laneCloseEv[c->activeLane];
+                        if (!ev) HIP_OK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+                        HIP_OK(hipEventRecord(ev, c->stream));
+                        c->laneClosePending[c->activeLane] = true;
+                    }
                 } catch (...) {
                     c->stream = fs;
                     throw;

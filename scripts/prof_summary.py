@@ -22,9 +22,14 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def short(name):
-    n = name.split("(")[0]
-    return n.replace("void ", "").strip()
+def short(name, kid=None):
+    n = name.split("(")[0].replace("void ", "").strip()
+    # generated kernels share one name across query shapes (each its own module): keep the modules apart
+    # (r05's traffic averaged the timed step's module with the host-delivery step's 8-byte one: 1.31x
+    # "write amplification" that no timed launch had)
+    if kid is not None and n.startswith("ngx_jit_"):
+        n += f"#{kid}"
+    return n
 
 
 def main():
@@ -41,14 +46,14 @@ def main():
     shutil.copy(stats, os.path.join(dst, f"{args.tag}_kernel_stats.csv"))
     trace = collections.defaultdict(list)
     for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))):
-        trace[short(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        trace[short(r["Kernel_Name"], r.get("Kernel_Id"))].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     pmc = {}
     for kind in ("fetch", "write"):
         d = collections.defaultdict(list)
         f = os.path.join(src, kind, "run_counter_collection.csv")
         if os.path.exists(f):
             for r in csv.DictReader(open(f)):
-                d[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+                d[short(r["Kernel_Name"], r.get("Kernel_Id"))].append(float(r["Counter_Value"]))
         pmc[kind] = d
     rows = []
     for k, durs in sorted(trace.items(), key=lambda kv: -sum(kv[1])):
@@ -81,7 +86,7 @@ def main():
     if args.dominant:
         dom = [r for r in rows if args.dominant in r["kernel"]]
         if dom:
-            d = dom[0]
+            d = max(dom, key=lambda r: (r["launches"], r["total_ms"]))     # the timed step's module
             traffic["kernel_class"] = args.kernel_class
             # the result layout the profiled bench ran with (bench.py uses the bytes only for the same one)
             traffic["compact"] = bool(bench and ((bench.get("roofline") or {}).get("stored_width") or {}).get("compact_results"))
@@ -96,7 +101,7 @@ def main():
     if os.path.exists(sqf):
         acc = collections.defaultdict(lambda: collections.defaultdict(list))
         for r in csv.DictReader(open(sqf)):
-            acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            acc[short(r["Kernel_Name"], r.get("Kernel_Id"))][r["Counter_Name"]].append(float(r["Counter_Value"]))
         sq = {}
         for k, d in acc.items():
             per = {c: sum(v) / len(v) for c, v in d.items()}

@@ -166,20 +166,22 @@ def test_batch_lanes(rmat, lanes, close_stream, fronts):
     items = [(q, "lean") for q in qs[:8]] + items + [(q, "compact") for q in qs[-8:]]
     preps = [_prepare(e, ds, q, m) for q, m in items]
     want = [_alone(e, ds, p) for p in preps]
-    assert e.get_flag("batch_lanes") == 3 and e.get_flag("batch_close_stream") == 1
+    assert e.get_flag("batch_lanes") == 4 and e.get_flag("batch_close_stream") == 1
     assert e.get_flag("batch_fronts") == 2
     e.set_flag("batch_lanes", lanes)
     e.set_flag("batch_close_stream", close_stream)
     e.set_flag("batch_fronts", fronts)
+    e.set_flag("batch_finals", 1)                   # one final stream: the close stream is used when asked
     try:
         before = e.get_flag("batch_overlaps")
         got = e.go_batch(preps, digests=True)
         overlaps = e.get_flag("batch_overlaps") - before
         plain = e.go_batch(preps[:12])                  # no digests: nothing read back between the queries
     finally:
-        e.set_flag("batch_lanes", 3)
+        e.set_flag("batch_lanes", 4)
         e.set_flag("batch_close_stream", 1)
         e.set_flag("batch_fronts", 2)
+        e.set_flag("batch_finals", 2)
     for (q, m), w, g in list(zip(items, want, got)) + list(zip(items[:12], want[:12], plain)):
         assert g[0] == w[0], (q, m, g, w)
         if g[0] == 0:
@@ -294,7 +296,7 @@ def test_batch_bad_plan_reports_every_query():
 
 @pytest.mark.parametrize("lanes,fronts", [(3, 2), (4, 2), (3, 1)])
 def test_batch_two_final_streams(rmat, lanes, fronts):
-    """Flag batch_finals 2: consecutive queries' final hops on two final streams (each close after its own
+    """Flag batch_finals 2 (the default): consecutive queries' final hops on two final streams (each close after its own
     final hop on that stream), so two final hops of different lanes may run at once: every query's code,
     rows, scanned edges and digest are what it has alone."""
     ds, o, e = rmat
@@ -313,8 +315,8 @@ def test_batch_two_final_streams(rmat, lanes, fronts):
         overlaps = e.get_flag("batch_overlaps") - before
         plain = e.go_batch(preps[:12])
     finally:
-        e.set_flag("batch_finals", 1)
-        e.set_flag("batch_lanes", 3)
+        e.set_flag("batch_finals", 2)
+        e.set_flag("batch_lanes", 4)
         e.set_flag("batch_fronts", 2)
     for (q, m), w, g in list(zip(items, want, got)) + list(zip(items[:12], want[:12], plain)):
         assert g[0] == w[0], (q, m, g, w)

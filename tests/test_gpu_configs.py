@@ -135,8 +135,8 @@ def test_c2_bench_step_vs_oracle(c2):
 def test_c2_bench_batch_pinned(c2):
     """The timed path itself at C2 (What's weak #2): bench.py's own timed plans — its
     sentence(i) seeds (rmat_seeds(..., 42, 42 + i)), 20 of them, compact YIELD-only device results — run
-    through ngx_go_batch (three lanes, two front streams, the close stream, deferred frees, per-lane rows)
-    with digests. Three small queries go first, so lanes 1 and 2 hold small scratch and grow in the middle
+    through ngx_go_batch (four lanes, two front streams, two final streams, deferred frees, per-lane rows)
+    with digests. Four small queries go first, so lanes 1 to 3 hold small scratch and grow in the middle
     of the batch when their first C2 query arrives. Every query's code, rows, edges and row digest equal
     the same plan through ngx_go; plan 0's rows, fetched, equal the oracle's (sorted 128-bit row digests)
     and their row digest is the batch's."""
@@ -145,28 +145,42 @@ def test_c2_bench_batch_pinned(c2):
     sents = [ngql.parse_go(q.replace("{S}", _seed_list(datagen.rmat_seeds(22, 1000, 16, 42, 42 + i, threads=16))))
              for i in range(20)]
     small = [ngql.parse_go(q.replace("{S}", _seed_list(datagen.rmat_seeds(22, 3, 16, 42, 900 + i, threads=16))))
-             for i in range(3)]
+             for i in range(4)]
     preps = [e.prepare_go(ds.space, s, on_device=True, compact=True, yield_only=True) for s in small + sents]
-    e.set_flag("release_lanes", 1)                  # lanes 1, 2 start empty: they grow inside the batch
-    assert e.get_flag("batch_lanes") == 3
+    e.set_flag("release_lanes", 1)                  # lanes 1 to 3 start empty: they grow inside the batch
+    assert e.get_flag("batch_lanes") == 4
     before = e.get_flag("batch_overlaps")
     got = e.go_batch(preps, digests=True)
     assert e.get_flag("batch_overlaps") - before >= len(preps) - 2
+    # the same batch with 4 reservation groups (64 K-row blocks filling up faster per group, more closes in
+    # flight per lane) and with one final stream: r06 found a lane's next final hop racing the lane's last
+    # close on two final streams (C2, 4 groups)
+    e.set_flag("resv_groups", 4)
+    try:
+        got4 = e.go_batch(preps, digests=True)
+    finally:
+        e.set_flag("resv_groups", 8)
+    e.set_flag("batch_finals", 1)
+    try:
+        got1 = e.go_batch(preps, digests=True)
+    finally:
+        e.set_flag("batch_finals", 2)
     for i, p in enumerate(preps):
         alone = e.go(ds.space, p, rows=False, device_digest=True)
         assert alone.ok
-        code, nrows, edges, dig = got[i]
-        assert code == 0 and (nrows, edges) == (alone.nrows, sum(alone.hop_edges)), i
-        assert tuple(dig) == tuple(alone.device_digest), i
+        for g in (got, got4, got1):
+            code, nrows, edges, dig = g[i]
+            assert code == 0 and (nrows, edges) == (alone.nrows, sum(alone.hop_edges)), i
+            assert tuple(dig) == tuple(alone.device_digest), i
     # plan 0 against the oracle: its fetched rows' 128-bit digests, and the batch digest of those rows
     ref = o.go(ds.space, sents[0], digest=True)
-    assert ref.ok and ref.nrows == got[3][1] and sum(ref.hop_scanned) == got[3][2]
+    assert ref.ok and ref.nrows == got[4][1] and sum(ref.hop_scanned) == got[4][2]
     r = e.go(ds.space, sents[0], on_device=True, fetch=True, compact=True, yield_only=True)
     assert r.ok
     cols = [np.ascontiguousarray(x) for x, _, _ in r.dev_cols]
     digests = oracle.digest_columns(r.col_types, r.nrows, [c.ctypes.data for c in cols], [None] * 4, [None] * 4)
     assert np.array_equal(digests, ref.digests)
-    assert oracle.row_digest([np.zeros(r.nrows, np.int64)] + cols) == tuple(got[3][3])
+    assert oracle.row_digest([np.zeros(r.nrows, np.int64)] + cols) == tuple(got[4][3])
     del cols, r, digests
 
 

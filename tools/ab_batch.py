@@ -6,7 +6,11 @@ prepared plans (seeds rmat_seeds(22, 1000, 16, 42, 42 + i)), after a 5-plan warm
 per variant, R rounds, and prints the median and spread of ms per step for each variant.
 
 Usage (GPU box): python tools/ab_batch.py [--rounds 8] [--steps 20] VARIANT ...
-  VARIANT = "base" or comma-separated NAME=VALUE engine flags, e.g. "batch_finals=2,batch_lanes=4"
+  VARIANT = "base" or comma-separated NAME=VALUE engine flags, e.g. "batch_finals=2,batch_lanes=4";
+  "env:NAME=VALUE" items set an environment variable for the variant (e.g. env:NGX_JIT_WAVES=8, read when
+  a generated kernel is compiled)
+With --final, each round also runs the 20 plans one at a time with HIP-event profiling and reports the
+final hop's average launch time per variant.
 """
 import argparse
 import os
@@ -28,6 +32,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--scale", type=int, default=22)
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--final", action="store_true")
     args = ap.parse_args()
     import torch
     from nebula_amd import datagen, engine, ngql
@@ -53,16 +58,23 @@ def main():
     edges = None
     parsed = []
     for v in args.variants:
-        flags = []
+        flags, envs = [], []
         if v != "base":
             for kv in v.split(","):
                 n, _, val = kv.partition("=")
-                flags.append((n, int(val)))
-        parsed.append((v, flags))
-    defaults = {n: eng.get_flag(n) for _, fl in parsed for n, _ in fl}
+                if n.startswith("env:"):
+                    envs.append((n[4:], val))
+                else:
+                    flags.append((n, int(val)))
+        parsed.append((v, (flags, envs)))
+    defaults = {n: eng.get_flag(n) for _, (fl, _) in parsed for n, _ in fl}
     res = {v: [] for v, _ in parsed}
+    fin = {v: [] for v, _ in parsed}
     for r in range(args.rounds):
-        for v, flags in (parsed if r % 2 == 0 else parsed[::-1]):
+        for v, (flags, envs) in (parsed if r % 2 == 0 else parsed[::-1]):
+            saved = {n: os.environ.get(n) for n, _ in envs}
+            for n, val in envs:
+                os.environ[n] = val
             for n, val in flags:
                 eng.set_flag(n, val)
             for code, _, _ in eng.go_batch(warm):
@@ -77,14 +89,29 @@ def main():
             assert edges is None or e == edges
             edges = e
             res[v].append(dt * 1e3 / args.steps)
+            if args.final:
+                eng.set_profiling(True)
+                s0 = eng.kernel_stats().get("final", (0, 0.0, 0))
+                for p in timed:
+                    assert eng.go(datagen.RMAT_SPACE, p, rows=False).ok
+                s1 = eng.kernel_stats().get("final", (0, 0.0, 0))
+                eng.set_profiling(False)
+                if s1[0] > s0[0]:
+                    fin[v].append((s1[1] - s0[1]) * 1e3 / (s1[0] - s0[0]))
             for n, _ in flags:
                 eng.set_flag(n, defaults[n])
+            for n, old in saved.items():
+                if old is None:
+                    os.environ.pop(n, None)
+                else:
+                    os.environ[n] = old
         print(f"[ab] round {r}: " + "  ".join(f"{v} {res[v][-1]:.4f}" for v, _ in parsed), flush=True)
     for v, _ in parsed:
         x = res[v]
         med = statistics.median(x)
+        fx = f"  final {statistics.median(fin[v]):.1f} us" if fin[v] else ""
         print(f"[ab] {v:40s} median {med:.4f} ms/step  min {min(x):.4f}  max {max(x):.4f}  "
-              f"TEPS {edges / args.steps / (med * 1e-3):.4g}", flush=True)
+              f"TEPS {edges / args.steps / (med * 1e-3):.4g}{fx}", flush=True)
     eng.close()
 
 
