@@ -1017,6 +1017,7 @@ struct VmEv {
     static constexpr bool kEflags = true, kTtl = true; // per-edge flags / TTL read when the slot has them
     static constexpr int kEtype = 0;                  // edge type read per slot
     static constexpr int kRowMask = 7;                // row arrays: written where FinalArgs::o* is set
+    static constexpr bool kNeedRow = true;            // programs may read the src row ($^ props, e._src)
     static constexpr bool kNtStore = false;
     static constexpr int kOutSrcW = 0, kOutDstW = 0, kOutRankW = 0;   // row array widths from FinalArgs
     static __device__ __forceinline__ void YV(const FinalArgs&, const EdgeCtx&, Val*) {}

@@ -46,7 +46,9 @@ def main():
     eng.load_csr(datagen.RMAT_SPACE, c.vpart, c.vid, c.slots)
     eng.commit(datagen.RMAT_SPACE)
     c.free()
-    print(f"[ab] C2 shard loaded in {time.time() - t0:.1f}s", flush=True)
+    info = eng.info(datagen.RMAT_SPACE)
+    print(f"[ab] C2 shard loaded in {time.time() - t0:.1f}s: {info.vertices} vertices, {info.edges} edges, "
+          f"{info.device_bytes / 2**30:.3f} GiB in HBM", flush=True)
 
     def plan(i):
         seeds = datagen.rmat_seeds(args.scale, 1000, 16, 42, 42 + i, threads=args.threads)
