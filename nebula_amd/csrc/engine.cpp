@@ -1565,7 +1565,7 @@ int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return NGX_E_DEVICE;
     if (hipSetDevice(c->device) != hipSuccess) return NGX_E_DEVICE;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return NGX_E_DEVICE;
-    if (c->world == 1) {                              // ngx_go_batch's pipeline (without them: one at a time)
+    {                                                 // ngx_go_batch's pipeline (without them: one at a time)
         // the hops (latency-bound) at the higher priority, the final hops (bandwidth-bound) at the lower:
         // 0.365 / 0.371 vs 0.374 / 0.412 ms per C2 step with both at the default, same box (r05)
         int prLo = 0, prHi = 0;
@@ -3313,8 +3313,10 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         a.mask = mask;
         if (isRecord && E) {
             // ngx_go_batch: this query's last final hop may overlap the next query (goDeferPoint): not with a
-            // device read-back left (multi-root walks), string arenas, profiling or host traces, nor at world > 1
-            const bool deferrable = c->pipe && isFinal && c->pinDev && !dyn && !rw && c->world == 1 && nStrOut == 0 &&
+            // device read-back left (multi-root walks), string arenas, profiling or host traces. World > 1 too
+            // (r06): the final hop is the shard's own work, no collective follows it; the next query's hops and
+            // collectives run on the one front stream beside it
+            const bool deferrable = c->pipe && isFinal && c->pinDev && !dyn && !rw && nStrOut == 0 &&
                                     !c->prof && !c->htrace && !c->traceGo && pipelinable(p);
             if (c->pipe) goPreFinalPoint(c);
             FinalStreamScope fss(c, deferrable);
@@ -4413,7 +4415,7 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
         if (digests) for (int k = 0; k < 3; k++) digests[3 * static_cast<size_t>(j.idx) + k] = j.digest[k];
         if (j.rc != NGX_OK && first == NGX_OK) first = j.rc;
     };
-    const bool pipe = c->batchPipeline && n > 1 && c->world == 1 && !c->prof && !c->htrace && !c->traceGo &&
+    const bool pipe = c->batchPipeline && n > 1 && !c->prof && !c->htrace && !c->traceGo &&
                       c->pipeStreams[0] && c->pipeStreams[1] && c->pipeStreams[2] && c->pipeStreams[3] && c->pipeEv[0] && c->pipeEv[1] &&
                       c->pipeEv[2] && c->pipeEv[3] && c->pipeEv[4] && coStacks(c);
     if (!pipe) {
@@ -4462,7 +4464,9 @@ extern "C" int32_t ngx_go_batch(ngx_ctx* c, const ngx_go_plan* const* plans, int
     c->stream = roles[0];
     c->finalStream = roles[1];
     // the third stream: a second front stream, or (one front stream) the close stream
-    c->pipeFronts = c->batchFronts == 2 ? 2 : 1;
+    // world > 1: one front stream, so every query's collectives and the kernels around them (exchange
+    // buffers, host collectives, the RCCL watchdog's stream query) stay in one order on every rank
+    c->pipeFronts = c->batchFronts == 2 && c->world == 1 ? 2 : 1;
     c->closeStream = c->batchCloseStream ? roles[3] : nullptr;
     // two final streams: the fourth role stream is the second final stream; each close follows its final
     // hop on that hop's stream

@@ -117,6 +117,27 @@ def main():
                                          col_types=next((p[2] for p in parts if p[3]), parts[0][2]))
 
     for i, q in enumerate(queries):
+        if q.get("batch"):
+            # ngx_go_batch over prepared device-resident plans (compact YIELD columns): each plan alone
+            # (ngx_go + device digest) and then all of them pipelined, on every shard
+            e.set_flag("pull_factor", q.get("pull_factor", default_pf))
+            e.set_flag("xchg_lists", q.get("xchg_lists", -1))
+            preps = [e.prepare_go(datagen.RMAT_SPACE, ngql.parse_go(t), on_device=True, compact=True, yield_only=True)
+                     for t in q["batch"]]
+            alone = []
+            for p in preps:
+                r = e.go(datagen.RMAT_SPACE, p, rows=False, device_digest=True)
+                alone.append([r.code, r.nrows, int(sum(r.hop_edges)) if r.ok else 0,
+                              list(r.device_digest) if r.ok else [0, 0, 0]])
+            ov = e.get_flag("batch_overlaps")
+            t0 = time.time()
+            got = e.go_batch(preps, digests=True)
+            print(f"[rank {rank}] batch {i}: {len(preps)} plans in {(time.time() - t0) * 1e3:.0f} ms",
+                  file=sys.stderr, flush=True)
+            np.save(f"{out}.{i}.npy", np.zeros((0, 2), np.uint64))
+            res.append({"batch": True, "alone": alone, "got": [[g[0], g[1], g[2], list(g[3])] for g in got],
+                        "overlaps": e.get_flag("batch_overlaps") - ov})
+            continue
         if q.get("pipe"):
             walks = e.get_flag("pipe_walks")
             t0 = time.time()

@@ -227,6 +227,61 @@ def test_multishard_go_matches_oracle(tmp_path, world, scale):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 3])
+def test_multishard_batch_pipeline(tmp_path, world):
+    """ngx_go_batch at world > 1 (What's missing #1): consecutive device-resident plans overlap
+    on every shard — a query's final hop runs on a final stream while the next query's hops and frontier
+    exchanges run on the front stream — and every plan's code, rows, scanned edges and row digest on every
+    shard equal that plan alone; the shards' digests merged (sum, xor, count) equal the oracle's rows."""
+    from nebula_amd import datagen, ngql
+    from oracle import oracle
+    from tests import fixtures
+
+    scale = 11
+    ds = fixtures.RmatDataset(scale, with_in=True, with_tag=True)
+    o = oracle.Oracle()
+    o.set_flags(threads=8)
+    ds.load_oracle(o)
+    texts = []
+    shapes = ["GO 3 STEPS FROM {S} OVER e WHERE e.p0 < 50 YIELD e._dst, e._rank, e.p0, e.p1",
+              "GO 2 STEPS FROM {S} OVER e REVERSELY YIELD e._dst, e.p1",
+              "GO 1 TO 3 STEPS FROM {S} OVER e WHERE e.p0 % 7 == 3 YIELD e._dst, e.p0",
+              "GO 2 STEPS FROM {S} OVER e WHERE e.p1 % (e.p0 - e.p0) > 1 YIELD e._dst",     # fails everywhere
+              "GO 3 STEPS FROM {S} OVER e BIDIRECT WHERE e.p0 > 90 YIELD e._dst, e.p0"]
+    for k in range(12):
+        seeds = datagen.sample_vids(900 + k, 1 << scale, (30, 1, 200)[k % 3])
+        texts.append(shapes[k % len(shapes)].replace("{S}", ", ".join(str(int(v)) for v in seeds)))
+    queries = [{"batch": texts}, {"batch": texts, "pull_factor": 0, "xchg_lists": 1}]
+    shards, _ = _run_shards(tmp_path, world, scale, queries, timeout=400)
+    for qi in range(len(queries)):
+        for r, s in enumerate(shards):
+            b = s[qi]
+            assert b["overlaps"] > 0, (r, b["overlaps"])
+            for j, (a, g) in enumerate(zip(b["alone"], b["got"])):
+                assert g[0] == a[0], (r, j, g, a)
+                if a[0] == 0:
+                    assert g[1:] == a[1:], (r, j, texts[j])
+        for j, t in enumerate(texts):
+            s = ngql.parse_go(t)
+            ref = o.go(ds.space, s)
+            codes = [sh[qi]["got"][j][0] for sh in shards]
+            # a graphd-side error fails the query wherever a shard evaluates a failing row (graphd fails the
+            # merged query on any shard's error)
+            assert (ref.ok and all(c == 0 for c in codes)) or (not ref.ok and any(c != 0 for c in codes)), (t, codes)
+            if not ref.ok:
+                continue
+            cols = [np.array([int(r[c][1]) for r in ref.rows], dtype=np.int64) for c in range(len(s.yields))]
+            want = oracle.row_digest([np.zeros(len(ref.rows), np.int64)] + cols)
+            sm, x, n = 0, 0, 0
+            for sh in shards:
+                d = sh[qi]["got"][j][3]
+                sm, x, n = (sm + d[0]) % (1 << 64), x ^ d[1], n + d[2]
+            assert (sm, x, n) == tuple(want), t
+            assert sum(sh[qi]["got"][j][2] for sh in shards) == sum(ref.hop_scanned), t
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
 def test_multishard_pull_decision_is_collective(tmp_path):
     """World 2 where the shards disagree about pulling: rank 0 cannot (pull_factor 0), rank 1 would
     pull every hop (pull_factor 1). Every shard still enters each intermediate hop's pull all-gather
