@@ -145,6 +145,30 @@ struct Timer {
     hipEvent_t a = nullptr, b = nullptr;
 };
 
+// the $$ owner fetch of one lane (fetchDstProps): request lists, exchange blocks, the global row ->
+// fetched-row map, and per record hop of the running query the fetched tag tables (device) with the host
+// copy of their string bytes (result cells read strings back through it)
+struct DstLane {
+    DBuf req, counts, recv, blobS, blobR, rows, map;
+    uint64_t mapRows = 0;
+    std::vector<DBuf> data;                             // per record hop: present / values / strings
+    std::vector<std::string> hostStr;                   // per record hop: its string bytes (host copy)
+    std::vector<const char*> devStr;                    // ... and where they live on the device
+    uint64_t bytes() const {
+        uint64_t b = req.cap + counts.cap + recv.cap + blobS.cap + blobR.cap + rows.cap + map.cap;
+        for (const DBuf& d : data) b += d.cap;
+        return b;
+    }
+    void release() {
+        for (DBuf* b : {&req, &counts, &recv, &blobS, &blobR, &rows, &map}) b->release();
+        for (DBuf& d : data) d.release();
+        data.clear();
+        hostStr.clear();
+        devStr.clear();
+        mapRows = 0;
+    }
+};
+
 // ROCTX range on the host timeline of rocprofv3 (--marker-trace): a query, each hop, each kernel class
 // launch (the reference's FLAGS_trace_go step log, GoExecutor.cpp:559-569). Without a
 // tool attached a push / pop is a check of a registration flag.
@@ -189,6 +213,7 @@ struct ngx_ctx {
     const uint64_t* resvRows = nullptr;                 // this query's last GO final launch's row count (device word)
     uint64_t strArenaMax = uint64_t(8) << 30;           // bytes of one record hop's result string arena (flag str_arena_max)
     bool resvClosePending = false;                      // counters handed out, their k_final_close not enqueued
+    DstLane dst;                                        // the $$ owner fetch's buffers (per lane)
     DBuf oFlags, rowCols, rowLen, rowOff, rowBytes;     // GetNeighbors response rows (encode_rows)
     DBuf dkTable, dkKeep, dkPre, dSrc, dDst, dRank, dType;   // YIELD DISTINCT (table, marks, compacted rows)
     std::vector<DBuf> strArena;                         // result string arenas, one per record hop (FinalArgs::strOut)
@@ -318,6 +343,7 @@ struct ngx_ctx {
         uint64_t resvTabWords = 0;
         uint32_t resvLastG = 0, resvLastStride = 0, resvParity = 0;
         bool resvClosePending = false;
+        DstLane dst;
     } parked[kMaxLanes];
     int activeLane = 0;
     // lanes of a pipelined batch (flag "batch_lanes", 2 .. kMaxLanes): up to lanes - 1 queries wait at their
@@ -381,7 +407,7 @@ struct ngx_ctx {
         NGX_LANE_SWAP(oSrc) NGX_LANE_SWAP(oDst) NGX_LANE_SWAP(oRank) NGX_LANE_SWAP(oType) NGX_LANE_SWAP(oColDesc)
         NGX_LANE_SWAP(resvTab) NGX_LANE_SWAP(resvCtl) NGX_LANE_SWAP(oCols) NGX_LANE_SWAP(oColView)
         NGX_LANE_SWAP(resvTabWords) NGX_LANE_SWAP(resvLastG) NGX_LANE_SWAP(resvLastStride) NGX_LANE_SWAP(resvParity)
-        NGX_LANE_SWAP(resvClosePending)
+        NGX_LANE_SWAP(resvClosePending) NGX_LANE_SWAP(dst)
 #undef NGX_LANE_SWAP
     }
     void initLanes() {
@@ -402,6 +428,7 @@ struct ngx_ctx {
         for (auto& cb : oCols) { cb.x.release(); cb.len.release(); cb.t.release(); }
         inStage.release();
         seedStage.release();
+        dst.release();
     }
     // the parked lanes' scratch and result rows freed (flag batch_release_lanes, or release_lanes = 1 once):
     // a pipelined batch leaves lanes 1 .. kMaxLanes - 1 holding buffers as large as lane 0's. Called with no
@@ -418,6 +445,7 @@ struct ngx_ctx {
                             &oType, &oColDesc, &resvTab, &resvCtl})
                 freed += b->cap;
             for (auto& cb : oCols) freed += cb.x.cap + cb.len.cap + cb.t.cap;
+            freed += dst.bytes();
             releaseLane();
             oCols.clear();
             oColView.clear();
@@ -437,6 +465,12 @@ struct ngx_ctx {
     }
     uint64_t releasedBytes = 0;
     bool batchReleaseLanes = false;
+    // $$ props at world > 1 (flag dst_props): -1 by size (replicas while every shard's tag data fits
+    // dstReplicaMax bytes), 0 replicas of every tag table over the global rows (gathered once per snapshot),
+    // 1 the owner fetch per record hop (GoExecutor::fetchVertexProps -> QueryVertexPropsProcessor)
+    int32_t dstProps = -1;
+    uint64_t dstReplicaMax = uint64_t(1) << 30;
+    uint64_t dstFetches = 0, dstFetchRows = 0;
     ~ngx_ctx() {                                       // also the cleanup of ngx_open's error paths
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
@@ -1994,6 +2028,12 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
         return NGX_OK;
     }
     if (n == "batch_release_lanes") { c->batchReleaseLanes = value != 0; return NGX_OK; }
+    if (n == "dst_props") {
+        if (value < -1 || value > 1) return fail(c, NGX_E_BAD_ARGUMENT, "dst_props: -1 (by size), 0 (replicas) or 1 (owner fetch)");
+        c->dstProps = static_cast<int32_t>(value);
+        return NGX_OK;
+    }
+    if (n == "dst_replica_max") { c->dstReplicaMax = static_cast<uint64_t>(std::max<int64_t>(value, 0)); return NGX_OK; }
     if (n == "release_lanes") {                       // action: free the parked lanes' buffers now
         if (value) c->releasedBytes += c->releaseParked();
         return NGX_OK;
@@ -2042,6 +2082,10 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "batch_pipeline") *value = c->batchPipeline ? 1 : 0;
     else if (n == "batch_lanes") *value = c->batchLanes;
     else if (n == "batch_finals") *value = c->batchFinals;
+    else if (n == "dst_props") *value = c->dstProps;
+    else if (n == "dst_replica_max") *value = static_cast<int64_t>(c->dstReplicaMax);
+    else if (n == "dst_fetches") *value = static_cast<int64_t>(c->dstFetches);
+    else if (n == "dst_fetch_rows") *value = static_cast<int64_t>(c->dstFetchRows);
     else if (n == "batch_release_lanes") *value = c->batchReleaseLanes ? 1 : 0;
     else if (n == "released_lane_bytes") *value = static_cast<int64_t>(c->releasedBytes);
     else if (n == "batch_close_stream") *value = c->batchCloseStream ? 1 : 0;
@@ -2346,6 +2390,328 @@ void exchangeFrontierList(ngx_ctx* c, const DeviceGraph& d, uint8_t epoch) {
     if (launchMergeList(recv, roff[W], c->visited.get<uint8_t>(d.vglobal) + d.gbase, epoch, c->stream))
         throw Error{NGX_E_DEVICE, "merge lists"};
     c->xchgListHops++;
+}
+
+// Variable-size all-to-all of device blocks: this rank sends block q (sendDev + soff[q], mat[me * W + q]
+// bytes) to rank q and receives rank p's block at recvDev + roff[p] (mat[p * W + me] bytes). Every rank
+// passes the same byte matrix mat[p * W + q]. Its own block is a device copy; the host collective moves
+// equal blocks of the largest count of any pair; RCCL sends and receives exactly.
+void allToAllV(ngx_ctx* c, const uint8_t* sendDev, const std::vector<uint64_t>& soff, uint8_t* recvDev,
+               const std::vector<uint64_t>& roff, const std::vector<uint64_t>& mat) {
+    const int W = c->world, me = c->rank;
+    const uint64_t self = mat[static_cast<size_t>(me) * W + me];
+    if (self) HIP_OK(hipMemcpyAsync(recvDev + roff[me], sendDev + soff[me], self, hipMemcpyDeviceToDevice, c->stream));
+    uint64_t block = 0;
+    for (int p = 0; p < W; p++)
+        for (int q = 0; q < W; q++) if (p != q) block = std::max<uint64_t>(block, mat[static_cast<size_t>(p) * W + q]);
+    if (block == 0) return;
+    if (c->xchg) {
+        std::vector<uint8_t> hs(block * W, 0), hr(block * W, 0);
+        for (int q = 0; q < W; q++) {
+            const uint64_t n = q == me ? 0 : mat[static_cast<size_t>(me) * W + q];
+            if (n) HIP_OK(hipMemcpyAsync(hs.data() + q * block, sendDev + soff[q], n, hipMemcpyDeviceToHost, c->stream));
+        }
+        HIP_OK(hipStreamSynchronize(c->stream));
+        if (c->xchg(c->xchgUser, NGX_XCHG_ALLTOALL, hs.data(), hr.data(), block) != 0) throw Error{NGX_E_DEVICE, "host exchange failed"};
+        for (int p = 0; p < W; p++) {
+            const uint64_t n = p == me ? 0 : mat[static_cast<size_t>(p) * W + me];
+            if (n) HIP_OK(hipMemcpyAsync(recvDev + roff[p], hr.data() + p * block, n, hipMemcpyHostToDevice, c->stream));
+        }
+        HIP_OK(hipStreamSynchronize(c->stream));
+    } else {
+        NCCL_OK(ncclGroupStart());
+        for (int q = 0; q < W; q++) {
+            if (q == me) continue;
+            const uint64_t ns = mat[static_cast<size_t>(me) * W + q], nr = mat[static_cast<size_t>(q) * W + me];
+            if (ns) NCCL_OK(ncclSend(sendDev + soff[q], ns, ncclUint8, q, c->comm, c->stream));
+            if (nr) NCCL_OK(ncclRecv(recvDev + roff[q], nr, ncclUint8, q, c->comm, c->stream));
+        }
+        NCCL_OK(ncclGroupEnd());
+        rcclWait(c, "dst props all-to-all");
+    }
+}
+
+// the byte matrix of an exchange: this rank's row (bytes to each rank) all-gathered
+std::vector<uint64_t> gatherMatrix(ngx_ctx* c, const std::vector<uint64_t>& row) {
+    const int W = c->world;
+    const std::vector<uint8_t> all = gatherHost(c, row.data(), static_cast<uint64_t>(W) * 8);
+    std::vector<uint64_t> m(static_cast<size_t>(W) * W);
+    std::memcpy(m.data(), all.data(), m.size() * 8);
+    return m;
+}
+
+// bytes of one fetched row's fixed record: per tag its present byte; per column its 8-byte value (int /
+// double bits / bool), its valid byte and, for strings, a 4-byte length (the bytes follow the records)
+uint64_t dstRecordBytes(const HostGraph& g) {
+    uint64_t b = 0;
+    for (const HostTag& t : g.tags) {
+        b += 1;
+        for (const HostColumn& col : t.cols) b += 9 + (col.type == T_STRING ? 4 : 0);
+    }
+    return b;
+}
+
+// $$ props at world > 1, fetched from their owners for one record hop (GoExecutor::fetchVertexProps,
+// GoExecutor.cpp:937-973, answered by QueryVertexPropsProcessor, src/storage/query/
+// QueryVertexPropsProcessor.cpp:16-58): every shard
+//   1. marks the global rows its record hop's edges lead to (the push expansion's kernel, a fresh epoch),
+//   2. lists them per owner (its own rows too) and sends each owner its list (counts all-gathered first),
+//   3. as an owner, reads the requested rows' tag values from its host tables and sends them back,
+//   4. stores what it receives as tag tables over the fetched rows only, and a global row -> fetched row
+//      map (FinalArgs::dstMap) that the final hop's $$ reads go through.
+// Collective: every shard calls it for every record hop (E = 0 too: it still answers its peers). Memory is
+// O(fetched rows) per query, not O(global rows) of every tag column per shard as the replicas are.
+struct DstFetch { const DTag* tags = nullptr; const DCol* cols = nullptr; const uint32_t* map = nullptr; };
+DstFetch fetchDstProps(ngx_ctx* c, Space& sp, size_t recIdx, const uint32_t* F, const uint64_t* estart,
+                       const uint64_t* chunkFirst, uint64_t nEnt, uint64_t E, const HopSlots& hs, bool pos32,
+                       const uint64_t* ebase) {
+    DeviceGraph& d = *sp.dev;
+    const HostGraph& g = *sp.host;
+    const int W = c->world, me = c->rank;
+    const auto& sb = d.shardBase;
+    DstLane& L = c->dst;
+    // 1. destination rows
+    ensureVisited(c, d.vglobal);
+    const uint8_t ep = nextEpoch(c);
+    if (E && launchExpandMark(F, estart, chunkFirst, nEnt, E, hs, static_cast<uint8_t*>(c->visited.p), ep, pos32, c->stream,
+                              nullptr, nullptr, ~0ULL, ebase))
+        throw Error{NGX_E_DEVICE, "dst marks"};
+    // 2. per owner lists (local offsets in the owner's range), counts all-gathered
+    uint64_t cap = 1;
+    for (int q = 0; q < W; q++) cap = std::max<uint64_t>(cap, sb[q + 1] - sb[q]);
+    uint32_t* lists = L.req.get<uint32_t>(cap * W);
+    unsigned long long* counts = L.counts.get<unsigned long long>(W);
+    HIP_OK(hipMemsetAsync(counts, 0, W * 8, c->stream));
+    ListXchgArgs la{};
+    la.visited = static_cast<const uint8_t*>(c->visited.p);
+    la.epoch = ep;
+    for (int q = 0; q <= W; q++) la.sb[q] = sb[q];
+    la.world = W;
+    la.rank = me;
+    la.list = lists;
+    la.cap = cap;
+    la.counts = counts;
+    la.includeSelf = 1;
+    if (launchPackLists(la, c->stream)) throw Error{NGX_E_DEVICE, "dst lists"};
+    std::vector<uint64_t> mine(W);
+    HIP_OK(hipMemcpyAsync(mine.data(), counts, W * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    const std::vector<uint64_t> m = gatherMatrix(c, mine);         // m[p * W + q]: rows p asks of q
+    std::vector<uint64_t> soff(W), roff(W + 1, 0), mat4(static_cast<size_t>(W) * W);
+    for (int q = 0; q < W; q++) soff[q] = static_cast<uint64_t>(q) * cap * 4;
+    for (int p = 0; p < W; p++) roff[p + 1] = roff[p] + m[static_cast<size_t>(p) * W + me] * 4;
+    for (size_t k = 0; k < mat4.size(); k++) mat4[k] = m[k] * 4;
+    uint8_t* recv = L.recv.get<uint8_t>(std::max<uint64_t>(roff[W], 4));
+    allToAllV(c, reinterpret_cast<const uint8_t*>(lists), soff, recv, roff, mat4);
+    // 3. as the owner: the requested rows' values from the host tables, one blob per requester
+    std::vector<uint32_t> asked(roff[W] / 4);
+    if (!asked.empty()) HIP_OK(hipMemcpyAsync(asked.data(), recv, roff[W], hipMemcpyDeviceToHost, c->stream));
+    std::vector<uint32_t> myReq;                                   // my lists, owner by owner (the row order)
+    uint64_t nReq = 0;
+    for (int q = 0; q < W; q++) nReq += m[static_cast<size_t>(me) * W + q];
+    myReq.resize(nReq);
+    {
+        uint64_t at = 0;
+        for (int q = 0; q < W; q++) {
+            const uint64_t n = m[static_cast<size_t>(me) * W + q];
+            if (n) HIP_OK(hipMemcpyAsync(myReq.data() + at, lists + q * cap, n * 4, hipMemcpyDeviceToHost, c->stream));
+            at += n;
+        }
+    }
+    HIP_OK(hipStreamSynchronize(c->stream));
+    const uint64_t rec = dstRecordBytes(g);
+    std::vector<uint64_t> boff(W + 1, 0);                          // blob of requester p at boff[p]
+    std::vector<uint8_t> blobs;
+    for (int p = 0; p < W; p++) {
+        const uint32_t* rows = asked.data() + roff[p] / 4;
+        const uint64_t n = (roff[p + 1] - roff[p]) / 4;
+        const uint64_t base = blobs.size();
+        blobs.resize(base + n * rec);
+        std::string bytes;
+        for (uint64_t i = 0; i < n; i++) {
+            const uint32_t r = rows[i];
+            if (r >= g.vid.size()) throw Error{NGX_E_DEVICE, "dst fetch: row outside the shard"};
+            uint8_t* o = blobs.data() + base + i * rec;
+            for (const HostTag& t : g.tags) {
+                *o++ = t.present[r];
+                for (const HostColumn& col : t.cols) {
+                    uint64_t v = 0;
+                    switch (col.type) {
+                        case T_INT: case T_TIMESTAMP: case T_VID: v = static_cast<uint64_t>(col.i64[r]); break;
+                        case T_FLOAT: case T_DOUBLE: std::memcpy(&v, &col.f64[r], 8); break;
+                        case T_BOOL: v = col.b[r]; break;
+                        default: break;
+                    }
+                    std::memcpy(o, &v, 8);
+                    o[8] = col.allValid ? 1 : col.valid[r];
+                    o += 9;
+                    if (col.type == T_STRING) {
+                        const uint32_t len = static_cast<uint32_t>(col.soff[r + 1] - col.soff[r]);
+                        std::memcpy(o, &len, 4);
+                        o += 4;
+                        bytes.append(col.sbytes, col.soff[r], len);
+                    }
+                }
+            }
+        }
+        blobs.insert(blobs.end(), bytes.begin(), bytes.end());
+        boff[p + 1] = blobs.size();
+    }
+    std::vector<uint64_t> brow(W);
+    for (int p = 0; p < W; p++) brow[p] = boff[p + 1] - boff[p];
+    const std::vector<uint64_t> bm = gatherMatrix(c, brow);       // bm[q * W + p]: bytes owner q sends p
+    uint8_t* bs = L.blobS.get<uint8_t>(std::max<uint64_t>(blobs.size(), 8));
+    if (!blobs.empty()) HIP_OK(hipMemcpyAsync(bs, blobs.data(), blobs.size(), hipMemcpyHostToDevice, c->stream));
+    std::vector<uint64_t> bro(W + 1, 0);
+    for (int q = 0; q < W; q++) bro[q + 1] = bro[q] + bm[static_cast<size_t>(q) * W + me];
+    uint8_t* br = L.blobR.get<uint8_t>(std::max<uint64_t>(bro[W], 8));
+    allToAllV(c, bs, boff, br, bro, bm);
+    std::vector<uint8_t> got(bro[W]);
+    if (!got.empty()) HIP_OK(hipMemcpyAsync(got.data(), br, got.size(), hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    // 4. tables over the fetched rows (owner order, each owner's list order) + the row map
+    struct ColOut { std::vector<uint8_t> val8, valid; std::vector<uint8_t> b; std::vector<uint64_t> soff; bool anyInvalid = false; };
+    std::vector<std::vector<ColOut>> cols(g.tags.size());
+    std::vector<std::vector<uint8_t>> present(g.tags.size(), std::vector<uint8_t>(nReq));
+    for (size_t k = 0; k < g.tags.size(); k++) {
+        cols[k].resize(g.tags[k].cols.size());
+        for (size_t j = 0; j < g.tags[k].cols.size(); j++) {
+            ColOut& co = cols[k][j];
+            const int32_t ty = g.tags[k].cols[j].type;
+            if (ty == T_BOOL) co.b.resize(nReq);
+            else if (ty != T_STRING) co.val8.resize(nReq * 8);
+            co.valid.resize(nReq);
+            if (ty == T_STRING) co.soff.assign(nReq + 1, 0);
+        }
+    }
+    std::string strBytes;
+    uint64_t at = 0;
+    for (int q = 0; q < W; q++) {
+        const uint64_t n = m[static_cast<size_t>(me) * W + q];
+        const uint8_t* blob = got.data() + bro[q];
+        if (bro[q + 1] - bro[q] < n * rec) throw Error{NGX_E_DEVICE, "dst fetch: short reply"};
+        const char* sbytes = reinterpret_cast<const char*>(blob + n * rec);
+        uint64_t scur = 0;
+        for (uint64_t i = 0; i < n; i++, at++) {
+            const uint8_t* o = blob + i * rec;
+            for (size_t k = 0; k < g.tags.size(); k++) {
+                present[k][at] = *o++;
+                for (size_t j = 0; j < g.tags[k].cols.size(); j++) {
+                    ColOut& co = cols[k][j];
+                    const int32_t ty = g.tags[k].cols[j].type;
+                    if (ty == T_BOOL) co.b[at] = o[0];
+                    else if (ty != T_STRING) std::memcpy(co.val8.data() + at * 8, o, 8);
+                    co.valid[at] = o[8];
+                    co.anyInvalid = co.anyInvalid || o[8] == 0;
+                    o += 9;
+                    if (ty == T_STRING) {
+                        uint32_t len;
+                        std::memcpy(&len, o, 4);
+                        o += 4;
+                        co.soff[at + 1] = len;                 // lengths now, offsets below
+                        (void)scur;
+                    }
+                }
+            }
+        }
+        // the owner appended each row's strings in (tag, column) order: re-cut them per column
+        for (uint64_t i = 0, r0 = at - n; i < n; i++) {
+            for (size_t k = 0; k < g.tags.size(); k++)
+                for (size_t j = 0; j < g.tags[k].cols.size(); j++) {
+                    ColOut& co = cols[k][j];
+                    if (g.tags[k].cols[j].type != T_STRING) continue;
+                    const uint64_t len = co.soff[r0 + i + 1];
+                    if (sbytes + scur + len > reinterpret_cast<const char*>(blob) + (bro[q + 1] - bro[q]))
+                        throw Error{NGX_E_DEVICE, "dst fetch: short string reply"};
+                    co.b.insert(co.b.end(), sbytes + scur, sbytes + scur + len);     // (per column, row order)
+                    scur += len;
+                }
+        }
+    }
+    // device layout: one allocation per record hop of the query; strings of every column in one block
+    if (L.data.size() <= recIdx) {
+        L.data.resize(recIdx + 1);
+        L.hostStr.resize(recIdx + 1);
+        L.devStr.resize(recIdx + 1, nullptr);
+    }
+    std::vector<uint8_t> img;
+    auto put = [&](const void* src, uint64_t n) {
+        const uint64_t o = (img.size() + 15) & ~uint64_t(15);
+        img.resize(o + n);
+        if (n) std::memcpy(img.data() + o, src, n);
+        return o;
+    };
+    struct Pend { uint64_t present; std::vector<uint64_t> data, valid, soff; };
+    std::vector<Pend> pend(g.tags.size());
+    std::string& hs8 = L.hostStr[recIdx];
+    hs8.clear();
+    std::vector<std::vector<uint64_t>> strBase(g.tags.size());
+    for (size_t k = 0; k < g.tags.size(); k++) {
+        pend[k].present = put(present[k].data(), nReq);
+        strBase[k].resize(g.tags[k].cols.size(), 0);
+        for (size_t j = 0; j < g.tags[k].cols.size(); j++) {
+            ColOut& co = cols[k][j];
+            const int32_t ty = g.tags[k].cols[j].type;
+            uint64_t dOff = ~0ULL, sOff = ~0ULL;
+            if (ty == T_STRING) {
+                for (uint64_t i = 0; i < nReq; i++) co.soff[i + 1] += co.soff[i];
+                strBase[k][j] = hs8.size();
+                hs8.append(reinterpret_cast<const char*>(co.b.data()), co.b.size());
+                for (uint64_t i = 0; i <= nReq; i++) co.soff[i] += strBase[k][j];   // offsets into the block
+                sOff = put(co.soff.data(), (nReq + 1) * 8);
+            } else if (ty == T_BOOL) {
+                dOff = put(co.b.data(), nReq);
+            } else {
+                dOff = put(co.val8.data(), nReq * 8);
+            }
+            pend[k].data.push_back(dOff);
+            pend[k].soff.push_back(sOff);
+            pend[k].valid.push_back(co.anyInvalid ? put(co.valid.data(), nReq) : ~0ULL);
+        }
+    }
+    const uint64_t strOff = put(hs8.data(), hs8.size());
+    // descriptors after the data
+    std::vector<DTag> tagsOut;
+    std::vector<DCol> colsOut;
+    uint8_t* dev = L.data[recIdx].get<uint8_t>(img.size() + (g.tags.size() + 1) * sizeof(DTag) + (d.cols.size() + 64) * sizeof(DCol) + 64);
+    for (size_t k = 0; k < g.tags.size(); k++) {
+        DTag t = d.tags[k];
+        t.present = dev + pend[k].present;
+        t.colBase = static_cast<int32_t>(colsOut.size());
+        tagsOut.push_back(t);
+        for (size_t j = 0; j < g.tags[k].cols.size(); j++) {
+            DCol dc{};
+            dc.type = g.tags[k].cols[j].type;
+            dc.width = 8;
+            if (pend[k].data[j] != ~0ULL) dc.data = dev + pend[k].data[j];
+            if (pend[k].soff[j] != ~0ULL) {
+                dc.soff = reinterpret_cast<const uint64_t*>(dev + pend[k].soff[j]);
+                dc.sbytes = reinterpret_cast<const char*>(dev + strOff);
+            }
+            if (pend[k].valid[j] != ~0ULL) dc.valid = dev + pend[k].valid[j];
+            colsOut.push_back(dc);
+        }
+    }
+    const uint64_t tOff = put(tagsOut.data(), tagsOut.size() * sizeof(DTag));
+    const uint64_t cOff = put(colsOut.data(), colsOut.size() * sizeof(DCol));
+    if (img.size() > L.data[recIdx].cap) throw Error{NGX_E_DEVICE, "dst fetch: table image larger than sized"};
+    HIP_OK(hipMemcpyAsync(dev, img.data(), img.size(), hipMemcpyHostToDevice, c->stream));
+    L.devStr[recIdx] = reinterpret_cast<const char*>(dev + strOff);
+    // the map: global row of fetched row i = sb[q] + list offset
+    std::vector<uint32_t> grow(nReq);
+    {
+        uint64_t i = 0;
+        for (int q = 0; q < W; q++)
+            for (uint64_t j = 0; j < m[static_cast<size_t>(me) * W + q]; j++, i++) grow[i] = static_cast<uint32_t>(sb[q] + myReq[i]);
+    }
+    uint32_t* drows = L.rows.get<uint32_t>(std::max<uint64_t>(nReq, 1));
+    if (nReq) HIP_OK(hipMemcpyAsync(drows, grow.data(), nReq * 4, hipMemcpyHostToDevice, c->stream));
+    uint32_t* map = L.map.get<uint32_t>(std::max<uint64_t>(d.vglobal, 1));
+    if (launchScatterIndex(drows, nReq, map, c->stream)) throw Error{NGX_E_DEVICE, "dst map"};
+    HIP_OK(hipStreamSynchronize(c->stream));                       // the host staging leaves scope
+    c->dstFetches++;
+    c->dstFetchRows += nReq;
+    return DstFetch{reinterpret_cast<const DTag*>(dev + tOff), reinterpret_cast<const DCol*>(dev + cOff), map};
 }
 
 // multi-root walk at world > 1: the expansion OR-ed root sets into next[] over global rows; every
@@ -2744,7 +3110,20 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     std::vector<Arena> arenas;                                   // this query's, in record-hop order
     // $$ props: tag tables over every global row (world > 1: replicas of the other shards' rows)
     const bool dstReplica = progs.usesDst && c->world > 1;
-    if (dstReplica) ensureDstReplicas(c, sp);
+    // owner fetch per record hop, or replicas over every global row (flag dst_props; by size: the replicas
+    // while every shard's tag data would take at most dstReplicaMax bytes on each shard)
+    bool ownerDst = false;
+    if (dstReplica) {
+        uint64_t local = 0;
+        for (const HostTag& t : sp.host->tags) {
+            local += t.present.size();
+            for (const HostColumn& col : t.cols) local += t.present.size() * 9 + col.sbytes.size();
+        }
+        ownerDst = c->dstProps == 1 ||
+                   (c->dstProps < 0 && !d.replicas && local * static_cast<uint64_t>(c->world) > c->dstReplicaMax);
+    }
+    if (dstReplica && !ownerDst) ensureDstReplicas(c, sp);
+    size_t dstRec = 0;                                           // record hops fetched so far (owner fetch)
     const DTag* dstTags = dstReplica ? d.rtags : d.dtags;
     const DCol* dstCols = dstReplica ? d.rcols : d.dcols;
     std::vector<int32_t> ySlotType(progs.yOff.size(), 0);
@@ -3311,6 +3690,12 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             mask = m;
         }
         a.mask = mask;
+        if (isRecord && ownerDst) {                              // every shard, E = 0 too (it answers its peers)
+            const DstFetch f = fetchDstProps(c, sp, dstRec++, F, estart, chunkFirst, nEnt, E, hs, pos32, ebase);
+            a.env.dtags = f.tags;
+            a.env.dcols = f.cols;
+            a.dstMap = f.map;
+        }
         if (isRecord && E) {
             // ngx_go_batch: this query's last final hop may overlap the next query (goDeferPoint): not with a
             // device read-back left (multi-root walks), string arenas, profiling or host traces. World > 1 too
@@ -3952,6 +4337,10 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     if (!builtRanges.empty()) HIP_OK(hipStreamSynchronize(c->stream));
     if (rw && rw->perRow && rw->inStrBytes)                      // YIELD $-.s: strings of the input table
         builtRanges.push_back(StrMap::Range{rw->inStrDev, rw->inStrBytes, rw->inStrHost});
+    for (size_t k = 0; k < dstRec && k < c->dst.hostStr.size(); k++)   // $$ strings of the owner fetches
+        if (!c->dst.hostStr[k].empty())
+            builtRanges.push_back(StrMap::Range{reinterpret_cast<uint64_t>(c->dst.devStr[k]), c->dst.hostStr[k].size(),
+                                                c->dst.hostStr[k].data()});
     StrMap sm{&d, reinterpret_cast<uint64_t>(dp.pool), &R.strings, &builtRanges};
     uint64_t nOut = n;
     R.r.nrows = nOut;

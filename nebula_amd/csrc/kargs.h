@@ -100,6 +100,7 @@ struct FinalArgs {
                                         // for the strings YIELD columns build; nullptr when none does
     uint32_t nStrOut;                   // columns that build strings (bits of strOutMask, y < 32)
     uint32_t strOutMask;
+    const uint32_t* dstMap;             // $$ owner fetch (world > 1): global row -> row of env.dtags' tables, or null
 };
 
 // rows a GO final launch may leave past its row count before k_final_close (outputs are sized for them)

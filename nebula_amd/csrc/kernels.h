@@ -386,8 +386,11 @@ struct ListXchgArgs {
     uint32_t* list;
     uint64_t cap;                                    // entries per peer in `list`
     unsigned long long* counts;                      // world words
+    int includeSelf;                                 // also list this rank's own rows (the $$ owner fetch)
 };
 int launchPackLists(const ListXchgArgs& a, hipStream_t s);
+// map[rows[i]] = i for i < n (the $$ owner fetch: global row -> index of its fetched tag values)
+int launchScatterIndex(const uint32_t* rows, uint64_t n, uint32_t* map, hipStream_t s);
 // own[rows[i]] = epoch for i < n
 int launchMergeList(const uint32_t* rows, uint64_t n, uint8_t* own, uint8_t epoch, hipStream_t s);
 

@@ -1794,7 +1794,7 @@ __global__ __launch_bounds__(1024) void k_pack_list(ListXchgArgs a) {
     __shared__ uint64_t sm[1024 / 64 + 1];
     __shared__ uint64_t sBase;
     const int q = blockIdx.y;
-    if (q == a.rank) return;
+    if (q == a.rank && !a.includeSelf) return;
     const uint64_t n = a.sb[q + 1] - a.sb[q];
     const uint64_t tile = static_cast<uint64_t>(blockIdx.x) * 4096;
     if (tile >= n) return;
@@ -1838,10 +1838,21 @@ __global__ void k_merge_list(const uint32_t* rows, uint64_t n, uint8_t* own, uin
     if (i < n) own[rows[i]] = epoch;
 }
 
+__global__ void k_scatter_index(const uint32_t* rows, uint64_t n, uint32_t* map) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) map[rows[i]] = static_cast<uint32_t>(i);
+}
+
+int launchScatterIndex(const uint32_t* rows, uint64_t n, uint32_t* map, hipStream_t s) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_scatter_index, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, rows, n, map);
+    return static_cast<int>(hipGetLastError());
+}
+
 int launchPackLists(const ListXchgArgs& a, hipStream_t s) {
     uint64_t maxRows = 0;
     for (int q = 0; q < a.world; q++)
-        if (q != a.rank) maxRows = std::max(maxRows, a.sb[q + 1] - a.sb[q]);
+        if (q != a.rank || a.includeSelf) maxRows = std::max(maxRows, a.sb[q + 1] - a.sb[q]);
     if (maxRows == 0 || a.world < 2 || a.world > kMaxWorld) return 0;
     hipLaunchKernelGGL(k_pack_list, dim3(static_cast<unsigned>((maxRows + 4095) / 4096), a.world), dim3(1024), 0, s, a);
     return static_cast<int>(hipGetLastError());

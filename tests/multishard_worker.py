@@ -122,6 +122,7 @@ def main():
             # (ngx_go + device digest) and then all of them pipelined, on every shard
             e.set_flag("pull_factor", q.get("pull_factor", default_pf))
             e.set_flag("xchg_lists", q.get("xchg_lists", -1))
+            e.set_flag("dst_props", q.get("dst_props", -1))
             preps = [e.prepare_go(datagen.RMAT_SPACE, ngql.parse_go(t), on_device=True, compact=True, yield_only=True)
                      for t in q["batch"]]
             alone = []
@@ -150,15 +151,18 @@ def main():
         pf = q.get("pull_factor", default_pf)
         e.set_flag("pull_factor", pf[rank] if isinstance(pf, list) else pf)     # a list: per rank
         e.set_flag("xchg_lists", q.get("xchg_lists", -1))
+        e.set_flag("dst_props", q.get("dst_props", -1))
         pulls = e.get_flag("pull_hops")
         lists = e.get_flag("xchg_list_hops")
+        fetches = e.get_flag("dst_fetches")
         r = e.go(datagen.RMAT_SPACE, ngql.parse_go(q["text"]), pushdown=q.get("pushdown", True), columnar=True,
                  rows=False, digest_fn=oracle.digest_columns)
         np.save(f"{out}.{i}.npy", r.digests if r.ok else np.zeros((0, 2), np.uint64))
         res.append({"ok": r.ok, "error": r.error, "col_types": list(r.col_types) if r.ok else [], "nrows": r.nrows,
                     "hop_edges": list(r.hop_edges), "hop_xchg": list(r.hop_xchg),
                     "jit_failed": e.get_flag("jit_failed"), "pull_hops": e.get_flag("pull_hops") - pulls,
-                    "list_hops": e.get_flag("xchg_list_hops") - lists})
+                    "list_hops": e.get_flag("xchg_list_hops") - lists,
+                    "dst_fetches": e.get_flag("dst_fetches") - fetches})
     e.close()
     with open(out, "w") as f:
         json.dump(res, f)

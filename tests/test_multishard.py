@@ -225,6 +225,45 @@ def test_multishard_go_matches_oracle(tmp_path, world, scale):
     assert sum(r["pull_hops"] for r in shards[0][:n]) == sum(r["pull_hops"] for r in shards[1][:n])
 
 
+DST_QUERIES = [
+    ("GO 2 STEPS FROM {S} OVER e WHERE $$.vt.v0 > 100 YIELD $$.vt.name, $$.vt.v0, e._dst", True),
+    ("GO FROM {S} OVER e REVERSELY WHERE $$.vt.name CONTAINS \"3\" YIELD $$.vt.v0 + e.p0, $^.vt.name", True),
+    ("GO 1 TO 3 STEPS FROM {S} OVER e WHERE e.p0 < 30 YIELD $$.vt.name, e._dst, $^.vt.v0", True),
+    ("GO 2 STEPS FROM {S} OVER e BIDIRECT YIELD DISTINCT $$.vt.name, $$.vt.v0", True),
+    ("GO 3 STEPS FROM {S} OVER e WHERE $$.vt.v0 % 5 == 1 && e.p0 > 20 YIELD upper($$.vt.name), e.p1", False),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("world,scale", [(2, 11), (8, 13)])
+def test_multishard_dst_props_both_modes(tmp_path, world, scale):
+    """$$ props at world > 1 (What's missing #2), both ways: replicas of every tag table over
+    the global rows (dst_props 0) and the owner fetch per record hop (dst_props 1: each shard sends the
+    owners the destination rows its record hop reads and gets their tag values back, strings included,
+    GoExecutor::fetchVertexProps -> QueryVertexPropsProcessor): merged rows equal the oracle's in both
+    modes, and the owner mode fetched once per record hop on every shard."""
+    from nebula_amd import datagen
+    from oracle import oracle
+    from tests import fixtures
+
+    ds = fixtures.RmatDataset(scale, with_in=True, with_tag=True)
+    o = oracle.Oracle()
+    o.set_flags(threads=8)
+    ds.load_oracle(o)
+    queries = []
+    for i, (text, push) in enumerate(DST_QUERIES):
+        seeds = datagen.sample_vids(1300 + i, 1 << scale, 40)
+        t = text.replace("{S}", ", ".join(str(int(v)) for v in seeds))
+        queries += [{"text": t, "pushdown": push, "dst_props": 0}, {"text": t, "pushdown": push, "dst_props": 1}]
+    shards, digests = _run_shards(tmp_path, world, scale, queries)
+    _check_merged(o, ds.space, queries, shards, digests)
+    for s in shards:
+        for q, r in zip(queries, s):
+            records = 3 if "1 TO 3" in q["text"] else 1
+            assert r["dst_fetches"] == (records if q["dst_props"] == 1 else 0), (q["text"], r["dst_fetches"])
+
+
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("world", [2, 3])
@@ -251,17 +290,23 @@ def test_multishard_batch_pipeline(tmp_path, world):
     for k in range(12):
         seeds = datagen.sample_vids(900 + k, 1 << scale, (30, 1, 200)[k % 3])
         texts.append(shapes[k % len(shapes)].replace("{S}", ", ".join(str(int(v)) for v in seeds)))
-    queries = [{"batch": texts}, {"batch": texts, "pull_factor": 0, "xchg_lists": 1}]
+    # and $$ plans in the owner-fetch mode (their fetch's collectives on the front stream, the previous
+    # query's final hop beside them)
+    dst = [f"GO 2 STEPS FROM {', '.join(str(int(v)) for v in datagen.sample_vids(990 + k, 1 << scale, 30))} OVER e "
+           "WHERE $$.vt.v0 > 100 YIELD $$.vt.v0, e._dst, e.p0" for k in range(4)]
+    queries = [{"batch": texts}, {"batch": texts, "pull_factor": 0, "xchg_lists": 1},
+               {"batch": dst + texts[:4], "dst_props": 1}]
     shards, _ = _run_shards(tmp_path, world, scale, queries, timeout=400)
     for qi in range(len(queries)):
+        btexts = queries[qi]["batch"]
         for r, s in enumerate(shards):
             b = s[qi]
             assert b["overlaps"] > 0, (r, b["overlaps"])
             for j, (a, g) in enumerate(zip(b["alone"], b["got"])):
                 assert g[0] == a[0], (r, j, g, a)
                 if a[0] == 0:
-                    assert g[1:] == a[1:], (r, j, texts[j])
-        for j, t in enumerate(texts):
+                    assert g[1:] == a[1:], (r, j, btexts[j])
+        for j, t in enumerate(btexts):
             s = ngql.parse_go(t)
             ref = o.go(ds.space, s)
             codes = [sh[qi]["got"][j][0] for sh in shards]
