@@ -48,3 +48,4 @@ def test_host_code_under_asan_and_ubsan(driver, tmp_path):
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])
     assert "OK (0 failures)" in r.stdout
     assert "oracle: 4 GO requests" in r.stdout
+    assert "export == generator csr" in r.stdout

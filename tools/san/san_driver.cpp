@@ -37,6 +37,21 @@ int32_t ngd_rmat(int32_t scale, int32_t ef, double A, double B, double C, uint64
                  int32_t etype, int32_t with_in, int32_t with_tag, int32_t tag, int32_t rank, int32_t world,
                  int32_t threads, ngd_rows* out);
 void ngd_free(ngd_rows* r);
+typedef struct {
+    uint64_t nv;
+    int32_t* vpart;
+    int64_t* vid;
+    int32_t nslots;
+    int32_t etype[2];
+    uint64_t ne[2];
+    uint64_t* off[2];
+    int64_t* dst[2];
+    int64_t* p0[2];
+    int64_t* p1[2];
+} ngd_csr;
+int32_t ngd_rmat_csr(int32_t scale, int32_t ef, double A, double B, double C, uint64_t seed, int32_t num_parts,
+                     int32_t etype, int32_t with_in, int32_t rank, int32_t world, int32_t threads, ngd_csr* out);
+void ngd_csr_free(ngd_csr* c);
 void* orc_engine_new();
 void orc_engine_free(void* e);
 void orc_buf_free(void* p);
@@ -182,6 +197,47 @@ void snapshots(const ngd_rows& r, const std::string& dir) {
     }
 }
 
+// The KV export (exportSnapshot over ngd_rmat's reference-format rows, at a size that takes its parallel
+// classify and bucketed sort: > 64 K rows) against the generator's own CSR of the same graph (ngd_rmat_csr,
+// pinned against the KV rows by tests/test_datagen_csr.py): vertex table, per slot the offsets, dst and
+// both prop columns, equal.
+void exportMatchesCsr(int scale) {
+    ngd_rows r{};
+    CHECK(ngd_rmat(scale, 8, 0.57, 0.19, 0.19, 77, kParts, kEdge, 1, 0, kTag, 0, 1, 4, &r) == 0, "rmat rows");
+    Space sp;
+    sp.id = kSpace;
+    sp.numParts = kParts;
+    addSchemas(sp);
+    stage(sp, r, 0, 1);
+    HostGraph g;
+    Error e = exportSnapshot(sp, 0, 1, g);
+    CHECK(e.code == NGX_OK, "export: %s", e.msg.c_str());
+    ngd_csr c{};
+    CHECK(ngd_rmat_csr(scale, 8, 0.57, 0.19, 0.19, 77, kParts, kEdge, 1, 0, 1, 4, &c) == 0, "rmat csr");
+    CHECK(g.vid.size() == c.nv, "vertex count %lu vs %lu", static_cast<unsigned long>(g.vid.size()), static_cast<unsigned long>(c.nv));
+    bool same = g.vid.size() == c.nv;
+    for (uint64_t i = 0; same && i < c.nv; i++) same = g.vid[i] == c.vid[i] && g.vpart[i] == c.vpart[i];
+    CHECK(same, "vertex tables differ");
+    CHECK(static_cast<int32_t>(g.slots.size()) == c.nslots, "slot count");
+    for (int32_t k = 0; k < c.nslots && k < static_cast<int32_t>(g.slots.size()); k++) {
+        // the export orders slots by signed type (negative first); match by type
+        int32_t j = -1;
+        for (int32_t q = 0; q < c.nslots; q++) if (c.etype[q] == g.slots[k].etype) j = q;
+        CHECK(j >= 0, "slot %d type %d missing", k, g.slots[k].etype);
+        if (j < 0) continue;
+        const HostSlot& hs = g.slots[k];
+        bool ok = hs.dst.size() == c.ne[j] && hs.off.size() == c.nv + 1 && hs.cols.size() == 2;
+        for (uint64_t v = 0; ok && v <= c.nv; v++) ok = hs.off[v] == c.off[j][v];
+        for (uint64_t i = 0; ok && i < c.ne[j]; i++)
+            ok = hs.dst[i] == c.dst[j][i] && hs.cols[0].i64[i] == c.p0[j][i] && hs.cols[1].i64[i] == c.p1[j][i];
+        CHECK(ok, "slot %d (type %d): export and generator CSR differ", k, hs.etype);
+    }
+    std::printf("export == generator csr: %lu rows, %lu vertices, %lu edges\n", static_cast<unsigned long>(r.n),
+                static_cast<unsigned long>(c.nv), static_cast<unsigned long>(g.edges));
+    ngd_csr_free(&c);
+    ngd_free(&r);
+}
+
 void compileBoth(const ExprNode& n, const Space& sp) {
     std::string err;
     StorageCtx sc;
@@ -288,6 +344,7 @@ int main(int argc, char** argv) {
     std::printf("rmat scale %d: %lu rows\n", scale, static_cast<unsigned long>(r.n));
     snapshots(r, dir);
     std::printf("snapshots done\n");
+    exportMatchesCsr(13);
     expressions(dir);
     oracleRuns(r, dir);
     ngd_free(&r);
