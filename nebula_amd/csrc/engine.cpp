@@ -117,6 +117,8 @@ void drainGraveyard() {
 
 // growable device buffer
 std::atomic<uint64_t> gDBufGen{0};
+std::atomic<uint64_t> gDBufBytes{0};                    // bytes allocated by DBuf growth (flag dbuf_alloc_bytes)
+const bool gDBufTrace = std::getenv("NGX_DBUF_TRACE") != nullptr;
 struct DBuf {
     void* p = nullptr;
     size_t cap = 0;
@@ -125,12 +127,15 @@ struct DBuf {
     T* get(size_t n) {
         size_t bytes = std::max<size_t>(n * sizeof(T), 64);
         if (bytes > cap) {
+            const size_t cap0 = cap;
             freeDevice(p);
             p = nullptr;
             size_t c = std::max(bytes, cap * 3 / 2);
             HIP_OK(hipMalloc(&p, c));
             cap = c;
             gen = gDBufGen.fetch_add(1, std::memory_order_relaxed) + 1;
+            gDBufBytes.fetch_add(c, std::memory_order_relaxed);
+            if (gDBufTrace) std::fprintf(stderr, "[ngx dbuf] alloc %zu bytes (asked %zu, had %zu)\n", c, bytes, cap0);
             if (gPoison.load(std::memory_order_relaxed)) {
                 HIP_OK(hipMemset(p, kPoisonByte, c));
                 HIP_OK(hipDeviceSynchronize());
@@ -1611,6 +1616,15 @@ int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
         for (auto& e : c->pipeRing)
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { c->pipeRing[0] = nullptr; break; }
+        for (auto& e : c->laneCloseEv)
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+        // every event recorded once now: an event's first record costs far more than a later one (r06: a
+        // process's first C2 batch, which reached ring events the 5-query warm-up had not, ran 0.31-0.32 vs
+        // 0.29 ms per step; tools/ab_batch.py --prewarm-warm)
+        for (auto e : c->pipeEv) if (e) (void)hipEventRecord(e, c->stream);
+        for (auto e : c->pipeRing) if (e) (void)hipEventRecord(e, c->stream);
+        for (auto e : c->laneCloseEv) if (e) (void)hipEventRecord(e, c->stream);
+        (void)hipStreamSynchronize(c->stream);
     }
     if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || c->cus < 1) c->cus = 256;
     if (const char* ht = std::getenv("NGX_HOST_TRACE")) c->htrace = std::string(ht) == "1";
@@ -2082,6 +2096,8 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "batch_pipeline") *value = c->batchPipeline ? 1 : 0;
     else if (n == "batch_lanes") *value = c->batchLanes;
     else if (n == "batch_finals") *value = c->batchFinals;
+    else if (n == "dbuf_allocs") *value = static_cast<int64_t>(gDBufGen.load());
+    else if (n == "dbuf_alloc_bytes") *value = static_cast<int64_t>(gDBufBytes.load());
     else if (n == "dst_props") *value = c->dstProps;
     else if (n == "dst_replica_max") *value = static_cast<int64_t>(c->dstReplicaMax);
     else if (n == "dst_fetches") *value = static_cast<int64_t>(c->dstFetches);
@@ -3401,16 +3417,24 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         HIP_OK(hipMemsetAsync(c->visited.p, 0, c->visitedSize, c->stream));
         c->epoch = 0;
     }
-    if (dyn) {
+    if (dyn || c->pipe) {
         // every buffer a hop's kernels use is sized for the whole query before the first launch: a
-        // DBuf that grew later would free memory still read by kernels already enqueued
+        // DBuf that grew later would free memory still read by kernels already enqueued. In a pipelined
+        // batch too (r06): a lane growing mid-batch as a later query's frontier outgrows the earlier ones'
+        // paid a hipMalloc inside the timed loop (a process's first C2 batch after a 5-query warm-up ran
+        // 0.31-0.32 vs 0.29-0.30 ms per step, tools/ab_batch.py)
         const uint64_t mult = std::max<uint64_t>(maxMultiplicity(svids), 1);
         const uint64_t rowsCap = std::max<uint64_t>(d.V, svids.size());
         c->F0.get<uint32_t>(rowsCap);
         c->F1.get<uint32_t>(rowsCap);
         c->estart.get<uint64_t>(rowsCap * static_cast<uint64_t>(hs.n) + 1);
         c->ebase.get<uint64_t>(rowsCap * static_cast<uint64_t>(hs.n) + 1);
-        c->chunkFirst.get<uint64_t>(std::max<uint64_t>((slotEdges * mult + kChunk - 1) / kChunk + 1, cfCap));
+        c->tileSums.get<uint64_t>((rowsCap * static_cast<uint64_t>(hs.n) + kTile - 1) / kTile + 1);
+        // (at least twice the slots' chunks: a later query whose seeds repeat a vid must not grow it inside
+        // a batch — r06, the one allocation left in a C2 batch, a hipMalloc plus a device-wide free)
+        const uint64_t cfBig = std::max<uint64_t>((slotEdges * std::max<uint64_t>(mult, 2) + kChunk - 1) / kChunk + 1, cfCap);
+        c->chunkFirst.get<uint64_t>(cfBig);
+        c->chunkFirst2.get<uint64_t>(cfBig);                // (a sparse hop swaps the two)
     }
     bool haveHeads = false;                                    // chunkFirst of the next hop already built
     uint64_t finalErrBits = 0;                                 // error bits published by the last final kernel

@@ -33,6 +33,10 @@ def main():
     ap.add_argument("--scale", type=int, default=22)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--final", action="store_true")
+    ap.add_argument("--prewarm", type=int, default=0, help="untimed batches of the timed plans before round 0")
+    ap.add_argument("--sleep-ms", type=float, default=0, help="idle host time before each timed batch")
+    ap.add_argument("--busy-ms", type=float, default=0, help="unrelated device work (buffer fills) before round 0")
+    ap.add_argument("--prewarm-warm", type=int, default=0, help="untimed batches of the warm-up plans only before round 0")
     args = ap.parse_args()
     import torch
     from nebula_amd import datagen, engine, ngql
@@ -72,6 +76,19 @@ def main():
     defaults = {n: eng.get_flag(n) for _, (fl, _) in parsed for n, _ in fl}
     res = {v: [] for v, _ in parsed}
     fin = {v: [] for v, _ in parsed}
+    if args.busy_ms:
+        buf = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+        t0 = time.perf_counter()
+        while (time.perf_counter() - t0) * 1e3 < args.busy_ms:
+            buf.fill_(1)
+            torch.cuda.synchronize()
+        del buf
+    for _ in range(args.prewarm_warm):
+        eng.go_batch(warm)
+    for _ in range(args.prewarm):
+        eng.go_batch(warm)
+        eng.go_batch(timed)
+    torch.cuda.synchronize()
     for r in range(args.rounds):
         for v, (flags, envs) in (parsed if r % 2 == 0 else parsed[::-1]):
             saved = {n: os.environ.get(n) for n, _ in envs}
@@ -79,13 +96,20 @@ def main():
                 os.environ[n] = val
             for n, val in flags:
                 eng.set_flag(n, val)
+            if args.sleep_ms:
+                time.sleep(args.sleep_ms / 1e3)
             for code, _, _ in eng.go_batch(warm):
                 assert code == 0
             torch.cuda.synchronize()
+            a0 = eng.get_flag("dbuf_allocs")
+            print(f"[ab] timed batch {v} round {r} begins", file=sys.stderr, flush=True)
             t = time.perf_counter()
             out = eng.go_batch(timed)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t
+            grown = eng.get_flag("dbuf_allocs") - a0
+            if grown:
+                print(f"[ab] {v}: {grown} device buffer allocations inside the timed batch", flush=True)
             assert all(o[0] == 0 for o in out), out
             e = sum(o[2] for o in out)
             assert edges is None or e == edges
