@@ -465,18 +465,32 @@ int32_t ngx_kernel_stats(ngx_ctx* ctx, const ngx_kernel_stat** out, int32_t* n);
  *   "batch_pipeline"  1 (default): ngx_go_batch overlaps consecutive device-resident queries (the next
  *          one's host work and first hops enqueued while this one's final hop runs); 0: strictly one
  *          after the other. Same results.
- *   "batch_lanes"  2 .. 4 (default 3): lanes of scratch and result rows a pipelined batch rotates over; up
+ *   "batch_lanes"  2 .. 4 (default 4): lanes of scratch and result rows a pipelined batch rotates over; up
  *          to lanes - 1 queries wait for their row counts while the next one runs its hops. Same results.
- *   "batch_fronts"  1 or 2 (default 2): streams the batch's hops run on (consecutive queries alternate).
- *   "batch_close_stream"  1 (default) / 0: an overlapped final hop's close on a stream of its own (the
- *          next final hop does not queue behind it). Same results.
+ *   "batch_fronts"  1 or 2 (default 2): streams the batch's hops run on (consecutive queries alternate;
+ *          world > 1 always 1, so every rank issues its collectives in one order).
+ *   "batch_finals"  1 or 2 (default 2): final streams of a batch; with 2 consecutive queries' final hops
+ *          alternate between them (each close after its final hop on the same stream). Same results.
+ *   "batch_close_stream"  1 (default) / 0: with one final stream, an overlapped final hop's close on a
+ *          stream of its own (the next final hop does not queue behind it). Same results.
+ *   "release_lanes"  1: free the parked lanes' scratch and result arrays now; "batch_release_lanes" 1 (default
+ *          0): after every batch. Read-only "released_lane_bytes".
+ *   "resv_groups"  1 .. 64 (default 8, a group per XCD): row-reservation counters of the GO final hop
+ *          (kargs.h resv*). Same rows; more groups shorten the final hop's reservation stream and lengthen
+ *          its close.
+ *   "dst_props"  world > 1 $$ props: -1 (default) by size, 0 tag replicas over every global row (gathered
+ *          once per snapshot), 1 fetched from their owners per record hop (GoExecutor::fetchVertexProps ->
+ *          QueryVertexPropsProcessor). "dst_replica_max" (bytes per shard, default 1 GiB): the size rule.
+ *          Collective like every GO: set it alike on every rank. Same results. Read-only "dst_fetches",
+ *          "dst_fetch_rows".
  *   "batch_cu_split"  0 (default) / 32, 64, 128: a batch's hops on that many CUs (groups of 8 spread over
  *          the XCDs), its final hops on the rest. Same results.
  *   "batch_event_ring"  1 (default): each cross-stream wait of a batch takes its own event. Same results.
  *   "compact_wg"  0 (default: 256 in a pipelined batch, else 1024), 256 or 1024: threads per workgroup of
  *          the next-frontier compaction. Same results.
  * Read-only counters for ngx_get_flag: "jit_compiled", "jit_hits", "jit_failed", "jit_compile_us",
- * "jit_cached", "jit_evicted", "batch_overlaps" (queries of ngx_go_batch that overlapped the next). */
+ * "jit_cached", "jit_evicted", "batch_overlaps" (queries of ngx_go_batch that overlapped the next),
+ * "dbuf_allocs" / "dbuf_alloc_bytes" (device scratch allocations of the process so far). */
 int32_t ngx_set_flag(ngx_ctx* ctx, const char* name, int64_t value);
 int32_t ngx_get_flag(ngx_ctx* ctx, const char* name, int64_t* value);
 /* why the last query ran on the interpreter kernels instead of a generated one ("" if it did not) */

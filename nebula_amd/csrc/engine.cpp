@@ -47,6 +47,9 @@ struct DeviceGraph {
     int32_t vidW = 8;                                   // narrowest signed width holding every vid of vid[]
     VIndex vindex{nullptr, 0};                          // (part, vid) -> row hash index (seed lookup)
     std::vector<DSlot> slots;
+    // per slot: the row holding CSR position c * kChunk, for every chunk c of the slot (+ a last row): the
+    // chunk map of a final hop over the whole slot (FinalArgs::denseMark)
+    std::vector<const uint64_t*> chunkRow;
     std::vector<int32_t> mirror;                        // per slot: the slot holding its exact transpose, or -1
     // per slot with a mirror: the pull hop's head image of the in-lists (kernels.h PullArgs)
     struct PullHead { const uint32_t* perm = nullptr; const uint32_t* head = nullptr; const uint8_t* nk = nullptr;
@@ -474,6 +477,10 @@ struct ngx_ctx {
     // dstReplicaMax bytes), 0 replicas of every tag table over the global rows (gathered once per snapshot),
     // 1 the owner fetch per record hop (GoExecutor::fetchVertexProps -> QueryVertexPropsProcessor)
     int32_t dstProps = -1;
+    // the final hop over every CSR position of its slot, reading the frontier from the marks (no next-frontier
+    // list, no entry arrays): after a pulled hop at world 1 with one OVER type (flag dense_final)
+    bool denseFinal = true;
+    uint64_t denseFinals = 0;
     uint64_t dstReplicaMax = uint64_t(1) << 30;
     uint64_t dstFetches = 0, dstFetchRows = 0;
     ~ngx_ctx() {                                       // also the cleanup of ngx_open's error paths
@@ -726,6 +733,19 @@ std::unique_ptr<DeviceGraph> upload(HostGraph& g, const Space& sp) {
         ds.eflags = s.anyFlags ? d->upload(s.eflags.data(), s.eflags.size()) : nullptr;
         uploadColumns(*d, s.cols, s.dst.size(), sp.narrow);
         d->slots.push_back(ds);
+        {
+            const uint64_t E = s.off.empty() ? 0 : s.off.back();
+            const uint64_t nCh = (E + kChunk - 1) / kChunk;
+            std::vector<uint64_t> cr(nCh + 1, 0);
+            uint64_t r = 0;
+            for (uint64_t ch = 0; ch < nCh; ch++) {
+                const uint64_t pos = ch * kChunk;
+                while (r + 1 < s.off.size() && s.off[r + 1] <= pos) r++;
+                cr[ch] = r;
+            }
+            cr[nCh] = s.off.size() >= 2 ? s.off.size() - 2 : 0;
+            d->chunkRow.push_back(d->upload(cr.data(), cr.size()));
+        }
     }
     for (auto& t : g.tags) {
         DTag dt{};
@@ -2047,6 +2067,7 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
         c->dstProps = static_cast<int32_t>(value);
         return NGX_OK;
     }
+    if (n == "dense_final") { c->denseFinal = value != 0; return NGX_OK; }
     if (n == "dst_replica_max") { c->dstReplicaMax = static_cast<uint64_t>(std::max<int64_t>(value, 0)); return NGX_OK; }
     if (n == "release_lanes") {                       // action: free the parked lanes' buffers now
         if (value) c->releasedBytes += c->releaseParked();
@@ -2099,6 +2120,8 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "dbuf_allocs") *value = static_cast<int64_t>(gDBufGen.load());
     else if (n == "dbuf_alloc_bytes") *value = static_cast<int64_t>(gDBufBytes.load());
     else if (n == "dst_props") *value = c->dstProps;
+    else if (n == "dense_final") *value = c->denseFinal ? 1 : 0;
+    else if (n == "dense_finals") *value = static_cast<int64_t>(c->denseFinals);
     else if (n == "dst_replica_max") *value = static_cast<int64_t>(c->dstReplicaMax);
     else if (n == "dst_fetches") *value = static_cast<int64_t>(c->dstFetches);
     else if (n == "dst_fetch_rows") *value = static_cast<int64_t>(c->dstFetchRows);
@@ -3437,6 +3460,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         c->chunkFirst2.get<uint64_t>(cfBig);                // (a sparse hop swaps the two)
     }
     bool haveHeads = false;                                    // chunkFirst of the next hop already built
+    bool denseNextFinal = false;                               // the final hop reads the marks of epoch denseEpoch
+    uint8_t denseEpoch = 0;
     uint64_t finalErrBits = 0;                                 // error bits published by the last final kernel
     bool haveFinalErrs = false;
     // device time of the query (HIP events) only while profiling: an event query costs ~10 us of host
@@ -3742,6 +3767,21 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             uint64_t Ef = E;                                    // edges the final launch evaluates
             uint64_t gridf = chunks;
             a.fin = nullptr;
+            a.denseMark = nullptr;
+            a.denseEp = 0;
+            if (isFinal && denseNextFinal) {
+                // every CSR position of the slot; entries = the shard's rows, the frontier = the marks
+                a.estart = hs.off[0];
+                a.ebase = hs.off[0];
+                a.chunkFirst = d.chunkRow[hs.slotIdx[0]];
+                a.nEnt = d.V;
+                a.E = slotEdges;
+                a.denseMark = marksA + d.gbase;
+                a.denseEp = denseEpoch;
+                Ef = slotEdges;
+                gridf = (slotEdges + kChunk - 1) / kChunk;
+                c->denseFinals++;
+            }
             if (rw && rw->perRow) {
                 // the hop's entries as (frontier row, input row) pairs: a frontier row once per input row
                 // of every root that reaches it, the input row travelling with the entry (FinalArgs::fin)
@@ -4071,6 +4111,12 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             haveBits = lbits != nullptr && !ca.bitsZero;
             c->bitsClean = false;
             const bool devNext = finalDev && h + 1 == steps;      // the next hop is the device-sized final one
+            // dense final hop next: after a pull (its frontier is most of the shard's edges), one OVER type
+            const bool denseNext = devNext && c->denseFinal && pull && !mask && !capped && !rw && hs.n == 1 && c->world == 1 &&
+                                   d.gbase == 0 && hs.slotIdx[0] >= 0 && hs.slotIdx[0] < static_cast<int32_t>(d.chunkRow.size());
+            ca.countOnly = denseNext ? 1 : 0;
+            denseNextFinal = denseNext;
+            denseEpoch = ep;
             ca.total = (dyn || devNext) ? dynStats + h : counters + 2;
             ca.pub = (dyn || devNext) ? Publish{nullptr, 0} : nextPub(c);
             ca.zero = nullptr;

@@ -101,6 +101,11 @@ struct FinalArgs {
     uint32_t nStrOut;                   // columns that build strings (bits of strOutMask, y < 32)
     uint32_t strOutMask;
     const uint32_t* dstMap;             // $$ owner fetch (world > 1): global row -> row of env.dtags' tables, or null
+    // dense final hop (one slot, world 1): the launch covers every CSR position of the slot; entries are the
+    // shard's rows (estart = ebase = the slot's off[], chunkFirst = the slot's chunkRow), and an edge counts
+    // only when its row's mark is denseEp (the frontier the compaction would have listed). null: off
+    const uint8_t* denseMark;
+    uint32_t denseEp;
 };
 
 // rows a GO final launch may leave past its row count before k_final_close (outputs are sized for them)

@@ -122,6 +122,8 @@ struct CompactArgs {
                                         // 4096-row tile; a workgroup that fits beside another query's final hop)
     int32_t bitsZero;                   // write every word of `bits` as 0 (no hop reads this frontier's bitmap:
                                         // the next hop is the final one), leaving it clean for a sparse hop
+    int32_t countOnly;                  // dense final hop next (FinalArgs::denseMark): the count launch, then
+                                        // one workgroup summing its tile totals into *total; no rows written
 };
 // Sparse intermediate hop (world 1, push, E far below the shard's rows): the expansion builds the next
 // frontier itself instead of a compaction sweeping every row (kernels.hip k_expand_sparse). Per edge one

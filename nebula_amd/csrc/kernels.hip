@@ -1563,6 +1563,19 @@ int launchCompactDegrees(const uint8_t* visited, uint64_t gbase, uint64_t V, uin
                  s, estart, hs.n, pub);
 }
 
+// the packed (rows << kFdShift | degrees) total of the count launch's tiles (countOnly: the frontier the
+// dense final hop reads from the marks, its size and edges for the statistics)
+__global__ __launch_bounds__(256) void k_tile_total(const uint64_t* tileSum, uint64_t tiles, uint64_t* total) {
+    __shared__ uint64_t sm[4];
+    uint64_t t = 0;
+    for (uint64_t i = threadIdx.x; i < tiles; i += 256) t += tileSum[i];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) *total = sm[0] + sm[1] + sm[2] + sm[3];
+}
+
 int launchCompactLb(const CompactArgs& a, hipStream_t s) {
     if (a.V >= kCompactLbMaxV || a.nzero > WG) return 1;
     // rows per lane: 4 unless the flag forces 8 or 16 (measured at C2: 8 rows per lane, every wave
@@ -1577,7 +1590,10 @@ int launchCompactLb(const CompactArgs& a, hipStream_t s) {
 #define NGX_COMPACT(ONE, CIT, WGS)                                                              \
     do {                                                                                        \
         hipLaunchKernelGGL((k_compact_count<ONE, CIT, WGS>), grid, dim3(WGS), 0, s, a);         \
-        hipLaunchKernelGGL((k_compact_write<ONE, CIT, WGS>), grid, dim3(WGS), 0, s, a);         \
+        if (a.countOnly)                                                                        \
+            hipLaunchKernelGGL(k_tile_total, dim3(1), dim3(256), 0, s, a.tileSum, static_cast<uint64_t>(grid.x), a.total); \
+        else                                                                                    \
+            hipLaunchKernelGGL((k_compact_write<ONE, CIT, WGS>), grid, dim3(WGS), 0, s, a);     \
     } while (0)
     if (small) {
         if (a.hs.n == 1) NGX_COMPACT(true, 16, 256);

@@ -13,6 +13,7 @@ pairs per hop, BIDIRECT / REVERSELY / OVER *), the NBA fixture (GoTest answers),
 are NOT the transpose of their out-edges (one in-edge missing or misdirected: pull must not be used),
 and enough queries in a row to wrap the one-byte mark epoch several times.
 """
+import numpy as np
 import pytest
 
 from nebula_amd import datagen, engine, ngql
@@ -226,3 +227,63 @@ def test_pull_epoch_wrap(rmat12):
     for i in range(140):
         got = e.go(ds.space, s)
         assert got.ok and fixtures.normalize_cells(got.rows) == ref, i
+
+
+DENSE_Q = RMAT_Q + [
+    "GO 3 STEPS FROM {S} OVER e WHERE $^.vt.v0 > 100 YIELD e._src, e._dst, $^.vt.name, $$.vt.v0",
+    "GO 2 STEPS FROM {S} OVER e REVERSELY WHERE e.p0 < 60 YIELD e._src, e._dst, e.p1",
+    "GO 3 STEPS FROM {S} OVER e WHERE e.p1 % (e.p0 - e.p0) > 1 YIELD e._dst",          # fails (division by zero)
+]
+
+
+@pytest.fixture(scope="module")
+def rmat12_host():
+    ds = fixtures.RmatDataset(12, with_in=True, with_tag=True)
+    o = oracle.Oracle()
+    o.set_flags(threads=8)
+    ds.load_oracle(o)
+    e = engine.Engine(0)
+    ds.load_engine(e)
+    yield ds, o, e
+    e.close()
+    o.close()
+
+
+@pytest.mark.parametrize("dense", [1, 0])
+def test_dense_final_hop(rmat12_host, dense):
+    """The final hop over every CSR position of its slot, reading the frontier from the pull's marks
+    (flag dense_final; no next-frontier list, no entry arrays), on and off: rows, hop statistics and
+    errors equal the oracle's, for typed cells, $^ / $$ props and src rows, REVERSELY, and a device-resident
+    compact YIELD-only result (the bench's layout) compared by row digest."""
+    ds, o, e = rmat12_host
+    e.set_flag("dense_final", dense)
+    e.set_flag("pull_factor", 1)
+    before = e.get_flag("dense_finals")
+    try:
+        for qi, q in enumerate(DENSE_Q):
+            seeds = datagen.sample_vids(1700 + qi, 1 << ds.scale, 30)
+            text = q.replace("{S}", ", ".join(str(int(v)) for v in seeds))
+            s = ngql.parse_go(text)
+            got, ref = e.go(ds.space, s), o.go(ds.space, s)
+            assert got.ok == ref.ok, (text, got.error, ref.error)
+            if not ref.ok:
+                continue
+            assert got.hop_edges == ref.hop_scanned, text
+            assert fixtures.normalize_cells(got.rows) == fixtures.normalize_cells(ref.rows), text
+        # the bench's placement
+        seeds = datagen.sample_vids(1799, 1 << ds.scale, 60)
+        s = ngql.parse_go(f"GO 3 STEPS FROM {', '.join(str(int(v)) for v in seeds)} OVER e WHERE e.p0 < 50 "
+                          "YIELD e._dst, e._rank, e.p0, e.p1")
+        ref = o.go(ds.space, s)
+        cols = [np.array([int(r[c][1]) for r in ref.rows], dtype=np.int64) for c in range(4)]
+        want = oracle.row_digest([np.zeros(len(ref.rows), np.int64)] + cols)
+        prep = e.prepare_go(ds.space, s, on_device=True, compact=True, yield_only=True)
+        r = e.go(ds.space, prep, rows=False, device_digest=True)
+        assert r.ok and r.hop_edges == ref.hop_scanned and tuple(r.device_digest) == tuple(want)
+        got = e.go_batch([prep] * 6, digests=True)
+        assert all(g[0] == 0 and tuple(g[3]) == tuple(want) for g in got)
+    finally:
+        e.set_flag("dense_final", 1)
+        e.set_flag("pull_factor", 200)
+    used = e.get_flag("dense_finals") - before
+    assert (used > 0) if dense else (used == 0)
