@@ -4111,9 +4111,12 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             haveBits = lbits != nullptr && !ca.bitsZero;
             c->bitsClean = false;
             const bool devNext = finalDev && h + 1 == steps;      // the next hop is the device-sized final one
-            // dense final hop next: after a pull (its frontier is most of the shard's edges), one OVER type
-            const bool denseNext = devNext && c->denseFinal && pull && !mask && !capped && !rw && hs.n == 1 && c->world == 1 &&
-                                   d.gbase == 0 && hs.slotIdx[0] >= 0 && hs.slotIdx[0] < static_cast<int32_t>(d.chunkRow.size());
+            // dense final hop next: after a pull (its frontier is most of the shard's edges), one OVER type; at
+            // world > 1 too (the pull marked this shard's own rows, no exchange follows it), host-sized there,
+            // but not with the $$ owner fetch (it expands the frontier list)
+            const bool denseNext = (devNext || (c->world > 1 && !dyn && h + 1 == steps && !ownerDst)) && c->denseFinal &&
+                                   pull && !mask && !capped && !rw && hs.n == 1 && recordFrom == steps &&
+                                   hs.slotIdx[0] >= 0 && hs.slotIdx[0] < static_cast<int32_t>(d.chunkRow.size());
             ca.countOnly = denseNext ? 1 : 0;
             denseNextFinal = denseNext;
             denseEpoch = ep;

@@ -1565,7 +1565,7 @@ int launchCompactDegrees(const uint8_t* visited, uint64_t gbase, uint64_t V, uin
 
 // the packed (rows << kFdShift | degrees) total of the count launch's tiles (countOnly: the frontier the
 // dense final hop reads from the marks, its size and edges for the statistics)
-__global__ __launch_bounds__(256) void k_tile_total(const uint64_t* tileSum, uint64_t tiles, uint64_t* total) {
+__global__ __launch_bounds__(256) void k_tile_total(const uint64_t* tileSum, uint64_t tiles, uint64_t* total, Publish pub) {
     __shared__ uint64_t sm[4];
     uint64_t t = 0;
     for (uint64_t i = threadIdx.x; i < tiles; i += 256) t += tileSum[i];
@@ -1573,7 +1573,11 @@ __global__ __launch_bounds__(256) void k_tile_total(const uint64_t* tileSum, uin
     for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
     if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = t;
     __syncthreads();
-    if (threadIdx.x == 0) *total = sm[0] + sm[1] + sm[2] + sm[3];
+    if (threadIdx.x == 0) {
+        const uint64_t t4 = sm[0] + sm[1] + sm[2] + sm[3];
+        *total = t4;
+        if (pub.slot) publishWords(pub.slot, pub.seq, t4, 0);      // a host-sized final hop (world > 1)
+    }
 }
 
 int launchCompactLb(const CompactArgs& a, hipStream_t s) {
@@ -1591,7 +1595,7 @@ int launchCompactLb(const CompactArgs& a, hipStream_t s) {
     do {                                                                                        \
         hipLaunchKernelGGL((k_compact_count<ONE, CIT, WGS>), grid, dim3(WGS), 0, s, a);         \
         if (a.countOnly)                                                                        \
-            hipLaunchKernelGGL(k_tile_total, dim3(1), dim3(256), 0, s, a.tileSum, static_cast<uint64_t>(grid.x), a.total); \
+            hipLaunchKernelGGL(k_tile_total, dim3(1), dim3(256), 0, s, a.tileSum, static_cast<uint64_t>(grid.x), a.total, a.pub); \
         else                                                                                    \
             hipLaunchKernelGGL((k_compact_write<ONE, CIT, WGS>), grid, dim3(WGS), 0, s, a);     \
     } while (0)

@@ -155,6 +155,7 @@ def main():
         pulls = e.get_flag("pull_hops")
         lists = e.get_flag("xchg_list_hops")
         fetches = e.get_flag("dst_fetches")
+        denses = e.get_flag("dense_finals")
         r = e.go(datagen.RMAT_SPACE, ngql.parse_go(q["text"]), pushdown=q.get("pushdown", True), columnar=True,
                  rows=False, digest_fn=oracle.digest_columns)
         np.save(f"{out}.{i}.npy", r.digests if r.ok else np.zeros((0, 2), np.uint64))
@@ -162,7 +163,8 @@ def main():
                     "hop_edges": list(r.hop_edges), "hop_xchg": list(r.hop_xchg),
                     "jit_failed": e.get_flag("jit_failed"), "pull_hops": e.get_flag("pull_hops") - pulls,
                     "list_hops": e.get_flag("xchg_list_hops") - lists,
-                    "dst_fetches": e.get_flag("dst_fetches") - fetches})
+                    "dst_fetches": e.get_flag("dst_fetches") - fetches,
+                    "dense_finals": e.get_flag("dense_finals") - denses})
     e.close()
     with open(out, "w") as f:
         json.dump(res, f)

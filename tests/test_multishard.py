@@ -222,6 +222,8 @@ def test_multishard_go_matches_oracle(tmp_path, world, scale):
     for s in shards:                                     # every shard takes the same pull decisions
         assert [r["pull_hops"] for r in s[n:m]] == [r["pull_hops"] for r in shards[0][n:m]]
     assert not pulled or sum(r["pull_hops"] for r in shards[0][n:m]) >= 5
+    # a final hop right after a pulled hop reads the frontier from the marks (dense final hop, r06)
+    assert not pulled or all(sum(r["dense_finals"] for r in s[n:m]) > 0 for s in shards)
     assert sum(r["pull_hops"] for r in shards[0][:n]) == sum(r["pull_hops"] for r in shards[1][:n])
 
 
