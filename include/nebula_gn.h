@@ -488,6 +488,10 @@ int32_t ngx_kernel_stats(ngx_ctx* ctx, const ngx_kernel_stat** out, int32_t* n);
  *   "batch_event_ring"  1 (default): each cross-stream wait of a batch takes its own event. Same results.
  *   "compact_wg"  0 (default: 256 in a pipelined batch, else 1024), 256 or 1024: threads per workgroup of
  *          the next-frontier compaction. Same results.
+ *   "dense_final"  1 (default): after a pulled hop the final hop covers every CSR position of its one
+ *          OVER slot and reads the pull's marks (no next-frontier list). Read-only "dense_finals". Same results.
+ *   "final_nt_loads" / "final_nt_stores"  0 (default) / 1: the generated GO final hop loads its columns /
+ *          stores its rows non-temporally (not kept in L2). Same results.
  * Read-only counters for ngx_get_flag: "jit_compiled", "jit_hits", "jit_failed", "jit_compile_us",
  * "jit_cached", "jit_evicted", "batch_overlaps" (queries of ngx_go_batch that overlapped the next),
  * "dbuf_allocs" / "dbuf_alloc_bytes" (device scratch allocations of the process so far). */

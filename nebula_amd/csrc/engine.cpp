@@ -273,7 +273,11 @@ struct ngx_ctx {
     uint64_t pullSegWords = 0;
     int32_t compactLaneRows = 0;                        // compaction rows per lane: 0 = by shard size, else 4 / 8 / 16
     int32_t compactWg = 0;                              // compaction workgroup threads: 0 = auto, 256 or 1024
-    bool finalNtStores = false;                         // generated final hops store result rows non-temporally
+    // generated GO final hops store result rows / load columns non-temporally (flags final_nt_stores /
+    // final_nt_loads). r06, both on: the batch 0.2796 vs 0.2833 ms/step on one box (8 rounds), 0.2898 vs
+    // 0.2901 on another (6); the final hop alone ~1% slower; either alone slower than neither. Kept off.
+    bool finalNtStores = false;
+    bool finalNtLoads = false;
     uint32_t resvGroups = kResvGroups;                  // GO final hop row-reservation groups (flag resv_groups, 1 .. kResvMaxGroups)
     int64_t pullFactor = 200;                           // pull when 100 x hop edges >= pullFactor x shard rows (0: never)
     uint64_t pullHops = 0;
@@ -2079,6 +2083,7 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
         return NGX_OK;
     }
     if (n == "final_nt_stores") { c->finalNtStores = value != 0; return NGX_OK; }
+    if (n == "final_nt_loads") { c->finalNtLoads = value != 0; return NGX_OK; }
     if (n == "resv_groups") {
         if (value < 1 || value > static_cast<int64_t>(kResvMaxGroups))
             return fail(c, NGX_E_BAD_ARGUMENT, "resv_groups: 1 .. " + std::to_string(kResvMaxGroups));
@@ -2135,6 +2140,7 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "compact_lane_rows") *value = c->compactLaneRows;
     else if (n == "compact_wg") *value = c->compactWg;
     else if (n == "final_nt_stores") *value = c->finalNtStores ? 1 : 0;
+    else if (n == "final_nt_loads") *value = c->finalNtLoads ? 1 : 0;
     else if (n == "resv_groups") *value = c->resvGroups;
     else if (n == "pull_hops") *value = static_cast<int64_t>(c->pullHops);
     else if (n == "sparse_hops") *value = static_cast<int64_t>(c->sparseHops);
@@ -3578,6 +3584,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
         jq.dstReplica = dstReplica;
         jq.rowMask = rowMask;
         jq.ntStore = c->finalNtStores ? 1 : 0;
+        jq.ntLoad = c->finalNtLoads ? 1 : 0;
         for (int k = 0; k < 3; k++) jq.outW[k] = outW[k];
         if (compact) jq.yW = yW;
         jq.input = rw && rw->perRow;

@@ -51,6 +51,7 @@ struct JitQuery {
     bool dstReplica = false;        // $$ props read the cross-shard replicas (8-byte, may lack values)
     int32_t rowMask = 7;            // row arrays written: 1 src, 2 dst, 4 rank (ngx_go_plan::yield_only)
     int32_t ntStore = 0;            // result stores non-temporal (flag final_nt_stores)
+    int32_t ntLoad = 0;             // global loads non-temporal, vm.h gld (flag final_nt_loads)
     bool fidx = false;              // GetNeighbors kernel: request-ordered rows with their frontier index
     bool input = false;             // GO over frontier entries that carry input rows (OP_INPUT, FinalArgs::fin)
     std::vector<int32_t> ySlot;     // per column: 0 any edge, else the signed type whose edges it reads

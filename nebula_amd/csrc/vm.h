@@ -50,10 +50,15 @@ struct VmEnv {
 
 // Loads through the global address space. Column pointers come from device-side tables (DCol, DTag),
 // which the compiler cannot prove global, so plain dereferences become flat loads (ordered with LDS
-// traffic: every wait on them also waits on lgkmcnt).
+// traffic: every wait on them also waits on lgkmcnt). NGX_GLD_NT (a generated kernel's own #define, flag
+// final_nt_loads): non-temporal loads, each line read once and not kept in L2.
 template <typename T>
 __device__ __forceinline__ T gld(const void* p, uint64_t i) {
+#ifdef NGX_GLD_NT
+    return __builtin_nontemporal_load(&((const __attribute__((address_space(1))) T*)p)[i]);
+#else
     return ((const __attribute__((address_space(1))) T*)p)[i];
+#endif
 }
 
 template <typename T>
