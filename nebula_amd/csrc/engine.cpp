@@ -484,6 +484,7 @@ struct ngx_ctx {
     // the final hop over every CSR position of its slot, reading the frontier from the marks (no next-frontier
     // list, no entry arrays): after a pulled hop at world 1 with one OVER type (flag dense_final)
     bool denseFinal = true;
+    bool denseCloseTotal = true;                        // its frontier total summed by the close (flag dense_close_total)
     uint64_t denseFinals = 0;
     uint64_t dstReplicaMax = uint64_t(1) << 30;
     uint64_t dstFetches = 0, dstFetchRows = 0;
@@ -2072,6 +2073,7 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
         return NGX_OK;
     }
     if (n == "dense_final") { c->denseFinal = value != 0; return NGX_OK; }
+    if (n == "dense_close_total") { c->denseCloseTotal = value != 0; return NGX_OK; }
     if (n == "dst_replica_max") { c->dstReplicaMax = static_cast<uint64_t>(std::max<int64_t>(value, 0)); return NGX_OK; }
     if (n == "release_lanes") {                       // action: free the parked lanes' buffers now
         if (value) c->releasedBytes += c->releaseParked();
@@ -2126,6 +2128,7 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "dbuf_alloc_bytes") *value = static_cast<int64_t>(gDBufBytes.load());
     else if (n == "dst_props") *value = c->dstProps;
     else if (n == "dense_final") *value = c->denseFinal ? 1 : 0;
+    else if (n == "dense_close_total") *value = c->denseCloseTotal ? 1 : 0;
     else if (n == "dense_finals") *value = static_cast<int64_t>(c->denseFinals);
     else if (n == "dst_replica_max") *value = static_cast<int64_t>(c->dstReplicaMax);
     else if (n == "dst_fetches") *value = static_cast<int64_t>(c->dstFetches);
@@ -3468,6 +3471,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     bool haveHeads = false;                                    // chunkFirst of the next hop already built
     bool denseNextFinal = false;                               // the final hop reads the marks of epoch denseEpoch
     uint8_t denseEpoch = 0;
+    const uint64_t* denseTiles = nullptr;                      // its frontier total: the close sums these
+    uint64_t denseTileN = 0;
     uint64_t finalErrBits = 0;                                 // error bits published by the last final kernel
     bool haveFinalErrs = false;
     // device time of the query (HIP events) only while profiling: an event query costs ~10 us of host
@@ -3853,6 +3858,11 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             a.rowsPub = rowsPub.slot;
             a.rowsSeq = rowsPub.seq;
             a.dynTotal = dynTotal;
+            if (isFinal && denseNextFinal && denseTiles != nullptr) {
+                if (dynTotal == nullptr) throw Error{NGX_E_DEVICE, "dense final hop without a device total"};
+                a.dynTiles = denseTiles;
+                a.nDynTiles = denseTileN;
+            }
             a.strOut = nullptr;
             a.nStrOut = nStrOut;
             a.strOutMask = strOutMask;
@@ -4125,6 +4135,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                                    pull && !mask && !capped && !rw && hs.n == 1 && recordFrom == steps &&
                                    hs.slotIdx[0] >= 0 && hs.slotIdx[0] < static_cast<int32_t>(d.chunkRow.size());
             ca.countOnly = denseNext ? 1 : 0;
+            // device-sized dense final hop: its close sums the count launch's tiles (no launch here)
+            ca.totalByClose = denseNext && devNext && !dyn && c->denseCloseTotal ? 1 : 0;
             denseNextFinal = denseNext;
             denseEpoch = ep;
             ca.total = (dyn || devNext) ? dynStats + h : counters + 2;
@@ -4140,6 +4152,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             c->timed("compact_degrees", 0, [&] {
                 if (launchCompactLb(ca, c->stream)) throw Error{NGX_E_DEVICE, "compact"};
             });
+            denseTiles = ca.totalByClose ? cmpTile : nullptr;
+            denseTileN = ca.totalByClose ? compactLbTiles(ca) : 0;
             if (ca.bits && ca.bitsZero) markBitsZero(c, ca.bits, (d.V + 63) / 64);
             haveEstart = true;
             haveEbase = true;

@@ -95,6 +95,8 @@ struct FinalArgs {
     uint32_t kl[kJitConsts];            // string literal lengths
     const uint64_t* dynTotal;           // device-driven hop: packed (frontier rows << kDynShift | E) written by
                                         // the kernel that built the frontier; nullptr: E / nEnt above
+    const uint64_t* dynTiles;           // dense final hop: the compaction count launch's tile words; the close
+    uint64_t nDynTiles;                 // sums them into *dynTotal before publishing it (no launch of its own)
     const uint32_t* fin;                // per frontier entry: its input row (multi-root pipe walks), or null
     char* strOut;                       // result string arena: kStrBuildBytes per (row - oBase, string column),
                                         // for the strings YIELD columns build; nullptr when none does

@@ -124,6 +124,8 @@ struct CompactArgs {
                                         // the next hop is the final one), leaving it clean for a sparse hop
     int32_t countOnly;                  // dense final hop next (FinalArgs::denseMark): the count launch, then
                                         // one workgroup summing its tile totals into *total; no rows written
+    int32_t totalByClose;               // countOnly, the total read on the device only: no summing launch, the
+                                        // final hop's close sums the tile words (FinalArgs::dynTiles)
 };
 // Sparse intermediate hop (world 1, push, E far below the shard's rows): the expansion builds the next
 // frontier itself instead of a compaction sweeping every row (kernels.hip k_expand_sparse). Per edge one
@@ -161,6 +163,8 @@ constexpr uint64_t kCompactTile = 4096;     // the smallest compaction tile (102
 // GO final kernel words: kargs.h (kResv*, kDoneOff). The seed / compaction kernels clear zero[k * kDoneOff]
 // for k < nzero.
 int launchCompactLb(const CompactArgs& a, hipStream_t s);
+// tile words the count launch of launchCompactLb(a) writes (a.tileSum[0 .. n))
+uint64_t compactLbTiles(const CompactArgs& a);
 // seed hop variant that also writes chunkFirst (cfCap entries) and clears zero[0 .. nzero)
 int launchSeedFrontierCf(const int32_t* qpart, const int64_t* qvid, uint64_t n, VIndex idx, const HopSlots& hs,
                          uint32_t* F, uint64_t* estart, Publish pub, uint64_t* chunkFirst, uint64_t cfCap,
@@ -230,6 +234,8 @@ struct CloseArgs {
     char* strOut;
     uint64_t oBase;
     const uint64_t* dynTotal;           // the final hop's packed (|F|, E) on the device, published beside R
+    const uint64_t* dynTiles;           // when set: *dynTotal = the sum of these words, written by the close
+    uint64_t nDynTiles;
     uint32_t resvTB, resvSeq, resvG, resvShift, resvStride, nStrOut;
 };
 struct CloseCols {

@@ -1063,6 +1063,7 @@ __global__ __launch_bounds__(WG) void k_final_in(FinalArgs a) { finalBody<VmEv, 
 struct CloseHead {
     uint64_t hLo[kResvMaxGroups], hHi[kResvMaxGroups], gV[kResvMaxGroups];
     uint64_t R, P, M;
+    uint64_t tsum[NW];                  // a.dynTiles: per-wave partial sums (workgroup 0)
     int nh;
 };
 // every workgroup: the groups' counts and last blocks (one load round trip), the holes sorted, R and
@@ -1091,6 +1092,13 @@ __device__ __forceinline__ void closeHead(const A& a, CloseHead& h, bool first) 
         }
     }
     if (threadIdx.x == WG - 1) h.P = gld<uint64_t>(a.resvCtl, 0);
+    if (first && a.dynTiles != nullptr) {                   // the dense final hop's frontier total (its
+        uint64_t t = 0;                                     // count launch's tiles, written before the final)
+        for (uint64_t i = threadIdx.x; i < a.nDynTiles; i += WG) t += gld<uint64_t>(a.dynTiles, i);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
+        if ((threadIdx.x & 63) == 0) h.tsum[threadIdx.x >> 6] = t;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         uint64_t R = 0;
@@ -1110,13 +1118,21 @@ __device__ __forceinline__ void closeHead(const A& a, CloseHead& h, bool first) 
         h.M = M;
         h.nh = nh;
         if (first) {
+            if (a.dynTiles != nullptr) {
+                uint64_t t = 0;
+                for (int w = 0; w < NW; w++) t += h.tsum[w];
+                *const_cast<uint64_t*>(a.dynTotal) = t;
+            }
             lbStore(a.resvCtl + (1 + G) * st, R);           // the row count (device copy; dyn hops read it)
             for (uint32_t g = 0; g <= G; g++) lbStore(a.resvNext + g * st, 0);   // the next launch's counters
             if (a.rowsPub != nullptr) {
                 uint64_t bits = 0;
                 for (int k = 0; k < 4; k++)
                     bits |= static_cast<uint64_t>(__hip_atomic_load(a.err + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) << k;
-                publishWords(a.rowsPub, a.rowsSeq, R, bits, a.dynTotal ? gld<uint64_t>(a.dynTotal, 0) : 0);
+                uint64_t tot = 0;
+                if (a.dynTiles != nullptr) for (int w = 0; w < NW; w++) tot += h.tsum[w];
+                else if (a.dynTotal != nullptr) tot = gld<uint64_t>(a.dynTotal, 0);
+                publishWords(a.rowsPub, a.rowsSeq, R, bits, tot);
             }
         }
     }
@@ -1580,8 +1596,16 @@ __global__ __launch_bounds__(256) void k_tile_total(const uint64_t* tileSum, uin
     }
 }
 
+uint64_t compactLbTiles(const CompactArgs& a) {
+    const bool small = a.wgThreads == 256;
+    const int cit = small ? 16 : a.laneRows != 0 ? a.laneRows : 4;
+    const uint64_t tile = static_cast<uint64_t>(small ? 256 : CWG) * cit;
+    return std::max<uint64_t>((a.V + tile - 1) / tile, 1);
+}
+
 int launchCompactLb(const CompactArgs& a, hipStream_t s) {
     if (a.V >= kCompactLbMaxV || a.nzero > WG) return 1;
+    if (a.totalByClose && !a.countOnly) return 1;
     // rows per lane: 4 unless the flag forces 8 or 16 (measured at C2: 8 rows per lane, every wave
     // resident at once, 48 vs 46 us per step for 4 with a second round of waves)
     // 256-thread workgroups (a pipelined batch: one finds room on a CU beside the other query's final-hop
@@ -1594,8 +1618,9 @@ int launchCompactLb(const CompactArgs& a, hipStream_t s) {
 #define NGX_COMPACT(ONE, CIT, WGS)                                                              \
     do {                                                                                        \
         hipLaunchKernelGGL((k_compact_count<ONE, CIT, WGS>), grid, dim3(WGS), 0, s, a);         \
-        if (a.countOnly)                                                                        \
+        if (a.countOnly && !a.totalByClose)                                                     \
             hipLaunchKernelGGL(k_tile_total, dim3(1), dim3(256), 0, s, a.tileSum, static_cast<uint64_t>(grid.x), a.total, a.pub); \
+        else if (a.countOnly) {}                                                                \
         else                                                                                    \
             hipLaunchKernelGGL((k_compact_write<ONE, CIT, WGS>), grid, dim3(WGS), 0, s, a);     \
     } while (0)
@@ -1696,6 +1721,8 @@ int launchFinalClose(const FinalArgs& a, hipStream_t s) {
         ca.strOut = a.strOut;
         ca.oBase = a.oBase;
         ca.dynTotal = a.dynTotal;
+        ca.dynTiles = a.dynTiles;
+        ca.nDynTiles = a.nDynTiles;
         ca.resvTB = a.resvTB;
         ca.resvSeq = a.resvSeq;
         ca.resvG = a.resvG;

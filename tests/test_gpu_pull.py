@@ -249,14 +249,16 @@ def rmat12_host():
     o.close()
 
 
-@pytest.mark.parametrize("dense", [1, 0])
-def test_dense_final_hop(rmat12_host, dense):
+@pytest.mark.parametrize("dense,close_total", [(1, 1), (1, 0), (0, 1)])
+def test_dense_final_hop(rmat12_host, dense, close_total):
     """The final hop over every CSR position of its slot, reading the frontier from the pull's marks
     (flag dense_final; no next-frontier list, no entry arrays), on and off: rows, hop statistics and
     errors equal the oracle's, for typed cells, $^ / $$ props and src rows, REVERSELY, and a device-resident
-    compact YIELD-only result (the bench's layout) compared by row digest."""
+    compact YIELD-only result (the bench's layout) compared by row digest. close_total 1: the hop's
+    frontier total (the statistics) summed by the final hop's close (flag dense_close_total), 0: its own launch."""
     ds, o, e = rmat12_host
     e.set_flag("dense_final", dense)
+    e.set_flag("dense_close_total", close_total)
     e.set_flag("pull_factor", 1)
     before = e.get_flag("dense_finals")
     try:
@@ -280,10 +282,12 @@ def test_dense_final_hop(rmat12_host, dense):
         prep = e.prepare_go(ds.space, s, on_device=True, compact=True, yield_only=True)
         r = e.go(ds.space, prep, rows=False, device_digest=True)
         assert r.ok and r.hop_edges == ref.hop_scanned and tuple(r.device_digest) == tuple(want)
+        assert r.hop_frontier == ref.hop_frontier, (r.hop_frontier, ref.hop_frontier)
         got = e.go_batch([prep] * 6, digests=True)
         assert all(g[0] == 0 and tuple(g[3]) == tuple(want) for g in got)
     finally:
         e.set_flag("dense_final", 1)
+        e.set_flag("dense_close_total", 1)
         e.set_flag("pull_factor", 200)
     used = e.get_flag("dense_finals") - before
     assert (used > 0) if dense else (used == 0)

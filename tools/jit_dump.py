@@ -19,8 +19,10 @@ def main():
         seeds = datagen.rmat_seeds(scale, 100, 16, 42, 1)
         s = ngql.parse_go("GO 3 STEPS FROM " + ", ".join(str(int(v)) for v in seeds) +
                           " OVER e WHERE e.p0 < 50 YIELD e._dst, e._rank, e.p0, e.p1")
-        r = e.go(ds.space, s, on_device=True)
-        print("rows", r.nrows, "jit", e.get_flag("jit_compiled"), e.jit_note())
+        # the bench's timed plan: compact, YIELD-only device results
+        p = e.prepare_go(ds.space, s, on_device=True, yield_only=True, compact=True)
+        r = e.go(ds.space, p, rows=False)
+        print("ok", r.ok, "jit", e.get_flag("jit_compiled"), e.jit_note(), "dense", e.get_flag("dense_finals"))
 
 
 if __name__ == "__main__":
