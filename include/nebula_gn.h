@@ -492,6 +492,8 @@ int32_t ngx_kernel_stats(ngx_ctx* ctx, const ngx_kernel_stat** out, int32_t* n);
  *          OVER slot and reads the pull's marks (no next-frontier list). Read-only "dense_finals". Same results.
  *          "dense_close_total" 1 (default): its frontier total (the hop statistics) is summed by its close
  *          instead of a launch of its own. Same results.
+ *          "dense_world_dev" 1 (default): at world > 1 too, that total stays on the device (published with
+ *          the row count) instead of a host wait after the count launch. Same results.
  *   "final_nt_loads" / "final_nt_stores"  0 (default) / 1: the generated GO final hop loads its columns /
  *          stores its rows non-temporally (not kept in L2). Same results.
  * Read-only counters for ngx_get_flag: "jit_compiled", "jit_hits", "jit_failed", "jit_compile_us",

@@ -485,6 +485,7 @@ struct ngx_ctx {
     // list, no entry arrays): after a pulled hop at world 1 with one OVER type (flag dense_final)
     bool denseFinal = true;
     bool denseCloseTotal = true;                        // its frontier total summed by the close (flag dense_close_total)
+    bool denseWorldDev = true;                          // world > 1: its totals kept on the device (flag dense_world_dev)
     uint64_t denseFinals = 0;
     uint64_t dstReplicaMax = uint64_t(1) << 30;
     uint64_t dstFetches = 0, dstFetchRows = 0;
@@ -2074,6 +2075,7 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
     }
     if (n == "dense_final") { c->denseFinal = value != 0; return NGX_OK; }
     if (n == "dense_close_total") { c->denseCloseTotal = value != 0; return NGX_OK; }
+    if (n == "dense_world_dev") { c->denseWorldDev = value != 0; return NGX_OK; }
     if (n == "dst_replica_max") { c->dstReplicaMax = static_cast<uint64_t>(std::max<int64_t>(value, 0)); return NGX_OK; }
     if (n == "release_lanes") {                       // action: free the parked lanes' buffers now
         if (value) c->releasedBytes += c->releaseParked();
@@ -2129,6 +2131,7 @@ int32_t ngx_get_flag(ngx_ctx* c, const char* name, int64_t* value) {
     else if (n == "dst_props") *value = c->dstProps;
     else if (n == "dense_final") *value = c->denseFinal ? 1 : 0;
     else if (n == "dense_close_total") *value = c->denseCloseTotal ? 1 : 0;
+    else if (n == "dense_world_dev") *value = c->denseWorldDev ? 1 : 0;
     else if (n == "dense_finals") *value = static_cast<int64_t>(c->denseFinals);
     else if (n == "dst_replica_max") *value = static_cast<int64_t>(c->dstReplicaMax);
     else if (n == "dst_fetches") *value = static_cast<int64_t>(c->dstFetches);
@@ -3443,7 +3446,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                        // a pull factor set below 1 (pull on any hop of E >= V / 100: tests, pull-heavy tuning)
                        // wants hop 1's direction from its real E, which only the seed hop knows
                        !(pullable && c->pullFactor < 100);
-    uint64_t* dynStats = (dyn || finalDev || spec1) ? c->dynStats.get<uint64_t>(steps + 2) : nullptr;
+    uint64_t* dynStats = (dyn || finalDev || spec1 || c->world > 1) ? c->dynStats.get<uint64_t>(steps + 2) : nullptr;
     const uint64_t pullMinE = pullable ? (static_cast<uint64_t>(c->pullFactor) * d.V + 99) / 100 : ~0ULL;
     if (dyn && c->epoch + 2 * static_cast<uint64_t>(steps) + 4 > 255) {   // no epoch wrap inside the query
         HIP_OK(hipMemsetAsync(c->visited.p, 0, c->visitedSize, c->stream));
@@ -3471,6 +3474,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
     bool haveHeads = false;                                    // chunkFirst of the next hop already built
     bool denseNextFinal = false;                               // the final hop reads the marks of epoch denseEpoch
     uint8_t denseEpoch = 0;
+    bool denseDevFinal = false;                                // world > 1: its totals from the device (close)
     const uint64_t* denseTiles = nullptr;                      // its frontier total: the close sums these
     uint64_t denseTileN = 0;
     uint64_t finalErrBits = 0;                                 // error bits published by the last final kernel
@@ -3690,7 +3694,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             if (nF == 0) break;                                    // GO_EXIT: empty frontier
             specPull = tryPull && fusedE >= pullMinE;
         }
-        const bool devE = finalDev && isFinal;                   // E below is an upper bound; the device has it
+        const bool devE = (finalDev || denseDevFinal) && isFinal;   // E below is an upper bound; the device has it
         uint64_t nEnt = nF * static_cast<uint64_t>(hs.n);
         uint64_t* estart = c->estart.get<uint64_t>(nEnt + 1);
         const uint64_t* ebase = haveEbase ? c->ebase.get<uint64_t>(nEnt + 1) : nullptr;
@@ -4135,12 +4139,17 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
                                    pull && !mask && !capped && !rw && hs.n == 1 && recordFrom == steps &&
                                    hs.slotIdx[0] >= 0 && hs.slotIdx[0] < static_cast<int32_t>(d.chunkRow.size());
             ca.countOnly = denseNext ? 1 : 0;
+            // world > 1: the dense final hop's grid is static, so its totals (the statistics) can stay on the
+            // device too, published by its close: no host wait after this launch (flag dense_world_dev)
+            const bool denseWorld = denseNext && !devNext && c->denseWorldDev;
+            const bool devTotal = devNext || denseWorld;
             // device-sized dense final hop: its close sums the count launch's tiles (no launch here)
-            ca.totalByClose = denseNext && devNext && !dyn && c->denseCloseTotal ? 1 : 0;
+            ca.totalByClose = denseNext && devTotal && !dyn && c->denseCloseTotal ? 1 : 0;
             denseNextFinal = denseNext;
+            denseDevFinal = denseWorld;
             denseEpoch = ep;
-            ca.total = (dyn || devNext) ? dynStats + h : counters + 2;
-            ca.pub = (dyn || devNext) ? Publish{nullptr, 0} : nextPub(c);
+            ca.total = (dyn || devTotal) ? dynStats + h : counters + 2;
+            ca.pub = (dyn || devTotal) ? Publish{nullptr, 0} : nextPub(c);
             ca.zero = nullptr;
             ca.nzero = 0;
             ca.err = errFlag;
@@ -4158,7 +4167,7 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             haveEstart = true;
             haveEbase = true;
             haveHeads = true;
-            if (dyn || devNext) {                               // upper bounds; the device has the real ones
+            if (dyn || devTotal) {                              // upper bounds; the device has the real ones
                 nF = d.V;
                 fusedE = slotEdges;
             } else {

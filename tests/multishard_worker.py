@@ -123,6 +123,7 @@ def main():
             e.set_flag("pull_factor", q.get("pull_factor", default_pf))
             e.set_flag("xchg_lists", q.get("xchg_lists", -1))
             e.set_flag("dst_props", q.get("dst_props", -1))
+            e.set_flag("dense_world_dev", q.get("dense_world_dev", 1))
             preps = [e.prepare_go(datagen.RMAT_SPACE, ngql.parse_go(t), on_device=True, compact=True, yield_only=True)
                      for t in q["batch"]]
             alone = []
@@ -152,6 +153,7 @@ def main():
         e.set_flag("pull_factor", pf[rank] if isinstance(pf, list) else pf)     # a list: per rank
         e.set_flag("xchg_lists", q.get("xchg_lists", -1))
         e.set_flag("dst_props", q.get("dst_props", -1))
+        e.set_flag("dense_world_dev", q.get("dense_world_dev", 1))
         pulls = e.get_flag("pull_hops")
         lists = e.get_flag("xchg_list_hops")
         fetches = e.get_flag("dst_fetches")

@@ -193,6 +193,9 @@ def test_multishard_go_matches_oracle(tmp_path, world, scale):
     # the same queries with every intermediate hop of E >= V / 100 pulled (world > 1 pull: all-gathered
     # frontier bitmap, each shard probing its own rows' in-edges)
     pulled = [dict(q, pull_factor=1) for q in queries] if world != 3 else []
+    # (world 2: also with the dense final hop sized on the host, its totals awaited after the count launch)
+    if world == 2:
+        pulled += [dict(q, pull_factor=1, dense_world_dev=0) for q in queries]
     # and with every hop pushed and its frontier exchanged as vid lists (counts, then the vids: SURVEY
     # §8e) instead of bitmaps
     listed = [dict(q, pull_factor=0, xchg_lists=1) for q in queries]
