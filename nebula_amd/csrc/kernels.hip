@@ -1118,10 +1118,15 @@ __device__ __forceinline__ void closeHead(const A& a, CloseHead& h, bool first) 
         h.M = M;
         h.nh = nh;
         if (first) {
+            // the hop's packed (|F|, E): summed here from the count launch's tiles (dense final hop, whose
+            // kernel never reads it; the word is the device copy the final kernel would otherwise take), or
+            // as the compaction left it
+            uint64_t tot = 0;
             if (a.dynTiles != nullptr) {
-                uint64_t t = 0;
-                for (int w = 0; w < NW; w++) t += h.tsum[w];
-                *const_cast<uint64_t*>(a.dynTotal) = t;
+                for (int w = 0; w < NW; w++) tot += h.tsum[w];
+                *const_cast<uint64_t*>(a.dynTotal) = tot;
+            } else if (a.dynTotal != nullptr) {
+                tot = gld<uint64_t>(a.dynTotal, 0);
             }
             lbStore(a.resvCtl + (1 + G) * st, R);           // the row count (device copy; dyn hops read it)
             for (uint32_t g = 0; g <= G; g++) lbStore(a.resvNext + g * st, 0);   // the next launch's counters
@@ -1129,9 +1134,6 @@ __device__ __forceinline__ void closeHead(const A& a, CloseHead& h, bool first) 
                 uint64_t bits = 0;
                 for (int k = 0; k < 4; k++)
                     bits |= static_cast<uint64_t>(__hip_atomic_load(a.err + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) << k;
-                uint64_t tot = 0;
-                if (a.dynTiles != nullptr) for (int w = 0; w < NW; w++) tot += h.tsum[w];
-                else if (a.dynTotal != nullptr) tot = gld<uint64_t>(a.dynTotal, 0);
                 publishWords(a.rowsPub, a.rowsSeq, R, bits, tot);
             }
         }
