@@ -86,21 +86,29 @@ def c2(rmat22):
     e.close()
 
 
-@pytest.mark.timeout(600)
-def test_c2_bench_step_vs_oracle(c2):
-    """The exact step bench.py times (its first plan: 1000 seeds, sample seed 42), on the graph bench.py
-    builds (in-edges stored, so hop 2 may pull), row for row against the oracle: sorted 128-bit row
-    digests and every hop's scanned edges, with pull at its default factor, forced on every
-    intermediate hop (factor 1) and off (factor 0), and once on the interpreter kernels."""
+@pytest.fixture(scope="module")
+def c2_ref(c2):
+    """bench.py's first timed plan (1000 seeds, sample seed 42) and the oracle's result of it (row digests),
+    computed once for the tests below"""
     ds, o, e = c2
     seeds = datagen.rmat_seeds(22, 1000, 16, 42, 42, threads=16)
     s = ngql.parse_go(C2_QUERY.replace("{S}", _seed_list(seeds)).replace("{K}", "50"))
-    ref = o.go(ds.space, s, digest=True)
+    return s, o.go(ds.space, s, digest=True)
+
+
+@pytest.mark.timeout(600)
+def test_c2_bench_step_vs_oracle(c2, c2_ref):
+    """The exact step bench.py times (its first plan: 1000 seeds, sample seed 42), on the graph bench.py
+    builds (in-edges stored, so hop 2 may pull), row for row against the oracle: sorted 128-bit row
+    digests and every hop's scanned edges, with pull at its default factor (hop 2 pulls: the hops a
+    factor of 1 would pull too), off (factor 0), and once on the interpreter kernels."""
+    ds, o, e = c2
+    s, ref = c2_ref
     assert ref.ok and ref.nrows > 20_000_000 and sum(ref.hop_scanned) > 60_000_000
     default = e.get_flag("pull_factor")
     pulls = {}
     try:
-        for factor, jit in ((default, 1), (1, 1), (0, 1), (default, 0)):
+        for factor, jit in ((default, 1), (0, 1), (default, 0)):
             e.set_flag("pull_factor", factor)
             e.set_flag("jit", jit)
             before = e.get_flag("pull_hops")
@@ -111,8 +119,7 @@ def test_c2_bench_step_vs_oracle(c2):
     finally:
         e.set_flag("pull_factor", default)
         e.set_flag("jit", 1)
-    # factor 1 pulls every intermediate hop with E >= V / 100 (hop 2 here; hop 1 scans ~1 % of V)
-    assert pulls[(1, 1)] >= 1 and pulls[(0, 1)] == 0 and pulls[(default, 1)] >= 1
+    assert pulls[(0, 1)] == 0 and pulls[(default, 1)] >= 1
     # the bench's own result placement: rows in HBM with compact integer arrays (compact_results), the
     # YIELD columns only (yield_only: no src row array), fetched and widened, digest for digest equal to
     # the oracle's rows; and with the row arrays (bench.py --row-arrays)
@@ -132,7 +139,7 @@ def test_c2_bench_step_vs_oracle(c2):
 
 
 @pytest.mark.timeout(300)
-def test_c2_bench_batch_pinned(c2):
+def test_c2_bench_batch_pinned(c2, c2_ref):
     """The timed path itself at C2 (What's weak #2): bench.py's own timed plans — its
     sentence(i) seeds (rmat_seeds(..., 42, 42 + i)), 20 of them, compact YIELD-only device results — run
     through ngx_go_batch (four lanes, two front streams, two final streams, deferred frees, per-lane rows)
@@ -173,7 +180,7 @@ def test_c2_bench_batch_pinned(c2):
             assert code == 0 and (nrows, edges) == (alone.nrows, sum(alone.hop_edges)), i
             assert tuple(dig) == tuple(alone.device_digest), i
     # plan 0 against the oracle: its fetched rows' 128-bit digests, and the batch digest of those rows
-    ref = o.go(ds.space, sents[0], digest=True)
+    _, ref = c2_ref                                 # the same plan as sents[0] (seed sample 42 + 0)
     assert ref.ok and ref.nrows == got[4][1] and sum(ref.hop_scanned) == got[4][2]
     r = e.go(ds.space, sents[0], on_device=True, fetch=True, compact=True, yield_only=True)
     assert r.ok
