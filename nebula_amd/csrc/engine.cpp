@@ -4133,8 +4133,8 @@ int32_t runGo(ngx_ctx* c, Space& sp, const ngx_go_plan& p, GoResultHolder& R, co
             c->bitsClean = false;
             const bool devNext = finalDev && h + 1 == steps;      // the next hop is the device-sized final one
             // dense final hop next: after a pull (its frontier is most of the shard's edges), one OVER type; at
-            // world > 1 too (the pull marked this shard's own rows, no exchange follows it), host-sized there,
-            // but not with the $$ owner fetch (it expands the frontier list)
+            // world > 1 too (the pull marked this shard's own rows, no exchange follows it), but not with the
+            // $$ owner fetch (it expands the frontier list)
             const bool denseNext = (devNext || (c->world > 1 && !dyn && h + 1 == steps && !ownerDst)) && c->denseFinal &&
                                    pull && !mask && !capped && !rw && hs.n == 1 && recordFrom == steps &&
                                    hs.slotIdx[0] >= 0 && hs.slotIdx[0] < static_cast<int32_t>(d.chunkRow.size());
