@@ -465,7 +465,7 @@ int32_t ngx_kernel_stats(ngx_ctx* ctx, const ngx_kernel_stat** out, int32_t* n);
  *   "batch_pipeline"  1 (default): ngx_go_batch overlaps consecutive device-resident queries (the next
  *          one's host work and first hops enqueued while this one's final hop runs); 0: strictly one
  *          after the other. Same results.
- *   "batch_lanes"  2 .. 4 (default 4): lanes of scratch and result rows a pipelined batch rotates over; up
+ *   "batch_lanes"  2 .. 8 (default 4): lanes of scratch and result rows a pipelined batch rotates over; up
  *          to lanes - 1 queries wait for their row counts while the next one runs its hops. Same results.
  *   "batch_fronts"  1 or 2 (default 2): streams the batch's hops run on (consecutive queries alternate;
  *          world > 1 always 1, so every rank issues its collectives in one order).

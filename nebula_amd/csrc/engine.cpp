@@ -197,7 +197,7 @@ struct ngx_ctx {
     uint64_t* pin = nullptr;                           // host-mapped [value, seq]: scan totals published by
     uint64_t* pinDev = nullptr;                        // k_scan_tiles (kernels.h Publish)
     uint64_t pinSeq = 0;                               // words [0, 2): scan totals; [kTailOff ..): query tail
-    static constexpr size_t kPinBytes = 8192;           // up to four lanes of 256 words (ngx_ctx::Lane)
+    static constexpr size_t kPinBytes = 16384;          // up to eight lanes of 256 words (ngx_ctx::Lane)
     static constexpr size_t kTailOff = 8;               // k_publish_tail: seq, error bits, extra words
     static constexpr uint32_t kSeedSlot = 80;           // the seed hop's publication (nextPub)
     static constexpr uint32_t kRowsSlot = 88;           // a record hop's row count (k_final_close)
@@ -334,7 +334,7 @@ struct ngx_ctx {
     // active (parked[activeLane] holds an empty set); useLane swaps sets.
     uint32_t pinLane = 0;
     static constexpr uint32_t kLaneWords = 256;
-    static constexpr int kMaxLanes = 4;                 // kPinBytes / (8 * kLaneWords)
+    static constexpr int kMaxLanes = 8;                 // kPinBytes / (8 * kLaneWords)
     struct Lane {
         DBuf visited, F0, F1, estart, ebase, chunkFirst, estart2, ebase2, chunkFirst2, tileSums, counters, lbStatus,
             seedPart, seedVid, cmpStatus[2], frontierBits, localBits, edgeMask, pullSeg, pullCtl, sparseCtl, dynStats, progBuf;
@@ -401,10 +401,10 @@ struct ngx_ctx {
     // that close still moves the earlier query's rows inside the lane's result arrays and reads its block
     // table after the earlier query has read its row count (published by the close's first workgroup), and
     // with two final streams nothing else orders the two (r06: a C2 batch at 4 groups failed on it)
-    hipEvent_t laneCloseEv[kMaxLanes] = {nullptr, nullptr, nullptr, nullptr};
-    bool laneClosePending[kMaxLanes] = {false, false, false, false};                           // C2: 0.302 vs 0.309 ms per step (tools/ab_batch.py, 10 rounds)
+    hipEvent_t laneCloseEv[kMaxLanes] = {};
+    bool laneClosePending[kMaxLanes] = {};                           // C2: 0.302 vs 0.309 ms per step (tools/ab_batch.py, 10 rounds)
     hipStream_t finalStream2 = nullptr, finalCur = nullptr;
-    void* coStack[kMaxLanes] = {nullptr, nullptr, nullptr, nullptr};
+    void* coStack[kMaxLanes] = {};
     static constexpr size_t kCoStackBytes = size_t(16) << 20;   // + a guard page below each
     void swapLane(Lane& L) {
 #define NGX_LANE_SWAP(f) std::swap(f, L.f);
@@ -1631,12 +1631,17 @@ int32_t ngx_open(const ngx_config* cfg, ngx_ctx** out) {
     if (hipSetDevice(c->device) != hipSuccess) return NGX_E_DEVICE;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return NGX_E_DEVICE;
     {                                                 // ngx_go_batch's pipeline (without them: one at a time)
-        // the hops (latency-bound) at the higher priority, the final hops (bandwidth-bound) at the lower:
-        // 0.365 / 0.371 vs 0.374 / 0.412 ms per C2 step with both at the default, same box (r05)
+        // the hops (latency-bound, streams 0 and 2) at the higher priority, the final hops (bandwidth-bound,
+        // streams 1 and 3: the two final streams, or the final and the close stream) at the lower: 0.365 /
+        // 0.371 vs 0.374 / 0.412 ms per C2 step with both at the default, same box (r05); r06, stream 3 at
+        // the lower too once it carries every second final hop: 0.2612 / 0.2648 vs 0.2753 / 0.2806 (two
+        // process pairs, 4 rounds each)
         int prLo = 0, prHi = 0;
         (void)hipDeviceGetStreamPriorityRange(&prLo, &prHi);
+        // (r06, priorities front / final / front / final, in-process medians: -1 / 1 / -1 / 1 0.2608 and 0.2574,
+        // 0 / 1 / -1 / 1 0.2580, -1 / 1 / 0 / 1 0.2585; either final stream at the normal 0: 0.277 - 0.280)
         for (int k = 0; k < 4; k++)
-            if (hipStreamCreateWithPriority(&c->pipeStreams[k], hipStreamNonBlocking, k == 1 ? prLo : prHi) != hipSuccess)
+            if (hipStreamCreateWithPriority(&c->pipeStreams[k], hipStreamNonBlocking, (k & 1) ? prLo : prHi) != hipSuccess)
                 c->pipeStreams[k] = nullptr;
         for (auto& e : c->pipeEv)
             if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
@@ -2082,7 +2087,7 @@ int32_t ngx_set_flag(ngx_ctx* c, const char* name, int64_t value) {
         return NGX_OK;
     }
     if (n == "batch_lanes") {
-        if (value < 2 || value > ngx_ctx::kMaxLanes) return fail(c, NGX_E_BAD_ARGUMENT, "batch_lanes: 2 .. 4");
+        if (value < 2 || value > ngx_ctx::kMaxLanes) return fail(c, NGX_E_BAD_ARGUMENT, "batch_lanes: 2 .. 8");
         c->batchLanes = static_cast<int32_t>(value);
         return NGX_OK;
     }

@@ -152,7 +152,7 @@ def test_batch_last_result_stays_on_device(rmat):
 
 
 @pytest.mark.parametrize("lanes,close_stream,fronts", [(2, 0, 2), (3, 0, 2), (4, 0, 2), (3, 0, 1), (3, 1, 1), (2, 1, 1),
-                                                        (3, 1, 2)])
+                                                        (3, 1, 2), (8, 0, 2)])
 def test_batch_lanes(rmat, lanes, close_stream, fronts):
     """Deeper pipelines (flag batch_lanes: up to lanes - 1 queries wait for their row counts while the next
     one runs its hops on its own lane and its own result rows), consecutive queries' hops on two front
@@ -190,7 +190,7 @@ def test_batch_lanes(rmat, lanes, close_stream, fronts):
                 assert tuple(g[3]) == tuple(w[3]), (q, m)
     assert overlaps >= 10
     with pytest.raises(Exception):
-        e.set_flag("batch_lanes", 5)
+        e.set_flag("batch_lanes", 9)
 
 
 def _digest_fixed(q, mode):
