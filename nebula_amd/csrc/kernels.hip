@@ -316,7 +316,7 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
                                                     uint64_t nEnt, uint64_t E, HopSlots hs, uint8_t* visited,
                                                     uint8_t epoch, const uint8_t* mask, const uint64_t* dyn,
                                                     uint64_t pullMinE, const uint64_t* ebase) {
-    __shared__ ChunkMap<ONE, false, P32> m;
+    __shared__ ChunkMap<ONE, false, P32, false> m;      // (no src rows: the expansion marks destinations)
     // direct-mapped LDS filter of the rows this workgroup already marked: a repeated destination
     // (hubs of a power-law graph) costs an LDS probe instead of another L2 byte-store transaction
     constexpr int kSeenBits = 11;
@@ -333,7 +333,7 @@ __global__ __launch_bounds__(WG) void k_expand_mark(const uint32_t* F, const uin
     for (uint32_t chunk = blockIdx.x; chunk < nChunks; chunk += gridDim.x) {
     const uint64_t base = static_cast<uint64_t>(chunk) * CE;
     const uint32_t cnt = static_cast<uint32_t>(E - base < CE ? E - base : CE);
-    buildMap<ONE, false, P32>(estart, chunkFirst, nEnt, chunk, nChunks, base, cnt, F, hs, m, ebase);
+    buildMap<ONE, false, P32, false>(estart, chunkFirst, nEnt, chunk, nChunks, base, cnt, F, hs, m, ebase);
     uint32_t g[CITEMS];
 #pragma unroll
     for (int k = 0; k < CITEMS; k++) {
@@ -549,7 +549,7 @@ __global__ __launch_bounds__(WGS) void k_compact_write(CompactArgs a) {
 constexpr int kSparseSub = CE / WG;                     // 8 slices of 256 edges per chunk
 template <bool ONE, bool P32>
 __global__ __launch_bounds__(WG) void k_expand_sparse(SparseArgs a) {
-    __shared__ ChunkMap<ONE, false, P32> m;
+    __shared__ ChunkMap<ONE, false, P32, false> m;      // (no src rows: the expansion marks destinations)
     __shared__ uint64_t sm[NW + 1];
     __shared__ uint64_t sBase;
     // direct-mapped LDS filter of the destinations this workgroup already sent an atomic for (as in
@@ -577,7 +577,7 @@ __global__ __launch_bounds__(WG) void k_expand_sparse(SparseArgs a) {
         const uint32_t chunk = item / kSparseSub, sub = item % kSparseSub;
         const uint64_t base = static_cast<uint64_t>(chunk) * CE;
         const uint32_t cnt = static_cast<uint32_t>(E - base < CE ? E - base : CE);
-        buildMap<ONE, false, P32>(a.estart, a.chunkFirst, nEnt, chunk, nChunks, base, cnt, a.F, a.hs, m, a.ebase);
+        buildMap<ONE, false, P32, false>(a.estart, a.chunkFirst, nEnt, chunk, nChunks, base, cnt, a.F, a.hs, m, a.ebase);
         const uint32_t p = sub * WG + threadIdx.x;          // this lane's edge of the chunk
         uint32_t g = kNoRow;
         if (p < cnt) {
