@@ -6,6 +6,8 @@
 #include "orc_query.h"
 
 #include <atomic>
+#include <functional>
+#include <thread>
 #include <numeric>
 
 namespace orc {
@@ -13,45 +15,87 @@ namespace orc {
 // ---------------------------------------------------------------- KVStore
 void KVStore::finalize(int threads) {
     if (sorted_) return;
-    // stable order for equal keys => the later put sits later; keep the last (RocksDB overwrite)
-    std::vector<uint64_t> order(ents_.size());
-    std::iota(order.begin(), order.end(), 0);
-    auto cmp = [this](uint64_t a, uint64_t b) {
-        int c = std::memcmp(blob_.data() + ents_[a].off, blob_.data() + ents_[b].off,
-                            std::min(ents_[a].klen, ents_[b].klen));
-        if (c != 0) return c < 0;
-        if (ents_[a].klen != ents_[b].klen) return ents_[a].klen < ents_[b].klen;
-        return a < b;
+    // RocksDB's bytewise order, the later put of a key kept (a stable order for equal keys: the put index
+    // breaks ties). Each entry carries its first 16 key bytes as two big-endian words, so most comparisons
+    // never touch the blob; the entries are bucketed by their first two key bytes (the key type and the
+    // part's low byte) and the buckets sorted in parallel, independently, and concatenated. (32 bytes: an
+    // edge key's part, src, type, rank and dst.)
+    struct SK {
+        uint64_t p[4];
+        uint64_t i;
+    };
+    const size_t n = ents_.size();
+    std::vector<SK> keys(n);
+    auto be = [](const char* k, size_t len) {
+        uint64_t v = 0;
+        for (size_t b = 0; b < 8; b++) v = (v << 8) | (b < len ? static_cast<uint8_t>(k[b]) : 0u);
+        return v;
     };
     threads = std::max(1, threads);
-    size_t n = order.size();
-    if (threads == 1 || n < (1u << 16)) {
-        std::sort(order.begin(), order.end(), cmp);
-    } else {
+    auto parallel = [&](size_t count, const std::function<void(size_t, size_t)>& f) {
+        const int t = count < (1u << 16) ? 1 : threads;
         std::vector<std::thread> ts;
-        std::vector<size_t> cuts;
-        for (int t = 0; t <= threads; t++) cuts.push_back(n * t / threads);
-        for (int t = 0; t < threads; t++) {
-            ts.emplace_back([&, t] { std::sort(order.begin() + cuts[t], order.begin() + cuts[t + 1], cmp); });
+        for (int k = 0; k < t; k++) ts.emplace_back([&, k] { f(count * k / t, count * (k + 1) / t); });
+        for (auto& th : ts) th.join();
+    };
+    parallel(n, [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; i++) {
+            const char* k = blob_.data() + ents_[i].off;
+            const size_t kl = ents_[i].klen;
+            SK x;
+            for (size_t w = 0; w < 4; w++) x.p[w] = kl > 8 * w ? be(k + 8 * w, kl - 8 * w) : 0;
+            x.i = i;
+            keys[i] = x;
+        }
+    });
+    auto cmp = [this](const SK& a, const SK& b) {
+        for (int w = 0; w < 4; w++)
+            if (a.p[w] != b.p[w]) return a.p[w] < b.p[w];
+        const Ent& ea = ents_[a.i];
+        const Ent& eb = ents_[b.i];
+        const uint32_t la = ea.klen > 32 ? ea.klen - 32 : 0, lb = eb.klen > 32 ? eb.klen - 32 : 0;
+        if (la && lb) {
+            const int c = std::memcmp(blob_.data() + ea.off + 32, blob_.data() + eb.off + 32, std::min(la, lb));
+            if (c != 0) return c < 0;
+        }
+        if (ea.klen != eb.klen) return ea.klen < eb.klen;      // (zero padding above: the shorter key first)
+        return a.i < b.i;
+    };
+    // buckets by the first two key bytes
+    std::vector<size_t> cnt(65537, 0);
+    for (const SK& k : keys) cnt[(k.p[0] >> 48) + 1]++;
+    for (size_t b = 1; b <= 65536; b++) cnt[b] += cnt[b - 1];
+    std::vector<SK> sorted(n);
+    {
+        std::vector<size_t> at(cnt.begin(), cnt.end() - 1);
+        for (const SK& k : keys) sorted[at[k.p[0] >> 48]++] = k;
+    }
+    keys.clear();
+    keys.shrink_to_fit();
+    std::vector<size_t> nonEmpty;
+    for (size_t b = 0; b < 65536; b++) if (cnt[b + 1] > cnt[b]) nonEmpty.push_back(b);
+    std::atomic<size_t> next{0};
+    {
+        std::vector<std::thread> ts;
+        for (int t = 0; t < (n < (1u << 16) ? 1 : threads); t++) {
+            ts.emplace_back([&] {
+                for (size_t j; (j = next.fetch_add(1)) < nonEmpty.size();) {
+                    const size_t b = nonEmpty[j];
+                    std::sort(sorted.begin() + cnt[b], sorted.begin() + cnt[b + 1], cmp);
+                }
+            });
         }
         for (auto& th : ts) th.join();
-        for (size_t w = 1; w < static_cast<size_t>(threads); w <<= 1) {
-            std::vector<std::thread> ms;
-            for (size_t t = 0; t + w < static_cast<size_t>(threads); t += 2 * w) {
-                size_t lo = cuts[t], mid = cuts[t + w], hi = cuts[std::min<size_t>(t + 2 * w, threads)];
-                ms.emplace_back([&, lo, mid, hi] {
-                    std::inplace_merge(order.begin() + lo, order.begin() + mid, order.begin() + hi, cmp);
-                });
-            }
-            for (auto& th : ms) th.join();
-        }
     }
     std::vector<Ent> out;
     out.reserve(n);
     for (size_t i = 0; i < n; i++) {
-        const Ent& e = ents_[order[i]];
-        if (!out.empty() && out.back().klen == e.klen &&
-            std::memcmp(blob_.data() + out.back().off, blob_.data() + e.off, e.klen) == 0) {
+        const Ent& e = ents_[sorted[i].i];
+        // the same key as the previous one: equal prefix words first (the blob only for longer keys)
+        const bool samePrefix = i > 0 && sorted[i].p[0] == sorted[i - 1].p[0] && sorted[i].p[1] == sorted[i - 1].p[1] &&
+                                sorted[i].p[2] == sorted[i - 1].p[2] && sorted[i].p[3] == sorted[i - 1].p[3];
+        if (samePrefix && out.back().klen == e.klen &&
+            (e.klen <= 32 || std::memcmp(blob_.data() + out.back().off + 32, blob_.data() + e.off + 32, e.klen - 32) == 0)) {
             out.back() = e;                       // same key: the later write wins
         } else {
             out.push_back(e);
