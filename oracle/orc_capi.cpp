@@ -206,7 +206,7 @@ int32_t orc_add_schema(void* e, int32_t space, int32_t isEdge, int32_t id, const
 void orc_put_kv(void* e, int32_t space, uint64_t n, const uint8_t* keys, const uint64_t* koff,
                 const uint8_t* vals, const uint64_t* voff) {
     auto& kv = static_cast<StorageEngine*>(e)->stores[space];
-    kv.reserve(kv.size() + n, 0);
+    kv.reserve(kv.size() + n, (koff[n] - koff[0]) + (voff[n] - voff[0]));   // (added to what the store holds)
     for (uint64_t i = 0; i < n; i++) {
         kv.put(reinterpret_cast<const char*>(keys + koff[i]), koff[i + 1] - koff[i],
                reinterpret_cast<const char*>(vals + voff[i]), voff[i + 1] - voff[i]);

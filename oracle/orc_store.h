@@ -80,7 +80,7 @@ class KVStore {
         uint32_t klen;
         uint32_t vlen;
     };
-    void reserve(size_t n, size_t bytes) { ents_.reserve(n); blob_.reserve(bytes); }
+    void reserve(size_t n, size_t moreBytes) { ents_.reserve(n); blob_.reserve(blob_.size() + moreBytes); }
     void put(const char* k, size_t kl, const char* v, size_t vl) {
         Ent e{blob_.size(), static_cast<uint32_t>(kl), static_cast<uint32_t>(vl)};
         blob_.insert(blob_.end(), k, k + kl);
