@@ -164,6 +164,14 @@ def _check_merged(o, space, queries, shards, digests):
             merged = np.unique(merged, axis=0)
         merged = oracle.sort_digests(merged.view(np.uint8).reshape(-1)) if len(merged) else merged
         assert len(merged) == ref.nrows, q["text"]
+        if not np.array_equal(merged, ref.digests):
+            # (diagnostics: how many rows differ, and which shard holds the extra ones)
+            a_ = {tuple(x) for x in merged.tolist()}
+            b_ = {tuple(x) for x in np.asarray(ref.digests).tolist()}
+            extra, missing = a_ - b_, b_ - a_
+            per = [sum(tuple(x) in extra for x in np.asarray(d).tolist()) for d in digests[i]]
+            print(f"query {i}: {len(extra)} rows not in the oracle's, {len(missing)} missing; per shard {per}; "
+                  f"shard rows {[len(d) for d in digests[i]]}; hop edges {[r.get('hop_edges') for r in res]}", flush=True)
         assert np.array_equal(merged, ref.digests), q["text"]
         # every shard scanned its own parts: the per-hop sums are the single-process scan
         hops = min(len(r["hop_edges"]) for r in res)
