@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--sleep-ms", type=float, default=0, help="idle host time before each timed batch")
     ap.add_argument("--busy-ms", type=float, default=0, help="unrelated device work (buffer fills) before round 0")
     ap.add_argument("--prewarm-warm", type=int, default=0, help="untimed batches of the warm-up plans only before round 0")
+    ap.add_argument("--spin-ms", type=float, default=0, help="host busy loop (no GPU work) before each timed batch")
     args = ap.parse_args()
     import torch
     from nebula_amd import datagen, engine, ngql
@@ -101,6 +102,10 @@ def main():
             for code, _, _ in eng.go_batch(warm):
                 assert code == 0
             torch.cuda.synchronize()
+            if args.spin_ms:
+                t_s = time.perf_counter()
+                while (time.perf_counter() - t_s) * 1e3 < args.spin_ms:
+                    pass
             a0 = eng.get_flag("dbuf_allocs")
             print(f"[ab] timed batch {v} round {r} begins", file=sys.stderr, flush=True)
             t = time.perf_counter()
