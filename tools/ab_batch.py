@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--busy-ms", type=float, default=0, help="unrelated device work (buffer fills) before round 0")
     ap.add_argument("--prewarm-warm", type=int, default=0, help="untimed batches of the warm-up plans only before round 0")
     ap.add_argument("--spin-ms", type=float, default=0, help="host busy loop (no GPU work) before each timed batch")
+    ap.add_argument("--commit-flag", action="append", default=[], help="NAME=VALUE engine flag set before the load")
     args = ap.parse_args()
     import torch
     from nebula_amd import datagen, engine, ngql
@@ -45,6 +46,9 @@ def main():
     t0 = time.time()
     c = datagen.rmat_csr(args.scale, 16, 42, 100, with_in=True, threads=args.threads)
     eng = engine.Engine(0)
+    for kv in args.commit_flag:
+        n, _, val = kv.partition("=")
+        eng.set_flag(n, int(val))
     eng.add_space(datagen.RMAT_SPACE, 100)
     for is_edge, sid, name, fields in datagen.rmat_schemas():
         eng.add_schema(datagen.RMAT_SPACE, is_edge, sid, name, fields)
