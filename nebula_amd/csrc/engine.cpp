@@ -245,7 +245,10 @@ struct ngx_ctx {
                 // 25 % headroom: result sizes vary from query to query, and re-pinning a GB-sized
                 // staging block costs more than the copy itself
                 size_t c = std::max(bytes + bytes / 4, cap * 3 / 2);
-                HIP_OK(hipHostMalloc(&p, c, hipHostMallocDefault));
+                // coherent (fine-grained): kernels read the seeds / inputs the host just wrote, and the copy
+                // kernel stores results the host reads after the stream synchronises; neither may meet a
+                // stale line the GPU kept cached from an earlier query (hipHostMallocDefault is non-coherent)
+                HIP_OK(hipHostMalloc(&p, c, hipHostMallocMapped | hipHostMallocCoherent));
                 cap = c;
             }
             return static_cast<char*>(p);
